@@ -1,0 +1,555 @@
+"""Generate golden fixtures by RUNNING THE REFERENCE'S OWN PYTHON in this container.
+
+Run once here (needs /root/reference; never runs on the GPU box):
+
+    python tests/golden/make_golden.py
+
+What it runs (reference paths relative to the reference repo root):
+  * src/deep_impact/indexing/indexer.py:31-68   Indexer.index  (impact TSV text, A8/A9)
+  * src/deep_impact/models/xlmr_original.py      DeepImpact (XLM-R) process_document,
+        process_query, forward, compute_term_impacts, get_impact_scores_batch (A3/A5/A7/A8)
+        -- instantiated from a small local config with seeded weights, and driven by the
+        locally built tokenizer of tests/golden/local_tokenizer.py (the real sentencepiece
+        model is a hub download that does not exist offline)
+  * src/deep_impact/indexing/quantize.py:27-47  quantize_file (A10)
+  * src/deep_impact/inverted_index/create.py    InvertedIndexCreator (A11)
+  * src/deep_impact/inverted_index/inverted_index.py:55-62  InvertedIndex.score (A12)
+  * src/deep_impact/evaluation/nano_beir_evaluator.py:70-137  SparseSearch (A14/A15)
+  * src/deep_impact/evaluation/metrics.py:26-57  Metrics.evaluate (F2)
+
+Three version shims, all documented in DESIGN.md: (1) transformers 5.x removed
+``encode_plus``; the wrapper below forwards it to ``__call__`` with the same
+arguments (the transformers 4.30 meaning).  (2) ``beir`` is not installed; a stub
+``EvaluateRetrieval`` satisfies the module-level import of nano_beir_evaluator.py
+(evaluation itself is not called).  (3) transformers 5.x ``init_weights`` needs
+state that the 4.30-era ``__init__`` never sets up; it is made a no-op because the
+seeded weights are loaded right after construction (strict load_state_dict).
+
+Outputs go to tests/golden/ next to this file.  Everything is small (< 2 MB).
+"""
+from __future__ import annotations
+
+import importlib.util
+import io
+import json
+import os
+import shutil
+import struct
+import sys
+import tempfile
+import types
+from pathlib import Path
+
+import numpy as np
+import torch
+
+HERE = Path(__file__).resolve().parent
+REF = Path("/root/reference")
+sys.dont_write_bytecode = True
+sys.path.insert(0, str(REF))
+sys.path.insert(0, str(HERE))
+
+import local_tokenizer  # noqa: E402
+
+# --- reference import preconditions ---------------------------------
+import src.utils.defaults as ref_defaults  # noqa: E402
+
+ref_defaults.LOG_DIR = Path(tempfile.mkdtemp(prefix="ref_logs_"))
+ref_defaults.DEVICE = torch.device("cpu")
+
+
+def load_by_path(name, rel):
+    spec = importlib.util.spec_from_file_location(name, REF / rel)
+    mod = importlib.util.module_from_spec(spec)
+    sys.modules[name] = mod
+    spec.loader.exec_module(mod)
+    return mod
+
+
+class _EncodePlusShim:
+    """transformers 5.x tokenizer wrapper exposing the 4.30 ``encode_plus``."""
+
+    def __init__(self, ft):
+        self._ft = ft
+
+    def encode_plus(self, text, **kw):
+        if "is_pretokenized" in kw:
+            kw["is_split_into_words"] = kw.pop("is_pretokenized")
+        return self._ft(text, **kw)
+
+    def __getattr__(self, item):
+        return getattr(self._ft, item)
+
+    def __setattr__(self, key, value):
+        if key == "_ft":
+            object.__setattr__(self, key, value)
+        else:
+            setattr(self._ft, key, value)
+
+
+def load_reference_models():
+    import transformers
+
+    shim = _EncodePlusShim(local_tokenizer.build_hf_tokenizer())
+    orig = transformers.AutoTokenizer.from_pretrained
+    transformers.AutoTokenizer.from_pretrained = classmethod(lambda cls, *a, **k: shim)
+    try:
+        xlmr = load_by_path("ref_xlmr_original", "src/deep_impact/models/xlmr_original.py")
+    finally:
+        transformers.AutoTokenizer.from_pretrained = orig
+    return xlmr
+
+
+def load_reference_sparse_search():
+    beir = types.ModuleType("beir")
+    beir_r = types.ModuleType("beir.retrieval")
+    beir_e = types.ModuleType("beir.retrieval.evaluation")
+
+    class EvaluateRetrieval:  # import-time stub only
+        pass
+
+    beir_e.EvaluateRetrieval = EvaluateRetrieval
+    sys.modules.update({"beir": beir, "beir.retrieval": beir_r,
+                        "beir.retrieval.evaluation": beir_e})
+    return load_by_path("ref_nano_beir", "src/deep_impact/evaluation/nano_beir_evaluator.py")
+
+
+# ------------------------------------------------------------------------------
+# deterministic synthetic data (BASELINE.md §2 generator, small sizes)
+# ------------------------------------------------------------------------------
+def synthetic_docs(n_docs, v_terms, seed=1234, max_terms=100):
+    rng = np.random.default_rng(seed)
+    docs = []
+    for _ in range(n_docs):
+        terms = np.unique(np.minimum(rng.zipf(1.2, 200), v_terms))[:max_terms]
+        rng.shuffle(terms)
+        imp = np.log1p(np.exp(rng.normal(-0.5, 1.5, len(terms)))).astype(np.float32)
+        docs.append(([f"▁t{t}" for t in terms], imp))
+    return docs
+
+
+def edge_docs():
+    """Hand-made docs: ties, punctuation-bearing terms, unicode, empty docs."""
+    f = np.float32
+    return [
+        (["▁world,", "▁it's", "▁3.5", "▁a:b", "▁x,y", "▁.", "▁Ünïcödé", "▁日本"],
+         np.array([1.0, 0.0005, 4.527, 2.25, 0.0015, 0.9995, 3.14159, 12.5], f)),
+        ([], np.array([], f)),
+        (["▁t1", "▁t2", "▁t3"], np.array([2.0, 2.0, 2.0], f)),
+        (["▁t2", "▁t1", "▁t4"], np.array([2.0, 2.0, 0.0001], f)),
+        (["▁zero"], np.array([0.0], f)),
+        (["▁t1", "▁big"], np.array([9.999, 19.9995], f)),
+    ]
+
+
+class _FakeEncoding:
+    def __init__(self, n):
+        self.ids = list(range(n))
+        self.attention_mask = [1] * n
+        self.type_ids = [0] * n
+
+
+class FakeModelCls:
+    """Model protocol of Indexer (indexer.py:33,46,57) driven by precomputed impacts.
+
+    A "document" is the index of an entry in FakeModelCls.docs; token i+1 of the
+    doc carries the impact of term i (token 0 plays <s>)."""
+
+    docs = []
+    S = 128
+    compute_term_impacts = None  # set to the reference staticmethod
+
+    @classmethod
+    def process_document(cls, doc_idx):
+        terms, _ = cls.docs[doc_idx]
+        return _FakeEncoding(cls.S), {t: i + 1 for i, t in enumerate(terms)}
+
+    def __call__(self, ids, mask, type_ids):
+        rows = ids[:, 0].tolist()
+        # ids[:,j] = j for our fake encoding; recover doc index from a side channel
+        out = torch.zeros(ids.shape[0], self.S, 1)
+        for r, doc_idx in enumerate(self._batch_docs[: ids.shape[0]]):
+            _, imp = self.docs[doc_idx]
+            out[r, 1:1 + len(imp), 0] = torch.from_numpy(imp)
+        self._batch_docs = self._batch_docs[ids.shape[0]:]
+        del rows
+        return out
+
+
+class _SerialPool:
+    def map(self, f, xs):
+        return [f(x) for x in xs]
+
+
+def run_reference_indexer(indexer_mod, xlmr_mod, docs, out_path, model_batch=32, pbs=1600):
+    """Drive the reference Indexer.index exactly as index.run does (index.py:32-44)."""
+    FakeModelCls.docs = docs
+    FakeModelCls.S = 2 + max((len(t) for t, _ in docs), default=0)
+    FakeModelCls.compute_term_impacts = staticmethod(xlmr_mod.DeepImpact.compute_term_impacts)
+    idx = indexer_mod.Indexer.__new__(indexer_mod.Indexer)
+    idx.model_cls = FakeModelCls
+    idx.model = FakeModelCls()
+    idx.pool = _SerialPool()
+    idx.batch_size = model_batch
+    with open(out_path, "w") as out:
+        batch = []
+        for i, d in enumerate(range(len(docs)), start=1):
+            if i % pbs == 0:
+                idx.model._batch_docs = list(batch)
+                idx.index(batch, out)
+                batch = []
+            batch.append(d)
+        idx.model._batch_docs = list(batch)
+        idx.index(batch, out)
+
+
+# ------------------------------------------------------------------------------
+def gen_round3(out):
+    """A9: f'{round(np.float32(x), 3)}' (indexer.py:132) on float32 edge values."""
+    rng = np.random.default_rng(7)
+    vals = [0.0, 0.0004999, 0.0005, 0.0005001, 0.0015, 0.0025, 1.0, 4.527, 4.5265, 4.5275,
+            0.1, 0.2, 0.3, 1e-8, 1e-30, 3.4e38, 65504.0, 16777216.0, 123456.789, 0.9995,
+            1.0005, 2.0005, 19.9995, 1e-3, 2e-3, 5e-4, 1.5e-3, 7.0, 99.9999, 1234.5675,
+            -0.0, -1e-9, -0.0004, -1.2345, 0.00049999997]
+    vals = np.array(vals, np.float32)
+    rand = np.concatenate([
+        rng.uniform(0, 20, 20000).astype(np.float32),
+        np.log1p(np.exp(rng.normal(-0.5, 1.5, 20000))).astype(np.float32),
+        (rng.integers(0, 20000, 5000) / 1000.0 + 0.0005).astype(np.float32),
+        rng.uniform(0, 1e-2, 5000).astype(np.float32),
+    ])
+    vals = np.concatenate([vals, rand])
+    strs = [f"{round(v, 3)}" for v in vals]  # the reference expression, verbatim
+    np.save(out / "round3_in.npy", vals.view(np.uint32))
+    (out / "round3_out.txt").write_text("\n".join(strs) + "\n")
+
+
+def gen_collection_pipeline(out, indexer_mod, xlmr_mod, quant_mod, create_mod, ii_mod):
+    docs = synthetic_docs(300, 2000) + edge_docs()
+    rng = np.random.default_rng(99)
+    order = rng.permutation(len(docs))
+    docs = [docs[i] for i in order]
+    run_reference_indexer(indexer_mod, xlmr_mod, docs, out / "collection.index", pbs=100)
+    # the documents themselves (terms + f32 impacts) as the encoder would emit them
+    with open(out / "collection.docs.json", "w") as f:
+        json.dump([{"terms": t, "impacts_f32_bits": imp.view(np.uint32).tolist()}
+                   for t, imp in docs], f, ensure_ascii=False)
+
+    # A10: the reference quantizer raises on empty lines (quantize.py:22,43) -- the
+    # quantize input therefore must not contain empty docs; keep a copy without them
+    lines = (out / "collection.index").read_text().split("\n")[:-1]
+    tmpd = Path(tempfile.mkdtemp(prefix="golden_"))
+    (tmpd / "noempty.index").write_text("\n".join(l for l in lines if l.strip()) + "\n")
+    quant_mod.quantize_file(tmpd / "noempty.index", out / "collection.quantized")
+    quant_mod.quantize_file(tmpd / "noempty.index", out / "collection.quantized.m7",
+                            max_val=7.0)
+    try:
+        quant_mod.quantize_file(out / "collection.index", out / "_tmp_q")
+        raise SystemExit("expected the reference quantizer to fail on an empty line")
+    except ValueError:
+        pass
+    (out / "_tmp_q").unlink(missing_ok=True)
+
+    # A10 edge: maxima m where int(m * (255/m)) == 254
+    ms = []
+    for i in range(1000, 10000):
+        m = i / 1000.0
+        if int(m * (255 / m)) == 254:
+            ms.append(m)
+        if len(ms) == 5:
+            break
+    with open(out / "q254.index", "w") as f:
+        for m in ms:
+            f.write(f"▁a: {m}, ▁b: {m / 2}, ▁c: 0.001\n")
+    quant_mod.quantize_file(out / "q254.index", out / "q254.quantized")
+    (out / "q254.max.json").write_text(json.dumps(ms))
+
+    # A11: on-disk index from the quantized collection
+    create_mod.InvertedIndexCreator(out / "collection.quantized", out / "index").run()
+    # a tie-heavy handmade quantized collection (empty line included)
+    (out / "ties.quantized").write_text(
+        "▁a: 5, ▁b: 3\n\n▁b: 3, ▁a: 5, ▁c: 1\n▁a: 5\n▁c: 9, ▁a: 2, ▁b,: 3, ▁x:y: 4\n▁b: 3\n")
+    create_mod.InvertedIndexCreator(out / "ties.quantized", out / "index_ties").run()
+
+    # A12: score() for ordered term lists (the reference iterates a set; a list
+    # fixes that order, which is all the reference's tie order depends on)
+    qrng = np.random.default_rng(1234)
+    vocab = [l for l in (out / "index" / "vocab.txt").read_text().split("\n")[:-1]]
+    queries = []
+    for _ in range(60):
+        ts = list(dict.fromkeys(f"▁t{t}" for t in np.minimum(qrng.zipf(1.3, 6), 2000)))
+        queries.append(ts)
+    queries += [["▁nope"], [], ["▁t1"], ["▁t2", "▁t1"], ["▁t1", "▁t2"], [vocab[0]],
+                ["▁world,", "▁a:b", "▁x,y", "▁."]]
+    index = ii_mod.InvertedIndex(out / "index")
+    res = {"queries": queries, "top1000": [], "top10": []}
+    for q in queries:
+        res["top1000"].append([[int(d), int(s)] for d, s in index.score(q, top_k=1000)])
+        res["top10"].append([[int(d), int(s)] for d, s in index.score(q, top_k=10)])
+    (out / "score.json").write_text(json.dumps(res, ensure_ascii=False))
+
+    ties = ii_mod.InvertedIndex(out / "index_ties")
+    tq = [["▁a", "▁b"], ["▁b", "▁a"], ["▁c", "▁b,", "▁x:y"], ["▁b"], ["▁a", "▁b", "▁c"]]
+    tres = {"queries": tq, "top2": [], "top1000": []}
+    for q in tq:
+        tres["top2"].append([[int(d), int(s)] for d, s in ties.score(q, top_k=2)])
+        tres["top1000"].append([[int(d), int(s)] for d, s in ties.score(q, top_k=1000)])
+    (out / "score_ties.json").write_text(json.dumps(tres, ensure_ascii=False))
+
+
+class FakeSparseModel:
+    """Model protocol of SparseSearch (nano_beir_evaluator.py:93,114)."""
+
+    def __init__(self, corpus_impacts, queries_terms):
+        self.ci = corpus_impacts
+        self.qt = queries_terms
+
+    def get_impact_scores_batch(self, texts):
+        return [[(t, np.float32(v)) for t, v in self.ci[x]] for x in texts]
+
+    def process_query(self, q):
+        return list(self.qt[q])  # a list: fixes the iteration order
+
+
+def gen_sparse_search(out, nb_mod):
+    rng = np.random.default_rng(5)
+    docs = synthetic_docs(250, 400, seed=77, max_terms=40)
+    corpus_impacts = {}
+    corpus = {}
+    for i, (terms, imp) in enumerate(docs):
+        imp = imp.copy()
+        imp[rng.random(len(imp)) < 0.1] = 0.0  # exercise the `score > 0` filter
+        key = f"text{i}"
+        corpus_impacts[key] = [(t, float(v)) for t, v in zip(terms, imp)]
+        corpus[f"doc{i:04d}"] = key
+    # exact float ties: two docs with identical impact lists
+    corpus_impacts["textA"] = [("▁t1", 0.5), ("▁t2", 0.25)]
+    corpus_impacts["textB"] = [("▁t2", 0.25), ("▁t1", 0.5)]
+    corpus["dupA"] = "textA"
+    corpus["dupB"] = "textB"
+    qrng = np.random.default_rng(11)
+    queries = {}
+    qterms = {}
+    for i in range(40):
+        ts = list(dict.fromkeys(f"▁t{t}" for t in np.minimum(qrng.zipf(1.3, 5), 400)))
+        queries[f"q{i}"] = f"query{i}"
+        qterms[f"query{i}"] = ts
+    queries["qtie"] = "querytie"
+    qterms["querytie"] = ["▁t1", "▁t2"]
+    queries["qnone"] = "querynone"
+    qterms["querynone"] = ["▁unknown"]
+    model = FakeSparseModel(corpus_impacts, qterms)
+    res = {}
+    for k in (1000, 5):
+        ss = nb_mod.SparseSearch(model, batch_size=16)
+        r = ss.search(queries, corpus, k=k)
+        res[str(k)] = {qid: [[d, float(s)] for d, s in docs_.items()] for qid, docs_ in r.items()}
+    fixture = {
+        "corpus": corpus,
+        "corpus_impacts": {k: [[t, float(np.float32(v))] for t, v in vs]
+                           for k, vs in corpus_impacts.items()},
+        "queries": queries,
+        "query_terms": qterms,
+        "results": res,
+        "numpy": np.__version__,
+    }
+    (out / "sparse_search.json").write_text(json.dumps(fixture, ensure_ascii=False))
+
+
+def gen_metrics(out, score_fixture_dir):
+    met_mod = load_by_path("ref_metrics", "src/deep_impact/evaluation/metrics.py")
+    # run file over the score fixture (qid = query index), qrels = synthetic
+    sc = json.loads((score_fixture_dir / "score.json").read_text())
+    rng = np.random.default_rng(3)
+    run_path = out / "metrics.run.tsv"
+    qrels_path = out / "metrics.qrels.tsv"
+    with open(run_path, "w") as rf, open(qrels_path, "w") as qf:
+        for qi, top in enumerate(sc["top1000"]):
+            if not top:
+                continue
+            for rank, (d, s) in enumerate(top, start=1):
+                rf.write(f"{qi}\t{d}\t{rank}\t{s}\n")
+            pos = set(int(x) for x in rng.choice(330, size=3, replace=False))
+            if rng.random() < 0.5 and top:
+                pos.add(int(top[min(len(top) - 1, int(rng.integers(0, 15)))][0]))
+            for p in sorted(pos):
+                qf.write(f"{qi}\t0\t{p}\t1\n")
+    m = met_mod.Metrics(run_path, qrels_path, mrr_depths=[10],
+                        recall_depths=[3, 10, 20, 50] + list(range(100, 1001, 100)))
+    m.evaluate()
+    nq = len(m.qrels)
+    res = {"n_queries": nq,
+           "mrr": {str(k): round(v / nq, 3) for k, v in m.mrr_sums.items()},
+           "recall": {str(k): round(v / nq, 3) for k, v in m.recall_sums.items()},
+           "mrr_sums": {str(k): v for k, v in m.mrr_sums.items()},
+           "recall_sums": {str(k): v for k, v in m.recall_sums.items()}}
+    (out / "metrics.json").write_text(json.dumps(res))
+
+
+# ------------------------------------------------------------------------------
+# encoder: the reference XLM-R DeepImpact class with seeded weights
+# ------------------------------------------------------------------------------
+def seeded_state_dict(model, seed, std=0.05):
+    """Deterministic weights: numpy default_rng(seed), keys in state_dict order.
+    Regenerated identically by improving-learned-index_amd tests (no reference)."""
+    rng = np.random.default_rng(seed)
+    sd = {}
+    for k, v in model.state_dict().items():
+        if not torch.is_floating_point(v):
+            sd[k] = v
+            continue
+        if k.endswith("LayerNorm.weight"):
+            a = 1.0 + 0.1 * rng.standard_normal(v.shape)
+        else:
+            a = std * rng.standard_normal(v.shape)
+        sd[k] = torch.from_numpy(a.astype(np.float32))
+    return sd
+
+
+ENC_TEXTS = [
+    "Hello world, it's 3.5 -- ok .",
+    "The learned sparse retrieval model computes an impact score for each document term.",
+    "the the the of of and world world , , . .",
+    "A very long passage " + " ".join(["about water and earth and the sea"] * 12),
+    "Ünïcödé text with numbers 123 456 and symbols @ # $ % ^ & *",
+    "",
+    "single",
+    "Search engines index passages; queries hit the inverted index and top-k results rank.",
+]
+
+
+def gen_encoder_xlmr(out, xlmr_mod, indexer_mod, name, cfg_kw, max_length, seed, std):
+    from transformers import XLMRobertaConfig
+
+    cfg = XLMRobertaConfig(**cfg_kw)
+    Cls = xlmr_mod.DeepImpact
+    Cls.max_length = max_length
+    # transformers 5.x: PreTrainedModel.init_weights needs state set by post_init();
+    # the weights are overwritten by load_state_dict below, so initialisation is moot.
+    Cls.init_weights = lambda self: None
+    torch.manual_seed(0)
+    model = Cls(cfg)
+    model.load_state_dict(seeded_state_dict(model, seed, std), strict=True)
+    model.eval()
+
+    # (1) A3 term extraction + A5/A7 forward + A8 gather straight from the reference
+    encs, maps, impacts = [], [], []
+    for t in ENC_TEXTS:
+        enc, m = Cls.process_document(t)
+        encs.append(enc)
+        maps.append(m)
+    ids = torch.tensor([e.ids for e in encs], dtype=torch.long)
+    mask = torch.tensor([e.attention_mask for e in encs], dtype=torch.long)
+    tids = torch.tensor([e.type_ids for e in encs], dtype=torch.long)
+    with torch.no_grad():
+        outp = model(ids, mask, tids)
+    ti = Cls.compute_term_impacts(maps, outp)
+    queries = [sorted(Cls.process_query(t)) for t in ENC_TEXTS]
+
+    # (2) the full Indexer path (indexer.py:31-68) -> impact TSV text
+    idx = indexer_mod.Indexer.__new__(indexer_mod.Indexer)
+    idx.model_cls = Cls
+    idx.model = model
+    idx.pool = _SerialPool()
+    idx.batch_size = 3
+    buf = io.StringIO()
+    idx.index(list(ENC_TEXTS), buf)
+
+    fixture = {
+        "config": cfg_kw, "max_length": max_length, "seed": seed, "std": std,
+        "texts": ENC_TEXTS,
+        "state_dict_shapes": [[k, list(v.shape), str(v.dtype)]
+                              for k, v in model.state_dict().items()],
+        "input_ids": ids.tolist(), "attention_mask": mask.tolist(),
+        "term_maps": [list(m.items()) for m in maps],
+        "token_impacts_f32_bits": outp.squeeze(-1).numpy().astype(np.float32)
+            .view(np.uint32).tolist() if cfg_kw["num_hidden_layers"] <= 2 else None,
+        "term_impacts_f32_bits": [[[t, int(np.float32(v).view(np.uint32))] for t, v in d]
+                                  for d in ti],
+        "query_terms_sorted": queries,
+        "impact_tsv": buf.getvalue(),
+    }
+    (out / f"encoder_{name}.json").write_text(json.dumps(fixture, ensure_ascii=False))
+
+
+def gen_encoder_bert(out, name, cfg_kw, seed, n_docs=4, seq=40):
+    """Upstream BERT/CoCondenser variant (original.py:10,19,21,155-177 commented;
+    soyuj/deeper-impact): BertModel + Linear(H,1) + ReLU.  token_type_ids are not
+    passed (original.py:79-84), so type row 0 is used."""
+    from transformers import BertConfig, BertModel
+
+    cfg = BertConfig(**cfg_kw)
+
+    class BertDeepImpact(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.bert = BertModel(cfg, add_pooling_layer=True)
+            self.impact_score_encoder = torch.nn.Sequential(torch.nn.Linear(cfg.hidden_size, 1),
+                                                            torch.nn.ReLU())
+
+        def forward(self, ids, mask):
+            h = self.bert(ids, attention_mask=mask).last_hidden_state
+            return self.impact_score_encoder(h)
+
+    torch.manual_seed(0)
+    model = BertDeepImpact()
+    model.load_state_dict(seeded_state_dict(model, seed, 0.05), strict=True)
+    model.eval()
+    rng = np.random.default_rng(seed + 1)
+    lens = [seq, seq // 2, 7, seq - 3][:n_docs]
+    ids = np.zeros((n_docs, seq), np.int64)
+    mask = np.zeros((n_docs, seq), np.int64)
+    for i, n in enumerate(lens):
+        ids[i, :n] = rng.integers(5, cfg.vocab_size, n)
+        ids[i, 0] = 101 % cfg.vocab_size
+        mask[i, :n] = 1
+    with torch.no_grad():
+        o = model(torch.from_numpy(ids), torch.from_numpy(mask)).squeeze(-1).numpy()
+    fixture = {"config": cfg_kw, "seed": seed, "std": 0.05, "input_ids": ids.tolist(),
+               "state_dict_shapes": [[k, list(v.shape), str(v.dtype)]
+                                     for k, v in model.state_dict().items()],
+               "attention_mask": mask.tolist(),
+               "token_impacts_f32_bits": o.astype(np.float32).view(np.uint32).tolist()}
+    (out / f"encoder_{name}.json").write_text(json.dumps(fixture))
+
+
+def main():
+    out = HERE
+    local_tokenizer.save(out / "tokenizer.json")
+    xlmr_mod = load_reference_models()
+    import src.deep_impact.indexing.indexer as indexer_mod
+    import src.deep_impact.indexing.quantize as quant_mod
+    import src.deep_impact.inverted_index.create as create_mod
+    import src.deep_impact.inverted_index.inverted_index as ii_mod
+
+    indexer_mod.DEVICE = torch.device("cpu")
+    for p in ("index", "index_ties"):
+        shutil.rmtree(out / p, ignore_errors=True)
+
+    gen_round3(out)
+    gen_collection_pipeline(out, indexer_mod, xlmr_mod, quant_mod, create_mod, ii_mod)
+    gen_sparse_search(out, load_reference_sparse_search())
+    gen_metrics(out, out)
+
+    vocab_size = local_tokenizer.build_tokenizer().get_vocab_size()
+    small = dict(vocab_size=vocab_size, hidden_size=64, num_hidden_layers=2,
+                 num_attention_heads=4, intermediate_size=128, max_position_embeddings=66,
+                 type_vocab_size=1, pad_token_id=1, bos_token_id=0, eos_token_id=2,
+                 layer_norm_eps=1e-5, hidden_act="gelu")
+    gen_encoder_xlmr(out, xlmr_mod, indexer_mod, "xlmr_small", small, max_length=64, seed=42,
+                     std=0.05)
+    base = dict(vocab_size=250002, hidden_size=768, num_hidden_layers=12,
+                num_attention_heads=12, intermediate_size=3072, max_position_embeddings=514,
+                type_vocab_size=1, pad_token_id=1, bos_token_id=0, eos_token_id=2,
+                layer_norm_eps=1e-5, hidden_act="gelu")
+    gen_encoder_xlmr(out, xlmr_mod, indexer_mod, "xlmr_base", base, max_length=128, seed=7,
+                     std=0.02)
+    bsmall = dict(vocab_size=300, hidden_size=64, num_hidden_layers=2, num_attention_heads=4,
+                  intermediate_size=128, max_position_embeddings=64, type_vocab_size=2,
+                  pad_token_id=0, layer_norm_eps=1e-12, hidden_act="gelu")
+    gen_encoder_bert(out, "bert_small", bsmall, seed=3)
+    print("golden fixtures written to", out)
+
+
+if __name__ == "__main__":
+    main()
