@@ -1,0 +1,234 @@
+"""ctypes binding of libdeepimpact_hip.so (the C ABI in include/deepimpact.h).
+
+The HIP library is the product path: there is no CPU fallback.  If the shared
+object is missing or cannot be loaded this module raises ImportError-like
+errors at first use, loudly.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from pathlib import Path
+
+import numpy as np
+
+_HERE = Path(__file__).resolve().parent
+LIB_PATH = Path(os.environ.get("DEEPIMPACT_HIP_LIB", _HERE / "libdeepimpact_hip.so"))
+
+DI_OK = 0
+DI_F_DEVICE_PTRS = 0x1
+DI_F_ASYNC = 0x2
+DI_F_TIMING = 0x4
+DI_F_LISTS_MAJOR = 0x8
+DI_MAX_QUERY_TERMS = 256
+DI_MAX_TOPK = 4096
+
+_ERRNAMES = {-1: "DI_EINVAL", -2: "DI_ENOMEM", -3: "DI_EHIP", -4: "DI_ERANGE",
+             -5: "DI_ENODEV", -6: "DI_EIO", -7: "DI_EFORMAT"}
+
+
+class DIError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"{_ERRNAMES.get(code, code)}: {msg}")
+        self.code = code
+
+
+class di_timing(ctypes.Structure):
+    _fields_ = [("ms", ctypes.c_double), ("launches", ctypes.c_int64)]
+
+
+P = ctypes.c_void_p
+I32, I64, U32, U64 = ctypes.c_int32, ctypes.c_int64, ctypes.c_uint32, ctypes.c_uint64
+
+# name -> (restype, argtypes); every symbol include/deepimpact.h declares
+SIGNATURES = {
+    "di_last_error": (ctypes.c_char_p, []),
+    "di_version": (ctypes.c_int, []),
+    "di_device_count": (ctypes.c_int, [P]),
+    "di_index_create": (ctypes.c_int, [P, I64, P, P, U32, U32, ctypes.c_int, P]),
+    "di_index_load_reference": (ctypes.c_int, [ctypes.c_char_p, U32, U32, ctypes.c_int, P]),
+    "di_build_reference_index": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_char_p]),
+    "di_index_search": (ctypes.c_int, [P, P, P, I32, I32, P, P, P, P, U32]),
+    "di_index_reserve": (ctypes.c_int, [P, I32, I32]),
+    "di_index_info": (ctypes.c_int, [P, P, P, P, P]),
+    "di_index_set_stream": (ctypes.c_int, [P, P]),
+    "di_index_sync": (ctypes.c_int, [P]),
+    "di_index_timing": (ctypes.c_int, [P, ctypes.c_char_p, P, ctypes.c_int]),
+    "di_index_destroy": (ctypes.c_int, [P]),
+    "di_topk_merge": (ctypes.c_int, [P, P, I32, I32, I32, P, P, ctypes.c_int, P, U32]),
+}
+
+_LIB = None
+
+
+def lib():
+    """Load the HIP library (raises if it is missing -- no fallback)."""
+    global _LIB
+    if _LIB is None:
+        if not LIB_PATH.exists():
+            raise RuntimeError(
+                f"{LIB_PATH} is missing: the HIP extension must be built "
+                f"(python -c 'import __graft_entry__; __graft_entry__.build()')")
+        L = ctypes.CDLL(str(LIB_PATH))
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _LIB = L
+    return _LIB
+
+
+def check(rc):
+    if rc != DI_OK:
+        raise DIError(rc, lib().di_last_error().decode("utf-8", "replace"))
+    return rc
+
+
+def ptr(a):
+    """ctypes pointer of a numpy array or a torch tensor (host or device)."""
+    if a is None:
+        return None
+    if isinstance(a, np.ndarray):
+        return ctypes.c_void_p(a.ctypes.data)
+    if hasattr(a, "data_ptr"):
+        return ctypes.c_void_p(a.data_ptr())
+    if isinstance(a, int):
+        return ctypes.c_void_p(a)
+    raise TypeError(type(a))
+
+
+def device_count():
+    n = ctypes.c_int(0)
+    check(lib().di_device_count(ctypes.byref(n)))
+    return n.value
+
+
+def version():
+    v = lib().di_version()
+    return (v >> 16, v & 0xFFFF)
+
+
+def csr(queries):
+    """list of term-id lists -> (uint32 terms, int32 cu)."""
+    cu = np.zeros(len(queries) + 1, np.int32)
+    for i, q in enumerate(queries):
+        cu[i + 1] = cu[i] + len(q)
+    flat = np.fromiter((t for q in queries for t in q), np.uint32, count=int(cu[-1]))
+    return flat, cu
+
+
+class DeviceIndex:
+    """Device-resident quantized index (one shard [doc_lo, doc_hi) of doc ids)."""
+
+    def __init__(self, handle):
+        self._h = handle
+
+    @classmethod
+    def from_postings(cls, term_off, pdoc, pval, doc_lo=0, doc_hi=0, device=0):
+        term_off = np.ascontiguousarray(term_off, np.int64)
+        pdoc = np.ascontiguousarray(pdoc, np.uint32)
+        pval = np.ascontiguousarray(pval, np.uint8)
+        if pdoc.size == 0:
+            pdoc = np.zeros(1, np.uint32)
+            pval = np.zeros(1, np.uint8)
+        h = ctypes.c_void_p()
+        check(lib().di_index_create(ptr(term_off), len(term_off) - 1, ptr(pdoc), ptr(pval),
+                                    doc_lo, doc_hi, device, ctypes.byref(h)))
+        return cls(h)
+
+    @classmethod
+    def from_reference_dir(cls, path, doc_lo=0, doc_hi=0, device=0):
+        h = ctypes.c_void_p()
+        check(lib().di_index_load_reference(str(path).encode(), doc_lo, doc_hi, device,
+                                            ctypes.byref(h)))
+        return cls(h)
+
+    def info(self):
+        nt, npo, nd, nb = I64(), I64(), U32(), I32()
+        check(lib().di_index_info(self._h, ctypes.byref(nt), ctypes.byref(npo),
+                                  ctypes.byref(nd), ctypes.byref(nb)))
+        return {"n_terms": nt.value, "n_postings": npo.value, "n_docs": nd.value,
+                "n_blocks": nb.value}
+
+    def search_csr(self, q_terms, cu_q, k, with_keys=False, timing=False):
+        q_terms = np.ascontiguousarray(q_terms, np.uint32)
+        if q_terms.size == 0:
+            q_terms = np.zeros(1, np.uint32)
+        cu_q = np.ascontiguousarray(cu_q, np.int32)
+        n_q = len(cu_q) - 1
+        docs = np.zeros((max(n_q, 1), k), np.uint32)
+        scores = np.zeros((max(n_q, 1), k), np.uint32)
+        n = np.zeros(max(n_q, 1), np.int32)
+        keys = np.zeros((max(n_q, 1), k), np.uint64) if with_keys else None
+        flags = DI_F_TIMING if timing else 0
+        check(lib().di_index_search(self._h, ptr(q_terms), ptr(cu_q), n_q, k, ptr(docs),
+                                    ptr(scores), ptr(n), ptr(keys), flags))
+        return docs[:n_q], scores[:n_q], n[:n_q], (keys[:n_q] if with_keys else None)
+
+    def search(self, queries, k=1000):
+        """queries: list of term-id lists (iteration order = tie order)."""
+        flat, cu = csr(queries)
+        docs, scores, n, _ = self.search_csr(flat, cu, k)
+        return [list(zip(docs[i, :n[i]].tolist(), scores[i, :n[i]].tolist()))
+                for i in range(len(queries))]
+
+    def search_device(self, q_terms, cu_q, n_q, k, out_doc, out_score, out_n, out_key=None,
+                      flags=DI_F_DEVICE_PTRS):
+        """All pointers are device pointers (torch tensors or ints)."""
+        check(lib().di_index_search(self._h, ptr(q_terms), ptr(cu_q), n_q, k, ptr(out_doc),
+                                    ptr(out_score), ptr(out_n), ptr(out_key), flags))
+
+    def reserve(self, max_q, k):
+        check(lib().di_index_reserve(self._h, max_q, k))
+
+    def set_stream(self, stream_ptr):
+        check(lib().di_index_set_stream(self._h, ctypes.c_void_p(stream_ptr)))
+
+    def sync(self):
+        check(lib().di_index_sync(self._h))
+
+    def timing(self, name, reset=False):
+        t = di_timing()
+        check(lib().di_index_timing(self._h, name.encode(), ctypes.byref(t), int(reset)))
+        return t.ms, t.launches
+
+    def close(self):
+        if self._h:
+            lib().di_index_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def topk_merge(keys, counts, k, device=0, stream=None, flags=0):
+    """keys: [n_q, n_lists, k] uint64, counts: [n_q, n_lists] int32 (host numpy, or device
+    tensors with DI_F_DEVICE_PTRS).  Returns (keys [n_q,k], n [n_q]) for host inputs."""
+    if flags & DI_F_DEVICE_PTRS:
+        raise ValueError("use topk_merge_device for device pointers")
+    keys = np.ascontiguousarray(keys, np.uint64)
+    counts = np.ascontiguousarray(counts, np.int32)
+    n_q, n_lists = counts.shape
+    assert keys.shape == (n_q, n_lists, k)
+    out = np.zeros((max(n_q, 1), k), np.uint64)
+    n = np.zeros(max(n_q, 1), np.int32)
+    check(lib().di_topk_merge(ptr(keys), ptr(counts), n_q, n_lists, k, ptr(out), ptr(n),
+                              device, ctypes.c_void_p(stream or 0), flags))
+    return out[:n_q], n[:n_q]
+
+
+def topk_merge_device(keys, counts, n_q, n_lists, k, out_key, out_n, device=0, stream=0,
+                      flags=DI_F_DEVICE_PTRS):
+    check(lib().di_topk_merge(ptr(keys), ptr(counts), n_q, n_lists, k, ptr(out_key),
+                              ptr(out_n), device, ctypes.c_void_p(stream), flags))
+
+
+def key_doc(keys):
+    return (np.uint64(0xFFFFFFFF) - (keys & np.uint64(0xFFFFFFFF))).astype(np.uint32)
+
+
+def key_score(keys):
+    return (keys >> np.uint64(48)).astype(np.uint32)

@@ -1,0 +1,181 @@
+// di_common.h -- shared host-side plumbing of libdeepimpact_hip.so:
+// error reporting across the C ABI, HIP checks, device buffers, per-kernel
+// HIP-event timing.  gfx950 only.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdint>
+#include <cstdio>
+#include <map>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "../../include/deepimpact.h"
+
+namespace di {
+
+// thread-local last error (di_last_error)
+void set_error(const char *fmt, ...) __attribute__((format(printf, 1, 2)));
+const char *last_error();
+
+struct Error {
+    int code;
+};
+
+[[noreturn]] inline void fail(int code, const char *msg) {
+    set_error("%s", msg);
+    throw Error{code};
+}
+
+#define DI_HIP(expr)                                                                    \
+    do {                                                                                \
+        hipError_t e_ = (expr);                                                         \
+        if (e_ != hipSuccess) {                                                         \
+            ::di::set_error("%s:%d %s: %s", __FILE__, __LINE__, #expr,                  \
+                            hipGetErrorString(e_));                                     \
+            throw ::di::Error{e_ == hipErrorOutOfMemory ? DI_ENOMEM : DI_EHIP};         \
+        }                                                                               \
+    } while (0)
+
+#define DI_REQUIRE(cond, code, ...)                                                     \
+    do {                                                                                \
+        if (!(cond)) {                                                                  \
+            ::di::set_error(__VA_ARGS__);                                               \
+            throw ::di::Error{code};                                                    \
+        }                                                                               \
+    } while (0)
+
+// Run a C-ABI body, translating exceptions into status codes.
+template <class F>
+int guard(F &&f) {
+    try {
+        f();
+        return DI_OK;
+    } catch (const Error &e) {
+        return e.code;
+    } catch (const std::bad_alloc &) {
+        set_error("host allocation failed");
+        return DI_ENOMEM;
+    } catch (...) {
+        set_error("unexpected C++ exception");
+        return DI_EINVAL;
+    }
+}
+
+// Owning device buffer (grows, never shrinks).
+struct DevBuf {
+    void *p = nullptr;
+    size_t bytes = 0;
+    DevBuf() = default;
+    DevBuf(const DevBuf &) = delete;
+    DevBuf &operator=(const DevBuf &) = delete;
+    ~DevBuf() {
+        if (p) (void)hipFree(p);
+    }
+    void reserve(size_t n) {
+        if (n <= bytes) return;
+        if (p) DI_HIP(hipFree(p));
+        p = nullptr;
+        bytes = 0;
+        DI_HIP(hipMalloc(&p, n ? n : 16));
+        bytes = n;
+    }
+    template <class T>
+    T *as() const {
+        return static_cast<T *>(p);
+    }
+};
+
+// Per-kernel timing with HIP events recorded on the launching stream.
+struct Timer {
+    struct Pending {
+        std::string name;
+        hipEvent_t a, b;
+    };
+    std::vector<Pending> pending;
+    std::map<std::string, std::pair<double, int64_t>> acc;
+    std::vector<hipEvent_t> pool;
+
+    hipEvent_t ev() {
+        if (!pool.empty()) {
+            hipEvent_t e = pool.back();
+            pool.pop_back();
+            return e;
+        }
+        hipEvent_t e;
+        DI_HIP(hipEventCreate(&e));
+        return e;
+    }
+    void begin(bool on, const char *name, hipStream_t s, hipEvent_t *a) {
+        if (!on) return;
+        *a = ev();
+        DI_HIP(hipEventRecord(*a, s));
+        pending.push_back({name, *a, nullptr});
+    }
+    void end(bool on, hipStream_t s) {
+        if (!on) return;
+        hipEvent_t b = ev();
+        DI_HIP(hipEventRecord(b, s));
+        pending.back().b = b;
+    }
+    // call after the stream has been synchronised
+    void resolve() {
+        for (auto &p : pending) {
+            float ms = 0.f;
+            DI_HIP(hipEventElapsedTime(&ms, p.a, p.b));
+            auto &e = acc[p.name];
+            e.first += ms;
+            e.second += 1;
+            pool.push_back(p.a);
+            pool.push_back(p.b);
+        }
+        pending.clear();
+    }
+    void get(const char *name, di_timing *out, bool reset) {
+        auto it = acc.find(name);
+        out->ms = it == acc.end() ? 0.0 : it->second.first;
+        out->launches = it == acc.end() ? 0 : it->second.second;
+        if (reset) acc.clear();
+    }
+    ~Timer() {
+        for (auto &p : pending) {
+            (void)hipEventDestroy(p.a);
+            if (p.b) (void)hipEventDestroy(p.b);
+        }
+        for (auto e : pool) (void)hipEventDestroy(e);
+    }
+};
+
+// RAII timing scope around one kernel launch.
+struct TimedLaunch {
+    Timer &t;
+    bool on;
+    hipStream_t s;
+    TimedLaunch(Timer &t_, bool on_, const char *name, hipStream_t s_) : t(t_), on(on_), s(s_) {
+        hipEvent_t a;
+        t.begin(on, name, s, &a);
+    }
+    ~TimedLaunch() noexcept(false) { t.end(on, s); }
+};
+
+inline void check_launch(const char *what) {
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        set_error("launch of %s failed: %s", what, hipGetErrorString(e));
+        throw Error{DI_EHIP};
+    }
+}
+
+// Copy `bytes` from a host or device pointer into a device buffer on stream s.
+inline const void *stage_in(const void *src, size_t bytes, bool device_ptrs, DevBuf &buf,
+                            hipStream_t s) {
+    if (device_ptrs || bytes == 0) return src;
+    buf.reserve(bytes);
+    DI_HIP(hipMemcpyAsync(buf.p, src, bytes, hipMemcpyHostToDevice, s));
+    return buf.p;
+}
+
+}  // namespace di

@@ -1,0 +1,72 @@
+"""Seeded synthetic workloads (BASELINE.md §2 / SURVEY.md §8d generators).
+
+There is no network and no MS MARCO here: benches and large parity tests use
+collections of the same shape, generated deterministically.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+
+def round3_f32(x):
+    """numpy's round(np.float32, 3): fl32(rint(fl32(x*1000)) / 1000)
+    (reference src/deep_impact/indexing/indexer.py:132)."""
+    x = np.asarray(x, np.float32)
+    return (np.rint(x * np.float32(1000)) / np.float32(1000)).astype(np.float32)
+
+
+def msmarco_like_docs(n_docs=100_000, v_terms=200_000, seed=1234, max_terms=100):
+    """Per doc: first `max_terms` unique values of min(zipf(1.2, 200), V) and
+    impacts float32(softplus(N(-0.5, 1.5))).  Returns (cu, term, impact_f32) CSR;
+    term ids are 0-based (zipf value - 1)."""
+    rng = np.random.default_rng(seed)
+    cu = np.zeros(n_docs + 1, np.int64)
+    terms, imps = [], []
+    for d in range(n_docs):
+        t = np.unique(np.minimum(rng.zipf(1.2, 200), v_terms))[:max_terms]
+        imp = np.log1p(np.exp(rng.normal(-0.5, 1.5, len(t)))).astype(np.float32)
+        terms.append(t - 1)
+        imps.append(imp)
+        cu[d + 1] = cu[d] + len(t)
+    return cu, np.concatenate(terms).astype(np.uint32), np.concatenate(imps)
+
+
+def quantize_like_reference(imp_f32, bits=8):
+    """Impact TSV text -> quantize.py semantics, without the text round trip:
+    the 3-decimal float32 prints as the shortest repr of its double, which
+    float() reads back exactly."""
+    v = round3_f32(imp_f32).astype(np.float64)
+    m = float(v.max()) if v.size else 0.0
+    scale = ((1 << bits) - 1) / m
+    return np.trunc(v * scale).astype(np.int64), m
+
+
+def postings_reference_order(cu, term, val, n_terms):
+    """CSR by term in the reference file order: value desc, doc asc
+    (create.py:41); zero values dropped (they are dropped by quantize.py:44)."""
+    n_docs = len(cu) - 1
+    doc = np.repeat(np.arange(n_docs, dtype=np.uint32), np.diff(cu))
+    keep = val > 0
+    doc, t, v = doc[keep], term[keep], val[keep]
+    order = np.lexsort((doc, -v, t))
+    t_sorted = t[order]
+    term_off = np.zeros(n_terms + 1, np.int64)
+    np.add.at(term_off, t_sorted.astype(np.int64) + 1, 1)
+    term_off = np.cumsum(term_off)
+    return term_off, doc[order].astype(np.uint32), v[order].astype(np.uint8)
+
+
+def msmarco_like_index(n_docs=100_000, v_terms=200_000, seed=1234):
+    cu, term, imp = msmarco_like_docs(n_docs, v_terms, seed)
+    q, _ = quantize_like_reference(imp)
+    return postings_reference_order(cu, term, q, v_terms)
+
+
+def msmarco_like_queries(n_q, v_terms=200_000, seed=1234, draws=6):
+    """Each query: the set of min(zipf(1.3, draws), V) (first-occurrence order)."""
+    rng = np.random.default_rng(seed)
+    out = []
+    for _ in range(n_q):
+        z = np.minimum(rng.zipf(1.3, draws), v_terms) - 1
+        out.append(list(dict.fromkeys(int(x) for x in z)))
+    return out

@@ -1,0 +1,134 @@
+/*
+ * deepimpact.h -- C ABI of libdeepimpact_hip.so, the MI355X-native (gfx950)
+ * DeeperImpact encode-and-retrieve path.
+ *
+ * The reference (Tommachilez/improving-learned-index) has no FFI layer: its
+ * boundary is a set of Python protocols and file formats.  Each
+ * entry point below names the reference interface it replaces (path:line,
+ * relative to the reference repository root).  The Python host side
+ * (improving-learned-index_amd/) binds these through ctypes; INTEGRATION.md
+ * shows the binding a maintainer would add to the reference itself.
+ *
+ * Conventions
+ *   - Every function returns DI_OK (0) or a negative DI_E* code; the message of
+ *     the last failure on the calling thread is di_last_error().  No C++
+ *     exception crosses the ABI.
+ *   - Array arguments are borrowed for the duration of the call.  Unless the
+ *     DI_F_DEVICE_PTRS flag is given they are host pointers; with it they are
+ *     device pointers on the handle's device (inputs already resident in HBM).
+ *   - Outputs are caller-allocated; their sizes are known before the call.
+ *   - One handle per device.  A handle is not thread-safe; different handles
+ *     may be used concurrently.  Each handle owns one HIP stream (replaceable
+ *     with di_*_set_stream); calls are synchronous at return unless
+ *     DI_F_ASYNC is given together with DI_F_DEVICE_PTRS.
+ */
+#ifndef DEEPIMPACT_H
+#define DEEPIMPACT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DI_OK 0
+#define DI_EINVAL (-1)   /* bad argument                                   */
+#define DI_ENOMEM (-2)   /* host or device allocation failed                */
+#define DI_EHIP (-3)     /* HIP runtime error                               */
+#define DI_ERANGE (-4)   /* a documented size limit was exceeded            */
+#define DI_ENODEV (-5)   /* no HIP device                                   */
+#define DI_EIO (-6)      /* file could not be read                          */
+#define DI_EFORMAT (-7)  /* file content does not follow the reference format */
+
+#define DI_F_DEVICE_PTRS 0x1u /* array arguments are device pointers           */
+#define DI_F_ASYNC 0x2u       /* do not synchronise the stream before return   */
+#define DI_F_TIMING 0x4u      /* record HIP events around every kernel         */
+#define DI_F_LISTS_MAJOR 0x8u /* di_topk_merge: keys are [list][query][k]       */
+
+/* Limits of the retrieval kernels (documented in DESIGN.md). */
+#define DI_MAX_QUERY_TERMS 256   /* known terms per query (first-touch key, u16 score) */
+#define DI_MAX_TOPK 4096
+#define DI_MAX_SPARSE_DOCS 16777215u /* float index: doc ids embedded in 24 bits   */
+
+const char *di_last_error(void);
+int di_version(void); /* (major << 16) | minor */
+int di_device_count(int *n);
+
+/* Per-kernel timing collected under DI_F_TIMING (HIP events on the launching
+ * stream).  `name` is the kernel's short name, e.g. "score_blocks".  Returns the
+ * summed milliseconds and the number of launches since the last reset. */
+typedef struct di_timing {
+    double ms;
+    int64_t launches;
+} di_timing;
+
+/* ======================================================================
+ * On-disk quantized index: build and score                  (A11, A12)
+ * ====================================================================== */
+typedef struct di_index di_index;
+
+/* Replaces InvertedIndexCreator (src/deep_impact/inverted_index/create.py:12-55)
+ * as the producer of the device index, and InvertedIndex.__init__
+ * (src/deep_impact/inverted_index/inverted_index.py:18-20).
+ * Input: postings in the reference file order -- term-major, value descending,
+ * doc ascending -- as CSR: term_off[n_terms+1] (posting index), pdoc[], pval[].
+ * Postings from the first zero value of a term on are dropped, exactly as
+ * InvertedIndex.term_docs stops there (inverted_index.py:50-51).
+ * Only docs in [doc_lo, doc_hi) are kept (one shard of a doc-id-sharded index);
+ * doc ids stay global.  doc_hi = 0 means "max doc + 1".                        */
+int di_index_create(const int64_t *term_off, int64_t n_terms, const uint32_t *pdoc,
+                    const uint8_t *pval, uint32_t doc_lo, uint32_t doc_hi, int device,
+                    di_index **out);
+
+/* Native host builder of the reference files: replaces InvertedIndexCreator.run
+ * (create.py:53-55) reading the collection like DeepImpactCollection
+ * (src/deep_impact/indexing/deep_impact_collection.py:6-33).  Writes
+ * <out_dir>/vocab.txt, inverted_index.idx, inverted_index.dat byte-identical to
+ * the reference.  Malformed lines fail with DI_EFORMAT where the reference raises. */
+int di_build_reference_index(const char *collection_path, const char *out_dir);
+
+/* Reads <dir>/inverted_index.idx and <dir>/inverted_index.dat (create.py:45-51,
+ * formats src/utils/defaults.py:22-37).  vocab.txt stays on the host side. */
+int di_index_load_reference(const char *dir, uint32_t doc_lo, uint32_t doc_hi, int device,
+                            di_index **out);
+
+/* Replaces InvertedIndex.score (inverted_index.py:55-62) for a batch of queries.
+ * q_terms: term ids of all queries in iteration order (the reference iterates a
+ * Python set; its order is the tie order), CSR by cu_q[n_q+1].  For each query
+ * the top-k (doc, score) pairs are written in the reference's order -- score
+ * descending, ties in first-touch order -- to out_doc/out_score[q*k ...] and the
+ * count to out_n[q].  out_key (may be NULL) receives the 64-bit merge keys used
+ * to combine shards (di_topk_merge).                                             */
+int di_index_search(di_index *ix, const uint32_t *q_terms, const int32_t *cu_q, int32_t n_q,
+                    int32_t k, uint32_t *out_doc, uint32_t *out_score, int32_t *out_n,
+                    uint64_t *out_key, uint32_t flags);
+
+/* Pre-allocates device workspace for batches of up to max_q queries at top-k. */
+int di_index_reserve(di_index *ix, int32_t max_q, int32_t k);
+int di_index_info(const di_index *ix, int64_t *n_terms, int64_t *n_postings, uint32_t *n_docs,
+                  int32_t *n_blocks);
+int di_index_set_stream(di_index *ix, void *hip_stream);
+int di_index_sync(di_index *ix);
+int di_index_timing(di_index *ix, const char *name, di_timing *out, int reset);
+int di_index_destroy(di_index *ix);
+
+/* Combine per-shard top-k lists (from di_index_search out_key, or the sparse
+ * index) into the global top-k: keys[(q*n_lists + l)*k + i], counts[q*n_lists+l]
+ * (with DI_F_LISTS_MAJOR: keys[(l*n_q + q)*k + i], counts[l*n_q + q] -- the layout
+ * an all-gather of per-shard results produces).
+ * The keys are unique and totally ordered, so the result equals a single-shard
+ * search over the whole collection.  Device pointers when DI_F_DEVICE_PTRS.
+ * Replaces nothing in the reference (it has no sharded retrieval). */
+int di_topk_merge(const uint64_t *keys, const int32_t *counts, int32_t n_q, int32_t n_lists,
+                  int32_t k, uint64_t *out_key, int32_t *out_n, int device, void *hip_stream,
+                  uint32_t flags);
+
+/* Decoding of a quantized-index merge key. */
+static inline uint32_t di_key_doc(uint64_t key) { return 0xFFFFFFFFu - (uint32_t)key; }
+static inline uint32_t di_key_score(uint64_t key) { return (uint32_t)(key >> 48); }
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DEEPIMPACT_H */

@@ -1,0 +1,144 @@
+"""GPU parity of the quantized-index scorer (di_index_search) -- A11/A12.
+
+Checked through the C ABI against (1) the reference's own outputs (golden
+fixtures) and (2) the oracle (oracle/oracle.c, pinned to the same fixtures) on
+seeded synthetic collections that cross the 32768-doc LDS blocks.  Integer work:
+bit-exact, including the reference's first-touch tie order.
+"""
+import json
+
+import numpy as np
+import pytest
+
+import oracle
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def L():
+    from improving_learned_index_amd import _lib
+
+    if _lib.device_count() < 1:
+        pytest.fail("no HIP device visible (GPU test run without a GPU)")
+    return _lib
+
+
+def test_golden_index_matches_reference(L):
+    from improving_learned_index_amd.inverted_index import InvertedIndex
+
+    fx = json.loads((GOLDEN / "score.json").read_text())
+    ix = InvertedIndex(GOLDEN / "index")
+    got1000 = ix.score_batch(fx["queries"], 1000)
+    got10 = ix.score_batch(fx["queries"], 10)
+    for q, g1000, g10, w1000, w10 in zip(fx["queries"], got1000, got10, fx["top1000"],
+                                         fx["top10"]):
+        assert [list(x) for x in g1000] == w1000, q
+        assert [list(x) for x in g10] == w10, q
+    # single-query interface == reference InvertedIndex.score
+    assert [list(x) for x in ix.score(fx["queries"][0], top_k=1000)] == fx["top1000"][0]
+
+
+def test_golden_ties_match_reference(L):
+    from improving_learned_index_amd.inverted_index import InvertedIndex
+
+    tx = json.loads((GOLDEN / "score_ties.json").read_text())
+    ix = InvertedIndex(GOLDEN / "index_ties")
+    for q, w2, w1000 in zip(tx["queries"], tx["top2"], tx["top1000"]):
+        assert [list(x) for x in ix.score(q, 2)] == w2
+        assert [list(x) for x in ix.score(q, 1000)] == w1000
+
+
+def _synthetic(n_docs, v_terms, seed):
+    from improving_learned_index_amd import synthetic as S
+
+    cu, term, imp = S.msmarco_like_docs(n_docs, v_terms, seed, max_terms=60)
+    q, _ = S.quantize_like_reference(imp)
+    return S.postings_reference_order(cu, term, q, v_terms)
+
+
+@pytest.fixture(scope="module")
+def synth():
+    term_off, pdoc, pval = _synthetic(70_000, 5000, seed=5)
+    ora = oracle.Index.__new__(oracle.Index)
+    ora.term_off, ora.pdoc, ora.pval = term_off, pdoc, pval
+    ora.n_docs = int(pdoc.max()) + 1
+    return term_off, pdoc, pval, ora
+
+
+def _queries(v_terms, n, seed, long_every=0):
+    rng = np.random.default_rng(seed)
+    qs = []
+    for i in range(n):
+        nd = int(rng.integers(1, 9))
+        if long_every and i % long_every == 0:
+            nd = int(rng.integers(100, 300))
+        z = np.minimum(rng.zipf(1.25, nd), v_terms) - 1
+        q = list(dict.fromkeys(int(x) for x in z))[:256]
+        qs.append(q)
+    qs += [[], [v_terms - 1], [0], [0, 1], [1, 0]]
+    return qs
+
+
+@pytest.mark.parametrize("k", [1, 10, 1000, 4096])
+def test_synthetic_matches_oracle(L, synth, k):
+    term_off, pdoc, pval, ora = synth
+    dev = L.DeviceIndex.from_postings(term_off, pdoc, pval)
+    info = dev.info()
+    assert info["n_blocks"] == 3 and info["n_docs"] == ora.n_docs
+    qs = _queries(5000, 120, seed=k, long_every=40)
+    got = dev.search(qs, k)
+    want = ora.score_ids(qs, k, n_threads=8)
+    for i, (g, w) in enumerate(zip(got, want)):
+        assert g == w, (i, len(g), len(w))
+
+
+def test_shards_merge_equals_single(L, synth):
+    term_off, pdoc, pval, ora = synth
+    k = 500
+    qs = _queries(5000, 60, seed=11)
+    full = L.DeviceIndex.from_postings(term_off, pdoc, pval)
+    _, _, n_full, key_full = full.search_csr(*L.csr(qs), k, with_keys=True)
+    cuts = [0, 20_000, 45_001, ora.n_docs]
+    keys = np.zeros((len(qs), 3, k), np.uint64)
+    counts = np.zeros((len(qs), 3), np.int32)
+    for s in range(3):
+        sh = L.DeviceIndex.from_postings(term_off, pdoc, pval, cuts[s], cuts[s + 1])
+        docs, _, n, key = sh.search_csr(*L.csr(qs), k, with_keys=True)
+        for i in range(len(qs)):
+            assert ((docs[i, :n[i]] >= cuts[s]) & (docs[i, :n[i]] < cuts[s + 1])).all()
+        keys[:, s, :] = key
+        counts[:, s] = n
+    mk, mn = L.topk_merge(keys, counts, k)
+    assert (mn == n_full).all()
+    for i in range(len(qs)):
+        assert (mk[i, :mn[i]] == key_full[i, :n_full[i]]).all()
+        w = ora.score_ids([qs[i]], k)[0]
+        assert list(zip(L.key_doc(mk[i, :mn[i]]).tolist(),
+                        L.key_score(mk[i, :mn[i]]).tolist())) == w
+
+
+def test_limits_and_errors(L, synth):
+    term_off, pdoc, pval, _ = synth
+    dev = L.DeviceIndex.from_postings(term_off, pdoc, pval)
+    with pytest.raises(L.DIError) as e:
+        dev.search([list(range(257))], 10)
+    assert e.value.code == -4
+    with pytest.raises(L.DIError):
+        dev.search([[5000]], 10)  # unknown term id
+    with pytest.raises(L.DIError):
+        dev.search([[1]], 0)
+    assert dev.search([], 10) == []
+    empty = L.DeviceIndex.from_postings(np.zeros(3, np.int64), np.zeros(0, np.uint32),
+                                        np.zeros(0, np.uint8))
+    assert empty.search([[0, 1]], 10) == [[]]
+
+
+def test_zero_values_stop_term_lists(L):
+    # inverted_index.py:50-51: a term list ends at its first 0 value
+    term_off = np.array([0, 4], np.int64)
+    pdoc = np.array([3, 1, 2, 0], np.uint32)
+    pval = np.array([9, 5, 0, 7], np.uint8)
+    dev = L.DeviceIndex.from_postings(term_off, pdoc, pval)
+    assert dev.search([[0]], 10) == [[(3, 9), (1, 5)]]
