@@ -183,7 +183,8 @@ score_blocks_kernel(const uint32_t *__restrict__ post, const int64_t *__restrict
     const uint32_t T = prefix;
     const uint32_t ties = sh.rs.tot[sh.rs.bin];
     // doc-order cut among the ties: the `need` smallest doc indices
-    uint32_t dcut = 0xFFFFFFFFu;
+    // (all ties when exactly `need` of them exist)
+    uint32_t dcut = 0;
     if (ties != need) {
         uint32_t dneed = need, dprefix = 0, dmask = 0;
         auto dkey = [](uint32_t, int idx) { return 0xFFFFu - (uint32_t)idx; };
