@@ -1,0 +1,306 @@
+// enc_misc.hip -- memory-bound encoder kernels (gfx950): embeddings + LayerNorm,
+// LayerNorm (+ the impact head), first-token term gather with the 3-decimal
+// rounding, and the 8-bit quantizer.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+
+#include "di_common.h"
+#include "enc_common.h"
+
+namespace di {
+
+constexpr int LN_MAX_PER_LANE = 16;  // H <= 1024
+
+__device__ __forceinline__ float wave_sum_f(float x) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d, 64);
+    return x;
+}
+
+// LayerNorm of one row held as v[i] = x[lane + 64 i] (two-pass, biased variance,
+// eps inside the sqrt -- torch.nn.functional.layer_norm).
+template <int PL>
+__device__ __forceinline__ void ln_row(float (&v)[PL], int H, const float *gamma,
+                                       const float *beta, float eps) {
+    const int lane = threadIdx.x & 63;
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < PL; ++i)
+        if (lane + 64 * i < H) s += v[i];
+    const float mean = wave_sum_f(s) / (float)H;
+    float q = 0.f;
+#pragma unroll
+    for (int i = 0; i < PL; ++i)
+        if (lane + 64 * i < H) {
+            float d = v[i] - mean;
+            q += d * d;
+        }
+    const float rstd = 1.0f / sqrtf(wave_sum_f(q) / (float)H + eps);
+#pragma unroll
+    for (int i = 0; i < PL; ++i) {
+        const int c = lane + 64 * i;
+        if (c < H) v[i] = (v[i] - mean) * rstd * gamma[c] + beta[c];
+    }
+}
+
+__device__ __forceinline__ int find_doc(const int32_t *cu, int n_docs, int row) {
+    int lo = 0, hi = n_docs;  // cu[lo] <= row < cu[hi]
+    while (hi - lo > 1) {
+        int mid = (lo + hi) >> 1;
+        if (cu[mid] <= row) lo = mid;
+        else hi = mid;
+    }
+    return lo;
+}
+
+// x0 = LN(word[id] + pos[p] + type[0]);  p = i (BERT) or pad + 1 + i (RoBERTa:
+// create_position_ids_from_input_ids on an unpadded row).  One wave per token.
+template <typename T, int PL>
+__global__ void __launch_bounds__(256)
+embed_ln_kernel(const int32_t *__restrict__ ids, const int32_t *__restrict__ cu, int n_docs,
+                int M, int H, const T *__restrict__ word, const T *__restrict__ pos,
+                const T *__restrict__ type0, const float *__restrict__ gamma,
+                const float *__restrict__ beta, float eps, int pos_offset, int vocab,
+                int max_pos, T *__restrict__ out, int32_t *__restrict__ err) {
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= M) return;
+    const int lane = threadIdx.x & 63;
+    const int d = find_doc(cu, n_docs, row);
+    const int p = row - cu[d] + pos_offset;
+    int id = ids[row];
+    if (id < 0 || id >= vocab || p >= max_pos) {
+        if (lane == 0) atomicOr(err, 1);
+        id = min(max(id, 0), vocab - 1);
+    }
+    const int pp = min(p, max_pos - 1);
+    const T *wr = word + (int64_t)id * H;
+    const T *pr = pos + (int64_t)pp * H;
+    float v[PL];
+#pragma unroll
+    for (int i = 0; i < PL; ++i) {
+        const int c = lane + 64 * i;
+        v[i] = (c < H) ? to_f32(wr[c]) + to_f32(pr[c]) + to_f32(type0[c]) : 0.f;
+    }
+    ln_row<PL>(v, H, gamma, beta, eps);
+#pragma unroll
+    for (int i = 0; i < PL; ++i) {
+        const int c = lane + 64 * i;
+        if (c < H) out[(int64_t)row * H + c] = from_f32<T>(v[i]);
+    }
+}
+
+// x = LN(pre) (pre = GEMM output + bias + residual, f32).  With head_w: the
+// impact head of the reference (xlmr_original.py:34-38, :77-85) on the f32 LN
+// output: impact = act(x . w + b), act = Softplus(beta 1, threshold 20) or ReLU.
+template <typename T, int PL>
+__global__ void __launch_bounds__(256)
+ln_kernel(const float *__restrict__ pre, int M, int H, const float *__restrict__ gamma,
+          const float *__restrict__ beta, float eps, T *__restrict__ out,
+          const float *__restrict__ head_w, float head_b, int act, float *__restrict__ impact) {
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= M) return;
+    const int lane = threadIdx.x & 63;
+    float v[PL];
+#pragma unroll
+    for (int i = 0; i < PL; ++i) {
+        const int c = lane + 64 * i;
+        v[i] = (c < H) ? pre[(int64_t)row * H + c] : 0.f;
+    }
+    ln_row<PL>(v, H, gamma, beta, eps);
+    if (out) {
+#pragma unroll
+        for (int i = 0; i < PL; ++i) {
+            const int c = lane + 64 * i;
+            if (c < H) out[(int64_t)row * H + c] = from_f32<T>(v[i]);
+        }
+    }
+    if (head_w) {
+        float s = 0.f;
+#pragma unroll
+        for (int i = 0; i < PL; ++i) {
+            const int c = lane + 64 * i;
+            if (c < H) s += v[i] * head_w[c];
+        }
+        s = wave_sum_f(s) + head_b;
+        if (lane == 0) {
+            float y;
+            if (act == 0)  // nn.Softplus(beta=1, threshold=20)
+                y = (s > 20.0f) ? s : log1pf(expf(s));
+            else
+                y = s > 0.f ? s : 0.f;
+            impact[row] = y;
+        }
+    }
+}
+
+// numpy's round(np.float32, 3) (reference indexer.py:132): fl32(rint(fl32(x*1000))/1000)
+__device__ __forceinline__ float round3(float x) {
+    float t = __fmul_rn(x, 1000.0f);
+    return __fdiv_rn(rintf(t), 1000.0f);
+}
+
+// compute_term_impacts (xlmr_original.py:205-225): impact of the first token of
+// every unique term.  term_tok is relative to the doc's first token.
+__global__ void gather_terms_kernel(const float *__restrict__ impact,
+                                    const int32_t *__restrict__ cu_seq,
+                                    const int32_t *__restrict__ cu_terms, int n_docs,
+                                    const int32_t *__restrict__ term_tok, int n_terms, int do_round,
+                                    float *__restrict__ out, int32_t *__restrict__ err) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n_terms) return;
+    const int d = find_doc(cu_terms, n_docs, i);
+    const int tok = term_tok[i];
+    const int len = cu_seq[d + 1] - cu_seq[d];
+    float v = 0.f;
+    if (tok < 0 || tok >= len) {
+        atomicOr(err, 2);
+    } else {
+        v = impact[cu_seq[d] + tok];
+    }
+    out[i] = do_round ? round3(v) : v;
+}
+
+template <typename T>
+void launch_embed_ln(const int32_t *ids, const int32_t *cu, int n_docs, int M, int H,
+                     const T *word, const T *pos, const T *type0, const float *gamma,
+                     const float *beta, float eps, int pos_offset, int vocab, int max_pos, T *out,
+                     int32_t *err, hipStream_t s) {
+    if (M == 0) return;
+    dim3 grid((M + 3) / 4);
+    if (H <= 256)
+        hipLaunchKernelGGL((embed_ln_kernel<T, 4>), grid, dim3(256), 0, s, ids, cu, n_docs, M, H,
+                           word, pos, type0, gamma, beta, eps, pos_offset, vocab, max_pos, out,
+                           err);
+    else if (H <= 768)
+        hipLaunchKernelGGL((embed_ln_kernel<T, 12>), grid, dim3(256), 0, s, ids, cu, n_docs, M,
+                           H, word, pos, type0, gamma, beta, eps, pos_offset, vocab, max_pos, out,
+                           err);
+    else
+        hipLaunchKernelGGL((embed_ln_kernel<T, LN_MAX_PER_LANE>), grid, dim3(256), 0, s, ids, cu,
+                           n_docs, M, H, word, pos, type0, gamma, beta, eps, pos_offset, vocab,
+                           max_pos, out, err);
+    check_launch("embed_ln");
+}
+
+template <typename T>
+void launch_ln(const float *pre, int M, int H, const float *gamma, const float *beta, float eps,
+               T *out, const float *head_w, float head_b, int act, float *impact, hipStream_t s) {
+    if (M == 0) return;
+    dim3 grid((M + 3) / 4);
+    if (H <= 256)
+        hipLaunchKernelGGL((ln_kernel<T, 4>), grid, dim3(256), 0, s, pre, M, H, gamma, beta, eps,
+                           out, head_w, head_b, act, impact);
+    else if (H <= 768)
+        hipLaunchKernelGGL((ln_kernel<T, 12>), grid, dim3(256), 0, s, pre, M, H, gamma, beta,
+                           eps, out, head_w, head_b, act, impact);
+    else
+        hipLaunchKernelGGL((ln_kernel<T, LN_MAX_PER_LANE>), grid, dim3(256), 0, s, pre, M, H,
+                           gamma, beta, eps, out, head_w, head_b, act, impact);
+    check_launch("ln");
+}
+
+void launch_gather_terms(const float *impact, const int32_t *cu_seq, const int32_t *cu_terms,
+                         int n_docs, const int32_t *term_tok, int n_terms, int do_round,
+                         float *out, int32_t *err, hipStream_t s) {
+    if (n_terms == 0) return;
+    hipLaunchKernelGGL(gather_terms_kernel, dim3((n_terms + 255) / 256), dim3(256), 0, s, impact,
+                       cu_seq, cu_terms, n_docs, term_tok, n_terms, do_round, out, err);
+    check_launch("gather_terms");
+}
+
+template void launch_embed_ln<bf16>(const int32_t *, const int32_t *, int, int, int, const bf16 *,
+                                    const bf16 *, const bf16 *, const float *, const float *,
+                                    float, int, int, int, bf16 *, int32_t *, hipStream_t);
+template void launch_embed_ln<float>(const int32_t *, const int32_t *, int, int, int,
+                                     const float *, const float *, const float *, const float *,
+                                     const float *, float, int, int, int, float *, int32_t *,
+                                     hipStream_t);
+template void launch_ln<bf16>(const float *, int, int, const float *, const float *, float, bf16 *,
+                              const float *, float, int, float *, hipStream_t);
+template void launch_ln<float>(const float *, int, int, const float *, const float *, float,
+                               float *, const float *, float, int, float *, hipStream_t);
+
+// ---------------------------------------------------------------------------
+// A10 quantizer (reference src/deep_impact/indexing/quantize.py:13-47):
+//   max_val = max(0, values) (fp64), scale = (2^bits - 1) / max_val (fp64),
+//   q = int(v * scale) (truncation, fp64 product).
+// ---------------------------------------------------------------------------
+__global__ void max_f32_kernel(const float *__restrict__ v, int64_t n,
+                               unsigned int *__restrict__ out_bits) {
+    float m = 0.f;  // find_max_value starts at 0
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x)
+        m = fmaxf(m, v[i]);
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) m = fmaxf(m, __shfl_xor(m, d, 64));
+    // non-negative floats order like their bit patterns (-0.0 and NaN -> 0)
+    if ((threadIdx.x & 63) == 0) atomicMax(out_bits, m > 0.f ? __float_as_uint(m) : 0u);
+}
+
+__global__ void quantize_kernel(const float *__restrict__ v, int64_t n,
+                                const unsigned int *__restrict__ max_bits, double max_given,
+                                int bits, int32_t *__restrict__ out) {
+    const double m = max_given > 0.0 ? max_given : (double)__uint_as_float(*max_bits);
+    const double scale = (double)((1 << bits) - 1) / m;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        double p = __dmul_rn((double)v[i], scale);
+        p = fmin(fmax(p, -2147483648.0), 2147483647.0);
+        out[i] = (int32_t)p;  // C conversion truncates toward zero, as Python int()
+    }
+}
+
+}  // namespace di
+
+namespace di {
+void launch_quantize(const float *v, int64_t n, double max_given, int bits, int32_t *out,
+                     unsigned int *max_bits, hipStream_t s) {
+    DI_HIP(hipMemsetAsync(max_bits, 0, sizeof(unsigned int), s));
+    if (n == 0) return;
+    int blocks = (int)std::min<int64_t>(2048, (n + 255) / 256);
+    if (!(max_given > 0.0)) {
+        hipLaunchKernelGGL(max_f32_kernel, dim3(blocks), dim3(256), 0, s, v, n, max_bits);
+        check_launch("max_f32");
+    }
+    hipLaunchKernelGGL(quantize_kernel, dim3(blocks), dim3(256), 0, s, v, n, max_bits,
+                       max_given, bits, out);
+    check_launch("quantize");
+}
+}  // namespace di
+
+extern "C" int di_quantize(const float *impacts, int64_t n, double max_val, int32_t bits,
+                           int32_t *out, double *max_used, int device, void *hip_stream,
+                           uint32_t flags) {
+    using namespace di;
+    return guard([&] {
+        DI_REQUIRE(impacts && out && n >= 0 && bits >= 1 && bits <= 16, DI_EINVAL,
+                   "bad argument");
+        int prev = 0;
+        DI_HIP(hipGetDevice(&prev));
+        DI_HIP(hipSetDevice(device));
+        hipStream_t s = (hipStream_t)hip_stream;
+        const bool dev = flags & DI_F_DEVICE_PTRS;
+        DevBuf bin, bout, bmax;
+        bmax.reserve(16);
+        const float *d_in = (const float *)stage_in(impacts, (size_t)n * 4, dev, bin, s);
+        int32_t *d_out = out;
+        if (!dev) {
+            bout.reserve((size_t)std::max<int64_t>(n, 1) * 4);
+            d_out = bout.as<int32_t>();
+        }
+        launch_quantize(d_in, n, max_val, bits, d_out, bmax.as<unsigned int>(), s);
+        unsigned int mb = 0;
+        DI_HIP(hipMemcpyAsync(&mb, bmax.p, 4, hipMemcpyDeviceToHost, s));
+        if (!dev && n)
+            DI_HIP(hipMemcpyAsync(out, d_out, (size_t)n * 4, hipMemcpyDeviceToHost, s));
+        DI_HIP(hipStreamSynchronize(s));
+        float mf;
+        std::memcpy(&mf, &mb, 4);
+        if (max_used) *max_used = max_val > 0.0 ? max_val : (double)mf;
+        DI_REQUIRE(max_val > 0.0 || n == 0 || mf > 0.f, DI_EINVAL,
+                   "max impact is 0: the reference divides by zero (quantize.py:37)");
+        (void)hipSetDevice(prev);
+    });
+}

@@ -1,0 +1,518 @@
+// encoder.hip -- DeeperImpact encoder on MI355X: weight residency and the
+// per-batch forward (host orchestration of the HIP kernels).
+//
+// Replaces, for a batch of documents, the reference's
+//   DeepImpact.forward            src/deep_impact/models/xlmr_original.py:41-85
+//   compute_term_impacts          src/deep_impact/models/xlmr_original.py:205-225
+//   round(impact, 3)              src/deep_impact/indexing/indexer.py:132
+// Documents arrive packed (cu_seqlens, no padding); every GEMM runs on real
+// tokens only.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "di_common.h"
+#include "enc_common.h"
+
+namespace di {
+
+template <typename T>
+void launch_gemm(int epi, const GemmArgs &g, hipStream_t s);
+template <typename T>
+void launch_attention(const T *qk, const T *vt, const int32_t *cu_seqlens, int n_docs,
+                      int max_len, int H, int ld_v, T *ctx, hipStream_t s);
+template <typename T>
+void launch_embed_ln(const int32_t *ids, const int32_t *cu, int n_docs, int M, int H,
+                     const T *word, const T *pos, const T *type0, const float *gamma,
+                     const float *beta, float eps, int pos_offset, int vocab, int max_pos, T *out,
+                     int32_t *err, hipStream_t s);
+template <typename T>
+void launch_ln(const float *pre, int M, int H, const float *gamma, const float *beta, float eps,
+               T *out, const float *head_w, float head_b, int act, float *impact, hipStream_t s);
+void launch_gather_terms(const float *impact, const int32_t *cu_seq, const int32_t *cu_terms,
+                         int n_docs, const int32_t *term_tok, int n_terms, int do_round,
+                         float *out, int32_t *err, hipStream_t s);
+
+struct Layer {
+    DevBuf w_qkv, b_qkv, w_o, b_o, ln1_g, ln1_b, w_i, b_i, w_out, b_out, ln2_g, ln2_b;
+};
+
+}  // namespace di
+
+using namespace di;
+
+struct di_encoder {
+    di_encoder_cfg cfg{};
+    int device = 0;
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    size_t esz = 2;  // bytes per activation/weight element (bf16 or f32)
+    DevBuf word, pos, type0, emb_g, emb_b, head_w;
+    float head_b = 0.f;
+    std::vector<std::unique_ptr<Layer>> layers;
+    // workspace
+    DevBuf X, qk, vt, ctx, pre, X1, Hff, impact, ids, cu, tt, cut, err;
+    int64_t cap_tokens = 0;
+    int ld_v = 0;
+    Timer timer;
+};
+
+namespace {
+
+struct DeviceScope {
+    int prev = -1;
+    explicit DeviceScope(int dev) {
+        DI_HIP(hipGetDevice(&prev));
+        if (prev != dev) DI_HIP(hipSetDevice(dev));
+    }
+    ~DeviceScope() {
+        int cur;
+        if (hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
+uint16_t f32_to_bf16_bits(float f) {  // round to nearest even (NaN stays NaN)
+    uint32_t u;
+    std::memcpy(&u, &f, 4);
+    if ((u & 0x7F800000u) == 0x7F800000u && (u & 0x7FFFFFu)) return (uint16_t)((u >> 16) | 0x40);
+    u += 0x7FFFu + ((u >> 16) & 1u);
+    return (uint16_t)(u >> 16);
+}
+
+float bf16_bits_to_f32(uint16_t h) {
+    uint32_t u = (uint32_t)h << 16;
+    float f;
+    std::memcpy(&f, &u, 4);
+    return f;
+}
+
+std::string strip_prefix(const std::string &k) {
+    for (const char *p : {"bert.", "roberta.", "model."})
+        if (k.rfind(p, 0) == 0) return k.substr(std::strlen(p));
+    return k;
+}
+
+struct HostTensor {
+    const di_tensor *t;
+    int64_t numel() const {
+        int64_t n = 1;
+        for (int i = 0; i < t->ndim; ++i) n *= t->shape[i];
+        return n;
+    }
+    float at(int64_t i) const {
+        if (t->dtype == DI_DTYPE_F32) return static_cast<const float *>(t->data)[i];
+        return bf16_bits_to_f32(static_cast<const uint16_t *>(t->data)[i]);
+    }
+};
+
+void upload(DevBuf &dst, const std::vector<const HostTensor *> &parts, int64_t rows_of_first,
+            bool as_f32_always, size_t esz) {
+    (void)rows_of_first;
+    int64_t n = 0;
+    for (auto *p : parts) n += p->numel();
+    const bool f32 = as_f32_always || esz == 4;
+    dst.reserve((size_t)n * (f32 ? 4 : 2));
+    if (f32) {
+        std::vector<float> h((size_t)n);
+        int64_t o = 0;
+        for (auto *p : parts)
+            for (int64_t i = 0; i < p->numel(); ++i) h[(size_t)o++] = p->at(i);
+        DI_HIP(hipMemcpy(dst.p, h.data(), (size_t)n * 4, hipMemcpyHostToDevice));
+    } else {
+        std::vector<uint16_t> h((size_t)n);
+        int64_t o = 0;
+        for (auto *p : parts) {
+            if (p->t->dtype == DI_DTYPE_BF16) {
+                std::memcpy(&h[(size_t)o], p->t->data, (size_t)p->numel() * 2);
+                o += p->numel();
+            } else {
+                const float *src = static_cast<const float *>(p->t->data);
+                for (int64_t i = 0; i < p->numel(); ++i) h[(size_t)o++] = f32_to_bf16_bits(src[i]);
+            }
+        }
+        DI_HIP(hipMemcpy(dst.p, h.data(), (size_t)n * 2, hipMemcpyHostToDevice));
+    }
+}
+
+void ensure_workspace(di_encoder *e, int64_t M, int n_docs, int64_t n_terms) {
+    const int H = e->cfg.hidden, F = e->cfg.intermediate;
+    if (M > e->cap_tokens) {
+        int64_t cap = std::max<int64_t>(M, 256);
+        const size_t es = e->esz;
+        e->X.reserve(cap * H * es);
+        e->X1.reserve(cap * H * es);
+        e->ctx.reserve(cap * H * es);
+        e->qk.reserve(cap * 2 * H * es);
+        e->Hff.reserve(cap * F * es);
+        e->pre.reserve(cap * H * 4);
+        e->impact.reserve(cap * 4);
+        e->ids.reserve(cap * 4);
+        e->ld_v = (int)(((cap + 64) + 63) / 64 * 64);
+        e->vt.reserve((size_t)H * e->ld_v * es);
+        DI_HIP(hipMemset(e->vt.p, 0, (size_t)H * e->ld_v * es));
+        e->cap_tokens = cap;
+    }
+    e->cu.reserve((size_t)(n_docs + 1) * 4);
+    e->cut.reserve((size_t)(n_docs + 1) * 4);
+    e->tt.reserve((size_t)std::max<int64_t>(n_terms, 1) * 4);
+    e->err.reserve(16);
+}
+
+template <typename T>
+void forward(di_encoder *e, const int32_t *d_ids, const int32_t *d_cu, int n_docs, int64_t M,
+             int max_len, bool timing, hipStream_t s) {
+    const auto &c = e->cfg;
+    const int H = c.hidden, F = c.intermediate;
+    const int pos_offset = (c.variant == DI_VARIANT_XLMR) ? c.pad_id + 1 : 0;
+    T *X = e->X.as<T>(), *X1 = e->X1.as<T>();
+    {
+        TimedLaunch tl(e->timer, timing, "embed_ln", s);
+        launch_embed_ln<T>(d_ids, d_cu, n_docs, (int)M, H, e->word.as<T>(), e->pos.as<T>(),
+                           e->type0.as<T>(), e->emb_g.as<float>(), e->emb_b.as<float>(),
+                           c.layer_norm_eps, pos_offset, c.vocab_size, c.max_positions, X,
+                           e->err.as<int32_t>(), s);
+    }
+    // keep V^T's padding keys finite-and-zero (read, then multiplied by p = 0)
+    DI_HIP(hipMemset2DAsync(e->vt.as<unsigned char>() + M * e->esz, (size_t)e->ld_v * e->esz, 0,
+                            std::min<int64_t>(64, e->ld_v - M) * e->esz, H, s));
+    for (size_t l = 0; l < e->layers.size(); ++l) {
+        Layer &L = *e->layers[l];
+        const bool last = l + 1 == e->layers.size();
+        GemmArgs g{};
+        g.M = (int)M;
+        g.hidden = H;
+        // QKV (V written transposed for the attention kernel)
+        g.A = X;
+        g.B = L.w_qkv.p;
+        g.bias = L.b_qkv.as<float>();
+        g.out = e->qk.p;
+        g.out2 = e->vt.p;
+        g.N = 3 * H;
+        g.K = H;
+        g.ld_out = 2 * H;
+        g.ld_v = e->ld_v;
+        {
+            TimedLaunch tl(e->timer, timing, "gemm_qkv", s);
+            launch_gemm<T>(EPI_QKV, g, s);
+        }
+        {
+            TimedLaunch tl(e->timer, timing, "attention", s);
+            launch_attention<T>(e->qk.as<T>(), e->vt.as<T>(), d_cu, n_docs, max_len, H, e->ld_v,
+                                e->ctx.as<T>(), s);
+        }
+        // attention output + residual -> LN1
+        g = GemmArgs{};
+        g.M = (int)M;
+        g.A = e->ctx.p;
+        g.B = L.w_o.p;
+        g.bias = L.b_o.as<float>();
+        g.resid = X;
+        g.out = e->pre.p;
+        g.N = H;
+        g.K = H;
+        g.ld_out = H;
+        {
+            TimedLaunch tl(e->timer, timing, "gemm_o", s);
+            launch_gemm<T>(EPI_BIAS_RESID, g, s);
+        }
+        {
+            TimedLaunch tl(e->timer, timing, "ln", s);
+            launch_ln<T>(e->pre.as<float>(), (int)M, H, L.ln1_g.as<float>(), L.ln1_b.as<float>(),
+                         c.layer_norm_eps, X1, nullptr, 0.f, c.activation, nullptr, s);
+        }
+        // FFN
+        g = GemmArgs{};
+        g.M = (int)M;
+        g.A = X1;
+        g.B = L.w_i.p;
+        g.bias = L.b_i.as<float>();
+        g.out = e->Hff.p;
+        g.N = F;
+        g.K = H;
+        g.ld_out = F;
+        {
+            TimedLaunch tl(e->timer, timing, "gemm_ffn1", s);
+            launch_gemm<T>(EPI_BIAS_GELU, g, s);
+        }
+        g = GemmArgs{};
+        g.M = (int)M;
+        g.A = e->Hff.p;
+        g.B = L.w_out.p;
+        g.bias = L.b_out.as<float>();
+        g.resid = X1;
+        g.out = e->pre.p;
+        g.N = H;
+        g.K = F;
+        g.ld_out = H;
+        {
+            TimedLaunch tl(e->timer, timing, "gemm_ffn2", s);
+            launch_gemm<T>(EPI_BIAS_RESID, g, s);
+        }
+        {
+            TimedLaunch tl(e->timer, timing, "ln", s);
+            // the last LayerNorm feeds only the impact head
+            launch_ln<T>(e->pre.as<float>(), (int)M, H, L.ln2_g.as<float>(), L.ln2_b.as<float>(),
+                         c.layer_norm_eps, last ? nullptr : X,
+                         last ? e->head_w.as<float>() : nullptr, e->head_b, c.activation,
+                         last ? e->impact.as<float>() : nullptr, s);
+        }
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+int di_encoder_create(const di_encoder_cfg *cfg, const di_tensor *w, int32_t n_w, int device,
+                      di_encoder **out) {
+    return guard([&] {
+        DI_REQUIRE(cfg && out && (n_w == 0 || w), DI_EINVAL, "null argument");
+        int ndev = 0;
+        DI_REQUIRE(hipGetDeviceCount(&ndev) == hipSuccess && ndev > 0, DI_ENODEV,
+                   "no HIP device");
+        DI_REQUIRE(device >= 0 && device < ndev, DI_EINVAL, "bad device %d", device);
+        const di_encoder_cfg &c = *cfg;
+        DI_REQUIRE(c.variant == DI_VARIANT_XLMR || c.variant == DI_VARIANT_BERT, DI_EINVAL,
+                   "bad variant");
+        DI_REQUIRE(c.activation == DI_ACT_SOFTPLUS || c.activation == DI_ACT_RELU, DI_EINVAL,
+                   "bad activation");
+        DI_REQUIRE(c.precision == DI_PREC_BF16 || c.precision == DI_PREC_FP32, DI_EINVAL,
+                   "bad precision");
+        DI_REQUIRE(c.hidden > 0 && c.hidden % 64 == 0 && c.hidden <= 1024, DI_EINVAL,
+                   "hidden=%d must be a multiple of 64, <= 1024", c.hidden);
+        DI_REQUIRE(c.heads > 0 && c.hidden / c.heads == 64 && c.hidden % c.heads == 0,
+                   DI_EINVAL, "head dim must be 64 (hidden=%d heads=%d)", c.hidden, c.heads);
+        DI_REQUIRE(c.intermediate > 0 && c.intermediate % 64 == 0, DI_EINVAL,
+                   "intermediate=%d must be a multiple of 64", c.intermediate);
+        DI_REQUIRE(c.layers > 0 && c.vocab_size > 0 && c.max_positions > 0, DI_EINVAL,
+                   "bad sizes");
+        DeviceScope ds(device);
+        std::unique_ptr<di_encoder> e(new di_encoder());
+        e->cfg = c;
+        e->device = device;
+        e->esz = c.precision == DI_PREC_BF16 ? 2 : 4;
+        DI_HIP(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
+        e->own_stream = true;
+
+        std::unordered_map<std::string, HostTensor> byname;
+        std::vector<HostTensor> ht((size_t)n_w);
+        for (int i = 0; i < n_w; ++i) {
+            DI_REQUIRE(w[i].name && w[i].data, DI_EINVAL, "tensor %d has no name/data", i);
+            DI_REQUIRE(w[i].dtype == DI_DTYPE_F32 || w[i].dtype == DI_DTYPE_BF16, DI_EINVAL,
+                       "tensor %s: dtype must be f32 or bf16", w[i].name);
+            ht[(size_t)i].t = &w[i];
+            std::string k = strip_prefix(w[i].name);
+            if (k == "embeddings.position_ids" || k.rfind("pooler.", 0) == 0) continue;
+            byname[k] = ht[(size_t)i];
+        }
+        std::unordered_map<std::string, int> used;
+        auto get = [&](const std::string &k, std::initializer_list<int64_t> shape)
+            -> const HostTensor * {
+            auto it = byname.find(k);
+            DI_REQUIRE(it != byname.end(), DI_EINVAL, "missing weight %s", k.c_str());
+            const di_tensor *t = it->second.t;
+            DI_REQUIRE(t->ndim == (int)shape.size(), DI_EINVAL, "weight %s: ndim %d", k.c_str(),
+                       t->ndim);
+            int i = 0;
+            for (int64_t d : shape) {
+                DI_REQUIRE(d < 0 || t->shape[i] == d, DI_EINVAL,
+                           "weight %s: dim %d is %lld, expected %lld", k.c_str(), i,
+                           (long long)t->shape[i], (long long)d);
+                ++i;
+            }
+            used[k] = 1;
+            return &it->second;
+        };
+        const int64_t H = c.hidden, F = c.intermediate;
+        const HostTensor *we = get("embeddings.word_embeddings.weight", {c.vocab_size, H});
+        const HostTensor *pe = get("embeddings.position_embeddings.weight", {-1, H});
+        DI_REQUIRE(pe->t->shape[0] >= c.max_positions, DI_EINVAL,
+                   "position table has %lld rows < max_positions %d",
+                   (long long)pe->t->shape[0], c.max_positions);
+        const HostTensor *te = get("embeddings.token_type_embeddings.weight", {-1, H});
+        upload(e->word, {we}, 0, false, e->esz);
+        upload(e->pos, {pe}, 0, false, e->esz);
+        {
+            // token_type_ids are not passed (xlmr_original.py:73): row 0 is used
+            di_tensor row0 = *te->t;
+            row0.ndim = 1;
+            row0.shape[0] = H;
+            HostTensor r0{&row0};
+            upload(e->type0, {&r0}, 0, false, e->esz);
+        }
+        upload(e->emb_g, {get("embeddings.LayerNorm.weight", {H})}, 0, true, 4);
+        upload(e->emb_b, {get("embeddings.LayerNorm.bias", {H})}, 0, true, 4);
+        for (int l = 0; l < c.layers; ++l) {
+            std::string p = "encoder.layer." + std::to_string(l) + ".";
+            auto L = std::make_unique<Layer>();
+            upload(L->w_qkv,
+                   {get(p + "attention.self.query.weight", {H, H}),
+                    get(p + "attention.self.key.weight", {H, H}),
+                    get(p + "attention.self.value.weight", {H, H})},
+                   0, false, e->esz);
+            upload(L->b_qkv,
+                   {get(p + "attention.self.query.bias", {H}),
+                    get(p + "attention.self.key.bias", {H}),
+                    get(p + "attention.self.value.bias", {H})},
+                   0, true, 4);
+            upload(L->w_o, {get(p + "attention.output.dense.weight", {H, H})}, 0, false, e->esz);
+            upload(L->b_o, {get(p + "attention.output.dense.bias", {H})}, 0, true, 4);
+            upload(L->ln1_g, {get(p + "attention.output.LayerNorm.weight", {H})}, 0, true, 4);
+            upload(L->ln1_b, {get(p + "attention.output.LayerNorm.bias", {H})}, 0, true, 4);
+            upload(L->w_i, {get(p + "intermediate.dense.weight", {F, H})}, 0, false, e->esz);
+            upload(L->b_i, {get(p + "intermediate.dense.bias", {F})}, 0, true, 4);
+            upload(L->w_out, {get(p + "output.dense.weight", {H, F})}, 0, false, e->esz);
+            upload(L->b_out, {get(p + "output.dense.bias", {H})}, 0, true, 4);
+            upload(L->ln2_g, {get(p + "output.LayerNorm.weight", {H})}, 0, true, 4);
+            upload(L->ln2_b, {get(p + "output.LayerNorm.bias", {H})}, 0, true, 4);
+            e->layers.push_back(std::move(L));
+        }
+        upload(e->head_w, {get("impact_score_encoder.0.weight", {1, H})}, 0, true, 4);
+        e->head_b = get("impact_score_encoder.0.bias", {1})->at(0);
+        // strict, as ModelCheckpoint.load -> load_state_dict (checkpoint.py:117)
+        for (auto &kv : byname)
+            DI_REQUIRE(used.count(kv.first), DI_EINVAL, "unexpected weight %s",
+                       kv.first.c_str());
+        *out = e.release();
+    });
+}
+
+int di_encode(di_encoder *e, const int32_t *tok_ids, const int32_t *cu_seqlens, int32_t n_docs,
+              int64_t n_tokens, int32_t max_len, const int32_t *term_tok, const int32_t *cu_terms,
+              int64_t n_terms, float *out, uint32_t flags) {
+    return guard([&] {
+        DI_REQUIRE(e && cu_seqlens && out && n_docs >= 0, DI_EINVAL, "bad argument");
+        DeviceScope ds(e->device);
+        const bool dev = flags & DI_F_DEVICE_PTRS;
+        const bool timing = flags & DI_F_TIMING;
+        const bool token_out = flags & DI_F_TOKEN_IMPACTS;
+        hipStream_t s = e->stream;
+        if (!dev) {
+            DI_REQUIRE(cu_seqlens[0] == 0, DI_EINVAL, "cu_seqlens[0] must be 0");
+            int32_t mx = 0;
+            for (int d = 0; d < n_docs; ++d) {
+                int32_t len = cu_seqlens[d + 1] - cu_seqlens[d];
+                DI_REQUIRE(len >= 0, DI_EINVAL, "cu_seqlens not monotone at %d", d);
+                mx = std::max(mx, len);
+            }
+            n_tokens = cu_seqlens[n_docs];
+            max_len = mx;
+            if (!token_out) {
+                DI_REQUIRE(term_tok && cu_terms && cu_terms[0] == 0, DI_EINVAL,
+                           "term arrays required");
+                n_terms = cu_terms[n_docs];
+            }
+        }
+        DI_REQUIRE(n_tokens >= 0 && n_tokens < (1ll << 31), DI_ERANGE, "n_tokens=%lld",
+                   (long long)n_tokens);
+        DI_REQUIRE(max_len <= e->cfg.max_positions, DI_ERANGE,
+                   "a document has %d tokens > max_positions %d", max_len,
+                   e->cfg.max_positions);
+        if (n_docs == 0) return;
+        ensure_workspace(e, n_tokens, n_docs, n_terms);
+        const int32_t *d_ids =
+            (const int32_t *)stage_in(tok_ids, (size_t)n_tokens * 4, dev, e->ids, s);
+        const int32_t *d_cu =
+            (const int32_t *)stage_in(cu_seqlens, (size_t)(n_docs + 1) * 4, dev, e->cu, s);
+        DI_HIP(hipMemsetAsync(e->err.p, 0, 4, s));
+        if (n_tokens > 0) {
+            if (e->esz == 2)
+                forward<bf16>(e, d_ids, d_cu, n_docs, n_tokens, max_len, timing, s);
+            else
+                forward<float>(e, d_ids, d_cu, n_docs, n_tokens, max_len, timing, s);
+        }
+        float *d_out = out;
+        DevBuf tmp;
+        if (token_out) {
+            if (dev)
+                DI_HIP(hipMemcpyAsync(out, e->impact.p, (size_t)n_tokens * 4,
+                                      hipMemcpyDeviceToDevice, s));
+            else
+                DI_HIP(hipMemcpyAsync(out, e->impact.p, (size_t)n_tokens * 4,
+                                      hipMemcpyDeviceToHost, s));
+        } else {
+            const int32_t *d_tt =
+                (const int32_t *)stage_in(term_tok, (size_t)n_terms * 4, dev, e->tt, s);
+            const int32_t *d_cut =
+                (const int32_t *)stage_in(cu_terms, (size_t)(n_docs + 1) * 4, dev, e->cut, s);
+            if (!dev) {
+                tmp.reserve((size_t)std::max<int64_t>(n_terms, 1) * 4);
+                d_out = tmp.as<float>();
+            }
+            {
+                TimedLaunch tl(e->timer, timing, "gather_terms", s);
+                launch_gather_terms(e->impact.as<float>(), d_cu, d_cut, n_docs, d_tt,
+                                    (int)n_terms, (flags & DI_F_ROUND3) ? 1 : 0, d_out,
+                                    e->err.as<int32_t>(), s);
+            }
+            if (!dev && n_terms)
+                DI_HIP(hipMemcpyAsync(out, d_out, (size_t)n_terms * 4, hipMemcpyDeviceToHost,
+                                      s));
+        }
+        if (!(flags & DI_F_ASYNC) || !dev) {
+            int32_t err = 0;
+            DI_HIP(hipMemcpyAsync(&err, e->err.p, 4, hipMemcpyDeviceToHost, s));
+            DI_HIP(hipStreamSynchronize(s));
+            e->timer.resolve();
+            DI_REQUIRE(!(err & 1), DI_EINVAL,
+                       "a token id is outside the vocabulary or a position exceeds the table");
+            DI_REQUIRE(!(err & 2), DI_EINVAL, "a term token index is outside its document");
+        }
+    });
+}
+
+int di_encoder_reserve(di_encoder *e, int64_t max_tokens, int32_t max_docs, int64_t max_terms) {
+    return guard([&] {
+        DI_REQUIRE(e && max_tokens >= 0 && max_docs >= 0 && max_terms >= 0, DI_EINVAL,
+                   "bad argument");
+        DeviceScope ds(e->device);
+        ensure_workspace(e, max_tokens, max_docs, max_terms);
+    });
+}
+
+int di_encoder_set_stream(di_encoder *e, void *stream) {
+    return guard([&] {
+        DI_REQUIRE(e, DI_EINVAL, "null handle");
+        DeviceScope ds(e->device);
+        if (e->own_stream && e->stream) DI_HIP(hipStreamDestroy(e->stream));
+        e->own_stream = stream == nullptr;
+        if (stream)
+            e->stream = (hipStream_t)stream;
+        else
+            DI_HIP(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
+    });
+}
+
+int di_encoder_sync(di_encoder *e) {
+    return guard([&] {
+        DI_REQUIRE(e, DI_EINVAL, "null handle");
+        DeviceScope ds(e->device);
+        DI_HIP(hipStreamSynchronize(e->stream));
+        e->timer.resolve();
+    });
+}
+
+int di_encoder_timing(di_encoder *e, const char *name, di_timing *out, int reset) {
+    return guard([&] {
+        DI_REQUIRE(e && name && out, DI_EINVAL, "null argument");
+        e->timer.get(name, out, reset != 0);
+    });
+}
+
+int di_encoder_destroy(di_encoder *e) {
+    return guard([&] {
+        if (!e) return;
+        {
+            DeviceScope ds(e->device);
+            if (e->own_stream && e->stream) (void)hipStreamDestroy(e->stream);
+        }
+        delete e;
+    });
+}
+
+}  // extern "C"

@@ -122,30 +122,52 @@ score_blocks_kernel(const uint32_t *__restrict__ post, const int64_t *__restrict
     }
 
     // ---- scatter: terms in query order, barrier between terms -------------
-    for (int j = 0; j < nt; ++j) {
-        const int64_t lo = sh.lo[j], hi = sh.hi[j];
-        const uint32_t first_bits = (uint32_t)(255 - j) << 8;
-        auto apply = [&](uint32_t p) {
-            uint32_t local = (p >> 8) & (BLOCK_DOCS - 1), v = p & 255u;
-            uint32_t w = sh.acc[local];
-            w = w ? w + (v << 16) : ((v << 16) | first_bits | v);
-            sh.acc[local] = w;
-        };
-        int64_t head_end = min(hi, (lo + 3) & ~(int64_t)3);
-        for (int64_t i = lo + tid; i < head_end; i += SC_THREADS) apply(post[i]);
-        int64_t body_end = head_end + ((hi - head_end) & ~(int64_t)3);
-        const uint4 *p4 = reinterpret_cast<const uint4 *>(post + head_end);
-        int64_t n4 = (body_end - head_end) >> 2;
-        for (int64_t i = tid; i < n4; i += SC_THREADS) {
-            uint4 v4 = p4[i];
-            apply(v4.x);
-            apply(v4.y);
-            apply(v4.z);
-            apply(v4.w);
+    // The postings of (term j, this block) are walked in rounds of SC_THREADS*U
+    // dwords (coalesced: lane-consecutive).  The next round's loads are issued
+    // before the current round is applied, also across a term boundary, so each
+    // term's barrier no longer exposes a memory round trip.
+    constexpr int U = 4;
+    constexpr int ROUND = SC_THREADS * U;
+    auto rounds = [&](int jj) { return (int)((sh.hi[jj] - sh.lo[jj] + ROUND - 1) / ROUND); };
+    auto load_round = [&](int jj, int rr, uint32_t (&r)[U]) {
+        const int64_t base = sh.lo[jj] + (int64_t)rr * ROUND + tid, hi = sh.hi[jj];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            int64_t i = base + (int64_t)u * SC_THREADS;
+            r[u] = (i < hi) ? post[i] : 0u;
         }
-        for (int64_t i = body_end + tid; i < hi; i += SC_THREADS) apply(post[i]);
-        __syncthreads();
+    };
+    int j = 0, rr = 0;
+    while (j < nt && rounds(j) == 0) ++j;
+    uint32_t cur[U], nxt[U];
+    if (j < nt) load_round(j, rr, cur);
+    while (j < nt) {
+        int jn = j, rn = rr + 1;
+        while (jn < nt && rn >= rounds(jn)) {
+            ++jn;
+            rn = 0;
+        }
+        if (jn < nt) load_round(jn, rn, nxt);
+        const uint32_t first_bits = (uint32_t)(255 - j) << 8;
+        uint32_t w[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) w[u] = sh.acc[(cur[u] >> 8) & (BLOCK_DOCS - 1)];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t v = cur[u] & 255u;  // 0 only for the padding lanes
+            if (v) {
+                uint32_t x = w[u];
+                x = x ? x + (v << 16) : ((v << 16) | first_bits | v);
+                sh.acc[(cur[u] >> 8) & (BLOCK_DOCS - 1)] = x;
+            }
+        }
+        if (jn != j) __syncthreads();  // term boundary (uniform across the block)
+#pragma unroll
+        for (int u = 0; u < U; ++u) cur[u] = nxt[u];
+        j = jn;
+        rr = rn;
     }
+    __syncthreads();
 
     // ---- block top-k: radix select on the 32-bit words ---------------------
     auto id_key = [](uint32_t w, int) { return w; };
@@ -215,30 +237,34 @@ score_blocks_kernel(const uint32_t *__restrict__ post, const int64_t *__restrict
 // ---------------------------------------------------------------------------
 // merge: per query, the top-k of n_lists candidate lists by 64-bit key
 // ---------------------------------------------------------------------------
-constexpr int MG_THREADS = 1024;
-constexpr int MG_WAVES = MG_THREADS / 64;
-constexpr int MG_LDS_KEYS = 16384;  // 128 KiB
+constexpr int MG_LDS_KEYS = 16384;  // fast path: every candidate fits in LDS
 
-struct MergeShared {
-    uint64_t keys[MG_LDS_KEYS];
-    RadixScratch<MG_WAVES> rs;
+template <int THREADS>
+struct alignas(16) MergeHead {  // 16-byte multiple: the u64 key array follows it
+    RadixScratch<THREADS / 64> rs;
     int32_t off[1025];
     uint32_t cnt;
     int32_t bad;
+    uint32_t pad[2];
 };
 
 enum DecodeMode : int { DECODE_QUANT = 0, DECODE_SPARSE = 1, DECODE_NONE = 2 };
 
-__global__ void __launch_bounds__(MG_THREADS)
+// keys: the LDS key array holds `cap` entries (power of two, <= MG_LDS_KEYS)
+template <int THREADS>
+__global__ void __launch_bounds__(THREADS)
 merge_topk_kernel(const uint64_t *__restrict__ keys, const int32_t *__restrict__ counts,
                   int n_lists, int k_in, int k, int64_t list_stride, int64_t cnt_stride,
-                  int64_t q_stride, int64_t cq_stride, uint64_t *__restrict__ out_key,
-                  uint32_t *__restrict__ out_doc, uint32_t *__restrict__ out_score,
-                  int32_t *__restrict__ out_n, int mode) {
+                  int64_t q_stride, int64_t cq_stride, int cap,
+                  uint64_t *__restrict__ out_key, uint32_t *__restrict__ out_doc,
+                  uint32_t *__restrict__ out_score, int32_t *__restrict__ out_n, int mode) {
     // key i of list l of query q: keys[q*q_stride + l*list_stride + i]
     // its count:                  counts[q*cq_stride + l*cnt_stride]
+    constexpr int WAVES = THREADS / 64;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    MergeShared &sh = *reinterpret_cast<MergeShared *>(smem);
+    MergeHead<THREADS> &sh = *reinterpret_cast<MergeHead<THREADS> *>(smem);
+    static_assert(sizeof(MergeHead<THREADS>) % 16 == 0, "key array must stay 16-byte aligned");
+    uint64_t *lk = reinterpret_cast<uint64_t *>(smem + sizeof(MergeHead<THREADS>));
     const int q = blockIdx.x, tid = threadIdx.x;
     const int32_t *cnt0 = counts + (int64_t)q * cq_stride;
     auto cnt = [&](int l) { return cnt0[(int64_t)l * cnt_stride]; };
@@ -246,11 +272,10 @@ merge_topk_kernel(const uint64_t *__restrict__ keys, const int32_t *__restrict__
 
     if (tid == 0) sh.bad = 0;
     __syncthreads();
-    // list lengths -> LDS, serial prefix by one thread (n_lists <= 1024 here)
     int64_t total = 0;
     const bool fast_lists = n_lists <= 1024;
     if (fast_lists) {
-        for (int l = tid; l < n_lists; l += MG_THREADS) {
+        for (int l = tid; l < n_lists; l += THREADS) {
             int c = cnt(l);
             if (c < 0) sh.bad = 1;
             sh.off[l + 1] = min(max(c, 0), k_in);
@@ -264,7 +289,7 @@ merge_topk_kernel(const uint64_t *__restrict__ keys, const int32_t *__restrict__
         total = sh.off[n_lists];
     } else {
         int64_t part = 0;
-        for (int l = tid; l < n_lists; l += MG_THREADS) {
+        for (int l = tid; l < n_lists; l += THREADS) {
             int c = cnt(l);
             if (c < 0) sh.bad = 1;
             part += min(max(c, 0), k_in);
@@ -280,36 +305,34 @@ merge_topk_kernel(const uint64_t *__restrict__ keys, const int32_t *__restrict__
         if (tid == 0) out_n[q] = -1;
         return;
     }
-    if (fast_lists && total <= MG_LDS_KEYS) {
+    const int take = (int)min<int64_t>(total, k);
+    uint64_t *ok = out_key ? out_key + (int64_t)q * k : nullptr;
+    if (fast_lists && total <= cap) {
         for (int l = 0; l < n_lists; ++l) {
             const int o = sh.off[l], c = sh.off[l + 1] - o;
             const uint64_t *s = src0 + (int64_t)l * list_stride;
-            for (int i = tid; i < c; i += MG_THREADS) sh.keys[o + i] = s[i];
+            for (int i = tid; i < c; i += THREADS) lk[o + i] = s[i];
         }
         __syncthreads();
-    }
-    const int take = (int)min<int64_t>(total, k);
-    uint64_t *ok = out_key ? out_key + (int64_t)q * k : nullptr;
-
-    if (total > MG_LDS_KEYS) {
-        // slow path: radix select the k-th largest key straight from global
+    } else {
+        // slow path: radix select the take-th largest key straight from global
         uint64_t prefix = 0, mask = 0;
         uint32_t need = (uint32_t)take;
         for (int shift = 56; shift >= 0; shift -= 8) {
-            radix_clear<MG_THREADS, MG_WAVES>(sh.rs);
+            radix_clear<THREADS, WAVES>(sh.rs);
             __syncthreads();
             RunLen rl;
             for (int l = 0; l < n_lists; ++l) {
                 int c = min(cnt(l), k_in);
                 const uint64_t *s = src0 + (int64_t)l * list_stride;
-                for (int i = tid; i < c; i += MG_THREADS) {
+                for (int i = tid; i < c; i += THREADS) {
                     uint64_t x = s[i];
                     if ((x & mask) == prefix) rl.add(sh.rs, (uint32_t)(x >> shift) & 255u);
                 }
             }
             rl.flush(sh.rs);
             __syncthreads();
-            radix_pick<MG_THREADS, MG_WAVES>(sh.rs, need);
+            radix_pick<THREADS, WAVES>(sh.rs, need);
             prefix |= (uint64_t)sh.rs.bin << shift;
             mask |= (uint64_t)255 << shift;
             need -= sh.rs.above;
@@ -321,11 +344,11 @@ merge_topk_kernel(const uint64_t *__restrict__ keys, const int32_t *__restrict__
         for (int l = 0; l < n_lists; ++l) {
             int c = min(cnt(l), k_in);
             const uint64_t *s = src0 + (int64_t)l * list_stride;
-            for (int i = tid; i < c; i += MG_THREADS) {
+            for (int i = tid; i < c; i += THREADS) {
                 uint64_t x = s[i];
                 if (x >= prefix) {
                     uint32_t pos = atomicAdd(&sh.cnt, 1u);
-                    if (pos < (uint32_t)MG_LDS_KEYS) sh.keys[pos] = x;
+                    if (pos < (uint32_t)cap) lk[pos] = x;
                 }
             }
         }
@@ -334,11 +357,11 @@ merge_topk_kernel(const uint64_t *__restrict__ keys, const int32_t *__restrict__
     }
     int n2 = 64;
     while (n2 < total) n2 <<= 1;
-    for (int i = (int)total + tid; i < n2; i += MG_THREADS) sh.keys[i] = 0;
+    for (int i = (int)total + tid; i < n2; i += THREADS) lk[i] = 0;
     __syncthreads();
-    bitonic_sort_desc<MG_THREADS>(sh.keys, n2);
-    for (int i = tid; i < take; i += MG_THREADS) {
-        uint64_t x = sh.keys[i];
+    bitonic_sort_desc<THREADS>(lk, n2);
+    for (int i = tid; i < take; i += THREADS) {
+        uint64_t x = lk[i];
         if (ok) ok[i] = x;
         if (mode == DECODE_QUANT) {
             out_doc[(int64_t)q * k + i] = 0xFFFFFFFFu - (uint32_t)x;
@@ -456,20 +479,21 @@ void build_index(di_index *ix, const int64_t *term_off, int64_t n_terms, const u
 // Kernels using more than 64 KiB of dynamic LDS must opt in, once per device.
 void enable_big_lds() {
     static_assert(sizeof(ScoreShared) <= 160 * 1024, "ScoreShared exceeds LDS");
-    static_assert(sizeof(MergeShared) <= 160 * 1024, "MergeShared exceeds LDS");
     DI_HIP(hipFuncSetAttribute((const void *)score_blocks_kernel,
                                hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)sizeof(ScoreShared)));
-    DI_HIP(hipFuncSetAttribute((const void *)merge_topk_kernel,
+    DI_HIP(hipFuncSetAttribute((const void *)merge_topk_kernel<1024>,
                                hipFuncAttributeMaxDynamicSharedMemorySize,
-                               (int)sizeof(MergeShared)));
+                               (int)(sizeof(MergeHead<1024>) + MG_LDS_KEYS * 8)));
+    DI_HIP(hipFuncSetAttribute((const void *)merge_topk_kernel<256>,
+                               hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)(sizeof(MergeHead<256>) + MG_LDS_KEYS * 8)));
 }
 
 void launch_merge(const uint64_t *keys, const int32_t *counts, int n_q, int n_lists, int k_in,
                   int k, uint64_t *out_key, uint32_t *out_doc, uint32_t *out_score,
                   int32_t *out_n, int mode, hipStream_t s, bool lists_major = false) {
     if (n_q == 0) return;
-    size_t lds = sizeof(MergeShared);
     int64_t ls = k_in, cs = 1, qs = (int64_t)n_lists * k_in, cqs = n_lists;
     if (lists_major) {
         ls = (int64_t)n_q * k_in;
@@ -477,9 +501,23 @@ void launch_merge(const uint64_t *keys, const int32_t *counts, int n_q, int n_li
         qs = k_in;
         cqs = 1;
     }
-    hipLaunchKernelGGL(merge_topk_kernel, dim3(n_q), dim3(MG_THREADS), lds, s, keys, counts,
-                       n_lists, k_in, k, ls, cs, qs, cqs, out_key, out_doc, out_score, out_n,
-                       mode);
+    // LDS key capacity: all candidates when they fit, else the k survivors of the
+    // slow path's radix select
+    int64_t want = (int64_t)n_lists * k_in;
+    if (n_lists > 1024 || want > MG_LDS_KEYS) want = k;
+    int cap = 64;
+    while (cap < want) cap <<= 1;
+    if (cap <= 256) {
+        size_t lds = sizeof(MergeHead<256>) + (size_t)cap * 8;
+        hipLaunchKernelGGL(merge_topk_kernel<256>, dim3(n_q), dim3(256), lds, s, keys, counts,
+                           n_lists, k_in, k, ls, cs, qs, cqs, cap, out_key, out_doc, out_score,
+                           out_n, mode);
+    } else {
+        size_t lds = sizeof(MergeHead<1024>) + (size_t)cap * 8;
+        hipLaunchKernelGGL(merge_topk_kernel<1024>, dim3(n_q), dim3(1024), lds, s, keys,
+                           counts, n_lists, k_in, k, ls, cs, qs, cqs, cap, out_key, out_doc,
+                           out_score, out_n, mode);
+    }
     check_launch("merge_topk");
 }
 

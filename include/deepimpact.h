@@ -124,6 +124,75 @@ int di_topk_merge(const uint64_t *keys, const int32_t *counts, int32_t n_q, int3
                   int32_t k, uint64_t *out_key, int32_t *out_n, int device, void *hip_stream,
                   uint32_t flags);
 
+/* ======================================================================
+ * Encoder: DeepImpact forward + first-occurrence gather     (A2, A5-A9)
+ * ====================================================================== */
+typedef struct di_encoder di_encoder;
+
+#define DI_VARIANT_XLMR 0 /* RoBERTa / XLM-R: positions pad_id+1+i (xlmr_original.py) */
+#define DI_VARIANT_BERT 1 /* BERT / CoCondenser: absolute positions (soyuj/deeper-impact) */
+#define DI_ACT_SOFTPLUS 0 /* nn.Softplus() head (xlmr_original.py:34-38)               */
+#define DI_ACT_RELU 1     /* nn.ReLU() head (original.py:44-47)                        */
+#define DI_PREC_BF16 0    /* bf16 MFMA, f32 accumulate/softmax/LayerNorm (fast)        */
+#define DI_PREC_FP32 1    /* f32 MFMA throughout (parity with the f32 reference)       */
+#define DI_DTYPE_F32 0
+#define DI_DTYPE_BF16 1
+
+#define DI_F_ROUND3 0x10u        /* di_encode: apply round(impact, 3) (indexer.py:132)  */
+#define DI_F_TOKEN_IMPACTS 0x20u /* di_encode: write per-token impacts [n_tokens]       */
+
+typedef struct di_encoder_cfg {
+    int32_t variant, activation, precision;
+    int32_t vocab_size, hidden, layers, heads, intermediate, max_positions, type_vocab, pad_id;
+    float layer_norm_eps;
+} di_encoder_cfg;
+
+/* One checkpoint tensor: the reference's state-dict key (ModelCheckpoint layout,
+ * src/utils/checkpoint.py:72-77: "bert.embeddings...", "bert.encoder.layer.N...",
+ * "impact_score_encoder.0.weight"), host data, row-major. */
+typedef struct di_tensor {
+    const char *name;
+    const void *data;
+    int32_t dtype; /* DI_DTYPE_* */
+    int32_t ndim;
+    int64_t shape[4];
+} di_tensor;
+
+/* Replaces DeepImpact.load + .to(cuda).eval() (xlmr_original.py:191-203,
+ * indexer.py:22-24).  Strict like load_state_dict (checkpoint.py:117): a missing
+ * or unexpected key is DI_EINVAL; "embeddings.position_ids" and "pooler.*" are
+ * ignored.  Head dim must be 64; hidden <= 1024. */
+int di_encoder_create(const di_encoder_cfg *cfg, const di_tensor *weights, int32_t n_weights,
+                      int device, di_encoder **out);
+
+/* Replaces DeepImpact.forward (xlmr_original.py:41-85) + compute_term_impacts
+ * (:205-225) [+ round(.,3) of indexer.py:132 with DI_F_ROUND3] for a batch.
+ * tok_ids: the documents' token ids packed without padding, CSR by
+ * cu_seqlens[n_docs+1] (each doc = what the tokenizer emitted incl. <s>/</s>).
+ * term_tok[cu_terms[d] .. cu_terms[d+1]): token index (within doc d) of the
+ * first token of each kept term, in term order.  out[cu_terms[d] + i] = impact.
+ * With DI_F_TOKEN_IMPACTS out[n_tokens] = impact of every token (no gather).
+ * n_tokens/max_len/n_terms are required with DI_F_DEVICE_PTRS (no host read of
+ * device arrays) and recomputed from the arrays otherwise. */
+int di_encode(di_encoder *enc, const int32_t *tok_ids, const int32_t *cu_seqlens, int32_t n_docs,
+              int64_t n_tokens, int32_t max_len, const int32_t *term_tok, const int32_t *cu_terms,
+              int64_t n_terms, float *out, uint32_t flags);
+int di_encoder_reserve(di_encoder *enc, int64_t max_tokens, int32_t max_docs, int64_t max_terms);
+int di_encoder_set_stream(di_encoder *enc, void *hip_stream);
+int di_encoder_sync(di_encoder *enc);
+int di_encoder_timing(di_encoder *enc, const char *name, di_timing *out, int reset);
+int di_encoder_destroy(di_encoder *enc);
+
+/* ======================================================================
+ * 8-bit quantizer                                          (A10)
+ * ====================================================================== */
+/* Replaces quantize_file's arithmetic (src/deep_impact/indexing/quantize.py:13-47):
+ * max_val <= 0 means "compute max(0, impacts)"; scale = (2^bits-1)/max_val in
+ * fp64; out[i] = int(impacts[i] * scale) (truncation).  impacts are the values
+ * the impact TSV holds (3-decimal float32).  *max_used receives the max. */
+int di_quantize(const float *impacts, int64_t n, double max_val, int32_t bits, int32_t *out,
+                double *max_used, int device, void *hip_stream, uint32_t flags);
+
 /* Decoding of a quantized-index merge key. */
 static inline uint32_t di_key_doc(uint64_t key) { return 0xFFFFFFFFu - (uint32_t)key; }
 static inline uint32_t di_key_score(uint64_t key) { return (uint32_t)(key >> 48); }

@@ -532,8 +532,9 @@ def main():
     gen_metrics(out, out)
 
     vocab_size = local_tokenizer.build_tokenizer().get_vocab_size()
-    small = dict(vocab_size=vocab_size, hidden_size=64, num_hidden_layers=2,
-                 num_attention_heads=4, intermediate_size=128, max_position_embeddings=66,
+    # head dim 64 (the HIP attention kernel's), tiny width otherwise
+    small = dict(vocab_size=vocab_size, hidden_size=128, num_hidden_layers=2,
+                 num_attention_heads=2, intermediate_size=256, max_position_embeddings=66,
                  type_vocab_size=1, pad_token_id=1, bos_token_id=0, eos_token_id=2,
                  layer_norm_eps=1e-5, hidden_act="gelu")
     gen_encoder_xlmr(out, xlmr_mod, indexer_mod, "xlmr_small", small, max_length=64, seed=42,
@@ -544,8 +545,8 @@ def main():
                 layer_norm_eps=1e-5, hidden_act="gelu")
     gen_encoder_xlmr(out, xlmr_mod, indexer_mod, "xlmr_base", base, max_length=128, seed=7,
                      std=0.02)
-    bsmall = dict(vocab_size=300, hidden_size=64, num_hidden_layers=2, num_attention_heads=4,
-                  intermediate_size=128, max_position_embeddings=64, type_vocab_size=2,
+    bsmall = dict(vocab_size=300, hidden_size=128, num_hidden_layers=2, num_attention_heads=2,
+                  intermediate_size=256, max_position_embeddings=64, type_vocab_size=2,
                   pad_token_id=0, layer_norm_eps=1e-12, hidden_act="gelu")
     gen_encoder_bert(out, "bert_small", bsmall, seed=3)
     print("golden fixtures written to", out)
