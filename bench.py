@@ -150,6 +150,180 @@ def retrieve_leg(args, rank, world, dev):
                  out_doc, out_score, out_n)
 
 
+MFMA_BF16_PEAK_TFLOPS = 2500.0  # MI355X dense bf16 (MI355X_MICROARCH.md; no sparsity)
+
+
+def synthetic_state_dict(cfg, seed=0):
+    """Random-init weights of the named architecture (no checkpoints offline):
+    N(0, 0.02) matrices/biases, LayerNorm gamma 1 + N(0, 0.02)."""
+    rng = np.random.default_rng(seed)
+    H, F, V, P = cfg.hidden, cfg.intermediate, cfg.vocab_size, cfg.max_positions
+
+    def n(*shape):
+        return torch.from_numpy((0.02 * rng.standard_normal(shape, dtype=np.float32)))
+
+    sd = {"bert.embeddings.word_embeddings.weight": n(V, H),
+          "bert.embeddings.position_embeddings.weight": n(P, H),
+          "bert.embeddings.token_type_embeddings.weight": n(cfg.type_vocab, H),
+          "bert.embeddings.LayerNorm.weight": 1 + n(H), "bert.embeddings.LayerNorm.bias": n(H)}
+    for l in range(cfg.layers):
+        p = f"bert.encoder.layer.{l}."
+        for m in ("query", "key", "value"):
+            sd[p + f"attention.self.{m}.weight"] = n(H, H)
+            sd[p + f"attention.self.{m}.bias"] = n(H)
+        sd[p + "attention.output.dense.weight"] = n(H, H)
+        sd[p + "attention.output.dense.bias"] = n(H)
+        sd[p + "attention.output.LayerNorm.weight"] = 1 + n(H)
+        sd[p + "attention.output.LayerNorm.bias"] = n(H)
+        sd[p + "intermediate.dense.weight"] = n(F, H)
+        sd[p + "intermediate.dense.bias"] = n(F)
+        sd[p + "output.dense.weight"] = n(H, F)
+        sd[p + "output.dense.bias"] = n(H)
+        sd[p + "output.LayerNorm.weight"] = 1 + n(H)
+        sd[p + "output.LayerNorm.bias"] = n(H)
+    sd["impact_score_encoder.0.weight"] = n(1, H)
+    sd["impact_score_encoder.0.bias"] = n(1)
+    return sd
+
+
+def synthetic_docs_tokens(n_docs, vocab, seed, max_len=300):
+    """SURVEY §8d: n_i = clip(round(N(200, 60)), 8, max_len); ids uniform [5, V);
+    <s> first; words = runs of 1+Geom(0.3) tokens, unique terms ~0.7 of words."""
+    rng = np.random.default_rng(seed)
+    lens = np.clip(np.rint(rng.normal(200, 60, n_docs)), 8, max_len).astype(np.int32)
+    cu = np.zeros(n_docs + 1, np.int32)
+    cu[1:] = np.cumsum(lens)
+    ids = rng.integers(5, vocab, int(cu[-1])).astype(np.int32)
+    ids[cu[:-1]] = 0
+    term_tok, cu_terms = [], [0]
+    for n in lens:
+        starts = [1]
+        while True:
+            nxt = starts[-1] + int(rng.geometric(0.3))  # word = 1 + Geom(0.3) tokens
+            if nxt >= n - 1:
+                break
+            starts.append(nxt)
+        keep = [s for s in starts if rng.random() < 0.7]
+        term_tok += keep
+        cu_terms.append(cu_terms[-1] + len(keep))
+    return ids, cu, lens, np.array(term_tok, np.int32), np.array(cu_terms, np.int32)
+
+
+def flops_per_doc(n, H=768, L=12):
+    """sum over layers (24 n H^2 + 4 n^2 H) + 2 n H (real tokens only)."""
+    n = np.asarray(n, np.float64)
+    return L * (24.0 * n * H * H + 4.0 * n * n * H) + 2.0 * n * H
+
+
+def encode_leg(args, rank, world, dev):
+    from improving_learned_index_amd.encoder import DeviceEncoder, EncoderConfig
+
+    t0 = time.time()
+    cfg = EncoderConfig.xlmr_base()
+    sd = synthetic_state_dict(cfg, seed=0)
+    enc = DeviceEncoder(sd, cfg, precision="bf16", device=dev)
+    ids, cu, lens, tt, ct = synthetic_docs_tokens(args.docs, cfg.vocab_size, seed=100 + rank,
+                                                  max_len=args.max_len)
+    log(f"[rank {rank}] encoder ready in {time.time() - t0:.1f}s: {args.docs} docs, "
+        f"{int(cu[-1])} tokens, {int(ct[-1])} terms per step")
+    stream = torch.cuda.current_stream()
+    enc.set_stream(stream.cuda_stream)
+    d_ids = torch.from_numpy(ids).cuda()
+    d_cu = torch.from_numpy(cu).cuda()
+    d_tt = torch.from_numpy(tt).cuda()
+    d_ct = torch.from_numpy(ct).cuda()
+    out = torch.empty(max(1, int(ct[-1])), dtype=torch.float32, device="cuda")
+    enc.reserve(int(cu[-1]), args.docs, int(ct[-1]))
+    flags = _lib.DI_F_DEVICE_PTRS | _lib.DI_F_ASYNC | 0x10  # DI_F_ROUND3
+
+    def step(timing):
+        enc.encode_device(d_ids, d_cu, args.docs, int(cu[-1]), int(lens.max()), d_tt, d_ct,
+                          int(ct[-1]), out, flags | (_lib.DI_F_TIMING if timing else 0))
+
+    for _ in range(args.warmup):
+        step(False)
+    torch.cuda.synchronize()
+    enc.sync()
+    enc.timing("gemm_qkv", reset=True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    for _ in range(args.steps):
+        step(True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t1
+    enc.sync()
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    kernels = {}
+    for name in ("embed_ln", "gemm_qkv", "attention", "gemm_o", "ln", "gemm_ffn1", "gemm_ffn2",
+                 "gather_terms"):
+        ms, n = enc.timing(name)
+        kernels[name] = {"ms_per_step": ms / max(args.steps, 1), "launches": n}
+    M, H, F, L = float(cu[-1]), cfg.hidden, cfg.intermediate, cfg.layers
+    gemm_flops = {"gemm_qkv": 2 * M * H * 3 * H, "gemm_o": 2 * M * H * H,
+                  "gemm_ffn1": 2 * M * H * F, "gemm_ffn2": 2 * M * F * H}
+    per_launch = {}
+    for k, f in gemm_flops.items():
+        ms, n = enc.timing(k)
+        avg = ms / max(n, 1) / 1000.0
+        per_launch[k] = (f, avg, f / avg / 1e12 if avg > 0 else 0.0)
+    dom = max(per_launch, key=lambda k: per_launch[k][1])
+    f, avg, tf = per_launch[dom]
+    model_flops = float(flops_per_doc(lens).sum())
+    docs_per_s = world * args.docs * args.steps / el
+    res = {
+        "value": docs_per_s,
+        "ms_per_step": 1000.0 * el / args.steps,
+        "tokens_per_step": int(cu[-1]),
+        "kernels": kernels,
+        "gemm_tflops": {k: round(v[2], 1) for k, v in per_launch.items()},
+        "model_tflops": round(model_flops * args.steps / el / 1e12 * 1.0, 1),
+        "model_flops_frac": round(model_flops * args.steps / el / 1e12 / MFMA_BF16_PEAK_TFLOPS, 4),
+        "roofline": {"kernel": f"gemm_nt_kernel<bf16> ({dom})", "bound": "mfma",
+                     "achieved": round(tf, 1), "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": round(tf / MFMA_BF16_PEAK_TFLOPS, 4), "traffic": None,
+                     "algorithmic_flops_per_launch": f, "avg_launch_ms": round(avg * 1000, 4),
+                     "launches": enc.timing(dom)[1]},
+    }
+    return res, (sd, cfg, ids, cu, lens, tt, ct, out)
+
+
+def cpu_baseline_encode(args, sd, cfg, ids, cu, lens, tt, ct, out):
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import encoder_ref
+
+    c = {"hidden_size": cfg.hidden, "num_attention_heads": cfg.heads,
+         "num_hidden_layers": cfg.layers, "layer_norm_eps": cfg.layer_norm_eps,
+         "pad_token_id": cfg.pad_id}
+    threads = torch.get_num_threads()
+    done, toks, t0 = 0, 0, time.perf_counter()
+    bs = 8
+    while time.perf_counter() - t0 < args.cpu_seconds and done < len(lens):
+        b = range(done, min(done + bs, len(lens)))
+        S_ = int(max(lens[i] for i in b))
+        pad = np.full((len(b), S_), cfg.pad_id, np.int64)
+        mask = np.zeros((len(b), S_), np.int64)
+        for r, i in enumerate(b):
+            pad[r, :lens[i]] = ids[cu[i]:cu[i + 1]]
+            mask[r, :lens[i]] = 1
+        with torch.no_grad():
+            encoder_ref.forward(sd, c, torch.from_numpy(pad), torch.from_numpy(mask), "xlmr",
+                                "softplus")
+        done += len(b)
+        toks += int(sum(lens[i] for i in b))
+    el = time.perf_counter() - t0
+    return {"value": round(done / el, 3), "unit": "docs/s", "cores": threads, "kind": "port",
+            "sample": f"{done} of the step's docs ({toks} tokens, batches of {bs} padded to "
+                      f"the batch max), fp32 PyTorch-CPU restatement oracle/encoder_ref.py, "
+                      f"{el:.1f}s"}
+
+
 def cpu_baseline_retrieve(args, term_off, pdoc, pval, queries, out_doc, out_score, out_n):
     sys.path.insert(0, str(ROOT / "oracle"))
     import oracle
@@ -189,6 +363,9 @@ def main():
     ap.add_argument("--k", type=int, default=1000)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--docs", type=int, default=1024, help="docs encoded per step per GPU")
+    ap.add_argument("--max-len", type=int, default=300)
+    ap.add_argument("--legs", default="encode,retrieve")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -201,31 +378,54 @@ def main():
         torch.cuda.set_device(0)
     dev = torch.cuda.current_device()
 
-    res, ctx = retrieve_leg(args, rank, world, dev)
+    legs = set(args.legs.split(","))
+    enc_res = ret_res = None
+    if "encode" in legs:
+        enc_res, enc_ctx = encode_leg(args, rank, world, dev)
+    if "retrieve" in legs:
+        ret_res, ret_ctx = retrieve_leg(args, rank, world, dev)
+    primary = enc_res if enc_res is not None else ret_res
     out = {
-        "metric": "queries/sec@top-1000 (MS MARCO passage shape, 100k docs per GPU)",
-        "value": round(res["value"], 2),
-        "unit": "queries/s",
+        "metric": "docs/sec encoded + queries/sec@top-1000, MS MARCO passage, 1/2/4/8 MI355X",
+        "value": round(primary["value"], 2),
+        "unit": "docs/s" if enc_res is not None else "queries/s",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": round(res["ms_per_step"], 4),
+        "ms_per_step": round(primary["ms_per_step"], 4),
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "u8",
-        "data": "synthetic (BASELINE.md §2 generator, seeded); quantized 8-bit impacts",
-        "config": {"workload": "configs[1] retrieve: 100k-doc MS MARCO-shaped slice per GPU, "
-                               f"{args.queries} dev.small-shaped queries, top-{args.k}",
-                   "docs_per_gpu": DOCS_PER_SHARD, "queries": args.queries, "k": args.k,
-                   "postings_per_query": round(res["postings_per_query"], 1),
-                   "parallelism": f"doc-sharded x{world}, RCCL all-gather of top-k"},
-        "kernel_ms": res["kernel_ms"],
-        "roofline": res["roofline"],
+        "dtype": "bf16" if enc_res is not None else "u8",
+        "data": "synthetic (seeded generators of BASELINE.md §2 / SURVEY §8d); random-init "
+                "xlm-roberta-base weights",
+        "config": {"workload": "configs[1]: MS MARCO passage 100k-doc slice shape, bf16 encode "
+                               "(xlm-roberta-base DeepImpact) + top-1000 retrieve of 6980 "
+                               "dev.small-shaped queries",
+                   "docs_per_step_per_gpu": args.docs, "max_length": args.max_len,
+                   "docs_per_shard": DOCS_PER_SHARD, "queries": args.queries, "k": args.k,
+                   "parallelism": f"doc-sharded x{world} (encode: no collective; retrieve: "
+                                  f"RCCL all-gather of per-shard top-k)"},
+        "roofline": primary["roofline"],
         "cpu_baseline": None,
     }
+    if enc_res is not None:
+        out["encode"] = {k: enc_res[k] for k in ("tokens_per_step", "kernels", "gemm_tflops",
+                                                 "model_tflops", "model_flops_frac")}
+    if ret_res is not None:
+        out["retrieve"] = {"value": round(ret_res["value"], 2), "unit": "queries/s",
+                           "ms_per_step": round(ret_res["ms_per_step"], 4),
+                           "postings_per_query": round(ret_res["postings_per_query"], 1),
+                           "kernel_ms": ret_res["kernel_ms"], "roofline": ret_res["roofline"],
+                           "cpu_baseline": None}
     if rank == 0 and world == 1 and not args.no_cpu:
-        out["cpu_baseline"] = cpu_baseline_retrieve(args, *ctx)
+        if enc_res is not None:
+            out["cpu_baseline"] = cpu_baseline_encode(args, *enc_ctx)
+        if ret_res is not None:
+            cb = cpu_baseline_retrieve(args, *ret_ctx)
+            out["retrieve"]["cpu_baseline"] = cb
+            if enc_res is None:
+                out["cpu_baseline"] = cb
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

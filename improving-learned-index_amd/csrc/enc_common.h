@@ -44,6 +44,7 @@ struct GemmArgs {
     int ld_out;         // row stride of out (elements)
     int ld_v;           // EPI_QKV: row stride of V^T (tokens, padded)
     int hidden;         // EPI_QKV: H (Q | K | V split points)
+    const int32_t *vcol;  // EPI_QKV: V^T column of every token row (doc-aligned layout)
 };
 
 }  // namespace di

@@ -6,9 +6,9 @@
 // src/deep_impact/models/xlmr_original.py:70-75).
 //
 // Tile 128x128, 4 waves (2x2, 64x64 each), K step = 128 bytes of each row
-// (64 bf16 / 32 f32); LDS double buffer (2 x (16+16) KiB), register-staged
-// global loads issued one K step ahead (T14 split), 16-byte XOR-swizzled LDS
-// chunks (T2) read with ds_read_b128.
+// (64 bf16 / 32 f32); LDS double buffer (2 x (16+16) KiB) filled by LDS-DMA
+// (global_load_lds_dwordx4) one K step ahead, 16-byte XOR-swizzled chunks (T2,
+// swizzle on the source address) read with ds_read_b128.
 //   bf16: v_mfma_f32_16x16x32_bf16, f32 accumulate        (fast mode)
 //   f32 : v_mfma_f32_16x16x4_f32 (exact f32 products)       (parity mode)
 #include <hip/hip_runtime.h>
@@ -69,42 +69,30 @@ __global__ void __launch_bounds__(G_THREADS) gemm_nt_kernel(GemmArgs g) {
     const T *B = static_cast<const T *>(g.B);
     const int M = g.M, N = g.N, K = g.K;
 
-    // staging: 4 chunks of A and 4 of B per thread per K step; thread t owns
-    // chunk (row, col) = ((t + 256 i) / 8, t % 8) of each 128 x 128-byte tile
-    const int scol = tid & 7;
-    const int srow0 = tid >> 3;  // + 32 i
-    const T *Ap[4];
-    const T *Bp[4];
-    int soff[4];
+    // Staging by LDS-DMA (global_load_lds_dwordx4): each wave moves 4 x 1 KiB of
+    // A and of B per K step.  The LDS image is lane-linear (1 KiB = 8 rows of
+    // 128 B), so the XOR swizzle goes on the per-lane SOURCE chunk (rule 21):
+    // LDS slot p of row r holds global chunk p ^ (r & 7); swz() reads it back.
+    typedef __attribute__((address_space(3))) void lds_void;
+    const T *Asrc[4];
+    const T *Bsrc[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-        const int r = srow0 + 32 * i;
-        Ap[i] = A + (int64_t)min(m0 + r, M - 1) * K + scol * EPC;
-        Bp[i] = B + (int64_t)min(n0 + r, N - 1) * K + scol * EPC;
-        soff[i] = swz(r, scol);
+        const int r = (wave * 4 + i) * 8 + (lane >> 3);
+        const int c = (lane & 7) ^ (r & 7);
+        Asrc[i] = A + (int64_t)min(m0 + r, M - 1) * K + c * EPC;
+        Bsrc[i] = B + (int64_t)min(n0 + r, N - 1) * K + c * EPC;
     }
-    uint4 ra0, ra1, ra2, ra3, rb0, rb1, rb2, rb3;
-#define GLOAD(k0)                                                        \
-    do {                                                                 \
-        ra0 = *reinterpret_cast<const uint4 *>(Ap[0] + (k0));            \
-        ra1 = *reinterpret_cast<const uint4 *>(Ap[1] + (k0));            \
-        ra2 = *reinterpret_cast<const uint4 *>(Ap[2] + (k0));            \
-        ra3 = *reinterpret_cast<const uint4 *>(Ap[3] + (k0));            \
-        rb0 = *reinterpret_cast<const uint4 *>(Bp[0] + (k0));            \
-        rb1 = *reinterpret_cast<const uint4 *>(Bp[1] + (k0));            \
-        rb2 = *reinterpret_cast<const uint4 *>(Bp[2] + (k0));            \
-        rb3 = *reinterpret_cast<const uint4 *>(Bp[3] + (k0));            \
-    } while (0)
-#define LSTORE(buf)                                                      \
-    do {                                                                 \
-        *reinterpret_cast<uint4 *>(&lds[buf][0][soff[0]]) = ra0;         \
-        *reinterpret_cast<uint4 *>(&lds[buf][0][soff[1]]) = ra1;         \
-        *reinterpret_cast<uint4 *>(&lds[buf][0][soff[2]]) = ra2;         \
-        *reinterpret_cast<uint4 *>(&lds[buf][0][soff[3]]) = ra3;         \
-        *reinterpret_cast<uint4 *>(&lds[buf][1][soff[0]]) = rb0;         \
-        *reinterpret_cast<uint4 *>(&lds[buf][1][soff[1]]) = rb1;         \
-        *reinterpret_cast<uint4 *>(&lds[buf][1][soff[2]]) = rb2;         \
-        *reinterpret_cast<uint4 *>(&lds[buf][1][soff[3]]) = rb3;         \
+#define STAGE(buf, k0)                                                                   \
+    do {                                                                                 \
+        _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                  \
+            __builtin_amdgcn_global_load_lds((const void *)(Asrc[i] + (k0)),             \
+                                             (lds_void *)&lds[buf][0][(wave * 4 + i) * 1024], \
+                                             16, 0, 0);                                  \
+            __builtin_amdgcn_global_load_lds((const void *)(Bsrc[i] + (k0)),             \
+                                             (lds_void *)&lds[buf][1][(wave * 4 + i) * 1024], \
+                                             16, 0, 0);                                  \
+        }                                                                                \
     } while (0)
 
     f32x4 acc[4][4];
@@ -114,39 +102,41 @@ __global__ void __launch_bounds__(G_THREADS) gemm_nt_kernel(GemmArgs g) {
         for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
     const int nk = K / BK;
-    GLOAD(0);
-    LSTORE(0);
+    STAGE(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     for (int t = 0; t < nk; ++t) {
         const int cur = t & 1;
-        if (t + 1 < nk) GLOAD((t + 1) * BK);
+        if (t + 1 < nk) {
+            if (cur) STAGE(0, (t + 1) * BK);
+            else STAGE(1, (t + 1) * BK);
+        }
+        // all fragments of this K step first: one LDS round trip per step
+        uint4 af[2][4], bfr[2][4];
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
             const int c = 4 * s + (lane >> 4);
-            uint4 af[4], bfr[4];
 #pragma unroll
             for (int mt = 0; mt < 4; ++mt) {
                 int r = wm * 64 + mt * 16 + (lane & 15);
-                af[mt] = *reinterpret_cast<const uint4 *>(&lds[cur][0][swz(r, c)]);
+                af[s][mt] = *reinterpret_cast<const uint4 *>(&lds[cur][0][swz(r, c)]);
             }
 #pragma unroll
             for (int nt = 0; nt < 4; ++nt) {
                 int r = wn * 64 + nt * 16 + (lane & 15);
-                bfr[nt] = *reinterpret_cast<const uint4 *>(&lds[cur][1][swz(r, c)]);
+                bfr[s][nt] = *reinterpret_cast<const uint4 *>(&lds[cur][1][swz(r, c)]);
             }
+        }
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
 #pragma unroll
             for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
-                for (int nt = 0; nt < 4; ++nt) mfma_step<T>(af[mt], bfr[nt], acc[mt][nt]);
-        }
-        if (t + 1 < nk) {
-            if (cur) LSTORE(0);
-            else LSTORE(1);
-        }
+                for (int nt = 0; nt < 4; ++nt) mfma_step<T>(af[s][mt], bfr[s][nt], acc[mt][nt]);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
     }
-#undef GLOAD
-#undef LSTORE
+#undef STAGE
 
     // ---- epilogue: lane holds rows (lane>>4)*4 + j of column lane&15 ----------
 #pragma unroll
@@ -162,7 +152,8 @@ __global__ void __launch_bounds__(G_THREADS) gemm_nt_kernel(GemmArgs g) {
                     T *vt = static_cast<T *>(g.out2) + (int64_t)(col - 2 * g.hidden) * g.ld_v;
 #pragma unroll
                     for (int j = 0; j < 4; ++j)
-                        if (row0 + j < M) vt[row0 + j] = from_f32<T>(acc[mt][nt][j] + bias);
+                        if (row0 + j < M)
+                            vt[g.vcol[row0 + j]] = from_f32<T>(acc[mt][nt][j] + bias);
                     continue;
                 }
             }

@@ -34,6 +34,8 @@ void launch_embed_ln(const int32_t *ids, const int32_t *cu, int n_docs, int M, i
 template <typename T>
 void launch_ln(const float *pre, int M, int H, const float *gamma, const float *beta, float eps,
                T *out, const float *head_w, float head_b, int act, float *impact, hipStream_t s);
+void launch_vt_cols(const int32_t *cu, int n_docs, int M, int32_t *vcol, hipStream_t s);
+int vt_ld(int64_t M, int n_docs);
 void launch_gather_terms(const float *impact, const int32_t *cu_seq, const int32_t *cu_terms,
                          int n_docs, const int32_t *term_tok, int n_terms, int do_round,
                          float *out, int32_t *err, hipStream_t s);
@@ -56,8 +58,9 @@ struct di_encoder {
     float head_b = 0.f;
     std::vector<std::unique_ptr<Layer>> layers;
     // workspace
-    DevBuf X, qk, vt, ctx, pre, X1, Hff, impact, ids, cu, tt, cut, err;
+    DevBuf X, qk, vt, vcol, ctx, pre, X1, Hff, impact, ids, cu, tt, cut, err;
     int64_t cap_tokens = 0;
+    int cap_docs = 0;
     int ld_v = 0;
     Timer timer;
 };
@@ -141,8 +144,9 @@ void upload(DevBuf &dst, const std::vector<const HostTensor *> &parts, int64_t r
 
 void ensure_workspace(di_encoder *e, int64_t M, int n_docs, int64_t n_terms) {
     const int H = e->cfg.hidden, F = e->cfg.intermediate;
-    if (M > e->cap_tokens) {
-        int64_t cap = std::max<int64_t>(M, 256);
+    if (M > e->cap_tokens || n_docs > e->cap_docs) {
+        int64_t cap = std::max<int64_t>(std::max<int64_t>(M, e->cap_tokens), 256);
+        const int capd = std::max(std::max(n_docs, e->cap_docs), 16);
         const size_t es = e->esz;
         e->X.reserve(cap * H * es);
         e->X1.reserve(cap * H * es);
@@ -152,11 +156,17 @@ void ensure_workspace(di_encoder *e, int64_t M, int n_docs, int64_t n_terms) {
         e->pre.reserve(cap * H * 4);
         e->impact.reserve(cap * 4);
         e->ids.reserve(cap * 4);
-        e->ld_v = (int)(((cap + 64) + 63) / 64 * 64);
-        e->vt.reserve((size_t)H * e->ld_v * es);
-        DI_HIP(hipMemset(e->vt.p, 0, (size_t)H * e->ld_v * es));
+        e->vcol.reserve(cap * 4);
+        const size_t vt_bytes = (size_t)H * vt_ld(cap, capd) * es;
+        if (vt_bytes > e->vt.bytes) {
+            e->vt.reserve(vt_bytes);
+            // never-written gap columns between documents must read as finite zeros
+            DI_HIP(hipMemset(e->vt.p, 0, vt_bytes));
+        }
         e->cap_tokens = cap;
+        e->cap_docs = capd;
     }
+    e->ld_v = vt_ld(M, n_docs);
     e->cu.reserve((size_t)(n_docs + 1) * 4);
     e->cut.reserve((size_t)(n_docs + 1) * 4);
     e->tt.reserve((size_t)std::max<int64_t>(n_terms, 1) * 4);
@@ -177,9 +187,7 @@ void forward(di_encoder *e, const int32_t *d_ids, const int32_t *d_cu, int n_doc
                            c.layer_norm_eps, pos_offset, c.vocab_size, c.max_positions, X,
                            e->err.as<int32_t>(), s);
     }
-    // keep V^T's padding keys finite-and-zero (read, then multiplied by p = 0)
-    DI_HIP(hipMemset2DAsync(e->vt.as<unsigned char>() + M * e->esz, (size_t)e->ld_v * e->esz, 0,
-                            std::min<int64_t>(64, e->ld_v - M) * e->esz, H, s));
+    launch_vt_cols(d_cu, n_docs, (int)M, e->vcol.as<int32_t>(), s);
     for (size_t l = 0; l < e->layers.size(); ++l) {
         Layer &L = *e->layers[l];
         const bool last = l + 1 == e->layers.size();
@@ -196,6 +204,7 @@ void forward(di_encoder *e, const int32_t *d_ids, const int32_t *d_cu, int n_doc
         g.K = H;
         g.ld_out = 2 * H;
         g.ld_v = e->ld_v;
+        g.vcol = e->vcol.as<int32_t>();
         {
             TimedLaunch tl(e->timer, timing, "gemm_qkv", s);
             launch_gemm<T>(EPI_QKV, g, s);
