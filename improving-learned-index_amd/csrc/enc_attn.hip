@@ -61,14 +61,22 @@ __device__ __forceinline__ void mma_chunk(const uint4 &a, const uint4 &b, f32x4 
 template <typename T>
 __global__ void __launch_bounds__(64)
 attention_kernel(const T *__restrict__ qk, const T *__restrict__ vt,
-                 const int32_t *__restrict__ cu_seqlens, int H, int ld_v, T *__restrict__ ctx) {
+                 const int32_t *__restrict__ cu_seqlens, int H, int ld_v, int n_qb, int n_heads,
+                 int n_pairs, T *__restrict__ ctx) {
     constexpr int KC = AttnOps<T>::KC, EPC = AttnOps<T>::EPC;
     constexpr int NCH = ATT_D / KC;  // k chunks over the head dim
-    const int doc = blockIdx.y, h = blockIdx.z;
+    // 1-D grid, XCD-grouped (speed only): the QB query blocks of one (doc, head)
+    // are ids j*8 + x for j in one run of QB -- all on XCD x under round-robin
+    // dispatch -- so they share K / V^T through that XCD's L2.
+    const int id = blockIdx.x, x = id & 7, j = id >> 3;
+    const int pair = (j / n_qb) * 8 + x;  // (doc, head) pair index
+    const int qb = j % n_qb;
+    if (pair >= n_pairs) return;
+    const int doc = pair / n_heads, h = pair % n_heads;
     const int lane = threadIdx.x;
     const int g = lane >> 4, c = lane & 15;
     const int tok0 = cu_seqlens[doc], n = cu_seqlens[doc + 1] - tok0;
-    const int q_base = blockIdx.x * (16 * QT);
+    const int q_base = qb * (16 * QT);
     if (q_base >= n) return;
     const int ldqk = 2 * H;
 
@@ -253,9 +261,12 @@ void launch_attention(const T *qk, const T *vt, const int32_t *cu_seqlens, int n
                       int max_len, int H, int ld_v, T *ctx, hipStream_t s) {
     DI_REQUIRE(H % ATT_D == 0, DI_EINVAL, "hidden %d is not a multiple of the head dim 64", H);
     if (n_docs == 0 || max_len == 0) return;
-    dim3 grid((max_len + 16 * QT - 1) / (16 * QT), n_docs, H / ATT_D);
-    hipLaunchKernelGGL(attention_kernel<T>, grid, dim3(64), 0, s, qk, vt, cu_seqlens, H, ld_v,
-                       ctx);
+    const int n_qb = (max_len + 16 * QT - 1) / (16 * QT), n_heads = H / ATT_D;
+    const int n_pairs = n_docs * n_heads;
+    const int64_t blocks = (int64_t)((n_pairs + 7) / 8) * 8 * n_qb;
+    DI_REQUIRE(blocks < (1ll << 31), DI_ERANGE, "attention grid too large");
+    hipLaunchKernelGGL(attention_kernel<T>, dim3((unsigned)blocks), dim3(64), 0, s, qk, vt,
+                       cu_seqlens, H, ld_v, n_qb, n_heads, n_pairs, ctx);
     check_launch("attention");
 }
 

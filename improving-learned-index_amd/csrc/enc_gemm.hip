@@ -13,6 +13,8 @@
 //   f32 : v_mfma_f32_16x16x4_f32 (exact f32 products)       (parity mode)
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "di_common.h"
 #include "enc_common.h"
 
@@ -56,15 +58,25 @@ __global__ void __launch_bounds__(G_THREADS) gemm_nt_kernel(GemmArgs g) {
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm = wave >> 1, wn = wave & 1;
-    // XCD-aware tile order: consecutive tile ids share an XCD's L2 when the
-    // dispatcher deals blocks round-robin over the 8 XCDs (speed only).
-    const int n_tn = gridDim.x, n_tiles = gridDim.x * gridDim.y;
+    // Tile order (speed only, never correctness):
+    //  (1) XCD remap (T1): the dispatcher deals blocks round-robin over the 8
+    //      XCDs, so block b runs on XCD b % 8; each XCD gets a contiguous range of
+    //      tile ids (bijective form of cdna_hip_programming.md §5).
+    //  (2) grouped order inside that range: GM M-tiles x all N-tiles, M fastest,
+    //      so the ~64 blocks an XCD runs at once touch ~8 A panels and ~8 B panels
+    //      (~3 MiB) -- they stay in the XCD's 4 MiB L2 instead of re-streaming
+    //      the whole weight matrix for every M tile.
+    const int n_tn = gridDim.x, n_tm = gridDim.y, n_tiles = n_tn * n_tm;
     int bid = blockIdx.y * gridDim.x + blockIdx.x;
     {
         const int q = n_tiles / 8, r = n_tiles % 8, x = bid % 8;
         bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
     }
-    const int m0 = (bid / n_tn) * GB_M, n0 = (bid % n_tn) * GB_N;
+    constexpr int GM = 8;
+    const int grp = bid / (GM * n_tn), first_m = grp * GM;
+    const int gsz = min(GM, n_tm - first_m);
+    const int in = bid % (GM * n_tn);
+    const int m0 = (first_m + in % gsz) * GB_M, n0 = (in / gsz) * GB_N;
     const T *A = static_cast<const T *>(g.A);
     const T *B = static_cast<const T *>(g.B);
     const int M = g.M, N = g.N, K = g.K;
@@ -138,41 +150,100 @@ __global__ void __launch_bounds__(G_THREADS) gemm_nt_kernel(GemmArgs g) {
     }
 #undef STAGE
 
-    // ---- epilogue: lane holds rows (lane>>4)*4 + j of column lane&15 ----------
+    // ---- epilogue -----------------------------------------------------------
+    // V part of the QKV projection: transposed element stores into V^T
+    if constexpr (EPI == EPI_QKV) {
+        if (n0 >= 2 * g.hidden) {  // a 128-column tile never straddles 2H (H % 64 == 0)
 #pragma unroll
-    for (int nt = 0; nt < 4; ++nt) {
-        const int col = n0 + wn * 64 + nt * 16 + (lane & 15);
-        if (col >= N) continue;
-        const float bias = g.bias ? g.bias[col] : 0.f;
+            for (int nt = 0; nt < 4; ++nt) {
+                const int col = n0 + wn * 64 + nt * 16 + (lane & 15);
+                if (col >= N) continue;
+                const float bias = g.bias[col];
+                T *vt = static_cast<T *>(g.out2) + (int64_t)(col - 2 * g.hidden) * g.ld_v;
 #pragma unroll
-        for (int mt = 0; mt < 4; ++mt) {
-            const int row0 = m0 + wm * 64 + mt * 16 + (lane >> 4) * 4;
-            if constexpr (EPI == EPI_QKV) {
-                if (col >= 2 * g.hidden) {
-                    T *vt = static_cast<T *>(g.out2) + (int64_t)(col - 2 * g.hidden) * g.ld_v;
+                for (int mt = 0; mt < 4; ++mt) {
+                    const int row0 = m0 + wm * 64 + mt * 16 + (lane >> 4) * 4;
 #pragma unroll
                     for (int j = 0; j < 4; ++j)
                         if (row0 + j < M)
                             vt[g.vcol[row0 + j]] = from_f32<T>(acc[mt][nt][j] + bias);
-                    continue;
                 }
             }
+            return;
+        }
+    }
+    // Everything else goes through LDS (the staging buffers are free now), 64
+    // rows per pass, so that global stores are whole 16-byte chunks of rows.
+    // bias / GELU are applied in registers; the residual is added on the way out.
+    using OutT = typename std::conditional<EPI == EPI_BIAS_RESID, float, T>::type;
+    constexpr int OE = sizeof(OutT);
+    constexpr int RS = GB_N * OE + 16;       // padded LDS row stride (bytes)
+    constexpr int CPR = GB_N * OE / 16;      // 16-byte chunks per row
+    unsigned char *ot = &lds[0][0][0];
+    float bias_v[4];
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int row = row0 + j;
-                if (row >= M) break;
-                float v = acc[mt][nt][j] + bias;
-                if constexpr (EPI == EPI_BIAS || EPI == EPI_QKV) {
-                    static_cast<T *>(g.out)[(int64_t)row * g.ld_out + col] = from_f32<T>(v);
-                } else if constexpr (EPI == EPI_BIAS_GELU) {
-                    static_cast<T *>(g.out)[(int64_t)row * g.ld_out + col] =
-                        from_f32<T>(gelu_erf(v));
-                } else {  // EPI_BIAS_RESID
-                    v += to_f32(static_cast<const T *>(g.resid)[(int64_t)row * N + col]);
-                    static_cast<float *>(g.out)[(int64_t)row * g.ld_out + col] = v;
+    for (int nt = 0; nt < 4; ++nt) {
+        const int col = n0 + wn * 64 + nt * 16 + (lane & 15);
+        bias_v[nt] = (g.bias && col < N) ? g.bias[col] : 0.f;
+    }
+#pragma unroll
+    for (int pass = 0; pass < 2; ++pass) {
+        if (wm == pass) {
+#pragma unroll
+            for (int nt = 0; nt < 4; ++nt) {
+                const int lc = wn * 64 + nt * 16 + (lane & 15);
+#pragma unroll
+                for (int mt = 0; mt < 4; ++mt) {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const int lr = mt * 16 + (lane >> 4) * 4 + j;  // row within the pass
+                        float v = acc[mt][nt][j] + bias_v[nt];
+                        if constexpr (EPI == EPI_BIAS_GELU) v = gelu_erf(v);
+                        *reinterpret_cast<OutT *>(ot + lr * RS + lc * OE) = from_f32<OutT>(v);
+                    }
                 }
             }
         }
+        __syncthreads();
+        const int row_base = m0 + pass * 64;
+#pragma unroll
+        for (int i = 0; i < 64 * CPR / G_THREADS; ++i) {
+            const int id = tid + i * G_THREADS;
+            const int lr = id / CPR, ch = id % CPR;
+            const int row = row_base + lr;
+            const int col0 = n0 + ch * (16 / OE);
+            if (row >= M) continue;
+            uint4 v = *reinterpret_cast<const uint4 *>(ot + lr * RS + ch * 16);
+            if (col0 + 16 / OE <= N) {
+                if constexpr (EPI == EPI_BIAS_RESID) {
+                    // 4 f32 outputs + 4 residual values of T
+                    const T *rp = static_cast<const T *>(g.resid) + (int64_t)row * N + col0;
+                    float r0, r1, r2, r3;
+                    if constexpr (sizeof(T) == 2) {
+                        bf16x4 rv = *reinterpret_cast<const bf16x4 *>(rp);
+                        r0 = (float)rv[0]; r1 = (float)rv[1]; r2 = (float)rv[2]; r3 = (float)rv[3];
+                    } else {
+                        float4 rv = *reinterpret_cast<const float4 *>(rp);
+                        r0 = rv.x; r1 = rv.y; r2 = rv.z; r3 = rv.w;
+                    }
+                    v.x = __float_as_uint(__uint_as_float(v.x) + r0);
+                    v.y = __float_as_uint(__uint_as_float(v.y) + r1);
+                    v.z = __float_as_uint(__uint_as_float(v.z) + r2);
+                    v.w = __float_as_uint(__uint_as_float(v.w) + r3);
+                }
+                *reinterpret_cast<uint4 *>(static_cast<OutT *>(g.out) + (int64_t)row * g.ld_out +
+                                           col0) = v;
+            } else {  // ragged N tail: element stores
+                const OutT *e = reinterpret_cast<const OutT *>(&v);
+                for (int q = 0; q < 16 / OE && col0 + q < N; ++q) {
+                    OutT x = e[q];
+                    if constexpr (EPI == EPI_BIAS_RESID)
+                        x += to_f32(static_cast<const T *>(g.resid)[(int64_t)row * N + col0 + q]);
+                    static_cast<OutT *>(g.out)[(int64_t)row * g.ld_out + col0 + q] = x;
+                }
+            }
+        }
+        __syncthreads();
     }
 }
 

@@ -25,6 +25,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <fstream>
 #include <memory>
@@ -79,7 +80,7 @@ score_blocks_kernel(const uint32_t *__restrict__ post, const int64_t *__restrict
                     const uint32_t *__restrict__ blk_off, int nb, int64_t n_terms,
                     uint32_t n_docs, uint32_t doc_lo, const uint32_t *__restrict__ q_terms,
                     const int32_t *__restrict__ cu_q, int k, uint64_t *__restrict__ cand_key,
-                    int32_t *__restrict__ cand_n) {
+                    int32_t *__restrict__ cand_n, int ablate) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     ScoreShared &sh = *reinterpret_cast<ScoreShared *>(smem);
 
@@ -126,7 +127,7 @@ score_blocks_kernel(const uint32_t *__restrict__ post, const int64_t *__restrict
     // dwords (coalesced: lane-consecutive).  The next round's loads are issued
     // before the current round is applied, also across a term boundary, so each
     // term's barrier no longer exposes a memory round trip.
-    constexpr int U = 4;
+    constexpr int U = 16;  // 64 B of postings in flight per lane, plus the next round
     constexpr int ROUND = SC_THREADS * U;
     auto rounds = [&](int jj) { return (int)((sh.hi[jj] - sh.lo[jj] + ROUND - 1) / ROUND); };
     auto load_round = [&](int jj, int rr, uint32_t (&r)[U]) {
@@ -137,7 +138,7 @@ score_blocks_kernel(const uint32_t *__restrict__ post, const int64_t *__restrict
             r[u] = (i < hi) ? post[i] : 0u;
         }
     };
-    int j = 0, rr = 0;
+    int j = (ablate & 1) ? nt : 0, rr = 0;  // ablate bit 0: skip the scatter (profiling)
     while (j < nt && rounds(j) == 0) ++j;
     uint32_t cur[U], nxt[U];
     if (j < nt) load_round(j, rr, cur);
@@ -169,6 +170,10 @@ score_blocks_kernel(const uint32_t *__restrict__ post, const int64_t *__restrict
     }
     __syncthreads();
 
+    if (ablate & 2) {  // profiling: skip the selection
+        if (tid == 0) cand_n[(int64_t)q * nb + b] = 0;
+        return;
+    }
     // ---- block top-k: radix select on the 32-bit words ---------------------
     auto id_key = [](uint32_t w, int) { return w; };
     uint32_t need = (uint32_t)k, prefix = 0, mask = 0;
@@ -390,6 +395,7 @@ struct di_index {
     int nb = 0;
     DevBuf post, term_start, blk_off;
     DevBuf ws_q, ws_cu, ws_ck, ws_cn, ws_doc, ws_score, ws_n, ws_key;
+    int ablate = 0;  // DI_PROFILE_ABLATE (profiling builds of the bench only)
     Timer timer;
 };
 
@@ -541,6 +547,7 @@ int di_index_create(const int64_t *term_off, int64_t n_terms, const uint32_t *pd
         DI_HIP(hipStreamCreateWithFlags(&ix->stream, hipStreamNonBlocking));
         ix->own_stream = true;
         enable_big_lds();
+        if (const char *ab = std::getenv("DI_PROFILE_ABLATE")) ix->ablate = std::atoi(ab);
         build_index(ix.get(), term_off, n_terms, pdoc, pval, doc_lo, doc_hi);
         *out = ix.release();
     });
@@ -661,7 +668,8 @@ int di_index_search(di_index *ix, const uint32_t *q_terms, const int32_t *cu_q, 
                                    sizeof(ScoreShared), s, ix->post.as<uint32_t>(),
                                    ix->term_start.as<int64_t>(), ix->blk_off.as<uint32_t>(), nb,
                                    ix->n_terms, ix->n_docs, ix->doc_lo, dq, dcu + q0, k,
-                                   ix->ws_ck.as<uint64_t>(), ix->ws_cn.as<int32_t>());
+                                   ix->ws_ck.as<uint64_t>(), ix->ws_cn.as<int32_t>(),
+                                   ix->ablate);
                 check_launch("score_blocks");
             }
             {
