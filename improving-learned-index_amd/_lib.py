@@ -64,6 +64,9 @@ SIGNATURES = {
     "di_encoder_timing": (ctypes.c_int, [P, ctypes.c_char_p, P, ctypes.c_int]),
     "di_encoder_destroy": (ctypes.c_int, [P]),
     "di_quantize": (ctypes.c_int, [P, I64, ctypes.c_double, I32, P, P, ctypes.c_int, P, U32]),
+    "di_quantize_file": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_double, I32,
+                                        ctypes.c_int, P]),
+    "di_format_impact_lines": (ctypes.c_int, [P, P, P, P, I32, P, I64, P]),
 }
 
 _LIB = None
@@ -240,3 +243,27 @@ def key_doc(keys):
 
 def key_score(keys):
     return (keys >> np.uint64(48)).astype(np.uint32)
+
+
+def format_impact_lines(doc_terms, doc_impacts):
+    """Native A9 formatter: list (per doc) of term lists + float32 impact arrays
+    (already rounded) -> the impact-TSV text of those docs (one line each)."""
+    n_docs = len(doc_terms)
+    enc = [t.encode("utf-8") for terms in doc_terms for t in terms]
+    blob = b"".join(enc)
+    term_off = np.zeros(len(enc) + 1, np.int64)
+    if enc:
+        term_off[1:] = np.cumsum([len(b) for b in enc])
+    cu = np.zeros(n_docs + 1, np.int64)
+    cu[1:] = np.cumsum([len(t) for t in doc_terms])
+    imp = np.ascontiguousarray(np.concatenate([np.asarray(x, np.float32) for x in doc_impacts])
+                               if n_docs else np.zeros(0, np.float32), np.float32)
+    if imp.size == 0:
+        imp = np.zeros(1, np.float32)
+    cap = len(blob) + 30 * (len(enc) + 1) + n_docs + 16
+    out = ctypes.create_string_buffer(cap)
+    n = ctypes.c_int64(0)
+    tb = ctypes.create_string_buffer(blob, len(blob) + 1)
+    check(lib().di_format_impact_lines(tb, ptr(term_off), ptr(imp), ptr(cu), n_docs, out, cap,
+                                       ctypes.byref(n)))
+    return out.raw[:n.value].decode("utf-8")

@@ -255,6 +255,46 @@ __global__ void quantize_kernel(const float *__restrict__ v, int64_t n,
 }  // namespace di
 
 namespace di {
+// f64 inputs (values parsed from impact-TSV text, quantize_file)
+__global__ void max_f64_kernel(const double *__restrict__ v, int64_t n,
+                               unsigned long long *__restrict__ out_bits) {
+    double m = 0.0;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x)
+        m = fmax(m, v[i]);
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) m = fmax(m, __shfl_xor(m, d, 64));
+    if ((threadIdx.x & 63) == 0)
+        atomicMax(out_bits, m > 0.0 ? (unsigned long long)__double_as_longlong(m) : 0ull);
+}
+
+__global__ void quantize_f64_kernel(const double *__restrict__ v, int64_t n,
+                                    const unsigned long long *__restrict__ max_bits,
+                                    double max_given, int bits, int32_t *__restrict__ out) {
+    const double m = max_given > 0.0 ? max_given : __longlong_as_double((long long)*max_bits);
+    const double scale = (double)((1 << bits) - 1) / m;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        double p = __dmul_rn(v[i], scale);
+        p = fmin(fmax(p, -2147483648.0), 2147483647.0);
+        out[i] = (int32_t)p;
+    }
+}
+
+void launch_quantize_f64(const double *v, int64_t n, double max_given, int bits, int32_t *out,
+                         unsigned long long *max_bits, hipStream_t s) {
+    DI_HIP(hipMemsetAsync(max_bits, 0, sizeof(unsigned long long), s));
+    if (n == 0) return;
+    int blocks = (int)std::min<int64_t>(2048, (n + 255) / 256);
+    if (!(max_given > 0.0)) {
+        hipLaunchKernelGGL(max_f64_kernel, dim3(blocks), dim3(256), 0, s, v, n, max_bits);
+        check_launch("max_f64");
+    }
+    hipLaunchKernelGGL(quantize_f64_kernel, dim3(blocks), dim3(256), 0, s, v, n, max_bits,
+                       max_given, bits, out);
+    check_launch("quantize_f64");
+}
+
 void launch_quantize(const float *v, int64_t n, double max_given, int bits, int32_t *out,
                      unsigned int *max_bits, hipStream_t s) {
     DI_HIP(hipMemsetAsync(max_bits, 0, sizeof(unsigned int), s));

@@ -1,0 +1,143 @@
+// text_format.cpp -- native writers/readers of the reference's text formats.
+//
+//  * impact TSV lines (reference src/deep_impact/indexing/indexer.py:62-68):
+//      ', '.join(f'{term}: {round(impact, 3)}') + '\n'  -- the number is the
+//      repr of the double value of the rounded float32 (pytext.h repr_double).
+//  * quantize_file (src/deep_impact/indexing/quantize.py:17-47): parse
+//      'term: score' pairs, quantize on the GPU (di_quantize_f64 semantics),
+//      keep values > 0, write 'term: val' lines.
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <string>
+#include <string_view>
+#include <vector>
+
+#include "di_common.h"
+#include "pytext.h"
+
+namespace di {
+void launch_quantize_f64(const double *v, int64_t n, double max_given, int bits, int32_t *out,
+                         unsigned long long *max_bits, hipStream_t s);
+}
+
+using namespace di;
+
+extern "C" int di_format_impact_lines(const char *terms, const int64_t *term_off,
+                                      const float *impacts, const int64_t *cu_doc_terms,
+                                      int32_t n_docs, char *out, int64_t out_cap,
+                                      int64_t *out_len) {
+    return guard([&] {
+        DI_REQUIRE(term_off && cu_doc_terms && out_len && n_docs >= 0, DI_EINVAL,
+                   "null argument");
+        std::string buf;
+        const int64_t nt = cu_doc_terms[n_docs];
+        buf.reserve((size_t)(term_off[nt] - term_off[0]) + (size_t)nt * 24 + (size_t)n_docs);
+        for (int32_t d = 0; d < n_docs; ++d) {
+            for (int64_t i = cu_doc_terms[d]; i < cu_doc_terms[d + 1]; ++i) {
+                if (i > cu_doc_terms[d]) buf += ", ";
+                buf.append(terms + term_off[i], (size_t)(term_off[i + 1] - term_off[i]));
+                buf += ": ";
+                py::repr_double((double)impacts[i], buf);
+            }
+            buf += '\n';
+        }
+        *out_len = (int64_t)buf.size();
+        DI_REQUIRE(out && (int64_t)buf.size() <= out_cap, DI_ERANGE,
+                   "output buffer too small: %lld bytes needed", (long long)buf.size());
+        std::memcpy(out, buf.data(), buf.size());
+    });
+}
+
+namespace {
+
+std::string read_all(const char *path) {
+    std::ifstream f(path, std::ios::binary | std::ios::ate);
+    DI_REQUIRE(f, DI_EIO, "cannot open %s", path);
+    std::string s((size_t)f.tellg(), '\0');
+    f.seekg(0);
+    f.read(s.data(), (std::streamsize)s.size());
+    return s;
+}
+
+}  // namespace
+
+// quantize_file: two passes of the reference become parse-once + one GPU kernel.
+extern "C" int di_quantize_file(const char *input_path, const char *output_path, double max_val,
+                                int32_t bits, int device, double *max_used) {
+    return guard([&] {
+        DI_REQUIRE(input_path && output_path, DI_EINVAL, "null argument");
+        std::string buf = read_all(input_path);
+        std::vector<std::string_view> terms;
+        std::vector<double> vals;
+        std::vector<int64_t> cu{0};
+        std::vector<std::string_view> pieces, tv;
+        int64_t line_no = 0;
+        // for doc_id, line in enumerate(f): for t in line.strip().split(', '):
+        //     term, score = t.strip().split(': ')         (quantize.py:21-22, :41-42)
+        py::for_each_line(buf, [&](std::string_view line) {
+            ++line_no;
+            py::split(py::strip(line), ", ", pieces);
+            for (auto t : pieces) {
+                py::split(py::strip(t), ": ", tv);
+                DI_REQUIRE(tv.size() == 2, DI_EFORMAT,
+                           "line %lld: '%.*s' is not 'term: score' (the reference raises "
+                           "ValueError)",
+                           (long long)line_no, (int)std::min<size_t>(t.size(), 200), t.data());
+                double v;
+                DI_REQUIRE(py::parse_float(tv[1], &v), DI_EFORMAT,
+                           "line %lld: could not convert '%.*s' to float", (long long)line_no,
+                           (int)std::min<size_t>(tv[1].size(), 64), tv[1].data());
+                terms.push_back(tv[0]);
+                vals.push_back(v);
+            }
+            cu.push_back((int64_t)terms.size());
+        });
+        const int64_t n = (int64_t)vals.size();
+        int prev = 0;
+        DI_HIP(hipGetDevice(&prev));
+        DI_HIP(hipSetDevice(device));
+        DevBuf dv, dq, dm;
+        dv.reserve((size_t)std::max<int64_t>(n, 1) * 8);
+        dq.reserve((size_t)std::max<int64_t>(n, 1) * 4);
+        dm.reserve(16);
+        if (n) DI_HIP(hipMemcpy(dv.p, vals.data(), (size_t)n * 8, hipMemcpyHostToDevice));
+        launch_quantize_f64(dv.as<double>(), n, max_val, bits, dq.as<int32_t>(),
+                            dm.as<unsigned long long>(), nullptr);
+        std::vector<int32_t> q((size_t)n);
+        unsigned long long mb = 0;
+        if (n) DI_HIP(hipMemcpy(q.data(), dq.p, (size_t)n * 4, hipMemcpyDeviceToHost));
+        DI_HIP(hipMemcpy(&mb, dm.p, 8, hipMemcpyDeviceToHost));
+        (void)hipSetDevice(prev);
+        double m;
+        std::memcpy(&m, &mb, 8);
+        if (!(max_val > 0.0)) {
+            DI_REQUIRE(m > 0.0, DI_EINVAL,
+                       "max impact is 0: the reference divides by zero (quantize.py:37)");
+            max_val = m;
+        }
+        if (max_used) *max_used = max_val;
+        std::string out;
+        out.reserve(buf.size());
+        char num[32];
+        for (size_t d = 0; d + 1 < cu.size(); ++d) {
+            bool first = true;
+            for (int64_t i = cu[d]; i < cu[d + 1]; ++i) {
+                if (q[(size_t)i] <= 0) continue;  // quantize.py:44
+                if (!first) out += ", ";
+                first = false;
+                out.append(terms[(size_t)i].data(), terms[(size_t)i].size());
+                out += ": ";
+                int len = std::snprintf(num, sizeof num, "%d", q[(size_t)i]);
+                out.append(num, (size_t)len);
+            }
+            out += '\n';
+        }
+        FILE *f = std::fopen(output_path, "wb");
+        DI_REQUIRE(f, DI_EIO, "cannot create %s", output_path);
+        size_t w = out.empty() ? 0 : std::fwrite(out.data(), 1, out.size(), f);
+        int rc = std::fclose(f);
+        DI_REQUIRE(w == out.size() && rc == 0, DI_EIO, "short write to %s", output_path);
+    });
+}

@@ -1,0 +1,87 @@
+"""CLI: create a DeepImpact impact TSV (drop-in for `python -m src.deep_impact.index`,
+reference src/deep_impact/index.py:12-68).
+
+    python -m improving_learned_index_amd.index --collection_path c.tsv \\
+        --output_file_path collection.index --model_checkpoint_path ckpt.pt \\
+        --tokenizer_path xlm-roberta-base/tokenizer.json [--max_length 300]
+
+Same flags as the reference plus --tokenizer_path / --max_length / --precision /
+--device / --variant (the reference hard-wires a hub tokenizer and 512 tokens).
+Output bytes are those of the reference (one line per input line, in order).
+Multi-GPU: --doc_range start:end encodes one doc-id shard; concatenating the
+shard outputs in order gives the single-GPU file.
+"""
+from __future__ import annotations
+
+import argparse
+import logging
+import time
+from pathlib import Path
+
+from .datasets import COLLECTION_TYPES, CollectionParser
+from .indexer import Indexer
+from .models import DeepImpact
+
+BATCH_SIZE = 32  # src/utils/defaults.py:15
+
+logger = logging.getLogger("index")
+
+
+def run(collection_path, collection_type, output_file_path, model_checkpoint_path,
+        num_processes=8, process_batch_size=50 * BATCH_SIZE, model_batch_size=BATCH_SIZE,
+        tokenizer_path=None, max_length=None, precision="bf16", device=0, variant="xlmr",
+        doc_range=None, pairwise=False):
+    if pairwise:
+        raise NotImplementedError("DeepPairwiseImpact is outside this build (SURVEY §8f F4)")
+    start = time.time()
+    model = DeepImpact.load(model_checkpoint_path, tokenizer_path=tokenizer_path,
+                            precision=precision, device=device, variant=variant,
+                            max_length=max_length)
+    indexer = Indexer(model, model_batch_size=model_batch_size, num_processes=num_processes)
+    lo, hi = (0, None) if doc_range is None else doc_range
+    with open(collection_path) as f, open(output_file_path, "w") as out:
+        batch = []
+        n = 0
+        for i, passage in enumerate(f, start=1):
+            if hi is not None and i - 1 >= hi:
+                break
+            if i - 1 < lo:
+                continue
+            if i % process_batch_size == 0:  # index.py:35 (first batch one short)
+                indexer.index(batch, out)
+                logger.info(f"Indexed {i} passages [Rate: {i / (time.time() - start):.2f} "
+                            f"passages/s]")
+                batch = []
+            doc_id, passage = CollectionParser.parse(passage, collection_type)
+            batch.append(passage)
+            n += 1
+        indexer.index(batch, out)
+    return n
+
+
+def main(argv=None):
+    p = argparse.ArgumentParser("Create a DeepImpact index by computing impacts of all document terms.")
+    p.add_argument("--collection_path", type=Path, required=True)
+    p.add_argument("--collection_type", type=str, default="msmarco", choices=COLLECTION_TYPES)
+    p.add_argument("--output_file_path", type=Path, required=True)
+    p.add_argument("--model_checkpoint_path", type=str, required=True)
+    p.add_argument("--num_processes", type=int, default=8)
+    p.add_argument("--process_batch_size", type=int, default=50 * BATCH_SIZE)
+    p.add_argument("--model_batch_size", type=int, default=BATCH_SIZE)
+    p.add_argument("--pairwise", action="store_true")
+    p.add_argument("--tokenizer_path", type=str, default=None)
+    p.add_argument("--max_length", type=int, default=None)
+    p.add_argument("--precision", choices=["bf16", "fp32"], default="bf16")
+    p.add_argument("--device", type=int, default=0)
+    p.add_argument("--variant", choices=["xlmr", "bert"], default="xlmr")
+    p.add_argument("--doc_range", type=str, default=None, help="start:end line range (shard)")
+    a = p.parse_args(argv)
+    dr = tuple(int(x) for x in a.doc_range.split(":")) if a.doc_range else None
+    logging.basicConfig(level=logging.INFO)
+    run(a.collection_path, a.collection_type, a.output_file_path, a.model_checkpoint_path,
+        a.num_processes, a.process_batch_size, a.model_batch_size, a.tokenizer_path,
+        a.max_length, a.precision, a.device, a.variant, dr, a.pairwise)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,70 @@
+"""Query driver over the on-disk index (reference src/deep_impact/evaluation/ranker.py
+and src/deep_impact/rank.py).
+
+The reference scores one query per Pool task (pickling the whole index each
+time, ranker.py:44-46); here every query of the file is scored by one batched
+GPU launch sequence (di_index_search).  The run file holds the same lines; the
+reference writes queries in imap_unordered completion order, this writes them
+in input order (a valid completion order of the reference).
+"""
+from __future__ import annotations
+
+import argparse
+from pathlib import Path
+from typing import Optional, Union
+
+from .datasets import COLLECTION_TYPES, Queries, QueryRelevanceDataset, RunFile
+from .inverted_index import InvertedIndex
+from .models import DeepImpact
+
+
+class Ranker:
+    def __init__(self, index_path: Union[str, Path], queries_path: Union[str, Path],
+                 output_path: Union[str, Path], num_workers: int = 4,
+                 qrels_path: Optional[Union[str, Path]] = None, pairwise: bool = False,
+                 dataset_type: Optional[str] = COLLECTION_TYPES[0], tokenizer_path=None,
+                 device: int = 0, top_k: int = 1000, batch_queries: int = 8192):
+        if pairwise:
+            raise NotImplementedError("pairwise terms are outside this build (SURVEY §8f F4)")
+        if tokenizer_path is not None:
+            DeepImpact.set_tokenizer(tokenizer_path)
+        self.queries = Queries(queries_path=queries_path, dataset_type=dataset_type)
+        self.query_iterator = list(self.queries.keys())
+        if qrels_path is not None:  # ranker.py:34-35
+            self.query_iterator = list(QueryRelevanceDataset(qrels_path=qrels_path).keys())
+        self.index = InvertedIndex(index_path=index_path, device=device)
+        self.run_file = RunFile(run_file_path=output_path)
+        self.top_k = top_k
+        self.batch_queries = batch_queries
+
+    def get_query_terms(self, qid):
+        return DeepImpact.process_query(query=self.queries[qid])
+
+    def run(self):
+        qids = self.query_iterator
+        for s in range(0, len(qids), self.batch_queries):
+            chunk = qids[s:s + self.batch_queries]
+            results = self.index.score_batch([self.get_query_terms(q) for q in chunk],
+                                             self.top_k)
+            for qid, scores in zip(chunk, results):
+                self.run_file.writelines(qid, scores)
+
+
+def main(argv=None):
+    p = argparse.ArgumentParser("Evaluate a DeepImpact by ranking qrels docs & computing evaluation metrics.")
+    p.add_argument("--index_path", type=Path, required=True)
+    p.add_argument("--queries_path", type=Path, required=True)
+    p.add_argument("--output_path", type=Path, required=True)
+    p.add_argument("--num_workers", type=int, default=4)
+    p.add_argument("--qrels_path", type=Path, default=None)
+    p.add_argument("--dataset_type", type=str, default=COLLECTION_TYPES[0], choices=COLLECTION_TYPES)
+    p.add_argument("--pairwise", action="store_true")
+    p.add_argument("--tokenizer_path", type=str, required=True)
+    p.add_argument("--device", type=int, default=0)
+    a = p.parse_args(argv)
+    Ranker(a.index_path, a.queries_path, a.output_path, a.num_workers, a.qrels_path, a.pairwise,
+           a.dataset_type, a.tokenizer_path, a.device).run()
+
+
+if __name__ == "__main__":
+    main()

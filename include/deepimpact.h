@@ -193,6 +193,25 @@ int di_encoder_destroy(di_encoder *enc);
 int di_quantize(const float *impacts, int64_t n, double max_val, int32_t bits, int32_t *out,
                 double *max_used, int device, void *hip_stream, uint32_t flags);
 
+/* quantize_file (quantize.py:27-47) end to end: parse the impact TSV exactly as
+ * the reference (line.strip().split(', '), t.strip().split(': '), float()),
+ * quantize on the GPU in fp64, write the quantized TSV.  Empty / malformed
+ * lines fail with DI_EFORMAT where the reference raises ValueError. */
+int di_quantize_file(const char *input_path, const char *output_path, double max_val,
+                     int32_t bits, int device, double *max_used);
+
+/* ======================================================================
+ * Impact TSV text                                          (A9)
+ * ====================================================================== */
+/* Replaces the formatting loop of Indexer.index (indexer.py:62-68): for each doc
+ * the terms (UTF-8, terms + term_off[i]..term_off[i+1]) and impacts (already
+ * rounded, DI_F_ROUND3) become ', '.join(f'{term}: {impact}') + '\n', numbers
+ * printed as Python's repr of the float64 value.  Writes *out_len bytes; returns
+ * DI_ERANGE (with *out_len = bytes needed) if out_cap is too small. */
+int di_format_impact_lines(const char *terms, const int64_t *term_off, const float *impacts,
+                           const int64_t *cu_doc_terms, int32_t n_docs, char *out,
+                           int64_t out_cap, int64_t *out_len);
+
 /* Decoding of a quantized-index merge key. */
 static inline uint32_t di_key_doc(uint64_t key) { return 0xFFFFFFFFu - (uint32_t)key; }
 static inline uint32_t di_key_score(uint64_t key) { return (uint32_t)(key >> 48); }
