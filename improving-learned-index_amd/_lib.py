@@ -67,6 +67,11 @@ SIGNATURES = {
     "di_quantize_file": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_double, I32,
                                         ctypes.c_int, P]),
     "di_format_impact_lines": (ctypes.c_int, [P, P, P, P, I32, P, I64, P]),
+    "di_sparse_create": (ctypes.c_int, [P, I64, P, P, U32, ctypes.c_int, P]),
+    "di_sparse_search": (ctypes.c_int, [P, P, P, I32, I32, P, P, P, P, U32]),
+    "di_sparse_info": (ctypes.c_int, [P, P, P, P, P]),
+    "di_sparse_timing": (ctypes.c_int, [P, ctypes.c_char_p, P, ctypes.c_int]),
+    "di_sparse_destroy": (ctypes.c_int, [P]),
 }
 
 _LIB = None
@@ -267,3 +272,49 @@ def format_impact_lines(doc_terms, doc_impacts):
     check(lib().di_format_impact_lines(tb, ptr(term_off), ptr(imp), ptr(cu), n_docs, out, cap,
                                        ctypes.byref(n)))
     return out.raw[:n.value].decode("utf-8")
+
+
+class DeviceSparseIndex:
+    """Device-resident float index (di_sparse_*), NanoBEIR's SparseSearch path."""
+
+    def __init__(self, term_off, pdoc, pimp, n_docs, device=0):
+        term_off = np.ascontiguousarray(term_off, np.int64)
+        pdoc = np.ascontiguousarray(pdoc, np.uint32)
+        pimp = np.ascontiguousarray(pimp, np.float32)
+        if pdoc.size == 0:
+            pdoc, pimp = np.zeros(1, np.uint32), np.zeros(1, np.float32)
+        h = ctypes.c_void_p()
+        check(lib().di_sparse_create(ptr(term_off), len(term_off) - 1, ptr(pdoc), ptr(pimp),
+                                     n_docs, device, ctypes.byref(h)))
+        self._h = h
+
+    def search_csr(self, q_terms, cu_q, k, with_keys=False):
+        q_terms = np.ascontiguousarray(q_terms, np.uint32)
+        if q_terms.size == 0:
+            q_terms = np.zeros(1, np.uint32)
+        cu_q = np.ascontiguousarray(cu_q, np.int32)
+        n_q = len(cu_q) - 1
+        docs = np.zeros((max(n_q, 1), k), np.uint32)
+        scores = np.zeros((max(n_q, 1), k), np.float32)
+        n = np.zeros(max(n_q, 1), np.int32)
+        keys = np.zeros((max(n_q, 1), k), np.uint64) if with_keys else None
+        check(lib().di_sparse_search(self._h, ptr(q_terms), ptr(cu_q), n_q, k, ptr(docs),
+                                     ptr(scores), ptr(n), ptr(keys), 0))
+        return docs[:n_q], scores[:n_q], n[:n_q], (keys[:n_q] if with_keys else None)
+
+    def search(self, queries, k):
+        flat, cu = csr(queries)
+        docs, scores, n, _ = self.search_csr(flat, cu, k)
+        return [list(zip(docs[i, :n[i]].tolist(), scores[i, :n[i]].tolist()))
+                for i in range(len(queries))]
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().di_sparse_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

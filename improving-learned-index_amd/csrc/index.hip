@@ -482,6 +482,9 @@ void build_index(di_index *ix, const int64_t *term_off, int64_t n_terms, const u
     DI_HIP(hipMemcpy(ix->blk_off.p, boff.data(), boff.size() * 4, hipMemcpyHostToDevice));
 }
 
+}  // namespace
+
+namespace di {
 // Kernels using more than 64 KiB of dynamic LDS must opt in, once per device.
 void enable_big_lds() {
     static_assert(sizeof(ScoreShared) <= 160 * 1024, "ScoreShared exceeds LDS");
@@ -527,7 +530,7 @@ void launch_merge(const uint64_t *keys, const int32_t *counts, int n_q, int n_li
     check_launch("merge_topk");
 }
 
-}  // namespace
+}  // namespace di
 
 extern "C" {
 

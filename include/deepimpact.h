@@ -125,6 +125,29 @@ int di_topk_merge(const uint64_t *keys, const int32_t *counts, int32_t n_q, int3
                   uint32_t flags);
 
 /* ======================================================================
+ * In-memory float index of the NanoBEIR evaluator           (A14, A15)
+ * ====================================================================== */
+typedef struct di_sparse di_sparse;
+
+/* Replaces SparseSearch._build_inverted_index (nano_beir_evaluator.py:78-101):
+ * per term, postings (doc = corpus position, float32 impact) in corpus order;
+ * impacts <= 0 are dropped (:98).  n_docs <= DI_MAX_SPARSE_DOCS. */
+int di_sparse_create(const int64_t *term_off, int64_t n_terms, const uint32_t *pdoc,
+                     const float *pimp, uint32_t n_docs, int device, di_sparse **out);
+
+/* Replaces SparseSearch.search's scoring (nano_beir_evaluator.py:113-133):
+ * float32 sums formed in the reference's order (bit-exact under numpy >= 2),
+ * top-k by score with ties in first-touch order.  out_key: merge keys
+ * (score bits << 32 | (255 - first term) << 24 | (0xFFFFFF - doc)). */
+int di_sparse_search(di_sparse *sp, const uint32_t *q_terms, const int32_t *cu_q, int32_t n_q,
+                     int32_t k, uint32_t *out_doc, float *out_score, int32_t *out_n,
+                     uint64_t *out_key, uint32_t flags);
+int di_sparse_info(const di_sparse *sp, int64_t *n_terms, int64_t *n_postings, uint32_t *n_docs,
+                   int32_t *n_blocks);
+int di_sparse_timing(di_sparse *sp, const char *name, di_timing *out, int reset);
+int di_sparse_destroy(di_sparse *sp);
+
+/* ======================================================================
  * Encoder: DeepImpact forward + first-occurrence gather     (A2, A5-A9)
  * ====================================================================== */
 typedef struct di_encoder di_encoder;

@@ -1,0 +1,70 @@
+"""GPU parity of the in-memory float index (A14/A15) against the reference's own
+SparseSearch output (fixture sparse_search.json: reference code run here, numpy
+2.x => float32 sums).  Bit-exact scores and order, including exact float ties."""
+import json
+
+import numpy as np
+import pytest
+
+import oracle
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+
+class FakeModel:
+    def __init__(self, fx):
+        self.ci, self.qt = fx["corpus_impacts"], fx["query_terms"]
+
+    def get_impact_scores_batch(self, texts):
+        return [[(t, np.float32(v)) for t, v in self.ci[x]] for x in texts]
+
+    def process_query(self, q):
+        return list(self.qt[q])
+
+
+@pytest.fixture(scope="module")
+def fx():
+    from improving_learned_index_amd import _lib
+
+    if _lib.device_count() < 1:
+        pytest.fail("no HIP device visible (GPU test run without a GPU)")
+    return json.loads((GOLDEN / "sparse_search.json").read_text())
+
+
+@pytest.mark.parametrize("k", [1000, 5])
+def test_sparse_search_matches_reference(fx, k):
+    from improving_learned_index_amd.nano_beir import SparseSearch
+
+    ss = SparseSearch(FakeModel(fx), batch_size=16, encode_batch_size=7)
+    got = ss.search(fx["queries"], fx["corpus"], k)
+    for qid, want in fx["results"][str(k)].items():
+        assert [[d, s] for d, s in got[qid].items()] == want, qid
+
+
+def test_sparse_multiblock_matches_oracle(fx):
+    """40k docs (3 LDS blocks of 16384) against the oracle's float32 scorer."""
+    from improving_learned_index_amd import _lib
+
+    rng = np.random.default_rng(9)
+    n_docs, V = 40000, 300
+    lists = {t: [] for t in range(V)}
+    for d in range(n_docs):
+        for t in np.unique(np.minimum(rng.zipf(1.3, 12), V) - 1):
+            lists[int(t)].append((d, np.float32(rng.integers(1, 40) / 8.0)))  # many exact ties
+    term_off = np.zeros(V + 1, np.int64)
+    term_off[1:] = np.cumsum([len(lists[t]) for t in range(V)])
+    pdoc = np.array([d for t in range(V) for d, _ in lists[t]], np.uint32)
+    pimp = np.array([x for t in range(V) for _, x in lists[t]], np.float32)
+    dev = _lib.DeviceSparseIndex(term_off, pdoc, pimp, n_docs)
+    ora = oracle.SparseIndex.__new__(oracle.SparseIndex)
+    ora.corpus_ids = list(range(n_docs))
+    ora.vocab = {t: t for t in range(V)}
+    ora.term_off, ora.pdoc, ora.pimp = term_off, pdoc, pimp
+    qs = [list(dict.fromkeys(int(x) for x in np.minimum(rng.zipf(1.2, 5), V) - 1))
+          for _ in range(50)]
+    for k in (10, 1000):
+        got = dev.search(qs, k)
+        want = ora.search(qs, k)
+        for g, w in zip(got, want):
+            assert [(d, float(s)) for d, s in g] == w
