@@ -141,7 +141,7 @@ typedef struct {
 
 static void score_one(const int64_t *term_off, const uint32_t *pdoc, const uint8_t *pval,
                       const uint32_t *qt, int nt, int k, uint32_t *acc, uint32_t *touched,
-                      uint32_t *od, uint32_t *os, int32_t *on) {
+                      uint16_t *ftk, uint32_t *od, uint32_t *os, int32_t *on, uint64_t *ok) {
     int64_t nt_touch = 0;
     uint32_t max_score = 0;
     for (int j = 0; j < nt; ++j) {
@@ -150,7 +150,11 @@ static void score_one(const int64_t *term_off, const uint32_t *pdoc, const uint8
             uint32_t v = pval[p];
             if (v == 0) break; /* inverted_index.py:50-51 */
             uint32_t d = pdoc[p];
-            if (acc[d] == 0) touched[nt_touch++] = d;
+            if (acc[d] == 0) {
+                touched[nt_touch++] = d;
+                /* first-touch key: earlier term, then larger value (list order) */
+                ftk[d] = (uint16_t)(((255 - j) << 8) | v);
+            }
             acc[d] += v;
             if (acc[d] > max_score) max_score = acc[d];
         }
@@ -170,7 +174,13 @@ static void score_one(const int64_t *term_off, const uint32_t *pdoc, const uint8
     for (int64_t i = 0; i < nt_touch; ++i) {
         uint32_t d = touched[i];
         int64_t pos = hist[acc[d]]++;
-        if (pos < kk) { od[pos] = d; os[pos] = acc[d]; }
+        if (pos < kk) {
+            od[pos] = d;
+            os[pos] = acc[d];
+            /* the shard-merge key of the HIP path (include/deepimpact.h) */
+            if (ok) ok[pos] = ((uint64_t)acc[d] << 48) | ((uint64_t)ftk[d] << 32) |
+                              (uint64_t)(0xFFFFFFFFu - d);
+        }
     }
     *on = kk;
     for (int64_t i = 0; i < nt_touch; ++i) acc[touched[i]] = 0;
@@ -180,7 +190,7 @@ static void score_one(const int64_t *term_off, const uint32_t *pdoc, const uint8
 OR_API int or_score(const int64_t *term_off, const uint32_t *pdoc, const uint8_t *pval,
                     uint32_t n_docs, const uint32_t *q_terms, const int32_t *cu_q, int n_q,
                     int k, uint32_t *out_doc, uint32_t *out_score, int32_t *out_n,
-                    int n_threads) {
+                    uint64_t *out_key, int n_threads) {
     if (n_threads < 1) n_threads = 1;
 #ifdef _OPENMP
 #pragma omp parallel num_threads(n_threads)
@@ -188,14 +198,17 @@ OR_API int or_score(const int64_t *term_off, const uint32_t *pdoc, const uint8_t
     {
         uint32_t *acc = (uint32_t *)calloc((size_t)n_docs + 1, sizeof(uint32_t));
         uint32_t *touched = (uint32_t *)malloc(((size_t)n_docs + 1) * sizeof(uint32_t));
+        uint16_t *ftk = (uint16_t *)malloc(((size_t)n_docs + 1) * sizeof(uint16_t));
 #ifdef _OPENMP
 #pragma omp for schedule(dynamic, 1)
 #endif
         for (int q = 0; q < n_q; ++q)
             score_one(term_off, pdoc, pval, q_terms + cu_q[q], cu_q[q + 1] - cu_q[q], k, acc,
-                      touched, out_doc + (int64_t)q * k, out_score + (int64_t)q * k, out_n + q);
+                      touched, ftk, out_doc + (int64_t)q * k, out_score + (int64_t)q * k,
+                      out_n + q, out_key ? out_key + (int64_t)q * k : NULL);
         free(acc);
         free(touched);
+        free(ftk);
     }
     return 0;
 }
