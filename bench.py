@@ -275,6 +275,10 @@ def encode_leg(args, rank, world, dev):
         per_launch[k] = (f, avg, f / avg / 1e12 if avg > 0 else 0.0)
     dom = max(per_launch, key=lambda k: per_launch[k][1])
     f, avg, tf = per_launch[dom]
+    # PMC names: EPI 1 = bias+GELU (FFN1), 2 = bias+residual (O and FFN2 share it), 3 = QKV
+    pmc_name = {"gemm_qkv": "gemm_nt_kernel<bf16,3>", "gemm_ffn1": "gemm_nt_kernel<bf16,1>",
+                "gemm_o": "gemm_nt_kernel<bf16,2>", "gemm_ffn2": "gemm_nt_kernel<bf16,2>"}[dom]
+    traffic, src = load_pmc_traffic(pmc_name)
     model_flops = float(flops_per_doc(lens).sum())
     docs_per_s = world * args.docs * args.steps / el
     res = {
@@ -287,8 +291,8 @@ def encode_leg(args, rank, world, dev):
         "model_flops_frac": round(model_flops * args.steps / el / 1e12 / MFMA_BF16_PEAK_TFLOPS, 4),
         "roofline": {"kernel": f"gemm_nt_kernel<bf16> ({dom})", "bound": "mfma",
                      "achieved": round(tf, 1), "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": round(tf / MFMA_BF16_PEAK_TFLOPS, 4), "traffic": None,
-                     "algorithmic_flops_per_launch": f, "avg_launch_ms": round(avg * 1000, 4),
+                     "frac": round(tf / MFMA_BF16_PEAK_TFLOPS, 4), "traffic": traffic,
+                     "traffic_source": src, "algorithmic_flops_per_launch": f, "avg_launch_ms": round(avg * 1000, 4),
                      "launches": enc.timing(dom)[1]},
     }
     return res, (sd, cfg, ids, cu, lens, tt, ct, out)

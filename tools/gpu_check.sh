@@ -16,7 +16,7 @@ if [ "${SKIP_BENCH:-0}" != "1" ]; then
 fi
 if [ "${PROFILE:-0}" = "1" ]; then
   cd /tmp && export TMPDIR=/tmp
-  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof" -o run --output-format csv \
+  timeout -k 10 600 rocprofv3 -M --kernel-trace --stats -d "$R/gpurun_out/prof" -o run --output-format csv \
      -- python3 "$R/bench.py" --steps 5 --warmup 1 --no-cpu ${BENCH_ARGS:-} > "$R/gpurun_out/prof_bench.json" 2> "$R/gpurun_out/prof.err"
   rc=$?; tail -5 "$R/gpurun_out/prof.err"; [ $rc -eq 0 ] || exit $rc
   find "$R/gpurun_out/prof" -name "*stats*" | head

@@ -14,7 +14,7 @@ for grp in "FETCH_SIZE" "WRITE_SIZE" \
            "GRBM_GUI_ACTIVE SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_SALU TCC_HIT_sum TCC_MISS_sum" \
            "SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA SQ_WAIT_INST_LDS SQ_INSTS_VMEM_WR SQ_LDS_UNALIGNED_STALL"; do
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --pmc $grp --kernel-trace -d "$OUT/p$i" -o run --output-format csv \
+  timeout -k 10 300 rocprofv3 -M --pmc $grp --kernel-trace -d "$OUT/p$i" -o run --output-format csv \
      -- python3 "$R/bench.py" --steps 3 --warmup 1 --no-cpu "$@" > "$OUT/p$i.json" 2> "$OUT/p$i.err"
   rc=$?
   if [ $rc -ne 0 ]; then tail -20 "$OUT/p$i.err"; exit $rc; fi

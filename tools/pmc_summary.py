@@ -5,13 +5,46 @@ WRITE_SIZE are KiB; on gfx950 FETCH_SIZE reads exactly half the bytes of a wide
 coalesced (16 B/lane) streaming read (MI355X_MICROARCH.md §HBM), hence the 2x.
 """
 import csv
+import re
 import json
 import sys
 from collections import defaultdict
 from pathlib import Path
 
 
+_TARGS = [(r"DF16b", "bf16"), (r"f", "f32"), (r"Li(\d+)E", None), (r"j", "u32"), (r"i", "i32")]
+
+
+def _short_mangled(name):
+    """_ZN2di14gemm_nt_kernelIDF16bLi1EEEv... -> gemm_nt_kernel<bf16,1> (binutils'
+    c++filt cannot demangle DF16b, and rocprofv3's own demangler garbles it)."""
+    m = re.match(r"_ZN2di(\d+)", name)
+    if not m:
+        return None
+    n = int(m.group(1))
+    pos = m.end()
+    ident = name[pos:pos + n]
+    pos += n
+    if pos >= len(name) or name[pos] != "I":
+        return ident
+    pos += 1
+    args = []
+    while pos < len(name) and name[pos] != "E":
+        for pat, rep in _TARGS:
+            mm = re.compile(pat).match(name, pos)
+            if mm:
+                args.append(rep if rep is not None else mm.group(1))
+                pos = mm.end()
+                break
+        else:
+            return ident
+    return f"{ident}<{','.join(args)}>"
+
+
 def short(name):
+    sm = _short_mangled(name)
+    if sm:
+        return sm
     n = name.split("(")[0]
     n = n.split("::")[-1]
     return n.split("<")[0] if "<" in n and not n.startswith("merge") else n
