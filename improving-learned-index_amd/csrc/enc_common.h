@@ -67,6 +67,8 @@ struct GemmArgs {
     int ld_v;           // EPI_QKV: row stride of V^T (tokens, padded)
     int hidden;         // EPI_QKV: H (Q | K | V split points)
     const int32_t *vcol;  // EPI_QKV: V^T column of every token row (doc-aligned layout)
+    int64_t a_rows;       // rows of A that may be read (>= M; slack lets 256-row tiles
+                          // read past M without clamping)
 };
 
 }  // namespace di

@@ -13,6 +13,7 @@
 //   f32 : v_mfma_f32_16x16x4_f32 (exact f32 products)       (parity mode)
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <type_traits>
 
 #include "di_common.h"
@@ -247,11 +248,21 @@ __global__ void __launch_bounds__(G_THREADS) gemm_nt_kernel(GemmArgs g) {
     }
 }
 
+bool gemm256_ok(int epi, const GemmArgs &g);
+void launch_gemm256(int epi, const GemmArgs &g, hipStream_t s);
+
 template <typename T>
 void launch_gemm(int epi, const GemmArgs &g, hipStream_t s) {
     DI_REQUIRE(g.K % (ROW_BYTES / (int)sizeof(T)) == 0, DI_EINVAL,
                "GEMM K=%d must be a multiple of %d", g.K, ROW_BYTES / (int)sizeof(T));
     if (g.M == 0) return;
+    if constexpr (std::is_same<T, bf16>::value) {
+        static const bool force128 = std::getenv("DI_GEMM128") != nullptr;  // A/B knob
+        if (!force128 && gemm256_ok(epi, g)) {
+            launch_gemm256(epi, g, s);
+            return;
+        }
+    }
     dim3 grid((g.N + GB_N - 1) / GB_N, (g.M + GB_M - 1) / GB_M);
     switch (epi) {
         case EPI_BIAS:

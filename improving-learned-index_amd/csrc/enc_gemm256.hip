@@ -1,0 +1,363 @@
+// enc_gemm256.hip -- 256x256-tile bf16 MFMA GEMM, 8-phase pipelined K loop (gfx950).
+//
+// Same contract as enc_gemm.hip (C[M,N] = A[M,K] * B[N,K]^T + fused epilogue; the
+// encoder's QKV / O / FFN1 / FFN2 projections, reference xlmr_original.py:70-75),
+// for the shapes of the encoder hot loop: N % 256 == 0, K % 128 == 0, A readable up
+// to round_up(M, 256) rows (the encoder's activation buffers carry that slack).
+//
+// Geometry: 512 threads = 8 waves as 2 (M) x 4 (N); wave (wr, wc) owns output rows
+// wr*128..+128 and columns wc*64..+64 = 8 x 4 fragments of 16x16 (128 accumulator
+// VGPRs).  K step (one "K tile") = 64; two LDS buffers of one K tile each
+// (A and B images 256 rows x 128 B, 64 KiB per buffer, 128 KiB total).
+//
+// Each K tile is split into four "half tiles" of 128 rows x 64 k (16 KiB, two
+// global_load_lds_dwordx4 per thread), chosen so that each half is read by the
+// fragment loads of exactly one phase:
+//   A0 = tile rows {0-63, 128-191}   read in phase 1   (A fragments mt 0..3 of both wr)
+//   A1 = tile rows {64-127, 192-255} read in phase 2   (mt 4..7)
+//   B0 = columns {wc*64 + 0..31}      read in phase 1   (nt 0..1)
+//   B1 = columns {wc*64 + 32..63}     read in phase 3   (nt 2..3)
+// Four phases per K tile, 16 MFMAs (16x16x32) each; the wave keeps the whole K
+// tile's fragments in registers (A 64 + B 32 VGPRs), so phase 4 reads nothing:
+//   phase: 1 A0+B0 -> C[mt0-3][nt0-1]   2 A1 -> C[mt4-7][nt0-1]
+//          3 B1    -> C[mt4-7][nt2-3]   4 --  -> C[mt0-3][nt2-3]
+// One half tile is prefetched per phase into the region read in the phase before
+// (write-after-read one phase later is safe because every wave retires its
+// fragment reads, lgkmcnt(0), before the phase's first barrier).  Per iteration of
+// 8 phases (K tiles 2i in buffer 0, 2i+1 in buffer 1):
+//   ph1 buf1<-B1(2i+1)  ph2 buf0<-A0(2i+2)  ph3 buf0<-B0(2i+2)  ph4 buf0<-A1(2i+2)
+//   ph5 buf0<-B1(2i+2)  ph6 buf1<-A0(2i+3)  ph7 buf1<-B0(2i+3)  ph8 buf1<-A1(2i+3)
+// Counted waits (never 0 in steady state): phase 4 waits vmcnt(6) -- everything
+// but the last three half tiles, i.e. all of K tile 2i+1 -- which phase 5 reads
+// after the barrier; phase 8 likewise retires K tile 2i+2 for the next phase 1.
+// The two wave groups (wr = 0, 1) run one barrier apart (group 1 executes one extra
+// barrier up front, group 0 one at the end), so on every SIMD one wave issues
+// MFMAs while the other loads fragments and issues its prefetch (ping-pong).
+// Raw s_barrier (inline asm, a compiler memory fence but no vmcnt(0)) keeps the
+// prefetch in flight across barriers; all LDS is one dynamic array.
+#include <hip/hip_runtime.h>
+
+#include <type_traits>
+
+#include "di_common.h"
+#include "enc_common.h"
+
+namespace di {
+
+constexpr int G2_T = 512;
+constexpr int G2_TILE = 256;
+constexpr int G2_BUF = 65536;                  // one K tile: A image 32 KiB + B image 32 KiB
+constexpr int G2_EPI_RS_MAX = 256 * 4 + 16;    // f32 epilogue staging row (bytes)
+constexpr int G2_LDS = (2 * G2_BUF > 128 * G2_EPI_RS_MAX) ? 2 * G2_BUF : 128 * G2_EPI_RS_MAX;
+
+#define G2_BAR() asm volatile("s_barrier" ::: "memory")
+
+template <int EPI>
+__global__ void __launch_bounds__(G2_T) gemm256_kernel(GemmArgs g) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    const int tid = threadIdx.x, lane = tid & 63;
+    // wave-uniform in SGPRs: the LDS-DMA destination (M0) is then scalar arithmetic
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wr = wave >> 2, wc = wave & 3;
+
+    // tile order: XCD remap (bijective) + grouped GM x all-N order (speed only)
+    const int n_tn = gridDim.x, n_tm = gridDim.y, n_tiles = n_tn * n_tm;
+    int bid = blockIdx.y * gridDim.x + blockIdx.x;
+    {
+        const int q = n_tiles / 8, r = n_tiles % 8, x = bid % 8;
+        bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
+    }
+    constexpr int GM = 4;
+    const int grp = bid / (GM * n_tn), first_m = grp * GM;
+    const int gsz = min(GM, n_tm - first_m);
+    const int in = bid % (GM * n_tn);
+    const int m0 = (first_m + in % gsz) * G2_TILE, n0 = (in / gsz) * G2_TILE;
+    const int M = g.M, N = g.N, K = g.K;
+    const int nk = K / 64;
+
+    // ---- staging sources (per lane) and LDS destinations (per wave) ----------
+    // LDS row i (0..127) of a half tile = instruction j (0..1), wave, lane>>3:
+    //   i = j*64 + wave*8 + (lane>>3);  slot lane&7 holds global chunk
+    //   (lane&7) ^ (i&7)  (XOR swizzle on the source, rule 21).
+    // A half h, row i -> tile row j*128 + h*64 + (i&63)
+    // B half h, row i -> tile col j*128 + (wave>>2)*64 + h*32 + (wave&3)*8 + (lane>>3)
+    const int chunk = ((lane & 7) ^ ((lane >> 3) & 7)) * 8;
+    const bf16 *a_src = static_cast<const bf16 *>(g.A) +
+                        (int64_t)(m0 + wave * 8 + (lane >> 3)) * K + chunk;
+    const bf16 *b_src = static_cast<const bf16 *>(g.B) +
+                        (int64_t)(n0 + (wave >> 2) * 64 + (wave & 3) * 8 + (lane >> 3)) * K +
+                        chunk;
+    const int64_t a_h = (int64_t)64 * K, a_j = (int64_t)128 * K;
+    const int64_t b_h = (int64_t)32 * K, b_j = (int64_t)128 * K;
+    typedef __attribute__((address_space(3))) void lds_void;
+#define G2_STAGE_A(buf, h, t)                                                                  \
+    do {                                                                                       \
+        __builtin_amdgcn_global_load_lds((const void *)(a_src + (h) * a_h + (t) * 64),         \
+                                         (lds_void *)(lds + (buf) * G2_BUF + (h) * 16384 +     \
+                                                      wave * 1024),                            \
+                                         16, 0, 0);                                            \
+        __builtin_amdgcn_global_load_lds((const void *)(a_src + (h) * a_h + a_j + (t) * 64),   \
+                                         (lds_void *)(lds + (buf) * G2_BUF + (h) * 16384 +     \
+                                                      8192 + wave * 1024),                     \
+                                         16, 0, 0);                                            \
+    } while (0)
+#define G2_STAGE_B(buf, h, t)                                                                  \
+    do {                                                                                       \
+        __builtin_amdgcn_global_load_lds((const void *)(b_src + (h) * b_h + (t) * 64),         \
+                                         (lds_void *)(lds + (buf) * G2_BUF + 32768 +           \
+                                                      (h) * 16384 + wave * 1024),              \
+                                         16, 0, 0);                                            \
+        __builtin_amdgcn_global_load_lds((const void *)(b_src + (h) * b_h + b_j + (t) * 64),   \
+                                         (lds_void *)(lds + (buf) * G2_BUF + 32768 +           \
+                                                      (h) * 16384 + 8192 + wave * 1024),       \
+                                         16, 0, 0);                                            \
+    } while (0)
+
+    // ---- fragment reads ------------------------------------------------------
+    // A fragment mt of wave wr: LDS row (mt>>2)*128 + wr*64 + (mt&3)*16 + (lane&15);
+    // B fragment nt of wave wc: LDS row (nt>>1)*128 + wc*32 + (nt&1)*16 + (lane&15).
+    // k-step s reads chunk 4s + (lane>>4), stored at slot chunk ^ (lane&7).
+    // Fragment reads are inline-asm ds_read_b128: the compiler then cannot see an
+    // LDS read behind an LDS-DMA it cannot disambiguate (one LDS object) and does
+    // not drain the prefetch with vmcnt(0); the phase's own lgkmcnt(0) + barrier
+    // (and sched_barrier) order them before the MFMAs.
+    const int xs = ((lane >> 4) ^ (lane & 7));
+    const int c0 = xs << 4, c1 = (xs ^ 4) << 4;
+    const uint32_t lds_base =
+        (uint32_t)(uintptr_t)((__attribute__((address_space(3))) unsigned char *)lds);
+    const uint32_t a_rd = lds_base + (wr * 64 + (lane & 15)) * 128;
+    const uint32_t b_rd = lds_base + 32768 + (wc * 32 + (lane & 15)) * 128;
+    // [buffer][k-step] base addresses; the fragment offsets fit the 16-bit immediate
+    const uint32_t ra[2][2] = {{a_rd + c0, a_rd + c1}, {a_rd + G2_BUF + c0, a_rd + G2_BUF + c1}};
+    const uint32_t rb[2][2] = {{b_rd + c0, b_rd + c1}, {b_rd + G2_BUF + c0, b_rd + G2_BUF + c1}};
+    uint4 af[8][2], bq[4][2];
+#define G2_LD(dst, addr, off) \
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(dst) : "v"(addr), "i"(off))
+#define G2_READ_A(buf, mlo)                                                                    \
+    do {                                                                                       \
+        _Pragma("unroll") for (int mm = 0; mm < 4; ++mm) {                                     \
+            G2_LD(af[(mlo) + mm][0], ra[buf][0], ((mlo) >> 2) * 16384 + mm * 2048);            \
+            G2_LD(af[(mlo) + mm][1], ra[buf][1], ((mlo) >> 2) * 16384 + mm * 2048);            \
+        }                                                                                      \
+    } while (0)
+#define G2_READ_B(buf, nlo)                                                                    \
+    do {                                                                                       \
+        _Pragma("unroll") for (int nn = 0; nn < 2; ++nn) {                                     \
+            G2_LD(bq[(nlo) + nn][0], rb[buf][0], ((nlo) >> 1) * 16384 + nn * 2048);            \
+            G2_LD(bq[(nlo) + nn][1], rb[buf][1], ((nlo) >> 1) * 16384 + nn * 2048);            \
+        }                                                                                      \
+    } while (0)
+
+    f32x4 acc[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+#define G2_MFMA(mlo, nlo)                                                                      \
+    do {                                                                                       \
+        __builtin_amdgcn_sched_barrier(0);                                                     \
+        __builtin_amdgcn_s_setprio(1);                                                         \
+        _Pragma("unroll") for (int s = 0; s < 2; ++s)                                          \
+            _Pragma("unroll") for (int mm = 0; mm < 4; ++mm)                                   \
+                _Pragma("unroll") for (int nn = 0; nn < 2; ++nn) {                             \
+                    bf16x8 av, bv;                                                             \
+                    __builtin_memcpy(&av, &af[(mlo) + mm][s], 16);                             \
+                    __builtin_memcpy(&bv, &bq[(nlo) + nn][s], 16);                             \
+                    acc[(mlo) + mm][(nlo) + nn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(     \
+                        av, bv, acc[(mlo) + mm][(nlo) + nn], 0, 0, 0);                         \
+                }                                                                              \
+        __builtin_amdgcn_s_setprio(0);                                                         \
+        __builtin_amdgcn_sched_barrier(0);                                                     \
+    } while (0)
+#define G2_SYNC_READS() asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory")
+
+    // ---- prologue: K tile 0 whole, K tile 1 minus its B1 half --------------------
+    G2_STAGE_A(0, 0, 0);
+    G2_STAGE_B(0, 0, 0);
+    G2_STAGE_A(0, 1, 0);
+    G2_STAGE_B(0, 1, 0);
+    G2_STAGE_A(1, 0, 1);
+    G2_STAGE_B(1, 0, 1);
+    G2_STAGE_A(1, 1, 1);
+    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    G2_BAR();
+    if (wr == 1) G2_BAR();  // group 1 runs one barrier behind group 0
+
+    for (int t = 0; t < nk; t += 2) {
+        const bool more = t + 2 < nk;  // K tiles t+2, t+3 exist (nk is even)
+        // phase 1: buffer 0, A0 + B0
+        G2_READ_B(0, 0);
+        G2_READ_A(0, 0);
+        G2_STAGE_B(1, 1, t + 1);
+        G2_SYNC_READS();
+        G2_BAR();
+        G2_MFMA(0, 0);
+        G2_BAR();
+        // phase 2: A1
+        G2_READ_A(0, 4);
+        if (more) G2_STAGE_A(0, 0, t + 2);
+        G2_SYNC_READS();
+        G2_BAR();
+        G2_MFMA(4, 0);
+        G2_BAR();
+        // phase 3: B1
+        G2_READ_B(0, 2);
+        if (more) G2_STAGE_B(0, 0, t + 2);
+        G2_SYNC_READS();
+        G2_BAR();
+        G2_MFMA(4, 2);
+        G2_BAR();
+        // phase 4: registers only; retire K tile t+1 for phase 5
+        if (more) {
+            G2_STAGE_A(0, 1, t + 2);
+            asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        G2_BAR();
+        G2_MFMA(0, 2);
+        G2_BAR();
+        // phase 5: buffer 1, A0 + B0
+        G2_READ_B(1, 0);
+        G2_READ_A(1, 0);
+        if (more) G2_STAGE_B(0, 1, t + 2);
+        G2_SYNC_READS();
+        G2_BAR();
+        G2_MFMA(0, 0);
+        G2_BAR();
+        // phase 6
+        G2_READ_A(1, 4);
+        if (more) G2_STAGE_A(1, 0, t + 3);
+        G2_SYNC_READS();
+        G2_BAR();
+        G2_MFMA(4, 0);
+        G2_BAR();
+        // phase 7
+        G2_READ_B(1, 2);
+        if (more) G2_STAGE_B(1, 0, t + 3);
+        G2_SYNC_READS();
+        G2_BAR();
+        G2_MFMA(4, 2);
+        G2_BAR();
+        // phase 8: retire K tile t+2 for the next phase 1
+        if (more) {
+            G2_STAGE_A(1, 1, t + 3);
+            asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        }
+        G2_BAR();
+        G2_MFMA(0, 2);
+        G2_BAR();
+    }
+    if (wr == 0) G2_BAR();  // re-align the two groups
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+#undef G2_STAGE_A
+#undef G2_STAGE_B
+#undef G2_LD
+#undef G2_READ_A
+#undef G2_READ_B
+#undef G2_MFMA
+#undef G2_SYNC_READS
+
+    // ---- epilogue ------------------------------------------------------------
+    // acc[mt][nt][j]: row wr*128 + mt*16 + (lane>>4)*4 + j, col wc*64 + nt*16 + (lane&15)
+    if constexpr (EPI == EPI_QKV) {
+        if (n0 >= 2 * g.hidden) {  // V columns: transposed element stores into V^T
+#pragma unroll
+            for (int nt = 0; nt < 4; ++nt) {
+                const int col = n0 + wc * 64 + nt * 16 + (lane & 15);
+                const float bias = g.bias[col];
+                bf16 *vt = static_cast<bf16 *>(g.out2) + (int64_t)(col - 2 * g.hidden) * g.ld_v;
+#pragma unroll
+                for (int mt = 0; mt < 8; ++mt) {
+                    const int row0 = m0 + wr * 128 + mt * 16 + (lane >> 4) * 4;
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        if (row0 + j < M) vt[g.vcol[row0 + j]] = (bf16)(acc[mt][nt][j] + bias);
+                }
+            }
+            return;
+        }
+    }
+    // Two passes of 128 rows through LDS (staging row padded by 16 B), then whole
+    // 16-byte row chunks to global; the residual is added on the way out.
+    using OutT = typename std::conditional<EPI == EPI_BIAS_RESID, float, bf16>::type;
+    constexpr int OE = sizeof(OutT);
+    constexpr int RS = G2_TILE * OE + 16;
+    constexpr int CPR = G2_TILE * OE / 16;
+    float bias_v[4];
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) bias_v[nt] = g.bias ? g.bias[n0 + wc * 64 + nt * 16 + (lane & 15)] : 0.f;
+#pragma unroll
+    for (int pass = 0; pass < 2; ++pass) {
+        // LDS row lr = wr*64 + (mt&3)*16 + (lane>>4)*4 + j  <->  tile row wr*128 + pass*64 + ...
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) {
+            const int lc = wc * 64 + nt * 16 + (lane & 15);
+#pragma unroll
+            for (int mm = 0; mm < 4; ++mm) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int lr = wr * 64 + mm * 16 + (lane >> 4) * 4 + j;
+                    float v = acc[pass * 4 + mm][nt][j] + bias_v[nt];
+                    if constexpr (EPI == EPI_BIAS_GELU) v = gelu_erf(v);
+                    *reinterpret_cast<OutT *>(lds + lr * RS + lc * OE) = from_f32<OutT>(v);
+                }
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < 128 * CPR / G2_T; ++i) {
+            const int id = tid + i * G2_T;
+            const int lr = id / CPR, ch = id % CPR;
+            const int row = m0 + (lr >> 6) * 128 + pass * 64 + (lr & 63);
+            const int col0 = n0 + ch * (16 / OE);
+            if (row < M) {
+                uint4 v = *reinterpret_cast<const uint4 *>(lds + lr * RS + ch * 16);
+                if constexpr (EPI == EPI_BIAS_RESID) {
+                    const bf16x4 rv = *reinterpret_cast<const bf16x4 *>(
+                        static_cast<const bf16 *>(g.resid) + (int64_t)row * N + col0);
+                    v.x = __float_as_uint(__uint_as_float(v.x) + (float)rv[0]);
+                    v.y = __float_as_uint(__uint_as_float(v.y) + (float)rv[1]);
+                    v.z = __float_as_uint(__uint_as_float(v.z) + (float)rv[2]);
+                    v.w = __float_as_uint(__uint_as_float(v.w) + (float)rv[3]);
+                }
+                *reinterpret_cast<uint4 *>(static_cast<OutT *>(g.out) + (int64_t)row * g.ld_out +
+                                           col0) = v;
+            }
+        }
+        __syncthreads();
+    }
+}
+#undef G2_BAR
+
+// Shapes the 8-phase kernel takes; everything else goes to the 128x128 kernel.
+bool gemm256_ok(int epi, const GemmArgs &g) {
+    const int64_t m_pad = ((int64_t)g.M + G2_TILE - 1) / G2_TILE * G2_TILE;
+    return g.N % G2_TILE == 0 && g.K % 128 == 0 && g.K >= 128 && g.a_rows >= m_pad &&
+           (epi != EPI_QKV || (2 * g.hidden) % G2_TILE == 0);
+}
+
+void launch_gemm256(int epi, const GemmArgs &g, hipStream_t s) {
+    static_assert(G2_LDS <= 160 * 1024, "LDS");
+    dim3 grid(g.N / G2_TILE, (g.M + G2_TILE - 1) / G2_TILE);
+    switch (epi) {
+#define G2_CASE(E)                                                                             \
+    case E:                                                                                    \
+        DI_HIP(hipFuncSetAttribute((const void *)gemm256_kernel<E>,                            \
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, G2_LDS));       \
+        hipLaunchKernelGGL((gemm256_kernel<E>), grid, dim3(G2_T), G2_LDS, s, g);               \
+        break;
+        G2_CASE(EPI_BIAS)
+        G2_CASE(EPI_BIAS_GELU)
+        G2_CASE(EPI_BIAS_RESID)
+        G2_CASE(EPI_QKV)
+#undef G2_CASE
+        default:
+            fail(DI_EINVAL, "bad GEMM epilogue");
+    }
+    check_launch("gemm256");
+}
+
+}  // namespace di

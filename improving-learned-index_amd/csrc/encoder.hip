@@ -60,6 +60,7 @@ struct di_encoder {
     // workspace
     DevBuf X, qk, vt, vcol, ctx, pre, X1, Hff, impact, ids, cu, tt, cut, err;
     int64_t cap_tokens = 0;
+    int64_t cap_rows = 0;  // allocated rows of the GEMM A operands (>= cap_tokens)
     int cap_docs = 0;
     int ld_v = 0;
     Timer timer;
@@ -148,11 +149,14 @@ void ensure_workspace(di_encoder *e, int64_t M, int n_docs, int64_t n_terms) {
         int64_t cap = std::max<int64_t>(std::max<int64_t>(M, e->cap_tokens), 256);
         const int capd = std::max(std::max(n_docs, e->cap_docs), 16);
         const size_t es = e->esz;
-        e->X.reserve(cap * H * es);
-        e->X1.reserve(cap * H * es);
-        e->ctx.reserve(cap * H * es);
+        // GEMM A operands (X, X1, ctx, Hff) carry rows up to a multiple of 256 so
+        // the 256-row GEMM tiles read them unclamped (GemmArgs::a_rows)
+        const int64_t capr = (cap + 255) / 256 * 256;
+        e->X.reserve(capr * H * es);
+        e->X1.reserve(capr * H * es);
+        e->ctx.reserve(capr * H * es);
         e->qk.reserve(cap * 2 * H * es);
-        e->Hff.reserve(cap * F * es);
+        e->Hff.reserve(capr * F * es);
         e->pre.reserve(cap * H * 4);
         e->impact.reserve(cap * 4);
         e->ids.reserve(cap * 4);
@@ -164,6 +168,7 @@ void ensure_workspace(di_encoder *e, int64_t M, int n_docs, int64_t n_terms) {
             DI_HIP(hipMemset(e->vt.p, 0, vt_bytes));
         }
         e->cap_tokens = cap;
+        e->cap_rows = capr;
         e->cap_docs = capd;
     }
     e->ld_v = vt_ld(M, n_docs);
@@ -193,6 +198,7 @@ void forward(di_encoder *e, const int32_t *d_ids, const int32_t *d_cu, int n_doc
         const bool last = l + 1 == e->layers.size();
         GemmArgs g{};
         g.M = (int)M;
+        g.a_rows = e->cap_rows;
         g.hidden = H;
         // QKV (V written transposed for the attention kernel)
         g.A = X;
@@ -217,6 +223,7 @@ void forward(di_encoder *e, const int32_t *d_ids, const int32_t *d_cu, int n_doc
         // attention output + residual -> LN1
         g = GemmArgs{};
         g.M = (int)M;
+        g.a_rows = e->cap_rows;
         g.A = e->ctx.p;
         g.B = L.w_o.p;
         g.bias = L.b_o.as<float>();
@@ -237,6 +244,7 @@ void forward(di_encoder *e, const int32_t *d_ids, const int32_t *d_cu, int n_doc
         // FFN
         g = GemmArgs{};
         g.M = (int)M;
+        g.a_rows = e->cap_rows;
         g.A = X1;
         g.B = L.w_i.p;
         g.bias = L.b_i.as<float>();
@@ -250,6 +258,7 @@ void forward(di_encoder *e, const int32_t *d_ids, const int32_t *d_cu, int n_doc
         }
         g = GemmArgs{};
         g.M = (int)M;
+        g.a_rows = e->cap_rows;
         g.A = e->Hff.p;
         g.B = L.w_out.p;
         g.bias = L.b_out.as<float>();
