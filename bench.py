@@ -276,8 +276,8 @@ def encode_leg(args, rank, world, dev):
     dom = max(per_launch, key=lambda k: per_launch[k][1])
     f, avg, tf = per_launch[dom]
     # PMC names: EPI 1 = bias+GELU (FFN1), 2 = bias+residual (O and FFN2 share it), 3 = QKV
-    pmc_name = {"gemm_qkv": "gemm_nt_kernel<bf16,3>", "gemm_ffn1": "gemm_nt_kernel<bf16,1>",
-                "gemm_o": "gemm_nt_kernel<bf16,2>", "gemm_ffn2": "gemm_nt_kernel<bf16,2>"}[dom]
+    pmc_name = {"gemm_qkv": "gemm256_kernel<3>", "gemm_ffn1": "gemm256_kernel<1>",
+                "gemm_o": "gemm256_kernel<2>", "gemm_ffn2": "gemm256_kernel<2>"}[dom]
     traffic, src = load_pmc_traffic(pmc_name)
     model_flops = float(flops_per_doc(lens).sum())
     docs_per_s = world * args.docs * args.steps / el
@@ -289,7 +289,7 @@ def encode_leg(args, rank, world, dev):
         "gemm_tflops": {k: round(v[2], 1) for k, v in per_launch.items()},
         "model_tflops": round(model_flops * args.steps / el / 1e12 * 1.0, 1),
         "model_flops_frac": round(model_flops * args.steps / el / 1e12 / MFMA_BF16_PEAK_TFLOPS, 4),
-        "roofline": {"kernel": f"gemm_nt_kernel<bf16> ({dom})", "bound": "mfma",
+        "roofline": {"kernel": f"{pmc_name} ({dom})", "bound": "mfma",
                      "achieved": round(tf, 1), "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": round(tf / MFMA_BF16_PEAK_TFLOPS, 4), "traffic": traffic,
                      "traffic_source": src, "algorithmic_flops_per_launch": f, "avg_launch_ms": round(avg * 1000, 4),

@@ -20,32 +20,42 @@ __device__ __forceinline__ float from_f32<float>(float x) { return x; }
 template <>
 __device__ __forceinline__ bf16 from_f32<bf16>(float x) { return (bf16)x; }
 
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
 // erf for f32 without branches: x clamped to [-4, 4] (erf is +-1 in f32 beyond),
 // x * P(x^2) / Q(x^2) rational minimax (the coefficients of Eigen's
 // generic_fast_erf_float); a few ulp, vs ~117 instructions for ocml erff.
-__device__ __forceinline__ float fast_erf(float x) {
-    x = fminf(fmaxf(x, -4.0f), 4.0f);
-    const float x2 = x * x;
-    float p = -2.72614225801306e-10f;
-    p = fmaf(x2, p, 2.77068142495902e-08f);
-    p = fmaf(x2, p, -2.10102402082508e-06f);
-    p = fmaf(x2, p, -5.69250639462346e-05f);
-    p = fmaf(x2, p, -7.34990630326855e-04f);
-    p = fmaf(x2, p, -2.95459980854025e-03f);
-    p = fmaf(x2, p, -1.60960333262415e-02f);
-    p *= x;
-    float q = -1.45660718464996e-05f;
-    q = fmaf(x2, q, -2.13374055278905e-04f);
-    q = fmaf(x2, q, -1.68282697438203e-03f);
-    q = fmaf(x2, q, -7.37332916720468e-03f);
-    q = fmaf(x2, q, -1.42647390514189e-02f);
-    return __fdividef(p, q);
+// Written on pairs so the epilogues run it as packed f32 math (v_pk_fma_f32).
+__device__ __forceinline__ f32x2 fast_erf2(f32x2 x) {
+    x = __builtin_elementwise_min(__builtin_elementwise_max(x, f32x2{-4.0f, -4.0f}),
+                                  f32x2{4.0f, 4.0f});
+    const f32x2 x2 = x * x;
+#define DI_C2(c) f32x2{c, c}
+    f32x2 p = DI_C2(-2.72614225801306e-10f);
+    p = __builtin_elementwise_fma(x2, p, DI_C2(2.77068142495902e-08f));
+    p = __builtin_elementwise_fma(x2, p, DI_C2(-2.10102402082508e-06f));
+    p = __builtin_elementwise_fma(x2, p, DI_C2(-5.69250639462346e-05f));
+    p = __builtin_elementwise_fma(x2, p, DI_C2(-7.34990630326855e-04f));
+    p = __builtin_elementwise_fma(x2, p, DI_C2(-2.95459980854025e-03f));
+    p = __builtin_elementwise_fma(x2, p, DI_C2(-1.60960333262415e-02f));
+    p = p * x;
+    f32x2 q = DI_C2(-1.45660718464996e-05f);
+    q = __builtin_elementwise_fma(x2, q, DI_C2(-2.13374055278905e-04f));
+    q = __builtin_elementwise_fma(x2, q, DI_C2(-1.68282697438203e-03f));
+    q = __builtin_elementwise_fma(x2, q, DI_C2(-7.37332916720468e-03f));
+    q = __builtin_elementwise_fma(x2, q, DI_C2(-1.42647390514189e-02f));
+#undef DI_C2
+    return p * f32x2{__builtin_amdgcn_rcpf(q.x), __builtin_amdgcn_rcpf(q.y)};
 }
 
-// GELU with erf, as torch.nn.functional.gelu (approximate='none')
-__device__ __forceinline__ float gelu_erf(float x) {
-    return 0.5f * x * (1.0f + fast_erf(x * 0.70710678118654752440f));
+// GELU with erf, as torch.nn.functional.gelu (approximate='none'):
+// 0.5 x (1 + erf(x / sqrt 2)) = h + h * erf(...), h = x / 2
+__device__ __forceinline__ f32x2 gelu_erf2(f32x2 x) {
+    const f32x2 e = fast_erf2(x * f32x2{0.70710678118654752440f, 0.70710678118654752440f});
+    const f32x2 h = x * f32x2{0.5f, 0.5f};
+    return __builtin_elementwise_fma(h, e, h);
 }
+__device__ __forceinline__ float gelu_erf(float x) { return gelu_erf2(f32x2{x, x}).x; }
 
 // GEMM epilogues
 enum GemmEpi : int {
@@ -69,6 +79,8 @@ struct GemmArgs {
     const int32_t *vcol;  // EPI_QKV: V^T column of every token row (doc-aligned layout)
     int64_t a_rows;       // rows of A that may be read (>= M; slack lets 256-row tiles
                           // read past M without clamping)
+    int tune_gm;          // 256-tile kernel: M tiles per group in the tile order (0 = default)
+    int ablate;           // profiling only (tools/gemm_check): 1 = skip the epilogue
 };
 
 }  // namespace di

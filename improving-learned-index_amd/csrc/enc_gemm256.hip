@@ -47,8 +47,7 @@ namespace di {
 constexpr int G2_T = 512;
 constexpr int G2_TILE = 256;
 constexpr int G2_BUF = 65536;                  // one K tile: A image 32 KiB + B image 32 KiB
-constexpr int G2_EPI_RS_MAX = 256 * 4 + 16;    // f32 epilogue staging row (bytes)
-constexpr int G2_LDS = (2 * G2_BUF > 128 * G2_EPI_RS_MAX) ? 2 * G2_BUF : 128 * G2_EPI_RS_MAX;
+constexpr int G2_LDS = 2 * G2_BUF;
 
 #define G2_BAR() asm volatile("s_barrier" ::: "memory")
 
@@ -67,7 +66,7 @@ __global__ void __launch_bounds__(G2_T) gemm256_kernel(GemmArgs g) {
         const int q = n_tiles / 8, r = n_tiles % 8, x = bid % 8;
         bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
     }
-    constexpr int GM = 4;
+    const int GM = g.tune_gm > 0 ? g.tune_gm : 4;
     const int grp = bid / (GM * n_tn), first_m = grp * GM;
     const int gsz = min(GM, n_tm - first_m);
     const int in = bid % (GM * n_tn);
@@ -84,9 +83,14 @@ __global__ void __launch_bounds__(G2_T) gemm256_kernel(GemmArgs g) {
     const int chunk = ((lane & 7) ^ ((lane >> 3) & 7)) * 8;
     const bf16 *a_src = static_cast<const bf16 *>(g.A) +
                         (int64_t)(m0 + wave * 8 + (lane >> 3)) * K + chunk;
+    // B rows are stored permuted inside each 32-column group: LDS row q = sub*16 +
+    // g*4 + r holds column g*8 + sub*4 + r, so that MFMA fragment nt (rows sub*16..+15
+    // of half nt>>1) gives, in the C^T layout below, every lane 8 consecutive output
+    // columns across the fragment pair (2h, 2h+1).
+    const int qb = (wave & 3) * 8 + (lane >> 3);  // LDS row within the 32-column group
+    const int b_col = ((qb >> 2) & 3) * 8 + (qb >> 4) * 4 + (qb & 3);
     const bf16 *b_src = static_cast<const bf16 *>(g.B) +
-                        (int64_t)(n0 + (wave >> 2) * 64 + (wave & 3) * 8 + (lane >> 3)) * K +
-                        chunk;
+                        (int64_t)(n0 + (wave >> 2) * 64 + b_col) * K + chunk;
     const int64_t a_h = (int64_t)64 * K, a_j = (int64_t)128 * K;
     const int64_t b_h = (int64_t)32 * K, b_j = (int64_t)128 * K;
     typedef __attribute__((address_space(3))) void lds_void;
@@ -165,7 +169,7 @@ __global__ void __launch_bounds__(G2_T) gemm256_kernel(GemmArgs g) {
                     __builtin_memcpy(&av, &af[(mlo) + mm][s], 16);                             \
                     __builtin_memcpy(&bv, &bq[(nlo) + nn][s], 16);                             \
                     acc[(mlo) + mm][(nlo) + nn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(     \
-                        av, bv, acc[(mlo) + mm][(nlo) + nn], 0, 0, 0);                         \
+                        bv, av, acc[(mlo) + mm][(nlo) + nn], 0, 0, 0);                         \
                 }                                                                              \
         __builtin_amdgcn_s_setprio(0);                                                         \
         __builtin_amdgcn_sched_barrier(0);                                                     \
@@ -249,9 +253,7 @@ __global__ void __launch_bounds__(G2_T) gemm256_kernel(GemmArgs g) {
         G2_MFMA(0, 2);
         G2_BAR();
     }
-    if (wr == 0) G2_BAR();  // re-align the two groups
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    if (wr == 0) G2_BAR();  // re-align the two groups (every barrier is matched)
 #undef G2_STAGE_A
 #undef G2_STAGE_B
 #undef G2_LD
@@ -261,73 +263,81 @@ __global__ void __launch_bounds__(G2_T) gemm256_kernel(GemmArgs g) {
 #undef G2_SYNC_READS
 
     // ---- epilogue ------------------------------------------------------------
-    // acc[mt][nt][j]: row wr*128 + mt*16 + (lane>>4)*4 + j, col wc*64 + nt*16 + (lane&15)
+    if (g.ablate & 1) {  // profiling: main loop only (accumulators kept live)
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(acc[i][j]));
+        return;
+    }
+    // C^T layout (the MFMA took the weight fragment as its first operand): lane l
+    // holds, for A fragment mt and weight-column half h, output row
+    //   m = m0 + wr*128 + mt*16 + (l & 15)
+    // and the 8 consecutive columns n = n0 + wc*64 + h*32 + (l >> 4)*8 + e, e = 0..7,
+    // in acc[mt][2h][0..3], acc[mt][2h+1][0..3].  Stores go straight from registers,
+    // 16 B (bf16) / 32 B (f32) per lane, no LDS round trip and no barrier.
+    const int row_l = m0 + wr * 128 + (lane & 15);
+    const int col_l = n0 + wc * 64 + (lane >> 4) * 8;
+    float bias_v[2][8];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const float4 b0 = *reinterpret_cast<const float4 *>(g.bias + col_l + h * 32);
+        const float4 b1 = *reinterpret_cast<const float4 *>(g.bias + col_l + h * 32 + 4);
+        bias_v[h][0] = b0.x; bias_v[h][1] = b0.y; bias_v[h][2] = b0.z; bias_v[h][3] = b0.w;
+        bias_v[h][4] = b1.x; bias_v[h][5] = b1.y; bias_v[h][6] = b1.z; bias_v[h][7] = b1.w;
+    }
     if constexpr (EPI == EPI_QKV) {
         if (n0 >= 2 * g.hidden) {  // V columns: transposed element stores into V^T
+            bf16 *vt = static_cast<bf16 *>(g.out2) + (int64_t)(col_l - 2 * g.hidden) * g.ld_v;
 #pragma unroll
-            for (int nt = 0; nt < 4; ++nt) {
-                const int col = n0 + wc * 64 + nt * 16 + (lane & 15);
-                const float bias = g.bias[col];
-                bf16 *vt = static_cast<bf16 *>(g.out2) + (int64_t)(col - 2 * g.hidden) * g.ld_v;
+            for (int mt = 0; mt < 8; ++mt) {
+                const int row = row_l + mt * 16;
+                if (row < M) {
+                    const int vc = g.vcol[row];
 #pragma unroll
-                for (int mt = 0; mt < 8; ++mt) {
-                    const int row0 = m0 + wr * 128 + mt * 16 + (lane >> 4) * 4;
+                    for (int h = 0; h < 2; ++h)
 #pragma unroll
-                    for (int j = 0; j < 4; ++j)
-                        if (row0 + j < M) vt[g.vcol[row0 + j]] = (bf16)(acc[mt][nt][j] + bias);
+                        for (int e = 0; e < 8; ++e)
+                            vt[(int64_t)(h * 32 + e) * g.ld_v + vc] =
+                                (bf16)(acc[mt][2 * h + (e >> 2)][e & 3] + bias_v[h][e]);
                 }
             }
             return;
         }
     }
-    // Two passes of 128 rows through LDS (staging row padded by 16 B), then whole
-    // 16-byte row chunks to global; the residual is added on the way out.
-    using OutT = typename std::conditional<EPI == EPI_BIAS_RESID, float, bf16>::type;
-    constexpr int OE = sizeof(OutT);
-    constexpr int RS = G2_TILE * OE + 16;
-    constexpr int CPR = G2_TILE * OE / 16;
-    float bias_v[4];
 #pragma unroll
-    for (int nt = 0; nt < 4; ++nt) bias_v[nt] = g.bias ? g.bias[n0 + wc * 64 + nt * 16 + (lane & 15)] : 0.f;
+    for (int mt = 0; mt < 8; ++mt) {
+        const int row = row_l + mt * 16;
+        if (row >= M) continue;
 #pragma unroll
-    for (int pass = 0; pass < 2; ++pass) {
-        // LDS row lr = wr*64 + (mt&3)*16 + (lane>>4)*4 + j  <->  tile row wr*128 + pass*64 + ...
+        for (int h = 0; h < 2; ++h) {
+            float v[8];
 #pragma unroll
-        for (int nt = 0; nt < 4; ++nt) {
-            const int lc = wc * 64 + nt * 16 + (lane & 15);
+            for (int e = 0; e < 8; ++e) v[e] = acc[mt][2 * h + (e >> 2)][e & 3] + bias_v[h][e];
+            if constexpr (EPI == EPI_BIAS_GELU) {
 #pragma unroll
-            for (int mm = 0; mm < 4; ++mm) {
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const int lr = wr * 64 + mm * 16 + (lane >> 4) * 4 + j;
-                    float v = acc[pass * 4 + mm][nt][j] + bias_v[nt];
-                    if constexpr (EPI == EPI_BIAS_GELU) v = gelu_erf(v);
-                    *reinterpret_cast<OutT *>(lds + lr * RS + lc * OE) = from_f32<OutT>(v);
+                for (int e = 0; e < 8; e += 2) {
+                    const f32x2 y = gelu_erf2(f32x2{v[e], v[e + 1]});
+                    v[e] = y.x;
+                    v[e + 1] = y.y;
                 }
             }
-        }
-        __syncthreads();
+            const int64_t o = (int64_t)row * g.ld_out + col_l + h * 32;
+            if constexpr (EPI == EPI_BIAS_RESID) {
+                const bf16x8 rv = *reinterpret_cast<const bf16x8 *>(
+                    static_cast<const bf16 *>(g.resid) + (int64_t)row * N + col_l + h * 32);
+                float *op = static_cast<float *>(g.out) + o;
+                *reinterpret_cast<float4 *>(op) = float4{v[0] + (float)rv[0], v[1] + (float)rv[1],
+                                                         v[2] + (float)rv[2], v[3] + (float)rv[3]};
+                *reinterpret_cast<float4 *>(op + 4) = float4{
+                    v[4] + (float)rv[4], v[5] + (float)rv[5], v[6] + (float)rv[6], v[7] + (float)rv[7]};
+            } else {
+                bf16x8 ov;
 #pragma unroll
-        for (int i = 0; i < 128 * CPR / G2_T; ++i) {
-            const int id = tid + i * G2_T;
-            const int lr = id / CPR, ch = id % CPR;
-            const int row = m0 + (lr >> 6) * 128 + pass * 64 + (lr & 63);
-            const int col0 = n0 + ch * (16 / OE);
-            if (row < M) {
-                uint4 v = *reinterpret_cast<const uint4 *>(lds + lr * RS + ch * 16);
-                if constexpr (EPI == EPI_BIAS_RESID) {
-                    const bf16x4 rv = *reinterpret_cast<const bf16x4 *>(
-                        static_cast<const bf16 *>(g.resid) + (int64_t)row * N + col0);
-                    v.x = __float_as_uint(__uint_as_float(v.x) + (float)rv[0]);
-                    v.y = __float_as_uint(__uint_as_float(v.y) + (float)rv[1]);
-                    v.z = __float_as_uint(__uint_as_float(v.z) + (float)rv[2]);
-                    v.w = __float_as_uint(__uint_as_float(v.w) + (float)rv[3]);
-                }
-                *reinterpret_cast<uint4 *>(static_cast<OutT *>(g.out) + (int64_t)row * g.ld_out +
-                                           col0) = v;
+                for (int e = 0; e < 8; ++e) ov[e] = (bf16)v[e];
+                *reinterpret_cast<bf16x8 *>(static_cast<bf16 *>(g.out) + o) = ov;
             }
         }
-        __syncthreads();
     }
 }
 #undef G2_BAR

@@ -178,6 +178,33 @@ int main(int argc, char **argv) {
                           {206426, 3072, 768, EPI_BIAS_GELU, 768},
                           {206426, 768, 3072, EPI_BIAS_RESID, 768}};
     const char *names[] = {"qkv", "o", "ffn1", "ffn2"};
+    // tile-order group size and epilogue ablation sweep on the 256 kernel
+    {
+        hipEvent_t a0, a1;
+        CK(hipEventCreate(&a0));
+        CK(hipEventCreate(&a1));
+        for (int i = 0; i < 4; ++i) {
+            const Case &c = bench[i];
+            const double flops = 2.0 * c.M * c.N * c.K;
+            for (int abl = 0; abl < 2; ++abl) {
+                for (int gm : {1, 2, 4, 8, 16}) {
+                    GemmArgs g = args(c, O1, V1, true);
+                    g.tune_gm = gm;
+                    g.ablate = abl;
+                    for (int w = 0; w < 2; ++w) launch_gemm<bf16>(c.epi, g, 0);
+                    CK(hipEventRecord(a0, 0));
+                    for (int w = 0; w < 10; ++w) launch_gemm<bf16>(c.epi, g, 0);
+                    CK(hipEventRecord(a1, 0));
+                    CK(hipEventSynchronize(a1));
+                    float ms;
+                    CK(hipEventElapsedTime(&ms, a0, a1));
+                    ms /= 10;
+                    printf("sweep %-5s ablate=%d gm=%2d  %.3f ms  %.0f TF\n", names[i], abl, gm, ms,
+                           flops / ms / 1e9);
+                }
+            }
+        }
+    }
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
