@@ -61,7 +61,7 @@ __device__ __forceinline__ float gelu_erf(float x) { return gelu_erf2(f32x2{x, x
 enum GemmEpi : int {
     EPI_BIAS = 0,        // out(T) = acc + bias
     EPI_BIAS_GELU = 1,   // out(T) = gelu(acc + bias)
-    EPI_BIAS_RESID = 2,  // out(f32) = acc + bias + resid(T)      (pre-LayerNorm)
+    EPI_BIAS_RESID = 2,  // out(T) = acc + bias + resid(T), one rounding (pre-LayerNorm)
     EPI_QKV = 3,         // Q,K -> qk[M][2H] (T);  V -> vt[H][ldv] transposed (T)
 };
 
@@ -81,6 +81,8 @@ struct GemmArgs {
                           // read past M without clamping)
     int tune_gm;          // 256-tile kernel: M tiles per group in the tile order (0 = default)
     int ablate;           // profiling only (tools/gemm_check): 1 = skip the epilogue
+    int stagger;          // 256-tile kernel: first-wave delay (shader cycles) of every other
+                          // CU's first tile, so the CUs' store bursts alternate (0 = off)
 };
 
 }  // namespace di

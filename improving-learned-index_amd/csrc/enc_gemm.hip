@@ -175,11 +175,13 @@ __global__ void __launch_bounds__(G_THREADS) gemm_nt_kernel(GemmArgs g) {
     }
     // Everything else goes through LDS (the staging buffers are free now), 64
     // rows per pass, so that global stores are whole 16-byte chunks of rows.
-    // bias / GELU are applied in registers; the residual is added on the way out.
-    using OutT = typename std::conditional<EPI == EPI_BIAS_RESID, float, T>::type;
-    constexpr int OE = sizeof(OutT);
-    constexpr int RS = GB_N * OE + 16;       // padded LDS row stride (bytes)
-    constexpr int CPR = GB_N * OE / 16;      // 16-byte chunks per row
+    // bias / GELU are applied in registers; the residual (EPI_BIAS_RESID) is added
+    // to the f32 staged value on the way out, then rounded once to T.
+    using StT = typename std::conditional<EPI == EPI_BIAS_RESID, float, T>::type;
+    constexpr int SE = sizeof(StT);
+    constexpr int RS = GB_N * SE + 16;       // padded LDS row stride (bytes)
+    constexpr int CPR = GB_N * SE / 16;      // 16-byte chunks per row
+    constexpr int EPCH = 16 / SE;            // elements per chunk
     unsigned char *ot = &lds[0][0][0];
     float bias_v[4];
 #pragma unroll
@@ -200,7 +202,7 @@ __global__ void __launch_bounds__(G_THREADS) gemm_nt_kernel(GemmArgs g) {
                         const int lr = mt * 16 + (lane >> 4) * 4 + j;  // row within the pass
                         float v = acc[mt][nt][j] + bias_v[nt];
                         if constexpr (EPI == EPI_BIAS_GELU) v = gelu_erf(v);
-                        *reinterpret_cast<OutT *>(ot + lr * RS + lc * OE) = from_f32<OutT>(v);
+                        *reinterpret_cast<StT *>(ot + lr * RS + lc * SE) = from_f32<StT>(v);
                     }
                 }
             }
@@ -212,36 +214,34 @@ __global__ void __launch_bounds__(G_THREADS) gemm_nt_kernel(GemmArgs g) {
             const int id = tid + i * G_THREADS;
             const int lr = id / CPR, ch = id % CPR;
             const int row = row_base + lr;
-            const int col0 = n0 + ch * (16 / OE);
+            const int col0 = n0 + ch * EPCH;
             if (row >= M) continue;
             uint4 v = *reinterpret_cast<const uint4 *>(ot + lr * RS + ch * 16);
-            if (col0 + 16 / OE <= N) {
-                if constexpr (EPI == EPI_BIAS_RESID) {
-                    // 4 f32 outputs + 4 residual values of T
-                    const T *rp = static_cast<const T *>(g.resid) + (int64_t)row * N + col0;
-                    float r0, r1, r2, r3;
+            T *op = static_cast<T *>(g.out) + (int64_t)row * g.ld_out + col0;
+            if constexpr (EPI == EPI_BIAS_RESID) {
+                const T *rp = static_cast<const T *>(g.resid) + (int64_t)row * N + col0;
+                const float *f = reinterpret_cast<const float *>(&v);
+                if (col0 + 4 <= N) {
                     if constexpr (sizeof(T) == 2) {
-                        bf16x4 rv = *reinterpret_cast<const bf16x4 *>(rp);
-                        r0 = (float)rv[0]; r1 = (float)rv[1]; r2 = (float)rv[2]; r3 = (float)rv[3];
+                        const bf16x4 rv = *reinterpret_cast<const bf16x4 *>(rp);
+                        bf16x4 o;
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) o[q] = (bf16)(f[q] + (float)rv[q]);
+                        *reinterpret_cast<bf16x4 *>(op) = o;
                     } else {
-                        float4 rv = *reinterpret_cast<const float4 *>(rp);
-                        r0 = rv.x; r1 = rv.y; r2 = rv.z; r3 = rv.w;
+                        const float4 rv = *reinterpret_cast<const float4 *>(rp);
+                        *reinterpret_cast<float4 *>(op) =
+                            make_float4(f[0] + rv.x, f[1] + rv.y, f[2] + rv.z, f[3] + rv.w);
                     }
-                    v.x = __float_as_uint(__uint_as_float(v.x) + r0);
-                    v.y = __float_as_uint(__uint_as_float(v.y) + r1);
-                    v.z = __float_as_uint(__uint_as_float(v.z) + r2);
-                    v.w = __float_as_uint(__uint_as_float(v.w) + r3);
+                } else {  // ragged N tail
+                    for (int q = 0; q < 4 && col0 + q < N; ++q)
+                        op[q] = from_f32<T>(f[q] + to_f32(rp[q]));
                 }
-                *reinterpret_cast<uint4 *>(static_cast<OutT *>(g.out) + (int64_t)row * g.ld_out +
-                                           col0) = v;
+            } else if (col0 + EPCH <= N) {
+                *reinterpret_cast<uint4 *>(op) = v;
             } else {  // ragged N tail: element stores
-                const OutT *e = reinterpret_cast<const OutT *>(&v);
-                for (int q = 0; q < 16 / OE && col0 + q < N; ++q) {
-                    OutT x = e[q];
-                    if constexpr (EPI == EPI_BIAS_RESID)
-                        x += to_f32(static_cast<const T *>(g.resid)[(int64_t)row * N + col0 + q]);
-                    static_cast<OutT *>(g.out)[(int64_t)row * g.ld_out + col0 + q] = x;
-                }
+                const T *e = reinterpret_cast<const T *>(&v);
+                for (int q = 0; q < EPCH && col0 + q < N; ++q) op[q] = e[q];
             }
         }
         __syncthreads();

@@ -59,6 +59,18 @@ __global__ void __launch_bounds__(G2_T) gemm256_kernel(GemmArgs g) {
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wr = wave >> 2, wc = wave & 3;
 
+    // Epilogue stagger (speed only): every block ends in a burst of stores that
+    // is HBM-write-bound when all CUs reach it together, and with equal work per
+    // tile they stay in lockstep.  Delaying every other CU's first tile by about
+    // half a tile keeps the two halves out of phase for the whole launch.
+    if (g.stagger > 0) {
+        const int b0 = blockIdx.y * gridDim.x + blockIdx.x;
+        if (b0 < 256 && ((b0 >> 3) & 1)) {
+            const uint64_t t0 = __builtin_amdgcn_s_memtime();
+            while (__builtin_amdgcn_s_memtime() - t0 < (uint64_t)g.stagger)
+                __builtin_amdgcn_s_sleep(8);
+        }
+    }
     // tile order: XCD remap (bijective) + grouped GM x all-N order (speed only)
     const int n_tn = gridDim.x, n_tm = gridDim.y, n_tiles = n_tn * n_tm;
     int bid = blockIdx.y * gridDim.x + blockIdx.x;
@@ -326,17 +338,13 @@ __global__ void __launch_bounds__(G2_T) gemm256_kernel(GemmArgs g) {
             if constexpr (EPI == EPI_BIAS_RESID) {
                 const bf16x8 rv = *reinterpret_cast<const bf16x8 *>(
                     static_cast<const bf16 *>(g.resid) + (int64_t)row * N + col_l + h * 32);
-                float *op = static_cast<float *>(g.out) + o;
-                *reinterpret_cast<float4 *>(op) = float4{v[0] + (float)rv[0], v[1] + (float)rv[1],
-                                                         v[2] + (float)rv[2], v[3] + (float)rv[3]};
-                *reinterpret_cast<float4 *>(op + 4) = float4{
-                    v[4] + (float)rv[4], v[5] + (float)rv[5], v[6] + (float)rv[6], v[7] + (float)rv[7]};
-            } else {
-                bf16x8 ov;
 #pragma unroll
-                for (int e = 0; e < 8; ++e) ov[e] = (bf16)v[e];
-                *reinterpret_cast<bf16x8 *>(static_cast<bf16 *>(g.out) + o) = ov;
+                for (int e = 0; e < 8; ++e) v[e] += (float)rv[e];
             }
+            bf16x8 ov;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) ov[e] = (bf16)v[e];
+            *reinterpret_cast<bf16x8 *>(static_cast<bf16 *>(g.out) + o) = ov;
         }
     }
 }

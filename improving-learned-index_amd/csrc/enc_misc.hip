@@ -91,12 +91,25 @@ embed_ln_kernel(const int32_t *__restrict__ ids, const int32_t *__restrict__ cu,
     }
 }
 
-// x = LN(pre) (pre = GEMM output + bias + residual, f32).  With head_w: the
-// impact head of the reference (xlmr_original.py:34-38, :77-85) on the f32 LN
-// output: impact = act(x . w + b), act = Softplus(beta 1, threshold 20) or ReLU.
+// Impact head of the reference (xlmr_original.py:34-38, :77-85) on the f32 LN
+// output row: impact = act(x . w + b), act = Softplus(beta 1, threshold 20) or ReLU.
+__device__ __forceinline__ void head_out(float s, float head_b, int act, float *impact, int row) {
+    s = wave_sum_f(s) + head_b;
+    if ((threadIdx.x & 63) == 0) {
+        float y;
+        if (act == 0)  // nn.Softplus(beta=1, threshold=20)
+            y = (s > 20.0f) ? s : log1pf(expf(s));
+        else
+            y = s > 0.f ? s : 0.f;
+        impact[row] = y;
+    }
+}
+
+// x = LN(pre) (pre = GEMM output + bias + residual, T), one wave per row; with
+// head_w also the impact head.  Generic layout: lane holds x[lane + 64 i].
 template <typename T, int PL>
 __global__ void __launch_bounds__(256)
-ln_kernel(const float *__restrict__ pre, int M, int H, const float *__restrict__ gamma,
+ln_kernel(const T *__restrict__ pre, int M, int H, const float *__restrict__ gamma,
           const float *__restrict__ beta, float eps, T *__restrict__ out,
           const float *__restrict__ head_w, float head_b, int act, float *__restrict__ impact) {
     const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -106,7 +119,7 @@ ln_kernel(const float *__restrict__ pre, int M, int H, const float *__restrict__
 #pragma unroll
     for (int i = 0; i < PL; ++i) {
         const int c = lane + 64 * i;
-        v[i] = (c < H) ? pre[(int64_t)row * H + c] : 0.f;
+        v[i] = (c < H) ? to_f32(pre[(int64_t)row * H + c]) : 0.f;
     }
     ln_row<PL>(v, H, gamma, beta, eps);
     if (out) {
@@ -123,16 +136,73 @@ ln_kernel(const float *__restrict__ pre, int M, int H, const float *__restrict__
             const int c = lane + 64 * i;
             if (c < H) s += v[i] * head_w[c];
         }
-        s = wave_sum_f(s) + head_b;
-        if (lane == 0) {
-            float y;
-            if (act == 0)  // nn.Softplus(beta=1, threshold=20)
-                y = (s > 20.0f) ? s : log1pf(expf(s));
-            else
-                y = s > 0.f ? s : 0.f;
-            impact[row] = y;
+        head_out(s, head_b, act, impact, row);
+    }
+}
+
+// Vector form for H = 256 NC: lane holds x[256 c + 4 lane + j], j < 4 -- one
+// 8-byte (bf16) / 16-byte (f32) access per chunk instead of four scalar ones.
+template <typename T>
+__device__ __forceinline__ void ld4(const T *p, float (&f)[4]);
+template <>
+__device__ __forceinline__ void ld4<bf16>(const bf16 *p, float (&f)[4]) {
+    const bf16x4 v = *reinterpret_cast<const bf16x4 *>(p);
+    f[0] = (float)v[0]; f[1] = (float)v[1]; f[2] = (float)v[2]; f[3] = (float)v[3];
+}
+template <>
+__device__ __forceinline__ void ld4<float>(const float *p, float (&f)[4]) {
+    const float4 v = *reinterpret_cast<const float4 *>(p);
+    f[0] = v.x; f[1] = v.y; f[2] = v.z; f[3] = v.w;
+}
+__device__ __forceinline__ void st4(bf16 *p, const float (&f)[4]) {
+    *reinterpret_cast<bf16x4 *>(p) = bf16x4{(bf16)f[0], (bf16)f[1], (bf16)f[2], (bf16)f[3]};
+}
+__device__ __forceinline__ void st4(float *p, const float (&f)[4]) {
+    *reinterpret_cast<float4 *>(p) = make_float4(f[0], f[1], f[2], f[3]);
+}
+
+template <typename T, int NC>
+__global__ void __launch_bounds__(256)
+ln_vec_kernel(const T *__restrict__ pre, int M, const float *__restrict__ gamma,
+              const float *__restrict__ beta, float eps, T *__restrict__ out,
+              const float *__restrict__ head_w, float head_b, int act, float *__restrict__ impact) {
+    constexpr int H = 256 * NC;
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= M) return;
+    const int lane = threadIdx.x & 63;
+    float v[NC][4];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) ld4<T>(pre + (int64_t)row * H + 256 * c + 4 * lane, v[c]);
+    float s = 0.f;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) s += (v[c][0] + v[c][1]) + (v[c][2] + v[c][3]);
+    const float mean = wave_sum_f(s) / (float)H;
+    float q = 0.f;
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const float d = v[c][j] - mean;
+            q += d * d;
+        }
+    const float rstd = 1.0f / sqrtf(wave_sum_f(q) / (float)H + eps);
+    float hs = 0.f;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+        float gm[4], bt[4];
+        ld4<float>(gamma + 256 * c + 4 * lane, gm);
+        ld4<float>(beta + 256 * c + 4 * lane, bt);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[c][j] = (v[c][j] - mean) * rstd * gm[j] + bt[j];
+        if (out) st4(out + (int64_t)row * H + 256 * c + 4 * lane, v[c]);
+        if (head_w) {
+            float w[4];
+            ld4<float>(head_w + 256 * c + 4 * lane, w);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) hs += v[c][j] * w[j];
         }
     }
+    if (head_w) head_out(hs, head_b, act, impact, row);
 }
 
 // numpy's round(np.float32, 3) (reference indexer.py:132): fl32(rint(fl32(x*1000))/1000)
@@ -185,11 +255,17 @@ void launch_embed_ln(const int32_t *ids, const int32_t *cu, int n_docs, int M, i
 }
 
 template <typename T>
-void launch_ln(const float *pre, int M, int H, const float *gamma, const float *beta, float eps,
+void launch_ln(const T *pre, int M, int H, const float *gamma, const float *beta, float eps,
                T *out, const float *head_w, float head_b, int act, float *impact, hipStream_t s) {
     if (M == 0) return;
     dim3 grid((M + 3) / 4);
-    if (H <= 256)
+    if (H == 768)
+        hipLaunchKernelGGL((ln_vec_kernel<T, 3>), grid, dim3(256), 0, s, pre, M, gamma, beta, eps,
+                           out, head_w, head_b, act, impact);
+    else if (H == 1024)
+        hipLaunchKernelGGL((ln_vec_kernel<T, 4>), grid, dim3(256), 0, s, pre, M, gamma, beta, eps,
+                           out, head_w, head_b, act, impact);
+    else if (H <= 256)
         hipLaunchKernelGGL((ln_kernel<T, 4>), grid, dim3(256), 0, s, pre, M, H, gamma, beta, eps,
                            out, head_w, head_b, act, impact);
     else if (H <= 768)
@@ -217,7 +293,7 @@ template void launch_embed_ln<float>(const int32_t *, const int32_t *, int, int,
                                      const float *, const float *, const float *, const float *,
                                      const float *, float, int, int, int, float *, int32_t *,
                                      hipStream_t);
-template void launch_ln<bf16>(const float *, int, int, const float *, const float *, float, bf16 *,
+template void launch_ln<bf16>(const bf16 *, int, int, const float *, const float *, float, bf16 *,
                               const float *, float, int, float *, hipStream_t);
 template void launch_ln<float>(const float *, int, int, const float *, const float *, float,
                                float *, const float *, float, int, float *, hipStream_t);

@@ -32,7 +32,7 @@ void launch_embed_ln(const int32_t *ids, const int32_t *cu, int n_docs, int M, i
                      const float *beta, float eps, int pos_offset, int vocab, int max_pos, T *out,
                      int32_t *err, hipStream_t s);
 template <typename T>
-void launch_ln(const float *pre, int M, int H, const float *gamma, const float *beta, float eps,
+void launch_ln(const T *pre, int M, int H, const float *gamma, const float *beta, float eps,
                T *out, const float *head_w, float head_b, int act, float *impact, hipStream_t s);
 void launch_vt_cols(const int32_t *cu, int n_docs, int M, int32_t *vcol, hipStream_t s);
 int vt_ld(int64_t M, int n_docs);
@@ -157,7 +157,7 @@ void ensure_workspace(di_encoder *e, int64_t M, int n_docs, int64_t n_terms) {
         e->ctx.reserve(capr * H * es);
         e->qk.reserve(cap * 2 * H * es);
         e->Hff.reserve(capr * F * es);
-        e->pre.reserve(cap * H * 4);
+        e->pre.reserve(cap * H * es);
         e->impact.reserve(cap * 4);
         e->ids.reserve(cap * 4);
         e->vcol.reserve(cap * 4);
@@ -238,7 +238,7 @@ void forward(di_encoder *e, const int32_t *d_ids, const int32_t *d_cu, int n_doc
         }
         {
             TimedLaunch tl(e->timer, timing, "ln", s);
-            launch_ln<T>(e->pre.as<float>(), (int)M, H, L.ln1_g.as<float>(), L.ln1_b.as<float>(),
+            launch_ln<T>(e->pre.as<T>(), (int)M, H, L.ln1_g.as<float>(), L.ln1_b.as<float>(),
                          c.layer_norm_eps, X1, nullptr, 0.f, c.activation, nullptr, s);
         }
         // FFN
@@ -274,7 +274,7 @@ void forward(di_encoder *e, const int32_t *d_ids, const int32_t *d_cu, int n_doc
         {
             TimedLaunch tl(e->timer, timing, "ln", s);
             // the last LayerNorm feeds only the impact head
-            launch_ln<T>(e->pre.as<float>(), (int)M, H, L.ln2_g.as<float>(), L.ln2_b.as<float>(),
+            launch_ln<T>(e->pre.as<T>(), (int)M, H, L.ln2_g.as<float>(), L.ln2_b.as<float>(),
                          c.layer_norm_eps, last ? nullptr : X,
                          last ? e->head_w.as<float>() : nullptr, e->head_b, c.activation,
                          last ? e->impact.as<float>() : nullptr, s);

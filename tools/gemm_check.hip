@@ -112,7 +112,7 @@ int main(int argc, char **argv) {
                 launch_gemm<bf16>(c.epi, args(c, O2, V2, true), 0);
                 CK(hipDeviceSynchronize());
                 const int ocols = c.epi == EPI_QKV ? 2 * c.hidden : c.N;
-                const size_t esz = c.epi == EPI_BIAS_RESID ? 4 : 2;
+                const size_t esz = 2;  // every epilogue writes bf16
                 const size_t nb = (size_t)M * ocols * esz;
                 std::vector<unsigned char> a(nb), b(nb);
                 CK(hipMemcpy(a.data(), O1, nb, hipMemcpyDeviceToHost));
@@ -187,10 +187,12 @@ int main(int argc, char **argv) {
             const Case &c = bench[i];
             const double flops = 2.0 * c.M * c.N * c.K;
             for (int abl = 0; abl < 2; ++abl) {
-                for (int gm : {1, 2, 4, 8, 16}) {
+                for (int stg : {0, 2000, 5000, 10000, 20000, 40000}) {
+                    const int gm = 8;
                     GemmArgs g = args(c, O1, V1, true);
                     g.tune_gm = gm;
                     g.ablate = abl;
+                    g.stagger = stg;
                     for (int w = 0; w < 2; ++w) launch_gemm<bf16>(c.epi, g, 0);
                     CK(hipEventRecord(a0, 0));
                     for (int w = 0; w < 10; ++w) launch_gemm<bf16>(c.epi, g, 0);
@@ -199,8 +201,8 @@ int main(int argc, char **argv) {
                     float ms;
                     CK(hipEventElapsedTime(&ms, a0, a1));
                     ms /= 10;
-                    printf("sweep %-5s ablate=%d gm=%2d  %.3f ms  %.0f TF\n", names[i], abl, gm, ms,
-                           flops / ms / 1e9);
+                    printf("sweep %-5s ablate=%d gm=%2d stagger=%5d  %.3f ms  %.0f TF\n", names[i],
+                           abl, gm, stg, ms, flops / ms / 1e9);
                 }
             }
         }
