@@ -9,6 +9,9 @@
 // tokens only.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+#include <type_traits>
+
 #include <cmath>
 #include <cstring>
 #include <memory>
@@ -35,6 +38,9 @@ template <typename T>
 void launch_ln(const T *pre, int M, int H, const float *gamma, const float *beta, float eps,
                T *out, const float *head_w, float head_b, int act, float *impact, hipStream_t s);
 void launch_vt_cols(const int32_t *cu, int n_docs, int M, int32_t *vcol, hipStream_t s);
+bool attention_v3_ok(int max_len, int H);
+void launch_attention_v3(const bf16 *qkv, const int32_t *cu_seqlens, int n_docs, int max_len,
+                         int H, bf16 *ctx, hipStream_t s);
 int vt_ld(int64_t M, int n_docs);
 void launch_gather_terms(const float *impact, const int32_t *cu_seq, const int32_t *cu_terms,
                          int n_docs, const int32_t *term_tok, int n_terms, int do_round,
@@ -155,7 +161,7 @@ void ensure_workspace(di_encoder *e, int64_t M, int n_docs, int64_t n_terms) {
         e->X.reserve(capr * H * es);
         e->X1.reserve(capr * H * es);
         e->ctx.reserve(capr * H * es);
-        e->qk.reserve(cap * 2 * H * es);
+        e->qk.reserve(cap * 3 * H * es);  // [M][3H] (v3 path) or [M][2H] + V^T
         e->Hff.reserve(capr * F * es);
         e->pre.reserve(cap * H * es);
         e->impact.reserve(cap * 4);
@@ -192,7 +198,14 @@ void forward(di_encoder *e, const int32_t *d_ids, const int32_t *d_cu, int n_doc
                            c.layer_norm_eps, pos_offset, c.vocab_size, c.max_positions, X,
                            e->err.as<int32_t>(), s);
     }
-    launch_vt_cols(d_cu, n_docs, (int)M, e->vcol.as<int32_t>(), s);
+    // attention path: DI_ATTN unset or 3 = v3 when it applies (bf16, max_len <= 320)
+    static const int attn_mode = [] {
+        const char *v = std::getenv("DI_ATTN");
+        return v ? std::atoi(v) : 3;
+    }();
+    const bool use_v3 = std::is_same<T, bf16>::value && attn_mode == 3 &&
+                        attention_v3_ok(max_len, H);
+    if (!use_v3) launch_vt_cols(d_cu, n_docs, (int)M, e->vcol.as<int32_t>(), s);
     for (size_t l = 0; l < e->layers.size(); ++l) {
         Layer &L = *e->layers[l];
         const bool last = l + 1 == e->layers.size();
@@ -200,25 +213,46 @@ void forward(di_encoder *e, const int32_t *d_ids, const int32_t *d_cu, int n_doc
         g.M = (int)M;
         g.a_rows = e->cap_rows;
         g.hidden = H;
-        // QKV (V written transposed for the attention kernel)
-        g.A = X;
-        g.B = L.w_qkv.p;
-        g.bias = L.b_qkv.as<float>();
-        g.out = e->qk.p;
-        g.out2 = e->vt.p;
-        g.N = 3 * H;
-        g.K = H;
-        g.ld_out = 2 * H;
-        g.ld_v = e->ld_v;
-        g.vcol = e->vcol.as<int32_t>();
-        {
-            TimedLaunch tl(e->timer, timing, "gemm_qkv", s);
-            launch_gemm<T>(EPI_QKV, g, s);
-        }
-        {
-            TimedLaunch tl(e->timer, timing, "attention", s);
-            launch_attention<T>(e->qk.as<T>(), e->vt.as<T>(), d_cu, n_docs, max_len, H, e->ld_v,
-                                e->ctx.as<T>(), s);
+        // QKV projection + attention.  bf16 with max_len <= 320: row-major [M][3H]
+        // and the persistent LDS-DMA attention (v3); otherwise Q|K row-major with V
+        // written transposed (doc-aligned V^T) for the generic attention kernels.
+        if (use_v3) {
+            g.A = X;
+            g.B = L.w_qkv.p;
+            g.bias = L.b_qkv.as<float>();
+            g.out = e->qk.p;
+            g.N = 3 * H;
+            g.K = H;
+            g.ld_out = 3 * H;
+            {
+                TimedLaunch tl(e->timer, timing, "gemm_qkv", s);
+                launch_gemm<T>(EPI_BIAS, g, s);
+            }
+            {
+                TimedLaunch tl(e->timer, timing, "attention", s);
+                launch_attention_v3(e->qk.as<bf16>(), d_cu, n_docs, max_len, H, e->ctx.as<bf16>(),
+                                    s);
+            }
+        } else {
+            g.A = X;
+            g.B = L.w_qkv.p;
+            g.bias = L.b_qkv.as<float>();
+            g.out = e->qk.p;
+            g.out2 = e->vt.p;
+            g.N = 3 * H;
+            g.K = H;
+            g.ld_out = 2 * H;
+            g.ld_v = e->ld_v;
+            g.vcol = e->vcol.as<int32_t>();
+            {
+                TimedLaunch tl(e->timer, timing, "gemm_qkv", s);
+                launch_gemm<T>(EPI_QKV, g, s);
+            }
+            {
+                TimedLaunch tl(e->timer, timing, "attention", s);
+                launch_attention<T>(e->qk.as<T>(), e->vt.as<T>(), d_cu, n_docs, max_len, H,
+                                    e->ld_v, e->ctx.as<T>(), s);
+            }
         }
         // attention output + residual -> LN1
         g = GemmArgs{};
