@@ -63,6 +63,8 @@ enum GemmEpi : int {
     EPI_BIAS_GELU = 1,   // out(T) = gelu(acc + bias)
     EPI_BIAS_RESID = 2,  // out(T) = acc + bias + resid(T), one rounding (pre-LayerNorm)
     EPI_QKV = 3,         // Q,K -> qk[M][2H] (T);  V -> vt[H][ldv] transposed (T)
+    EPI_BIAS_RESID_LN = 4,  // as EPI_BIAS_RESID into out, then LayerNorm of the whole
+                            // rows -> ln_out (and / or the impact head); 256-col tiles only
 };
 
 struct GemmArgs {
@@ -83,6 +85,15 @@ struct GemmArgs {
     int ablate;           // profiling only (tools/gemm_check): 1 = skip the epilogue
     int stagger;          // 256-tile kernel: first-wave delay (shader cycles) of every other
                           // CU's first tile, so the CUs' store bursts alternate (0 = off)
+    // EPI_BIAS_RESID_LN: LayerNorm(gamma, beta, eps) of the out rows -> ln_out (may be
+    // null); with head_w, impact[row] = act(LN(row) . head_w + head_b)
+    const float *ln_gamma, *ln_beta;
+    float ln_eps;
+    void *ln_out;
+    const float *head_w;
+    float head_b;
+    int act;
+    float *impact;
 };
 
 }  // namespace di

@@ -39,6 +39,7 @@ void launch_ln(const T *pre, int M, int H, const float *gamma, const float *beta
                T *out, const float *head_w, float head_b, int act, float *impact, hipStream_t s);
 void launch_vt_cols(const int32_t *cu, int n_docs, int M, int32_t *vcol, hipStream_t s);
 bool attention_v3_ok(int max_len, int H);
+bool gemm_fused_ln_ok(const GemmArgs &g);
 void launch_attention_v3(const bf16 *qkv, const int32_t *cu_seqlens, int n_docs, int max_len,
                          int H, bf16 *ctx, hipStream_t s);
 int vt_ld(int64_t M, int n_docs);
@@ -254,7 +255,7 @@ void forward(di_encoder *e, const int32_t *d_ids, const int32_t *d_cu, int n_doc
                                     e->ld_v, e->ctx.as<T>(), s);
             }
         }
-        // attention output + residual -> LN1
+        // attention output + residual -> LN1 (fused into the GEMM when it can be)
         g = GemmArgs{};
         g.M = (int)M;
         g.a_rows = e->cap_rows;
@@ -266,11 +267,16 @@ void forward(di_encoder *e, const int32_t *d_ids, const int32_t *d_cu, int n_doc
         g.N = H;
         g.K = H;
         g.ld_out = H;
+        g.ln_gamma = L.ln1_g.as<float>();
+        g.ln_beta = L.ln1_b.as<float>();
+        g.ln_eps = c.layer_norm_eps;
+        g.ln_out = X1;
+        const bool fuse_o = std::is_same<T, bf16>::value && gemm_fused_ln_ok(g);
         {
             TimedLaunch tl(e->timer, timing, "gemm_o", s);
-            launch_gemm<T>(EPI_BIAS_RESID, g, s);
+            launch_gemm<T>(fuse_o ? EPI_BIAS_RESID_LN : EPI_BIAS_RESID, g, s);
         }
-        {
+        if (!fuse_o) {
             TimedLaunch tl(e->timer, timing, "ln", s);
             launch_ln<T>(e->pre.as<T>(), (int)M, H, L.ln1_g.as<float>(), L.ln1_b.as<float>(),
                          c.layer_norm_eps, X1, nullptr, 0.f, c.activation, nullptr, s);
@@ -290,6 +296,7 @@ void forward(di_encoder *e, const int32_t *d_ids, const int32_t *d_cu, int n_doc
             TimedLaunch tl(e->timer, timing, "gemm_ffn1", s);
             launch_gemm<T>(EPI_BIAS_GELU, g, s);
         }
+        // FFN output + residual -> LN2; the last LayerNorm feeds only the impact head
         g = GemmArgs{};
         g.M = (int)M;
         g.a_rows = e->cap_rows;
@@ -301,13 +308,21 @@ void forward(di_encoder *e, const int32_t *d_ids, const int32_t *d_cu, int n_doc
         g.N = H;
         g.K = F;
         g.ld_out = H;
+        g.ln_gamma = L.ln2_g.as<float>();
+        g.ln_beta = L.ln2_b.as<float>();
+        g.ln_eps = c.layer_norm_eps;
+        g.ln_out = last ? nullptr : X;
+        g.head_w = last ? e->head_w.as<float>() : nullptr;
+        g.head_b = e->head_b;
+        g.act = c.activation;
+        g.impact = last ? e->impact.as<float>() : nullptr;
+        const bool fuse_f = std::is_same<T, bf16>::value && gemm_fused_ln_ok(g);
         {
             TimedLaunch tl(e->timer, timing, "gemm_ffn2", s);
-            launch_gemm<T>(EPI_BIAS_RESID, g, s);
+            launch_gemm<T>(fuse_f ? EPI_BIAS_RESID_LN : EPI_BIAS_RESID, g, s);
         }
-        {
+        if (!fuse_f) {
             TimedLaunch tl(e->timer, timing, "ln", s);
-            // the last LayerNorm feeds only the impact head
             launch_ln<T>(e->pre.as<T>(), (int)M, H, L.ln2_g.as<float>(), L.ln2_b.as<float>(),
                          c.layer_norm_eps, last ? nullptr : X,
                          last ? e->head_w.as<float>() : nullptr, e->head_b, c.activation,

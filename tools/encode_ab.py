@@ -1,0 +1,29 @@
+"""Developer A/B check of encoder code paths on the GPU box: encodes a fixed synthetic
+batch (bench weights/lengths) and writes the per-token impacts to a .npy, so two runs
+with different DI_* knobs (e.g. DI_FUSED_LN=1, DI_ATTN=1) can be compared:
+    python tools/encode_ab.py out_a.npy && DI_FUSED_LN=1 python tools/encode_ab.py out_b.npy
+    python tools/encode_ab.py --compare out_a.npy out_b.npy
+"""
+import sys
+from pathlib import Path
+
+import numpy as np
+
+sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
+
+if sys.argv[1] == "--compare":
+    a, b = np.load(sys.argv[2]), np.load(sys.argv[3])
+    d = np.abs(a - b)
+    print(f"n={a.size} identical={np.mean(a == b):.6f} max_abs={d.max():.3e} "
+          f"max_rel={np.max(d / (np.abs(a) + 1e-3)):.3e}")
+    sys.exit(0)
+
+import bench  # noqa: E402
+from improving_learned_index_amd.encoder import DeviceEncoder, EncoderConfig  # noqa: E402
+
+cfg = EncoderConfig.xlmr_base()
+enc = DeviceEncoder(bench.synthetic_state_dict(cfg, seed=0), cfg, precision="bf16", device=0)
+ids, cu, lens, tt, ct = bench.synthetic_docs_tokens(256, cfg.vocab_size, seed=100, max_len=300)
+out = enc.encode_packed(ids, cu, token_impacts=True)
+np.save(sys.argv[1], out)
+print("saved", out.shape, float(out.mean()))

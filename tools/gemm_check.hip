@@ -186,8 +186,8 @@ int main(int argc, char **argv) {
         for (int i = 0; i < 4; ++i) {
             const Case &c = bench[i];
             const double flops = 2.0 * c.M * c.N * c.K;
-            for (int abl = 0; abl < 2; ++abl) {
-                for (int stg : {0, 2000, 5000, 10000, 20000, 40000}) {
+            for (int abl : {0, 1, 2, 4, 6}) {
+                for (int stg : {0, 10000}) {
                     const int gm = 8;
                     GemmArgs g = args(c, O1, V1, true);
                     g.tune_gm = gm;
