@@ -262,7 +262,7 @@ def encode_leg(args, rank, world, dev):
         el = float(t.item())
     kernels = {}
     for name in ("embed_ln", "gemm_qkv", "attention", "gemm_o", "ln", "gemm_ffn1", "gemm_ffn2",
-                 "gather_terms"):
+                 "row_ln", "head", "gather_terms"):
         ms, n = enc.timing(name)
         kernels[name] = {"ms_per_step": ms / max(args.steps, 1), "launches": n}
     M, H, F, L = float(cu[-1]), cfg.hidden, cfg.intermediate, cfg.layers

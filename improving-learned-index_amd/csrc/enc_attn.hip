@@ -571,12 +571,16 @@ attention_lds_kernel(const bf16 *__restrict__ qk, const bf16 *__restrict__ vt,
 //            ds_read_b64_tr_b16: per 16-lane group, lane 4q+p addresses key row
 //            q of a 4-row block, columns 4p..4p+3; lane i receives column i.
 // Eight waves, 32 queries (two 16-query tiles) per wave-block, blocks round robin.
+// DB = true : two buffers of 320 K + 320 V rows (80 KiB each, 160 KiB: the whole
+//             CU), next pair prefetched during the current one; n <= 320.
+// DB = false: one buffer of 512 + 512 rows (128 KiB), no prefetch; n <= 512.
 constexpr int ATT3_WAVES = 8;
-constexpr int ATT3_MAXLEN = 320;
-constexpr int ATT3_KROWS = 320;                 // K image rows (n rounded to 8)
-constexpr int ATT3_VROWS = 320;                 // V image rows (n rounded to 32)
-constexpr int ATT3_BUF = (ATT3_KROWS + ATT3_VROWS) * 128;  // 80 KiB
-constexpr int ATT3_LDS = 2 * ATT3_BUF;                     // 160 KiB: the whole CU
+template <bool DB>
+struct Att3 {
+    static constexpr int ROWS = DB ? 320 : 512;  // K and V image rows each
+    static constexpr int BUF = 2 * ROWS * 128;
+    static constexpr int LDS = DB ? 2 * BUF : BUF;
+};
 
 __device__ __forceinline__ uint2 ds_read_tr_b16(uint32_t addr) {
     uint2 r;
@@ -584,6 +588,7 @@ __device__ __forceinline__ uint2 ds_read_tr_b16(uint32_t addr) {
     return r;
 }
 
+template <bool DB>
 __global__ void __launch_bounds__(64 * ATT3_WAVES, 1)
 attention_v3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu_seqlens, int H,
                     int n_heads, int n_pairs, bf16 *__restrict__ ctx) {
@@ -606,13 +611,13 @@ attention_v3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
         const int chunk = ((lane & 7) ^ r_in) * 8;  // source chunk (elements), swizzled
         const bf16 *kbase = qkv + (int64_t)tok0 * ld + H + h * ATT_D + chunk;
         const bf16 *vbase = qkv + (int64_t)tok0 * ld + 2 * H + h * ATT_D + chunk;
-        unsigned char *buf = lds + b * ATT3_BUF;
+        unsigned char *buf = lds + b * Att3<DB>::BUF;
         for (int pc = wave; pc < nk8 + nv8; pc += ATT3_WAVES) {
             const bool is_k = pc < nk8;
             const int piece = is_k ? pc : pc - nk8;
             const int r = min(piece * 8 + r_in, n - 1);
             const bf16 *src = (is_k ? kbase : vbase) + (int64_t)r * ld;
-            unsigned char *dst = buf + (is_k ? 0 : ATT3_KROWS * 128) + piece * 1024;
+            unsigned char *dst = buf + (is_k ? 0 : Att3<DB>::ROWS * 128) + piece * 1024;
             __builtin_amdgcn_global_load_lds((const void *)src, (lds_void *)dst, 16, 0, 0);
         }
     };
@@ -625,8 +630,9 @@ attention_v3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
     const int tq = c >> 2, tp = c & 3;
 
     int p = blockIdx.x, b = 0;
-    if (p < n_pairs) stage(p, 0);
-    for (; p < n_pairs; p += gridDim.x, b ^= 1) {
+    if (DB && p < n_pairs) stage(p, 0);
+    for (; p < n_pairs; p += gridDim.x, b ^= (DB ? 1 : 0)) {
+        if (!DB) stage(p, 0);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this pair's copy (+ old stores)
         __syncthreads();
         const int doc = p / n_heads, h = p % n_heads;
@@ -659,10 +665,10 @@ attention_v3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
                     asm volatile("" : "+v"(t.x), "+v"(t.y), "+v"(t.z), "+v"(t.w));
                     qf[i][qt][ch] = t;
                 }
-        if (p + (int)gridDim.x < n_pairs) stage(p + gridDim.x, b ^ 1);
+        if (DB && p + (int)gridDim.x < n_pairs) stage(p + gridDim.x, b ^ 1);
 
-        const uint32_t kim = lds_base + b * ATT3_BUF;
-        const uint32_t vim = kim + ATT3_KROWS * 128;
+        const uint32_t kim = lds_base + b * Att3<DB>::BUF;
+        const uint32_t vim = kim + Att3<DB>::ROWS * 128;
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
             const int qb = wave + i * ATT3_WAVES;
@@ -755,12 +761,11 @@ attention_v3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
     }
 }
 
-bool attention_v3_ok(int max_len, int H) { return max_len <= ATT3_MAXLEN && H % ATT_D == 0; }
+bool attention_v3_ok(int max_len, int H) { return max_len <= 512 && H % ATT_D == 0; }
 
 void launch_attention_v3(const bf16 *qkv, const int32_t *cu_seqlens, int n_docs, int max_len,
                          int H, bf16 *ctx, hipStream_t s) {
-    DI_REQUIRE(attention_v3_ok(max_len, H), DI_EINVAL, "attention v3: max_len %d > %d", max_len,
-               ATT3_MAXLEN);
+    DI_REQUIRE(attention_v3_ok(max_len, H), DI_EINVAL, "attention v3: max_len %d > 512", max_len);
     if (n_docs == 0 || max_len == 0) return;
     static int n_cu = [] {
         int dev = 0, v = 0;
@@ -769,11 +774,18 @@ void launch_attention_v3(const bf16 *qkv, const int32_t *cu_seqlens, int n_docs,
         return v > 0 ? v : 256;
     }();
     const int n_heads = H / ATT_D, n_pairs = n_docs * n_heads;
-    DI_HIP(hipFuncSetAttribute((const void *)attention_v3_kernel,
-                               hipFuncAttributeMaxDynamicSharedMemorySize, ATT3_LDS));
     const int grid = std::min(n_pairs, n_cu);
-    hipLaunchKernelGGL(attention_v3_kernel, dim3(grid), dim3(64 * ATT3_WAVES), ATT3_LDS, s, qkv,
-                       cu_seqlens, H, n_heads, n_pairs, ctx);
+    if (max_len <= Att3<true>::ROWS) {
+        DI_HIP(hipFuncSetAttribute((const void *)attention_v3_kernel<true>,
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, Att3<true>::LDS));
+        hipLaunchKernelGGL(attention_v3_kernel<true>, dim3(grid), dim3(64 * ATT3_WAVES),
+                           Att3<true>::LDS, s, qkv, cu_seqlens, H, n_heads, n_pairs, ctx);
+    } else {
+        DI_HIP(hipFuncSetAttribute((const void *)attention_v3_kernel<false>,
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, Att3<false>::LDS));
+        hipLaunchKernelGGL(attention_v3_kernel<false>, dim3(grid), dim3(64 * ATT3_WAVES),
+                           Att3<false>::LDS, s, qkv, cu_seqlens, H, n_heads, n_pairs, ctx);
+    }
     check_launch("attention_v3");
 }
 

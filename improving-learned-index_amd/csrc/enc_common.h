@@ -65,6 +65,14 @@ enum GemmEpi : int {
     EPI_QKV = 3,         // Q,K -> qk[M][2H] (T);  V -> vt[H][ldv] transposed (T)
     EPI_BIAS_RESID_LN = 4,  // as EPI_BIAS_RESID into out, then LayerNorm of the whole
                             // rows -> ln_out (and / or the impact head); 256-col tiles only
+    // LayerNorm folding (bf16, 256-col tiles): the GEMM that consumes LN(x) takes the
+    // un-normalised x and weights W' = W diag(gamma) and corrects per row / column:
+    //   LN(x) W^T + b = r (x W'^T) - r mu s + c,  s = W' 1,  c = b + W beta
+    EPI_FOLD = 5,           // out(T) = r acc - r mu s + c           (row params: row_ln)
+    EPI_FOLD_GELU = 6,      // out(T) = gelu(r acc - r mu s + c)
+    EPI_RESID_STATS = 7,    // out(T) = acc + bias + LNin(resid), plus per-row partial
+                            // (sum, sum of squares, head dot) of the rounded out over
+                            // this tile's 256 columns -> stats_out[n0/256][row]
 };
 
 struct GemmArgs {
@@ -94,6 +102,16 @@ struct GemmArgs {
     float head_b;
     int act;
     float *impact;
+    // LayerNorm folding: row statistics as float4 partials (sum, sumsq, dot, 0) per
+    // 256-column tile: stats[t * stats_ld + row], t < n_part
+    const float2 *row_ln;     // EPI_FOLD*: (rstd, -rstd mean) of A's rows; EPI_RESID_STATS:
+                              // of resid's rows (null: plain residual)
+    float4 *stats_out;        // EPI_RESID_STATS
+    int stats_ld, n_part, ln_h;
+    const float *col_s, *col_c;          // EPI_FOLD*
+    const float *res_gamma, *res_beta;   // EPI_RESID_STATS: LN params of resid
+    const float *head_wg;                // EPI_RESID_STATS: w * gamma for the dot partial
 };
+
 
 }  // namespace di

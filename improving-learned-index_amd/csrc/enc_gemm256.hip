@@ -47,7 +47,13 @@ namespace di {
 constexpr int G2_T = 512;
 constexpr int G2_TILE = 256;
 constexpr int G2_BUF = 65536;                  // one K tile: A image 32 KiB + B image 32 KiB
-constexpr int G2_LDS = 2 * G2_BUF;
+// Epilogue parameters of the tile, staged by LDS-DMA with the prologue (their load
+// latency then hides behind the K loop): 256 row params (float2) + up to four
+// 256-column float vectors (bias or c, s or gamma, beta, head w*gamma).
+constexpr int G2_PAR = 2 * G2_BUF;            // byte offset of the parameter area
+constexpr int G2_PAR_ROW = 0, G2_PAR_C0 = 2048, G2_PAR_C1 = 3072, G2_PAR_C2 = 4096,
+              G2_PAR_C3 = 5120;
+constexpr int G2_LDS = 2 * G2_BUF + 6144;
 
 #define G2_BAR() asm volatile("s_barrier" ::: "memory")
 
@@ -199,6 +205,32 @@ __global__ void __launch_bounds__(G2_T) gemm256_kernel(GemmArgs g) {
     } while (0)
 #define G2_SYNC_READS() asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory")
 
+    // ---- epilogue parameters (wave 0; older than every stage load, so the
+    // prologue's counted wait retires them) -----------------------------------------
+    {
+        constexpr bool FOLD = EPI == EPI_FOLD || EPI == EPI_FOLD_GELU;
+        constexpr bool RS = EPI == EPI_RESID_STATS;
+        if (wave == 0) {
+            auto par1k = [&](const void *src, int off) {  // 1 KiB: 16 B per lane
+                __builtin_amdgcn_global_load_lds(
+                    (const void *)(static_cast<const char *>(src) + lane * 16),
+                    (lds_void *)(lds + G2_PAR + off), 16, 0, 0);
+            };
+            par1k((FOLD ? g.col_c : g.bias) + n0, G2_PAR_C0);
+            if (FOLD) par1k(g.col_s + n0, G2_PAR_C1);
+            if (RS && g.row_ln) {
+                par1k(g.res_gamma + n0, G2_PAR_C1);
+                par1k(g.res_beta + n0, G2_PAR_C2);
+            }
+            if (RS && g.head_wg) par1k(g.head_wg + n0, G2_PAR_C3);
+            if (FOLD || (RS && g.row_ln)) {
+                int m0r = m0;
+                asm volatile("" : "+s"(m0r));
+                par1k(g.row_ln + m0r, G2_PAR_ROW);
+                par1k(g.row_ln + m0r + 128, G2_PAR_ROW + 1024);
+            }
+        }
+    }
     // ---- prologue: K tile 0 whole, K tile 1 minus its B1 half --------------------
     G2_STAGE_A(0, 0, 0);
     G2_STAGE_B(0, 0, 0);
@@ -303,14 +335,21 @@ __global__ void __launch_bounds__(G2_T) gemm256_kernel(GemmArgs g) {
     asm volatile("" : "+s"(m0e));
     const int row_l = m0e + wr * 128 + (lane & 15);
     const int col_l = n0 + wc * 64 + (lane >> 4) * 8;
-    float bias_v[2][8];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-        const float4 b0 = *reinterpret_cast<const float4 *>(g.bias + col_l + h * 32);
-        const float4 b1 = *reinterpret_cast<const float4 *>(g.bias + col_l + h * 32 + 4);
-        bias_v[h][0] = b0.x; bias_v[h][1] = b0.y; bias_v[h][2] = b0.z; bias_v[h][3] = b0.w;
-        bias_v[h][4] = b1.x; bias_v[h][5] = b1.y; bias_v[h][6] = b1.z; bias_v[h][7] = b1.w;
-    }
+    // tile-local indices into the staged parameters
+    const int prow = wr * 128 + (lane & 15);          // + mt * 16
+    const int pcol = wc * 64 + (lane >> 4) * 8;        // + h * 32 + e
+    auto par8 = [&](int off, int h, float (&v)[8]) {   // 8 column params from LDS
+        const float4 a = *reinterpret_cast<const float4 *>(lds + G2_PAR + off + (pcol + h * 32) * 4);
+        const float4 b = *reinterpret_cast<const float4 *>(lds + G2_PAR + off + (pcol + h * 32 + 4) * 4);
+        v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+        v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+    };
+    auto prow2 = [&](int mt) {  // (rstd, -rstd mean) of row prow + 16 mt
+        return *reinterpret_cast<const float2 *>(lds + G2_PAR + G2_PAR_ROW + (prow + mt * 16) * 8);
+    };
+    float bias_v[2][8];  // (the folded epilogues carry their bias inside col_c)
+    par8(G2_PAR_C0, 0, bias_v[0]);
+    par8(G2_PAR_C0, 1, bias_v[1]);
     if constexpr (EPI == EPI_QKV) {
         if (n0 >= 2 * g.hidden) {  // V columns: transposed element stores into V^T
             bf16 *vt = static_cast<bf16 *>(g.out2) + (int64_t)(col_l - 2 * g.hidden) * g.ld_v;
@@ -330,6 +369,128 @@ __global__ void __launch_bounds__(G2_T) gemm256_kernel(GemmArgs g) {
             return;
         }
     }
+    if constexpr (EPI == EPI_FOLD || EPI == EPI_FOLD_GELU) {
+        // LN folded into this GEMM: y = r acc - r mu s + c  (per row r, mu; per column s, c)
+        float ra[8], rb[8];
+#pragma unroll
+        for (int mt = 0; mt < 8; ++mt) {
+            const float2 p = prow2(mt);
+            ra[mt] = p.x;
+            rb[mt] = p.y;
+        }
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            float cs[8];
+            par8(G2_PAR_C1, h, cs);
+            const float(&cc)[8] = bias_v[h];
+#pragma unroll
+            for (int mt = 0; mt < 8; ++mt) {
+                const int row = row_l + mt * 16;
+                if (row >= M) continue;
+                float v[8];
+#pragma unroll
+                for (int e = 0; e < 8; ++e)
+                    v[e] = fmaf(ra[mt], acc[mt][2 * h + (e >> 2)][e & 3], fmaf(rb[mt], cs[e], cc[e]));
+                if constexpr (EPI == EPI_FOLD_GELU) {
+#pragma unroll
+                    for (int e = 0; e < 8; e += 2) {
+                        const f32x2 y = gelu_erf2(f32x2{v[e], v[e + 1]});
+                        v[e] = y.x;
+                        v[e + 1] = y.y;
+                    }
+                }
+                bf16x8 ov;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) ov[e] = (bf16)v[e];
+                *reinterpret_cast<bf16x8 *>(static_cast<bf16 *>(g.out) + (int64_t)row * g.ld_out +
+                                            col_l + h * 32) = ov;
+            }
+        }
+    } else if constexpr (EPI == EPI_RESID_STATS) {
+        // out = acc + bias + LN(resid) (resid normalised on the fly from its row
+        // statistics, or plain), and this tile's partial statistics of the rounded out
+        const bool res_ln = g.row_ln != nullptr;
+        float ra[8], rb[8], ss[8], sq[8], sd[8];
+#pragma unroll
+        for (int mt = 0; mt < 8; ++mt) {
+            ss[mt] = sq[mt] = sd[mt] = 0.f;
+            ra[mt] = 1.f;
+            rb[mt] = 0.f;
+            if (res_ln) {
+                const float2 p = prow2(mt);
+                ra[mt] = p.x;
+                rb[mt] = p.y;
+            }
+        }
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            float gm[8], bt[8], wg[8];
+            if (res_ln) {
+                par8(G2_PAR_C1, h, gm);
+                par8(G2_PAR_C2, h, bt);
+            } else {
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    gm[e] = 1.f;
+                    bt[e] = 0.f;
+                }
+            }
+            if (g.head_wg) {
+                par8(G2_PAR_C3, h, wg);
+            } else {
+#pragma unroll
+                for (int e = 0; e < 8; ++e) wg[e] = 0.f;
+            }
+#pragma unroll
+            for (int mt = 0; mt < 8; ++mt) {
+                const int row = row_l + mt * 16;
+                if (row >= M) continue;
+                const bf16x8 rv = *reinterpret_cast<const bf16x8 *>(
+                    static_cast<const bf16 *>(g.resid) + (int64_t)row * N + col_l + h * 32);
+                bf16x8 ov;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    const float res = fmaf(gm[e], fmaf(ra[mt], (float)rv[e], rb[mt]), bt[e]);
+                    ov[e] = (bf16)(acc[mt][2 * h + (e >> 2)][e & 3] + bias_v[h][e] + res);
+                    const float yb = (float)ov[e];
+                    ss[mt] += yb;
+                    sq[mt] = fmaf(yb, yb, sq[mt]);
+                    sd[mt] = fmaf(yb, wg[e], sd[mt]);
+                }
+                *reinterpret_cast<bf16x8 *>(static_cast<bf16 *>(g.out) + (int64_t)row * g.ld_out +
+                                            col_l + h * 32) = ov;
+            }
+        }
+        // partials: the 4 lane groups (lanes l, l^16, l^32, l^48 share a row), then
+        // the 4 wc waves through LDS (the staging buffers are free), fixed order
+#pragma unroll
+        for (int mt = 0; mt < 8; ++mt) {
+#pragma unroll
+            for (int d = 16; d <= 32; d <<= 1) {
+                ss[mt] += __shfl_xor(ss[mt], d, 64);
+                sq[mt] += __shfl_xor(sq[mt], d, 64);
+                sd[mt] += __shfl_xor(sd[mt], d, 64);
+            }
+        }
+        float4 *part = reinterpret_cast<float4 *>(lds);  // [4 wc][256 rows]
+        if (lane < 16) {
+#pragma unroll
+            for (int mt = 0; mt < 8; ++mt)
+                part[wc * G2_TILE + wr * 128 + mt * 16 + lane] = make_float4(ss[mt], sq[mt], sd[mt], 0.f);
+        }
+        __syncthreads();
+        if (tid < G2_TILE && m0e + tid < M) {
+            float4 t = part[tid];
+#pragma unroll
+            for (int w = 1; w < 4; ++w) {
+                const float4 u = part[w * G2_TILE + tid];
+                t.x += u.x;
+                t.y += u.y;
+                t.z += u.z;
+            }
+            g.stats_out[(int64_t)(n0 / G2_TILE) * g.stats_ld + m0e + tid] = t;
+        }
+    } else {
 #pragma unroll
     for (int mt = 0; mt < 8; ++mt) {
         const int row = row_l + mt * 16;
@@ -366,6 +527,7 @@ __global__ void __launch_bounds__(G2_T) gemm256_kernel(GemmArgs g) {
             }
         }
     }
+    }  // generic epilogues
     if constexpr (LN) __syncthreads();  // every wave is past its LDS reads of this tile
     }  // column tiles
 
@@ -516,6 +678,9 @@ void launch_gemm256(int epi, const GemmArgs &g, hipStream_t s) {
         G2_CASE(EPI_BIAS_RESID)
         G2_CASE(EPI_QKV)
         G2_CASE(EPI_BIAS_RESID_LN)
+        G2_CASE(EPI_FOLD)
+        G2_CASE(EPI_FOLD_GELU)
+        G2_CASE(EPI_RESID_STATS)
 #undef G2_CASE
         default:
             fail(DI_EINVAL, "bad GEMM epilogue");

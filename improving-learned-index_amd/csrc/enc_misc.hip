@@ -205,6 +205,60 @@ ln_vec_kernel(const T *__restrict__ pre, int M, const float *__restrict__ gamma,
     if (head_w) head_out(hs, head_b, act, impact, row);
 }
 
+// LayerNorm folding: per-row (rstd, -rstd * mean) from the row-statistics partials
+// of the producing GEMM (biased variance as torch layer_norm; fixed summation order).
+__global__ void row_ln_kernel(const float4 *__restrict__ st, int ld, int n_part, int M, int H,
+                              float eps, float2 *__restrict__ out) {
+    const int m = blockIdx.x * blockDim.x + threadIdx.x;
+    if (m >= M) return;
+    float s = 0.f, q = 0.f;
+    for (int t = 0; t < n_part; ++t) {
+        const float4 v = st[(int64_t)t * ld + m];
+        s += v.x;
+        q += v.y;
+    }
+    const float mean = s / (float)H;
+    const float rstd = 1.0f / sqrtf(fmaxf(q / (float)H - mean * mean, 0.f) + eps);
+    out[m] = make_float2(rstd, -rstd * mean);
+}
+
+void launch_row_ln(const float4 *st, int ld, int n_part, int M, int H, float eps, float2 *out,
+                   hipStream_t s) {
+    if (M == 0) return;
+    hipLaunchKernelGGL(row_ln_kernel, dim3((M + 255) / 256), dim3(256), 0, s, st, ld, n_part, M,
+                       H, eps, out);
+    check_launch("row_ln");
+}
+
+// Impact head when the last LayerNorm is folded (encoder LN folding): from the
+// row statistics of the last FFN output (sum, sumsq, dot with w * gamma),
+//   LN(x) . w + b = r (x . (w gamma) - mu sw) + cw,  sw = sum(w gamma), cw = b + w . beta
+__global__ void head_from_stats_kernel(const float4 *__restrict__ st, int ld, int n_part, int M,
+                                       int H, float eps, float sw, float cw, int act,
+                                       float *__restrict__ impact) {
+    const int m = blockIdx.x * blockDim.x + threadIdx.x;
+    if (m >= M) return;
+    float s = 0.f, q = 0.f, d = 0.f;
+    for (int t = 0; t < n_part; ++t) {
+        const float4 v = st[(int64_t)t * ld + m];
+        s += v.x;
+        q += v.y;
+        d += v.z;
+    }
+    const float mean = s / (float)H;
+    const float rstd = 1.0f / sqrtf(fmaxf(q / (float)H - mean * mean, 0.f) + eps);
+    const float x = rstd * (d - mean * sw) + cw;
+    impact[m] = act == 0 ? ((x > 20.0f) ? x : log1pf(expf(x))) : (x > 0.f ? x : 0.f);
+}
+
+void launch_head_from_stats(const float4 *st, int ld, int n_part, int M, int H, float eps,
+                            float sw, float cw, int act, float *impact, hipStream_t s) {
+    if (M == 0) return;
+    hipLaunchKernelGGL(head_from_stats_kernel, dim3((M + 255) / 256), dim3(256), 0, s, st, ld,
+                       n_part, M, H, eps, sw, cw, act, impact);
+    check_launch("head_from_stats");
+}
+
 // numpy's round(np.float32, 3) (reference indexer.py:132): fl32(rint(fl32(x*1000))/1000)
 __device__ __forceinline__ float round3(float x) {
     float t = __fmul_rn(x, 1000.0f);

@@ -40,6 +40,10 @@ void launch_ln(const T *pre, int M, int H, const float *gamma, const float *beta
 void launch_vt_cols(const int32_t *cu, int n_docs, int M, int32_t *vcol, hipStream_t s);
 bool attention_v3_ok(int max_len, int H);
 bool gemm_fused_ln_ok(const GemmArgs &g);
+void launch_head_from_stats(const float4 *st, int ld, int n_part, int M, int H, float eps,
+                            float sw, float cw, int act, float *impact, hipStream_t s);
+void launch_row_ln(const float4 *st, int ld, int n_part, int M, int H, float eps, float2 *out,
+                   hipStream_t s);
 void launch_attention_v3(const bf16 *qkv, const int32_t *cu_seqlens, int n_docs, int max_len,
                          int H, bf16 *ctx, hipStream_t s);
 int vt_ld(int64_t M, int n_docs);
@@ -49,6 +53,7 @@ void launch_gather_terms(const float *impact, const int32_t *cu_seq, const int32
 
 struct Layer {
     DevBuf w_qkv, b_qkv, w_o, b_o, ln1_g, ln1_b, w_i, b_i, w_out, b_out, ln2_g, ln2_b;
+    DevBuf s_qkv, c_qkv, s_i, c_i;  // LN folding: per-column s = W' 1, c = b + W beta
 };
 
 }  // namespace di
@@ -66,6 +71,11 @@ struct di_encoder {
     std::vector<std::unique_ptr<Layer>> layers;
     // workspace
     DevBuf X, qk, vt, vcol, ctx, pre, X1, Hff, impact, ids, cu, tt, cut, err;
+    // LayerNorm folding (bf16): the GEMM consuming LN(x) reads x and folds LN in
+    bool folded = false;
+    DevBuf stats1, stats2, head_wg;  // row-statistics partials; w * gamma_last
+    DevBuf rln1, rln2;               // per-row (rstd, -rstd mean) of P1 / P2
+    float head_sw = 0.f, head_cw = 0.f;
     int64_t cap_tokens = 0;
     int64_t cap_rows = 0;  // allocated rows of the GEMM A operands (>= cap_tokens)
     int cap_docs = 0;
@@ -121,6 +131,48 @@ struct HostTensor {
     }
 };
 
+// LayerNorm folding of a linear layer that consumes LN(x) = (x - mu) r gamma + beta:
+//   W' = W diag(gamma) (bf16),  s = W' 1 (of the rounded W'),  c = b + W beta
+// so that LN(x) W^T + b = r (x W'^T) - r mu s + c  (GEMM epilogue EPI_FOLD*).
+void fold_upload(DevBuf &w_dst, DevBuf &s_dst, DevBuf &c_dst,
+                 const std::vector<const HostTensor *> &w_parts,
+                 const std::vector<const HostTensor *> &b_parts, int K, const HostTensor *gamma,
+                 const HostTensor *beta) {
+    int64_t rows = 0;
+    for (auto *p : w_parts) rows += p->numel() / K;
+    std::vector<uint16_t> w((size_t)(rows * K));
+    std::vector<float> sv((size_t)rows), cv((size_t)rows);
+    std::vector<float> gm((size_t)K), bt((size_t)K);
+    for (int k = 0; k < K; ++k) {
+        gm[(size_t)k] = gamma->at(k);
+        bt[(size_t)k] = beta->at(k);
+    }
+    int64_t r = 0, rb = 0;
+    for (auto *p : w_parts) {
+        const int64_t pr = p->numel() / K;
+        for (int64_t i = 0; i < pr; ++i, ++r) {
+            double s = 0.0, c = 0.0;
+            for (int k = 0; k < K; ++k) {
+                const float wv = p->at(i * K + k);
+                const uint16_t wb = f32_to_bf16_bits(wv * gm[(size_t)k]);
+                w[(size_t)(r * K + k)] = wb;
+                s += (double)bf16_bits_to_f32(wb);
+                c += (double)wv * (double)bt[(size_t)k];
+            }
+            sv[(size_t)r] = (float)s;
+            cv[(size_t)r] = (float)c;
+        }
+    }
+    for (auto *p : b_parts)
+        for (int64_t i = 0; i < p->numel(); ++i, ++rb) cv[(size_t)rb] += p->at(i);
+    w_dst.reserve(w.size() * 2);
+    DI_HIP(hipMemcpy(w_dst.p, w.data(), w.size() * 2, hipMemcpyHostToDevice));
+    s_dst.reserve(sv.size() * 4);
+    DI_HIP(hipMemcpy(s_dst.p, sv.data(), sv.size() * 4, hipMemcpyHostToDevice));
+    c_dst.reserve(cv.size() * 4);
+    DI_HIP(hipMemcpy(c_dst.p, cv.data(), cv.size() * 4, hipMemcpyHostToDevice));
+}
+
 void upload(DevBuf &dst, const std::vector<const HostTensor *> &parts, int64_t rows_of_first,
             bool as_f32_always, size_t esz) {
     (void)rows_of_first;
@@ -173,6 +225,13 @@ void ensure_workspace(di_encoder *e, int64_t M, int n_docs, int64_t n_terms) {
             e->vt.reserve(vt_bytes);
             // never-written gap columns between documents must read as finite zeros
             DI_HIP(hipMemset(e->vt.p, 0, vt_bytes));
+        }
+        if (e->folded) {
+            const size_t sb = (size_t)(H / 256) * capr * 16;  // float4 per row and 256 columns
+            e->stats1.reserve(sb);
+            e->stats2.reserve(sb);
+            e->rln1.reserve((size_t)capr * 8);
+            e->rln2.reserve((size_t)capr * 8);
         }
         e->cap_tokens = cap;
         e->cap_rows = capr;
@@ -331,6 +390,135 @@ void forward(di_encoder *e, const int32_t *d_ids, const int32_t *d_cu, int n_doc
     }
 }
 
+// bf16 forward with every LayerNorm after the embeddings folded into its consumers
+// (EPI_FOLD* / EPI_RESID_STATS, see enc_common.h): no LayerNorm pass over the
+// activations.  Buffers: X holds the layer input (the normalised embeddings, then
+// the un-normalised FFN output P2 of the previous layer), X1 the attention-block
+// output P1; stats2 / stats1 their row-statistics partials.
+void forward_folded(di_encoder *e, const int32_t *d_ids, const int32_t *d_cu, int n_docs,
+                    int64_t M, int max_len, bool timing, hipStream_t s) {
+    const auto &c = e->cfg;
+    const int H = c.hidden, F = c.intermediate;
+    const int pos_offset = (c.variant == DI_VARIANT_XLMR) ? c.pad_id + 1 : 0;
+    DI_REQUIRE(attention_v3_ok(max_len, H), DI_EINVAL, "max_len %d > 512", max_len);
+    bf16 *X = e->X.as<bf16>(), *X1 = e->X1.as<bf16>();
+    float4 *st1 = e->stats1.as<float4>(), *st2 = e->stats2.as<float4>();
+    float2 *rl1 = e->rln1.as<float2>(), *rl2 = e->rln2.as<float2>();
+    const int ld = (int)e->cap_rows, n_part = H / 256;
+    {
+        TimedLaunch tl(e->timer, timing, "embed_ln", s);
+        launch_embed_ln<bf16>(d_ids, d_cu, n_docs, (int)M, H, e->word.as<bf16>(),
+                              e->pos.as<bf16>(), e->type0.as<bf16>(), e->emb_g.as<float>(),
+                              e->emb_b.as<float>(), c.layer_norm_eps, pos_offset, c.vocab_size,
+                              c.max_positions, X, e->err.as<int32_t>(), s);
+    }
+    auto base = [&]() {
+        GemmArgs g{};
+        g.M = (int)M;
+        g.a_rows = e->cap_rows;
+        g.hidden = H;
+        g.stats_ld = ld;
+        g.n_part = n_part;
+        g.ln_h = H;
+        g.ln_eps = c.layer_norm_eps;
+        return g;
+    };
+    for (size_t l = 0; l < e->layers.size(); ++l) {
+        Layer &L = *e->layers[l];
+        const Layer *P = l > 0 ? e->layers[l - 1].get() : nullptr;
+        const bool last = l + 1 == e->layers.size();
+        // QKV: layer 0 reads the normalised embeddings; later layers fold LN2(l-1)
+        GemmArgs g = base();
+        g.A = X;
+        g.B = L.w_qkv.p;
+        g.bias = L.b_qkv.as<float>();
+        g.out = e->qk.p;
+        g.N = 3 * H;
+        g.K = H;
+        g.ld_out = 3 * H;
+        if (P) {
+            g.row_ln = rl2;
+            g.col_s = L.s_qkv.as<float>();
+            g.col_c = L.c_qkv.as<float>();
+        }
+        {
+            TimedLaunch tl(e->timer, timing, "gemm_qkv", s);
+            launch_gemm<bf16>(P ? EPI_FOLD : EPI_BIAS, g, s);
+        }
+        {
+            TimedLaunch tl(e->timer, timing, "attention", s);
+            launch_attention_v3(e->qk.as<bf16>(), d_cu, n_docs, max_len, H, e->ctx.as<bf16>(), s);
+        }
+        // O: P1 = ctx W_o^T + b_o + LN2(l-1)(X)  (plain X on layer 0) -> X1, stats1
+        g = base();
+        g.A = e->ctx.p;
+        g.B = L.w_o.p;
+        g.bias = L.b_o.as<float>();
+        g.resid = X;
+        g.out = X1;
+        g.N = H;
+        g.K = H;
+        g.ld_out = H;
+        g.stats_out = st1;
+        if (P) {
+            g.row_ln = rl2;
+            g.res_gamma = P->ln2_g.as<float>();
+            g.res_beta = P->ln2_b.as<float>();
+        }
+        {
+            TimedLaunch tl(e->timer, timing, "gemm_o", s);
+            launch_gemm<bf16>(EPI_RESID_STATS, g, s);
+        }
+        {
+            TimedLaunch tl(e->timer, timing, "row_ln", s);
+            launch_row_ln(st1, ld, n_part, (int)M, H, c.layer_norm_eps, rl1, s);
+        }
+        // FFN1 on LN1(P1), folded
+        g = base();
+        g.A = X1;
+        g.B = L.w_i.p;
+        g.out = e->Hff.p;
+        g.N = F;
+        g.K = H;
+        g.ld_out = F;
+        g.row_ln = rl1;
+        g.col_s = L.s_i.as<float>();
+        g.col_c = L.c_i.as<float>();
+        {
+            TimedLaunch tl(e->timer, timing, "gemm_ffn1", s);
+            launch_gemm<bf16>(EPI_FOLD_GELU, g, s);
+        }
+        // FFN2: P2 = Hff W_out^T + b_out + LN1(P1) -> X, stats2 (+ head dot, last layer)
+        g = base();
+        g.A = e->Hff.p;
+        g.B = L.w_out.p;
+        g.bias = L.b_out.as<float>();
+        g.resid = X1;
+        g.out = X;
+        g.N = H;
+        g.K = F;
+        g.ld_out = H;
+        g.row_ln = rl1;
+        g.res_gamma = L.ln1_g.as<float>();
+        g.res_beta = L.ln1_b.as<float>();
+        g.stats_out = st2;
+        g.head_wg = last ? e->head_wg.as<float>() : nullptr;
+        {
+            TimedLaunch tl(e->timer, timing, "gemm_ffn2", s);
+            launch_gemm<bf16>(EPI_RESID_STATS, g, s);
+        }
+        if (!last) {
+            TimedLaunch tl(e->timer, timing, "row_ln", s);
+            launch_row_ln(st2, ld, n_part, (int)M, H, c.layer_norm_eps, rl2, s);
+        }
+    }
+    {
+        TimedLaunch tl(e->timer, timing, "head", s);
+        launch_head_from_stats(st2, ld, n_part, (int)M, H, c.layer_norm_eps, e->head_sw,
+                               e->head_cw, c.activation, e->impact.as<float>(), s);
+    }
+}
+
 }  // namespace
 
 extern "C" {
@@ -414,33 +602,62 @@ int di_encoder_create(const di_encoder_cfg *cfg, const di_tensor *w, int32_t n_w
         }
         upload(e->emb_g, {get("embeddings.LayerNorm.weight", {H})}, 0, true, 4);
         upload(e->emb_b, {get("embeddings.LayerNorm.bias", {H})}, 0, true, 4);
+        // LayerNorm folding: bf16 with shapes the 256-tile GEMM takes (DI_NO_LN_FOLD: off)
+        e->folded = e->esz == 2 && H % 256 == 0 && F % 256 == 0 && H <= 1024 &&
+                    std::getenv("DI_NO_LN_FOLD") == nullptr;
+        const HostTensor *prev_g2 = nullptr, *prev_b2 = nullptr;  // LN2 of layer l-1
         for (int l = 0; l < c.layers; ++l) {
             std::string p = "encoder.layer." + std::to_string(l) + ".";
             auto L = std::make_unique<Layer>();
-            upload(L->w_qkv,
-                   {get(p + "attention.self.query.weight", {H, H}),
-                    get(p + "attention.self.key.weight", {H, H}),
-                    get(p + "attention.self.value.weight", {H, H})},
-                   0, false, e->esz);
-            upload(L->b_qkv,
-                   {get(p + "attention.self.query.bias", {H}),
-                    get(p + "attention.self.key.bias", {H}),
-                    get(p + "attention.self.value.bias", {H})},
-                   0, true, 4);
+            const std::vector<const HostTensor *> wqkv = {
+                get(p + "attention.self.query.weight", {H, H}),
+                get(p + "attention.self.key.weight", {H, H}),
+                get(p + "attention.self.value.weight", {H, H})};
+            const std::vector<const HostTensor *> bqkv = {
+                get(p + "attention.self.query.bias", {H}), get(p + "attention.self.key.bias", {H}),
+                get(p + "attention.self.value.bias", {H})};
+            if (e->folded && l > 0)  // layer 0 reads the (normalised) embedding output
+                fold_upload(L->w_qkv, L->s_qkv, L->c_qkv, wqkv, bqkv, H, prev_g2, prev_b2);
+            else
+                upload(L->w_qkv, wqkv, 0, false, e->esz);
+            upload(L->b_qkv, bqkv, 0, true, 4);
             upload(L->w_o, {get(p + "attention.output.dense.weight", {H, H})}, 0, false, e->esz);
             upload(L->b_o, {get(p + "attention.output.dense.bias", {H})}, 0, true, 4);
             upload(L->ln1_g, {get(p + "attention.output.LayerNorm.weight", {H})}, 0, true, 4);
             upload(L->ln1_b, {get(p + "attention.output.LayerNorm.bias", {H})}, 0, true, 4);
-            upload(L->w_i, {get(p + "intermediate.dense.weight", {F, H})}, 0, false, e->esz);
-            upload(L->b_i, {get(p + "intermediate.dense.bias", {F})}, 0, true, 4);
+            const HostTensor *wi = get(p + "intermediate.dense.weight", {F, H});
+            const HostTensor *bi = get(p + "intermediate.dense.bias", {F});
+            if (e->folded)
+                fold_upload(L->w_i, L->s_i, L->c_i, {wi}, {bi}, H,
+                            get(p + "attention.output.LayerNorm.weight", {H}),
+                            get(p + "attention.output.LayerNorm.bias", {H}));
+            else
+                upload(L->w_i, {wi}, 0, false, e->esz);
+            upload(L->b_i, {bi}, 0, true, 4);
             upload(L->w_out, {get(p + "output.dense.weight", {H, F})}, 0, false, e->esz);
             upload(L->b_out, {get(p + "output.dense.bias", {H})}, 0, true, 4);
-            upload(L->ln2_g, {get(p + "output.LayerNorm.weight", {H})}, 0, true, 4);
-            upload(L->ln2_b, {get(p + "output.LayerNorm.bias", {H})}, 0, true, 4);
+            prev_g2 = get(p + "output.LayerNorm.weight", {H});
+            prev_b2 = get(p + "output.LayerNorm.bias", {H});
+            upload(L->ln2_g, {prev_g2}, 0, true, 4);
+            upload(L->ln2_b, {prev_b2}, 0, true, 4);
             e->layers.push_back(std::move(L));
         }
-        upload(e->head_w, {get("impact_score_encoder.0.weight", {1, H})}, 0, true, 4);
+        const HostTensor *hw = get("impact_score_encoder.0.weight", {1, H});
+        upload(e->head_w, {hw}, 0, true, 4);
         e->head_b = get("impact_score_encoder.0.bias", {1})->at(0);
+        if (e->folded) {  // head on the folded last LayerNorm: w * gamma, sums
+            std::vector<float> wg((size_t)H);
+            double sw = 0.0, cw = e->head_b;
+            for (int k = 0; k < H; ++k) {
+                wg[(size_t)k] = hw->at(k) * prev_g2->at(k);
+                sw += wg[(size_t)k];
+                cw += (double)hw->at(k) * prev_b2->at(k);
+            }
+            e->head_wg.reserve((size_t)H * 4);
+            DI_HIP(hipMemcpy(e->head_wg.p, wg.data(), (size_t)H * 4, hipMemcpyHostToDevice));
+            e->head_sw = (float)sw;
+            e->head_cw = (float)cw;
+        }
         // strict, as ModelCheckpoint.load -> load_state_dict (checkpoint.py:117)
         for (auto &kv : byname)
             DI_REQUIRE(used.count(kv.first), DI_EINVAL, "unexpected weight %s",
@@ -489,7 +706,10 @@ int di_encode(di_encoder *e, const int32_t *tok_ids, const int32_t *cu_seqlens, 
         DI_HIP(hipMemsetAsync(e->err.p, 0, 4, s));
         if (n_tokens > 0) {
             if (e->esz == 2)
-                forward<bf16>(e, d_ids, d_cu, n_docs, n_tokens, max_len, timing, s);
+                if (e->folded)
+                    forward_folded(e, d_ids, d_cu, n_docs, n_tokens, max_len, timing, s);
+                else
+                    forward<bf16>(e, d_ids, d_cu, n_docs, n_tokens, max_len, timing, s);
             else
                 forward<float>(e, d_ids, d_cu, n_docs, n_tokens, max_len, timing, s);
         }

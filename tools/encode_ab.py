@@ -14,15 +14,19 @@ sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
 if sys.argv[1] == "--compare":
     a, b = np.load(sys.argv[2]), np.load(sys.argv[3])
     d = np.abs(a - b)
+    r = d / (np.abs(b) + 1e-3)
     print(f"n={a.size} identical={np.mean(a == b):.6f} max_abs={d.max():.3e} "
-          f"max_rel={np.max(d / (np.abs(a) + 1e-3)):.3e}")
+          f"max_rel={r.max():.3e} median_rel={np.median(r):.3e} p99_rel={np.quantile(r, 0.99):.3e}")
     sys.exit(0)
 
 import bench  # noqa: E402
 from improving_learned_index_amd.encoder import DeviceEncoder, EncoderConfig  # noqa: E402
 
 cfg = EncoderConfig.xlmr_base()
-enc = DeviceEncoder(bench.synthetic_state_dict(cfg, seed=0), cfg, precision="bf16", device=0)
+import os  # noqa: E402
+
+prec = "fp32" if os.environ.get("AB_FP32") else "bf16"
+enc = DeviceEncoder(bench.synthetic_state_dict(cfg, seed=0), cfg, precision=prec, device=0)
 ids, cu, lens, tt, ct = bench.synthetic_docs_tokens(256, cfg.vocab_size, seed=100, max_len=300)
 out = enc.encode_packed(ids, cu, token_impacts=True)
 np.save(sys.argv[1], out)
