@@ -5,9 +5,10 @@
 // reference's tie order.
 //
 // Device layout ("doc-blocked, impact-ordered postings"):
-//   docs of a shard are cut into blocks of BLOCK_DOCS = 32768; every term's
-//   postings are grouped by block (block-major, then the reference order
-//   value-desc/doc-asc).  One posting = one u32: (doc_in_block << 8) | value.
+//   docs of a shard are cut into nb = ceil(n_docs / 32768) equal blocks (a multiple
+//   of 64 docs each, at most 32768); every term's postings are grouped by block
+//   (block-major, then the reference order value-desc/doc-asc).  One posting = one
+//   u32: (doc_in_block << 8) | value.
 //   term_start[t] (i64) + blk_off[t*(NB+1)+b] (u32) locate the sublist (t, b).
 //
 // score_blocks: one 1024-thread workgroup per (query, block).  The block's
@@ -19,7 +20,9 @@
 //   there: comparing words reproduces the reference's order exactly -- score
 //   descending, then first-touch order (term order, then impact desc inside
 //   that term's list, then doc asc).  A block-wide radix select keeps the
-//   block's top-k (ties in the last digit by doc ascending).
+//   block's top-k (ties in the last digit by doc ascending).  With <= 16 query
+//   terms the k-th score comes from one 4096-bin score histogram instead, and the
+//   docs tied at it are ordered from a compact list.
 // merge_topk: one workgroup per query sorts the <= NB*k block candidates by
 //   the 64-bit key  word(32) | ~doc(32)  and writes doc/score/key.
 #include <hip/hip_runtime.h>
@@ -38,27 +41,42 @@
 
 namespace di {
 
-constexpr int BLOCK_DOCS = 32768;
+constexpr int MAX_BLOCK_DOCS = 32768;  // LDS accumulators per workgroup (128 KiB)
 constexpr int SC_THREADS = 1024;
 constexpr int SC_WAVES = SC_THREADS / 64;
-constexpr int SC_PER_THREAD = BLOCK_DOCS / SC_THREADS;  // 32
+constexpr int SC_PER_THREAD = MAX_BLOCK_DOCS / SC_THREADS;  // 32
 constexpr int MAX_TERMS = DI_MAX_QUERY_TERMS;
+// Fast selection: with at most 16 query terms every score is below 255 * 16 < 4096,
+// so one pass of a 4096-bin score histogram finds the k-th score; the docs tied at
+// that score (a few, typically) are ordered from a compact list in LDS.
+constexpr int FAST_TERMS = 16;
+constexpr int HIST_BINS = 4096;
+constexpr int TIE_CAP = HIST_BINS;
 
 struct ScoreShared {
-    uint32_t acc[BLOCK_DOCS];  // 128 KiB
-    RadixScratch<SC_WAVES> rs;
-    int64_t lo[MAX_TERMS];
-    int64_t hi[MAX_TERMS];
-    uint32_t emit;  // output cursor
-    uint32_t tie_need;
+    uint32_t acc[MAX_BLOCK_DOCS];  // 128 KiB
+    union {
+        RadixScratch<SC_WAVES> rs;  // general radix path
+        uint32_t hist[HIST_BINS];   // fast path: score histogram, then the tie list
+    } u;
+    union {
+        int64_t bounds[2][MAX_TERMS];  // scatter: sublist [lo, hi) of every query term
+        uint32_t h256[256];            // fast path: digit histogram over the tie list
+    } v;
+    uint32_t wsum[SC_WAVES];
+    uint32_t emit;   // output cursor
+    uint32_t n_tie;  // tie-list cursor
+    uint32_t bad;
+    uint32_t thr, above, ties, bin, bin_above;
 };
+static_assert(sizeof(RadixScratch<SC_WAVES>) >= HIST_BINS * 4, "histogram overlays the radix scratch");
 
 // One radix pass over the block's words (i-major: lanes read consecutive words,
 // conflict-free).  KeyF: word,index -> key;  Pred: word,index,key -> bool.
 template <class KeyF, class Pred>
 __device__ __forceinline__ void score_radix_pass(ScoreShared &sh, int n_local, int shift,
                                                  uint32_t need, KeyF key, Pred pred) {
-    radix_clear<SC_THREADS, SC_WAVES>(sh.rs);
+    radix_clear<SC_THREADS, SC_WAVES>(sh.u.rs);
     __syncthreads();
     RunLen rl;
 #pragma unroll 4
@@ -67,139 +85,366 @@ __device__ __forceinline__ void score_radix_pass(ScoreShared &sh, int n_local, i
         if (idx < n_local) {
             uint32_t w = sh.acc[idx];
             uint32_t kk = key(w, idx);
-            if (pred(w, idx, kk)) rl.add(sh.rs, (kk >> shift) & 255u);
+            if (pred(w, idx, kk)) rl.add(sh.u.rs, (kk >> shift) & 255u);
         }
     }
-    rl.flush(sh.rs);
+    rl.flush(sh.u.rs);
     __syncthreads();
-    radix_pick<SC_THREADS, SC_WAVES>(sh.rs, need);
+    radix_pick<SC_THREADS, SC_WAVES>(sh.u.rs, need);
 }
 
-__global__ void __launch_bounds__(SC_THREADS)
-score_blocks_kernel(const uint32_t *__restrict__ post, const int64_t *__restrict__ term_start,
-                    const uint32_t *__restrict__ blk_off, int nb, int64_t n_terms,
-                    uint32_t n_docs, uint32_t doc_lo, const uint32_t *__restrict__ q_terms,
-                    const int32_t *__restrict__ cu_q, int k, uint64_t *__restrict__ cand_key,
-                    int32_t *__restrict__ cand_n, int ablate) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    ScoreShared &sh = *reinterpret_cast<ScoreShared *>(smem);
+// Sweep of the block's accumulator words: f(w, idx) for idx < round4(n_local), 4
+// consecutive words per lane per ds_read_b128, 4 reads in flight before any is
+// used (a read-then-use loop is LDS-latency bound).  Words past the zeroed range
+// come as 0; f runs in wave-uniform control flow (it may ballot).
+template <class F>
+__device__ __forceinline__ void sweep_words(const uint32_t *acc, int n_local, F f) {
+    const uint4 *a4 = reinterpret_cast<const uint4 *>(acc);
+    const int n4 = (n_local + 3) >> 2;
+    constexpr int G = 4;  // uint4 reads in flight per lane
+    for (int i0 = 0; i0 < SC_PER_THREAD / 4; i0 += G) {
+        if (i0 * SC_THREADS >= n4) break;  // (uniform)
+        uint4 x[G];
+#pragma unroll
+        for (int i = 0; i < G; ++i) {
+            const int q4 = (i0 + i) * SC_THREADS + (int)threadIdx.x;
+            const uint4 y = a4[min(q4, n4 - 1)];
+            x[i] = q4 < n4 ? y : make_uint4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (int i = 0; i < G; ++i) {
+            const int base = 4 * ((i0 + i) * SC_THREADS + (int)threadIdx.x);
+            f(x[i].x, base);
+            f(x[i].y, base + 1);
+            f(x[i].z, base + 2);
+            f(x[i].w, base + 3);
+        }
+    }
+}
 
-    const int b = blockIdx.x % nb;
-    const int q = blockIdx.x / nb;
-    const int tid = threadIdx.x;
-    const int64_t block_first = (int64_t)b * BLOCK_DOCS;
-    const int n_local = (int)min((int64_t)BLOCK_DOCS, (int64_t)n_docs - block_first);
+// Block-wide stable compaction over the accumulator words into two lists:
+// cls(w, idx) -> bit 0: list A, bit 1: list B.  One counting sweep, one exclusive
+// block scan of the packed per-thread counts, one writing sweep calling
+// out(list, pos, w, idx) -- no atomics.  Returns the packed totals (A | B << 16;
+// each list holds at most 32768).  Ends with a barrier.
+template <class Cls, class Out>
+__device__ __forceinline__ uint32_t compact_words(ScoreShared &sh, int n_local, Cls cls,
+                                                  Out out) {
+    uint32_t cnt = 0;
+    sweep_words(sh.acc, n_local, [&](uint32_t w, int idx) {
+        const uint32_t c = cls(w, idx);
+        cnt += (c & 1u) + ((c & 2u) << 15);
+    });
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t incl = wave_prefix_sum(cnt);
+    if (lane == 63) sh.wsum[wave] = incl;
+    __syncthreads();
+    uint32_t base = incl - cnt, total = 0;
+    for (int w2 = 0; w2 < SC_WAVES; ++w2) {
+        const uint32_t x = sh.wsum[w2];
+        if (w2 < wave) base += x;
+        total += x;
+    }
+    uint32_t pa = base & 0xFFFFu, pb = base >> 16;
+    sweep_words(sh.acc, n_local, [&](uint32_t w, int idx) {
+        const uint32_t c = cls(w, idx);
+        if (c & 1u) out(0, pa++, w, idx);
+        if (c & 2u) out(1, pb++, w, idx);
+    });
+    __syncthreads();
+    return total;
+}
+
+// Wave-aggregated append: lanes with `take` get consecutive slots of *cursor (one
+// LDS atomic per wave and call).  Call from wave-uniform control flow.
+__device__ __forceinline__ bool wave_append(bool take, uint32_t *cursor, uint32_t &pos) {
+    const uint64_t m = __ballot(take);
+    if (m == 0) return false;
+    const int lane = threadIdx.x & 63;
+    const int leader = __builtin_ctzll(m);
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(cursor, (uint32_t)__builtin_popcountll(m));
+    base = __shfl(base, leader, 64);
+    pos = base + (uint32_t)__builtin_popcountll(m & ((1ull << lane) - 1ull));
+    return take;
+}
+
+// One work item = (query q, doc block b): accumulate, select the block's top-k.
+__device__ __forceinline__ void score_item(ScoreShared &sh, int item,
+                                           const uint32_t *__restrict__ post,
+                                           const int64_t *__restrict__ term_start,
+                                           const uint32_t *__restrict__ blk_off, int nb,
+                                           int block_docs, int64_t n_terms, uint32_t n_docs,
+                                           uint32_t doc_lo, const uint32_t *__restrict__ q_terms,
+                                           const int32_t *__restrict__ cu_q, int k,
+                                           uint64_t *__restrict__ cand_key,
+                                           int32_t *__restrict__ cand_n, int ablate) {
+    int64_t *lo = sh.v.bounds[0], *hi = sh.v.bounds[1];
+
+    const int b = item % nb;
+    const int q = item / nb;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int64_t block_first = (int64_t)b * block_docs;
+    const int n_local = (int)min((int64_t)block_docs, (int64_t)n_docs - block_first);
     const int q0 = cu_q[q], nt = cu_q[q + 1] - q0;
     uint64_t *ck = cand_key + ((int64_t)q * nb + b) * k;
+    int32_t *cn = cand_n + (int64_t)q * nb + b;
 
     if (nt > MAX_TERMS || nt < 0 || n_local <= 0) {
-        if (tid == 0) cand_n[(int64_t)q * nb + b] = (nt > MAX_TERMS || nt < 0) ? -1 : 0;
+        if (tid == 0) *cn = (nt > MAX_TERMS || nt < 0) ? -1 : 0;
         return;
     }
-    if (tid == 0) sh.tie_need = 0;
+    const bool fast = nt <= FAST_TERMS;
+    if (tid == 0) {
+        sh.bad = 0;
+        sh.emit = 0;
+        sh.n_tie = 0;
+    }
     __syncthreads();
 
-    // sublist bounds for this block, zero the accumulators
+    // sublist bounds for this block, zero the accumulators (and the fast histogram)
     for (int j = tid; j < nt; j += SC_THREADS) {
-        uint32_t t = q_terms[q0 + j];
+        const uint32_t t = q_terms[q0 + j];
         if (t >= n_terms) {  // invalid id (device-pointer callers are not pre-checked)
-            sh.tie_need = 1;
-            sh.lo[j] = sh.hi[j] = 0;
+            sh.bad = 1;
+            lo[j] = hi[j] = 0;
             continue;
         }
         const uint32_t *bo = blk_off + (int64_t)t * (nb + 1) + b;
-        sh.lo[j] = term_start[t] + bo[0];
-        sh.hi[j] = term_start[t] + bo[1];
+        lo[j] = term_start[t] + bo[0];
+        hi[j] = term_start[t] + bo[1];
     }
     {
         uint4 *a4 = reinterpret_cast<uint4 *>(sh.acc);
-        for (int i = tid; i < BLOCK_DOCS / 4; i += SC_THREADS) a4[i] = make_uint4(0, 0, 0, 0);
+        const int n4 = (n_local + 3) >> 2;
+        for (int i = tid; i < n4; i += SC_THREADS) a4[i] = make_uint4(0, 0, 0, 0);
+        if (fast) reinterpret_cast<uint4 *>(sh.u.hist)[tid] = make_uint4(0, 0, 0, 0);
     }
-    if (tid == 0) sh.emit = 0;
     __syncthreads();
-    if (sh.tie_need) {
-        if (tid == 0) cand_n[(int64_t)q * nb + b] = -1;
+    if (sh.bad) {
+        if (tid == 0) *cn = -1;
         return;
     }
 
     // ---- scatter: terms in query order, barrier between terms -------------
     // The postings of (term j, this block) are walked in rounds of SC_THREADS*U
-    // dwords (coalesced: lane-consecutive).  The next round's loads are issued
-    // before the current round is applied, also across a term boundary, so each
-    // term's barrier no longer exposes a memory round trip.
-    constexpr int U = 16;  // 64 B of postings in flight per lane, plus the next round
+    // dwords (coalesced: lane-consecutive).  Every load is unconditional (clamped
+    // address, the value of a lane past the end is dropped afterwards): a load behind
+    // a per-lane condition makes the compiler branch around it and drain the counter
+    // (vmcnt(0)) element by element.
+    constexpr int U = 16;
     constexpr int ROUND = SC_THREADS * U;
-    auto rounds = [&](int jj) { return (int)((sh.hi[jj] - sh.lo[jj] + ROUND - 1) / ROUND); };
+    auto rounds = [&](int jj) { return (int)((hi[jj] - lo[jj] + ROUND - 1) / ROUND); };
+    // wave-uniform base pointer + 32-bit lane offsets (one VGPR per address)
     auto load_round = [&](int jj, int rr, uint32_t (&r)[U]) {
-        const int64_t base = sh.lo[jj] + (int64_t)rr * ROUND + tid, hi = sh.hi[jj];
+        const int64_t b0 = lo[jj] + (int64_t)rr * ROUND;
+        const uint32_t *p = post + b0;
+        const int last = (int)(hi[jj] - 1 - b0);  // >= 0: the round is not empty
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            int64_t i = base + (int64_t)u * SC_THREADS;
-            r[u] = (i < hi) ? post[i] : 0u;
+            const int i = tid + u * SC_THREADS;
+            const uint32_t x = p[min(i, last)];
+            r[u] = i <= last ? x : 0u;
         }
     };
     int j = (ablate & 1) ? nt : 0, rr = 0;  // ablate bit 0: skip the scatter (profiling)
     while (j < nt && rounds(j) == 0) ++j;
-    uint32_t cur[U], nxt[U];
-    if (j < nt) load_round(j, rr, cur);
+    // One round = 16 loads per lane in flight, then apply them; the 16 waves of the
+    // CU overlap one another's load latency with their LDS work (a register prefetch
+    // of the next round costs spills and buys nothing: the copy at the back-edge
+    // waits for the loads anyway).
     while (j < nt) {
+        uint32_t cur[U];
+        load_round(j, rr, cur);
+        const uint32_t first_bits = (uint32_t)(255 - j) << 8;
+        uint32_t w[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) w[u] = sh.acc[(cur[u] >> 8) & (MAX_BLOCK_DOCS - 1)];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t v = cur[u] & 255u;  // 0 only for the padding lanes
+            if (v) {
+                const uint32_t x = w[u];
+                sh.acc[(cur[u] >> 8) & (MAX_BLOCK_DOCS - 1)] =
+                    x ? x + (v << 16) : ((v << 16) | first_bits | v);
+            }
+        }
         int jn = j, rn = rr + 1;
         while (jn < nt && rn >= rounds(jn)) {
             ++jn;
             rn = 0;
         }
-        if (jn < nt) load_round(jn, rn, nxt);
-        const uint32_t first_bits = (uint32_t)(255 - j) << 8;
-        uint32_t w[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) w[u] = sh.acc[(cur[u] >> 8) & (BLOCK_DOCS - 1)];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const uint32_t v = cur[u] & 255u;  // 0 only for the padding lanes
-            if (v) {
-                uint32_t x = w[u];
-                x = x ? x + (v << 16) : ((v << 16) | first_bits | v);
-                sh.acc[(cur[u] >> 8) & (BLOCK_DOCS - 1)] = x;
-            }
-        }
-        if (jn != j) __syncthreads();  // term boundary (uniform across the block)
-#pragma unroll
-        for (int u = 0; u < U; ++u) cur[u] = nxt[u];
+        // term boundary: this round's LDS writes land before any wave reads the next term
+        if (jn != j && jn < nt) __syncthreads();
         j = jn;
         rr = rn;
     }
     __syncthreads();
 
     if (ablate & 2) {  // profiling: skip the selection
-        if (tid == 0) cand_n[(int64_t)q * nb + b] = 0;
+        if (tid == 0) *cn = 0;
         return;
     }
-    // ---- block top-k: radix select on the 32-bit words ---------------------
-    auto id_key = [](uint32_t w, int) { return w; };
-    uint32_t need = (uint32_t)k, prefix = 0, mask = 0;
-    // pass 0 also counts touched docs
-    score_radix_pass(sh, n_local, 24, need, id_key,
-                     [](uint32_t w, int, uint32_t) { return w != 0; });
-    const uint32_t touched = sh.rs.total;
     const uint64_t doc_base = (uint64_t)doc_lo + (uint64_t)block_first;
-    auto emit = [&](uint32_t w, int idx) {
-        uint32_t pos = atomicAdd(&sh.emit, 1u);
-        uint32_t doc = (uint32_t)(doc_base + (uint64_t)idx);
+    auto cand = [&](uint32_t pos, uint32_t w, int idx) {
+        const uint32_t doc = (uint32_t)(doc_base + (uint64_t)idx);
         if (pos < (uint32_t)k) ck[pos] = ((uint64_t)w << 32) | (uint64_t)(0xFFFFFFFFu - doc);
     };
-    if (touched <= (uint32_t)k) {
-        for (int i = 0; i < SC_PER_THREAD; ++i) {
-            int idx = i * SC_THREADS + tid;
-            if (idx < n_local && sh.acc[idx]) emit(sh.acc[idx], idx);
+    auto emit_all_touched = [&]() {
+        const uint32_t n = compact_words(sh, n_local, [](uint32_t w, int) { return w ? 1u : 0u; },
+                                         [&](int, uint32_t pos, uint32_t w, int idx) {
+                                             cand(pos, w, idx);
+                                         });
+        if (tid == 0) *cn = (int32_t)min(n & 0xFFFFu, (uint32_t)k);
+    };
+
+    uint32_t prefix = 0, mask = 0, need = (uint32_t)k;
+    int shift = 24;  // next digit of the general radix path
+    if (fast) {
+        // ---- fast path: score histogram -> k-th score T -------------------
+        uint32_t *hist = sh.u.hist;
+        sweep_words(sh.acc, n_local, [&](uint32_t w, int) {
+            if (w) atomicAdd(&hist[w >> 16], 1u);
+        });
+        __syncthreads();
+        // thread t owns bins 4t..4t+3; s = touched docs with score >= 4t
+        const uint4 h4 = reinterpret_cast<const uint4 *>(hist)[tid];
+        const uint32_t c = h4.x + h4.y + h4.z + h4.w;
+        uint32_t s = wave_suffix_sum(c);
+        if (lane == 0) sh.wsum[wave] = s;
+        __syncthreads();
+        uint32_t total = 0;
+        for (int w2 = 0; w2 < SC_WAVES; ++w2) {
+            const uint32_t x = sh.wsum[w2];
+            total += x;
+            if (w2 > wave) s += x;
+        }
+        __syncthreads();  // wsum is reused by the compaction
+        if (total <= (uint32_t)k) {  // every touched doc is a candidate
+            emit_all_touched();
+            return;
+        }
+        if (s >= need && s - c < need) {  // exactly one thread: T is in its bins
+            const uint32_t hv[4] = {h4.x, h4.y, h4.z, h4.w};
+            uint32_t above = s - c;
+            int e = 3;
+            for (; e > 0; --e) {
+                if (above + hv[e] >= need) break;
+                above += hv[e];
+            }
+            sh.thr = (uint32_t)(4 * tid + e);
+            sh.above = above;
+            sh.ties = hv[e];
         }
         __syncthreads();
-        if (tid == 0) cand_n[(int64_t)q * nb + b] = (int32_t)min(sh.emit, (uint32_t)k);
-        return;
+        if (ablate & 4) {  // profiling: stop after the threshold
+            if (tid == 0) *cn = 0;
+            return;
+        }
+        const uint32_t T = sh.thr, ties = sh.ties;  // T >= 1: every touched score is
+        const uint32_t above = sh.above;             // nonzero
+        need -= above;
+        if (ties == need || ties <= (uint32_t)TIE_CAP) {
+            // scores above T are in; the ties at T all go in, or into a list (the
+            // histogram is consumed) as (low 16 bits of the word, 0xFFFF - idx):
+            // unique, and larger = first-touch earlier, then doc smaller
+            const bool all_ties = ties == need;
+            uint32_t *tl = sh.u.hist;
+            compact_words(
+                sh, n_local,
+                [T, all_ties](uint32_t w, int) -> uint32_t {
+                    const uint32_t sc = w >> 16;
+                    return (sc > T || (all_ties && sc == T)) ? 1u : (sc == T ? 2u : 0u);
+                },
+                [&](int list, uint32_t pos, uint32_t w, int idx) {
+                    if (list == 0)
+                        cand(pos, w, idx);
+                    else
+                        tl[pos] = ((w & 0xFFFFu) << 16) | (0xFFFFu - (uint32_t)idx);
+                });
+            if (ablate & 8) {  // profiling: stop after the compaction
+                if (tid == 0) *cn = 0;
+                return;
+            }
+            if (!all_ties) {
+                // radix select of the `need` largest tie keys (4 digits, small list)
+                uint32_t *h = sh.v.h256;
+                uint32_t tp = 0, tm = 0, tneed = need;
+                for (int sft = 24; sft >= 0; sft -= 8) {
+                    if (tid < 256) h[tid] = 0;
+                    __syncthreads();
+                    for (uint32_t i = tid; i < ties; i += SC_THREADS) {
+                        const uint32_t x = tl[i];
+                        if ((x & tm) == tp) atomicAdd(&h[(x >> sft) & 255u], 1u);
+                    }
+                    __syncthreads();
+                    if (wave == 0) {
+                        const uint32_t c4 = h[4 * lane] + h[4 * lane + 1] + h[4 * lane + 2] +
+                                            h[4 * lane + 3];
+                        const uint32_t S = wave_suffix_sum(c4);
+                        if (S >= tneed && S - c4 < tneed) {
+                            uint32_t ab = S - c4;
+                            int e = 3;
+                            for (; e > 0; --e) {
+                                const uint32_t he = h[4 * lane + e];
+                                if (ab + he >= tneed) break;
+                                ab += he;
+                            }
+                            sh.bin = (uint32_t)(4 * lane + e);
+                            sh.bin_above = ab;
+                        }
+                    }
+                    __syncthreads();
+                    tp |= sh.bin << sft;
+                    tm |= 255u << sft;
+                    tneed -= sh.bin_above;
+                }
+                // the keys are unique: exactly `need` ties are >= tp; they follow the
+                // `above` candidates
+                if (tid == 0) sh.emit = above;
+                __syncthreads();
+                for (uint32_t i0 = 0; i0 < ties; i0 += SC_THREADS) {
+                    const uint32_t i = i0 + tid;
+                    const uint32_t x = i < ties ? tl[i] : 0u;
+                    uint32_t pos;
+                    if (wave_append(i < ties && x >= tp, &sh.emit, pos))
+                        cand(pos, (T << 16) | (x >> 16), (int)(0xFFFFu - (x & 0xFFFFu)));
+                }
+                __syncthreads();
+                // sh.emit == k by construction; anything else is a selection bug
+                if (tid == 0) *cn = sh.emit == (uint32_t)k ? k : -2;
+            } else {
+                if (tid == 0) *cn = k;
+            }
+            return;
+        }
+        // more ties than the list holds: the general path finishes from score T
+        // (digits 15..8 and 7..0 of the word, then doc order)
+        prefix = T << 16;
+        mask = 0xFFFF0000u;
+        shift = 8;
     }
-    for (int shift = 24;; shift -= 8) {
-        prefix |= sh.rs.bin << shift;
+
+    // ---- general path: block-wide radix select on the 32-bit words ----------
+    auto id_key = [](uint32_t w, int) { return w; };
+    if (shift == 24) {  // pass 0 also counts touched docs
+        score_radix_pass(sh, n_local, 24, need, id_key,
+                         [](uint32_t w, int, uint32_t) { return w != 0; });
+        if (sh.u.rs.total <= (uint32_t)k) {
+            __syncthreads();
+            emit_all_touched();
+            return;
+        }
+    } else {
+        score_radix_pass(sh, n_local, shift, need, id_key,
+                         [prefix, mask](uint32_t w, int, uint32_t) {
+                             return w != 0 && (w & mask) == prefix;
+                         });
+    }
+    for (;; shift -= 8) {
+        prefix |= sh.u.rs.bin << shift;
         mask |= 255u << shift;
-        need -= sh.rs.above;
+        need -= sh.u.rs.above;
         if (shift == 0) break;
         __syncthreads();
         score_radix_pass(sh, n_local, shift - 8, need, id_key,
@@ -208,35 +453,52 @@ score_blocks_kernel(const uint32_t *__restrict__ post, const int64_t *__restrict
                          });
     }
     const uint32_t T = prefix;
-    const uint32_t ties = sh.rs.tot[sh.rs.bin];
+    const uint32_t ties = sh.u.rs.tot[sh.u.rs.bin];
     // doc-order cut among the ties: the `need` smallest doc indices
     // (all ties when exactly `need` of them exist)
     uint32_t dcut = 0;
     if (ties != need) {
         uint32_t dneed = need, dprefix = 0, dmask = 0;
         auto dkey = [](uint32_t, int idx) { return 0xFFFFu - (uint32_t)idx; };
-        for (int shift = 8;; shift -= 8) {
+        for (int sft = 8;; sft -= 8) {
             __syncthreads();
-            score_radix_pass(sh, n_local, shift, dneed, dkey,
+            score_radix_pass(sh, n_local, sft, dneed, dkey,
                              [T, dprefix, dmask](uint32_t w, int, uint32_t kk) {
                                  return w == T && (kk & dmask) == dprefix;
                              });
-            dprefix |= sh.rs.bin << shift;
-            dmask |= 255u << shift;
-            dneed -= sh.rs.above;
-            if (shift == 0) break;
+            dprefix |= sh.u.rs.bin << sft;
+            dmask |= 255u << sft;
+            dneed -= sh.u.rs.above;
+            if (sft == 0) break;
         }
         dcut = dprefix;  // keep ties whose (0xFFFF - idx) >= dcut
     }
-    for (int i = 0; i < SC_PER_THREAD; ++i) {
-        int idx = i * SC_THREADS + tid;
-        if (idx >= n_local) break;
-        uint32_t w = sh.acc[idx];
-        if (w > T || (w == T && (0xFFFFu - (uint32_t)idx) >= dcut)) emit(w, idx);
-    }
     __syncthreads();
-    // sh.emit == k by construction; anything else is a selection bug -> flag it
-    if (tid == 0) cand_n[(int64_t)q * nb + b] = sh.emit == (uint32_t)k ? k : -2;
+    const uint32_t n = compact_words(
+        sh, n_local,
+        [T, dcut](uint32_t w, int idx) -> uint32_t {
+            return (w != 0 && (w > T || (w == T && (0xFFFFu - (uint32_t)idx) >= dcut))) ? 1u : 0u;
+        },
+        [&](int, uint32_t pos, uint32_t w, int idx) { cand(pos, w, idx); });
+    // exactly k by construction; anything else is a selection bug -> flag it
+    if (tid == 0) *cn = (n & 0xFFFFu) == (uint32_t)k ? k : -2;
+}
+
+// Persistent: one workgroup per CU walks the (query, block) items, so the per-
+// workgroup launch cost (16 waves, 150 KiB of LDS) is paid once per CU, not per item.
+__global__ void __launch_bounds__(SC_THREADS)
+score_blocks_kernel(const uint32_t *__restrict__ post, const int64_t *__restrict__ term_start,
+                    const uint32_t *__restrict__ blk_off, int nb, int block_docs, int64_t n_terms,
+                    uint32_t n_docs, uint32_t doc_lo, const uint32_t *__restrict__ q_terms,
+                    const int32_t *__restrict__ cu_q, int k, uint64_t *__restrict__ cand_key,
+                    int32_t *__restrict__ cand_n, int n_items, int ablate) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    ScoreShared &sh = *reinterpret_cast<ScoreShared *>(smem);
+    for (int item = blockIdx.x; item < n_items; item += gridDim.x) {
+        score_item(sh, item, post, term_start, blk_off, nb, block_docs, n_terms, n_docs, doc_lo,
+                   q_terms, cu_q, k, cand_key, cand_n, ablate);
+        __syncthreads();  // every wave is done with the LDS of this item
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -392,10 +654,10 @@ struct di_index {
     bool own_stream = false;
     int64_t n_terms = 0, n_post = 0;
     uint32_t n_docs = 0, doc_lo = 0;  // shard [doc_lo, doc_lo + n_docs)
-    int nb = 0;
+    int nb = 0, block_docs = 0;
     DevBuf post, term_start, blk_off;
     DevBuf ws_q, ws_cu, ws_ck, ws_cn, ws_doc, ws_score, ws_n, ws_key;
-    int ablate = 0;  // DI_PROFILE_ABLATE (profiling builds of the bench only)
+    int ablate = 0;  // DI_PROFILE_ABLATE: profiling only (1 no scatter, 2 no selection, 4 stop at the k-th score)
     Timer timer;
 };
 
@@ -431,11 +693,16 @@ void build_index(di_index *ix, const int64_t *term_off, int64_t n_terms, const u
     }
     DI_REQUIRE(doc_hi >= doc_lo, DI_EINVAL, "doc_hi < doc_lo");
     const uint32_t nd = doc_hi - doc_lo;
-    const int nb = (int)((nd + BLOCK_DOCS - 1) / BLOCK_DOCS);
+    const int nb = (int)((nd + MAX_BLOCK_DOCS - 1) / MAX_BLOCK_DOCS);
+    // equal blocks (no small tail block costing a whole workgroup per query)
+    const uint32_t bd =
+        nb ? (uint32_t)std::min<uint64_t>(MAX_BLOCK_DOCS, ((nd + nb - 1) / nb + 63) / 64 * 64)
+           : (uint32_t)MAX_BLOCK_DOCS;
     ix->n_terms = n_terms;
     ix->n_docs = nd;
     ix->doc_lo = doc_lo;
     ix->nb = nb;
+    ix->block_docs = (int)bd;
     const int64_t stride = nb + 1;
     std::vector<int64_t> tstart(std::max<int64_t>(n_terms, 1), 0);
     std::vector<uint32_t> boff((size_t)std::max<int64_t>(n_terms * stride, 1), 0);
@@ -448,7 +715,7 @@ void build_index(di_index *ix, const int64_t *term_off, int64_t n_terms, const u
             if (pval[p] == 0) break;  // inverted_index.py:50-51
             uint32_t d = pdoc[p];
             if (d < doc_lo || d >= doc_hi) continue;
-            cnt[(d - doc_lo) / BLOCK_DOCS]++;
+            cnt[(d - doc_lo) / bd]++;
         }
         tstart[t] = total;
         uint32_t run = 0;
@@ -470,8 +737,8 @@ void build_index(di_index *ix, const int64_t *term_off, int64_t n_terms, const u
             uint32_t d = pdoc[p];
             if (d < doc_lo || d >= doc_hi) continue;
             uint32_t r = d - doc_lo;
-            int b = (int)(r / BLOCK_DOCS);
-            packed[tstart[t] + cur[b]++] = ((r % BLOCK_DOCS) << 8) | pval[p];
+            int b = (int)(r / bd);
+            packed[tstart[t] + cur[b]++] = ((r % bd) << 8) | pval[p];
         }
     }
     ix->post.reserve(packed.size() * 4);
@@ -485,6 +752,13 @@ void build_index(di_index *ix, const int64_t *term_off, int64_t n_terms, const u
 }  // namespace
 
 namespace di {
+int n_cu() {
+    int dev = 0, v = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev);
+    return v > 0 ? v : 256;
+}
+
 // Kernels using more than 64 KiB of dynamic LDS must opt in, once per device.
 void enable_big_lds() {
     static_assert(sizeof(ScoreShared) <= 160 * 1024, "ScoreShared exceeds LDS");
@@ -667,11 +941,13 @@ int di_index_search(di_index *ix, const uint32_t *q_terms, const int32_t *cu_q, 
                 DI_HIP(hipMemsetAsync(ix->ws_cn.p, 0, (size_t)nq * nb * 4, s));
             } else {
                 TimedLaunch tl(ix->timer, timing, "score_blocks", s);
-                hipLaunchKernelGGL(score_blocks_kernel, dim3(nq * nb), dim3(SC_THREADS),
-                                   sizeof(ScoreShared), s, ix->post.as<uint32_t>(),
-                                   ix->term_start.as<int64_t>(), ix->blk_off.as<uint32_t>(), nb,
-                                   ix->n_terms, ix->n_docs, ix->doc_lo, dq, dcu + q0, k,
-                                   ix->ws_ck.as<uint64_t>(), ix->ws_cn.as<int32_t>(),
+                const int n_items = nq * nb;
+                hipLaunchKernelGGL(score_blocks_kernel, dim3(std::min(n_items, n_cu())),
+                                   dim3(SC_THREADS), sizeof(ScoreShared), s,
+                                   ix->post.as<uint32_t>(), ix->term_start.as<int64_t>(),
+                                   ix->blk_off.as<uint32_t>(), nb, ix->block_docs, ix->n_terms,
+                                   ix->n_docs, ix->doc_lo, dq, dcu + q0, k,
+                                   ix->ws_ck.as<uint64_t>(), ix->ws_cn.as<int32_t>(), n_items,
                                    ix->ablate);
                 check_launch("score_blocks");
             }
