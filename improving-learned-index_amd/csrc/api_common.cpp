@@ -22,6 +22,14 @@ void set_error(const char *fmt, ...) {
 
 const char *last_error() { return g_err.c_str(); }
 
+// compute units of the current device (persistent-kernel grid sizes)
+int n_cu() {
+    int dev = 0, v = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev);
+    return v > 0 ? v : 256;
+}
+
 }  // namespace di
 
 extern "C" {

@@ -20,6 +20,7 @@ namespace di {
 // thread-local last error (di_last_error)
 void set_error(const char *fmt, ...) __attribute__((format(printf, 1, 2)));
 const char *last_error();
+int n_cu();  // compute units of the current device
 
 struct Error {
     int code;

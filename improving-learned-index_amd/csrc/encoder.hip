@@ -44,6 +44,7 @@ void launch_head_from_stats(const float4 *st, int ld, int n_part, int M, int H, 
                             float sw, float cw, int act, float *impact, hipStream_t s);
 void launch_row_ln(const float4 *st, int ld, int n_part, int M, int H, float eps, float2 *out,
                    hipStream_t s);
+int gemm_stats_cols();
 void launch_attention_v3(const bf16 *qkv, const int32_t *cu_seqlens, int n_docs, int max_len,
                          int H, bf16 *ctx, hipStream_t s);
 int vt_ld(int64_t M, int n_docs);
@@ -227,7 +228,7 @@ void ensure_workspace(di_encoder *e, int64_t M, int n_docs, int64_t n_terms) {
             DI_HIP(hipMemset(e->vt.p, 0, vt_bytes));
         }
         if (e->folded) {
-            const size_t sb = (size_t)(H / 256) * capr * 16;  // float4 per row and 256 columns
+            const size_t sb = (size_t)(H / 128) * capr * 16;  // float4 per row and 128 (or 256) columns
             e->stats1.reserve(sb);
             e->stats2.reserve(sb);
             e->rln1.reserve((size_t)capr * 8);
@@ -404,7 +405,7 @@ void forward_folded(di_encoder *e, const int32_t *d_ids, const int32_t *d_cu, in
     bf16 *X = e->X.as<bf16>(), *X1 = e->X1.as<bf16>();
     float4 *st1 = e->stats1.as<float4>(), *st2 = e->stats2.as<float4>();
     float2 *rl1 = e->rln1.as<float2>(), *rl2 = e->rln2.as<float2>();
-    const int ld = (int)e->cap_rows, n_part = H / 256;
+    const int ld = (int)e->cap_rows, n_part = H / gemm_stats_cols();
     {
         TimedLaunch tl(e->timer, timing, "embed_ln", s);
         launch_embed_ln<bf16>(d_ids, d_cu, n_docs, (int)M, H, e->word.as<bf16>(),

@@ -752,13 +752,6 @@ void build_index(di_index *ix, const int64_t *term_off, int64_t n_terms, const u
 }  // namespace
 
 namespace di {
-int n_cu() {
-    int dev = 0, v = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev);
-    return v > 0 ? v : 256;
-}
-
 // Kernels using more than 64 KiB of dynamic LDS must opt in, once per device.
 void enable_big_lds() {
     static_assert(sizeof(ScoreShared) <= 160 * 1024, "ScoreShared exceeds LDS");
