@@ -275,9 +275,10 @@ def encode_leg(args, rank, world, dev):
         per_launch[k] = (f, avg, f / avg / 1e12 if avg > 0 else 0.0)
     dom = max(per_launch, key=lambda k: per_launch[k][1])
     f, avg, tf = per_launch[dom]
-    # PMC names: EPI 1 = bias+GELU (FFN1), 2 = bias+residual (O and FFN2 share it), 3 = QKV
-    pmc_name = {"gemm_qkv": "gemm256_kernel<3>", "gemm_ffn1": "gemm256_kernel<1>",
-                "gemm_o": "gemm256_kernel<2>", "gemm_ffn2": "gemm256_kernel<2>"}[dom]
+    # PMC names (bf16 xlm-roberta-base runs the LayerNorm-folded forward): EPI 5 = folded
+    # QKV, 6 = folded FFN1 + GELU, 7 = residual + row statistics (O and FFN2 share it)
+    pmc_name = {"gemm_qkv": "gemm256_kernel<5>", "gemm_ffn1": "gemm256_kernel<6>",
+                "gemm_o": "gemm256_kernel<7>", "gemm_ffn2": "gemm256_kernel<7>"}[dom]
     traffic, src = load_pmc_traffic(pmc_name)
     model_flops = float(flops_per_doc(lens).sum())
     docs_per_s = world * args.docs * args.steps / el

@@ -46,8 +46,7 @@ def short(name):
     if sm:
         return sm
     n = name.split("(")[0]
-    n = n.split("::")[-1]
-    return n.split("<")[0] if "<" in n and not n.startswith("merge") else n
+    return n.split("::")[-1]  # keeps template arguments: gemm256_kernel<6> != <7>
 
 
 def main(root):
