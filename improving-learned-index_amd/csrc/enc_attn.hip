@@ -629,43 +629,49 @@ attention_v3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
     // ds_read_b64_tr_b16 lane role inside its 16-lane group: row q, column quad p
     const int tq = c >> 2, tp = c & 3;
 
-    int p = blockIdx.x, b = 0;
-    if (DB && p < n_pairs) stage(p, 0);
-    for (; p < n_pairs; p += gridDim.x, b ^= (DB ? 1 : 0)) {
-        if (!DB) stage(p, 0);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this pair's copy (+ old stores)
-        __syncthreads();
-        const int doc = p / n_heads, h = p % n_heads;
-        const int tok0 = cu_seqlens[doc], n = cu_seqlens[doc + 1] - tok0;
-        const int n_qb = (n + 16 * QTB - 1) / (16 * QTB);
-        // Q fragments of this wave's (at most two) query blocks, before the prefetch
-        uint4 qf[2][QTB][2];
+    // Q of pair p comes one pair ahead (inline-asm global loads: the compiler sees no
+    // pending load, so it neither waits nor drains the K/V prefetch for them), into the
+    // register set not in use; the wait at the top of the pair retires it.  The two
+    // sets are used in turn (the loop is unrolled by two: no register copies).
+    auto load_q = [&](int pp, uint4 (&qd)[2][QTB][2]) {
+        const int dd = pp / n_heads, hh = pp % n_heads;
+        const int t0 = cu_seqlens[dd], nn = cu_seqlens[dd + 1] - t0;
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
             const int q_base = (wave + i * ATT3_WAVES) * 16 * QTB;
 #pragma unroll
             for (int qt = 0; qt < QTB; ++qt) {
-                const int qrow = tok0 + min(q_base + 16 * qt + c, n - 1);
+                const int qrow = t0 + min(q_base + 16 * qt + c, nn - 1);
 #pragma unroll
-                for (int ch = 0; ch < 2; ++ch)
-                    qf[i][qt][ch] = *reinterpret_cast<const uint4 *>(
-                        qkv + (int64_t)qrow * ld + h * ATT_D + ch * 32 + 8 * g);
+                for (int ch = 0; ch < 2; ++ch) {
+                    const bf16 *src = qkv + (int64_t)qrow * ld + hh * ATT_D + ch * 32 + 8 * g;
+                    asm volatile("global_load_dwordx4 %0, %1, off"
+                                 : "=v"(qd[i][qt][ch])
+                                 : "v"(src)
+                                 : "memory");
+                }
             }
         }
-        // retire the Q loads here, before the prefetch is issued: the opaque asm
-        // makes the compiler's own wait for them land at this point (a later one
-        // would have to be vmcnt(0) and drain the prefetch too)
+    };
+    auto run_pair = [&](int p, int b, uint4 (&qc)[2][QTB][2], uint4 (&qn)[2][QTB][2]) {
+        if (!DB) stage(p, 0);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // K/V and Q of this pair
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
             for (int qt = 0; qt < QTB; ++qt)
 #pragma unroll
-                for (int ch = 0; ch < 2; ++ch) {
-                    uint4 t = qf[i][qt][ch];
-                    asm volatile("" : "+v"(t.x), "+v"(t.y), "+v"(t.z), "+v"(t.w));
-                    qf[i][qt][ch] = t;
-                }
-        if (DB && p + (int)gridDim.x < n_pairs) stage(p + gridDim.x, b ^ 1);
+                for (int ch = 0; ch < 2; ++ch)  // the loaded values exist from here on
+                    asm volatile("" : "+v"(qc[i][qt][ch].x), "+v"(qc[i][qt][ch].y),
+                                 "+v"(qc[i][qt][ch].z), "+v"(qc[i][qt][ch].w));
+        __syncthreads();
+        const int doc = p / n_heads, h = p % n_heads;
+        const int tok0 = cu_seqlens[doc], n = cu_seqlens[doc + 1] - tok0;
+        const int n_qb = (n + 16 * QTB - 1) / (16 * QTB);
+        if (p + (int)gridDim.x < n_pairs) {
+            load_q(p + gridDim.x, qn);
+            if (DB) stage(p + gridDim.x, b ^ 1);
+        }
 
         const uint32_t kim = lds_base + b * Att3<DB>::BUF;
         const uint32_t vim = kim + Att3<DB>::ROWS * 128;
@@ -723,7 +729,7 @@ attention_v3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
                         s[t] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
                         for (int ch = 0; ch < 2; ++ch)
-                            mma_chunk(kf[t][ch], qf[i][qt][ch], s[t], bf16{});
+                            mma_chunk(kf[t][ch], qc[i][qt][ch], s[t], bf16{});
                     }
                     if (tail) {
 #pragma unroll
@@ -758,6 +764,21 @@ attention_v3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
             }
         }
         __syncthreads();  // every wave is done with buffer b before it is restaged
+    };
+    uint4 qa[2][QTB][2], qb2[2][QTB][2];
+    int p = blockIdx.x, b = 0;
+    if (p < n_pairs) {
+        if (DB) stage(p, 0);
+        load_q(p, qa);
+    }
+    while (p < n_pairs) {
+        run_pair(p, b, qa, qb2);
+        p += gridDim.x;
+        b ^= (DB ? 1 : 0);
+        if (p >= n_pairs) break;
+        run_pair(p, b, qb2, qa);
+        p += gridDim.x;
+        b ^= (DB ? 1 : 0);
     }
 }
 
