@@ -98,7 +98,7 @@ __device__ __forceinline__ void score_radix_pass(ScoreShared &sh, int n_local, i
 // used (a read-then-use loop is LDS-latency bound).  Words past the zeroed range
 // come as 0; f runs in wave-uniform control flow (it may ballot).
 template <class F>
-__device__ __forceinline__ void sweep_words(const uint32_t *acc, int n_local, F f) {
+__device__ __forceinline__ void sweep_words(const uint32_t *acc, int n_local, int tid, F f) {
     const uint4 *a4 = reinterpret_cast<const uint4 *>(acc);
     const int n4 = (n_local + 3) >> 2;
     constexpr int G = 4;  // uint4 reads in flight per lane
@@ -107,13 +107,13 @@ __device__ __forceinline__ void sweep_words(const uint32_t *acc, int n_local, F 
         uint4 x[G];
 #pragma unroll
         for (int i = 0; i < G; ++i) {
-            const int q4 = (i0 + i) * SC_THREADS + (int)threadIdx.x;
+            const int q4 = (i0 + i) * SC_THREADS + tid;
             const uint4 y = a4[min(q4, n4 - 1)];
             x[i] = q4 < n4 ? y : make_uint4(0, 0, 0, 0);
         }
 #pragma unroll
         for (int i = 0; i < G; ++i) {
-            const int base = 4 * ((i0 + i) * SC_THREADS + (int)threadIdx.x);
+            const int base = 4 * ((i0 + i) * SC_THREADS + tid);
             f(x[i].x, base);
             f(x[i].y, base + 1);
             f(x[i].z, base + 2);
@@ -128,14 +128,14 @@ __device__ __forceinline__ void sweep_words(const uint32_t *acc, int n_local, F 
 // out(list, pos, w, idx) -- no atomics.  Returns the packed totals (A | B << 16;
 // each list holds at most 32768).  Ends with a barrier.
 template <class Cls, class Out>
-__device__ __forceinline__ uint32_t compact_words(ScoreShared &sh, int n_local, Cls cls,
+__device__ __forceinline__ uint32_t compact_words(ScoreShared &sh, int n_local, int tid, Cls cls,
                                                   Out out) {
     uint32_t cnt = 0;
-    sweep_words(sh.acc, n_local, [&](uint32_t w, int idx) {
+    sweep_words(sh.acc, n_local, tid, [&](uint32_t w, int idx) {
         const uint32_t c = cls(w, idx);
         cnt += (c & 1u) + ((c & 2u) << 15);
     });
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int lane = tid & 63, wave = tid >> 6;
     const uint32_t incl = wave_prefix_sum(cnt);
     if (lane == 63) sh.wsum[wave] = incl;
     __syncthreads();
@@ -146,7 +146,7 @@ __device__ __forceinline__ uint32_t compact_words(ScoreShared &sh, int n_local, 
         total += x;
     }
     uint32_t pa = base & 0xFFFFu, pb = base >> 16;
-    sweep_words(sh.acc, n_local, [&](uint32_t w, int idx) {
+    sweep_words(sh.acc, n_local, tid, [&](uint32_t w, int idx) {
         const uint32_t c = cls(w, idx);
         if (c & 1u) out(0, pa++, w, idx);
         if (c & 2u) out(1, pb++, w, idx);
@@ -169,6 +169,34 @@ __device__ __forceinline__ bool wave_append(bool take, uint32_t *cursor, uint32_
     return take;
 }
 
+// One scatter round over postings p[0..last] (lane-consecutive, U per lane): all
+// loads first (unconditional: clamped address, a lane past the end drops its value
+// afterwards -- a load behind a per-lane condition makes the compiler branch around it
+// and drain vmcnt element by element), then the LDS reads, then the writes.  A doc
+// occurs once per term, so the read-modify-write needs no atomics.
+template <int UU>
+__device__ __forceinline__ void scatter_round(uint32_t *acc, const uint32_t *p, int last, int tid,
+                                              uint32_t first_bits) {
+    uint32_t cur[UU], w[UU];
+#pragma unroll
+    for (int u = 0; u < UU; ++u) {
+        const int i = tid + u * SC_THREADS;
+        const uint32_t x = p[min(i, last)];
+        cur[u] = i <= last ? x : 0u;
+    }
+#pragma unroll
+    for (int u = 0; u < UU; ++u) w[u] = acc[(cur[u] >> 8) & (MAX_BLOCK_DOCS - 1)];
+#pragma unroll
+    for (int u = 0; u < UU; ++u) {
+        const uint32_t v = cur[u] & 255u;  // 0 only for the padding lanes
+        if (v) {
+            const uint32_t x = w[u];
+            acc[(cur[u] >> 8) & (MAX_BLOCK_DOCS - 1)] =
+                x ? x + (v << 16) : ((v << 16) | first_bits | v);
+        }
+    }
+}
+
 // One work item = (query q, doc block b): accumulate, select the block's top-k.
 __device__ __forceinline__ void score_item(ScoreShared &sh, int item,
                                            const uint32_t *__restrict__ post,
@@ -183,7 +211,11 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int item,
 
     const int b = item % nb;
     const int q = item / nb;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    // opaque per item: keeps the per-thread index arithmetic of the sweeps from being
+    // hoisted out of the persistent item loop (it spilled there)
+    int tid = threadIdx.x;
+    asm volatile("" : "+v"(tid));
+    const int lane = tid & 63, wave = tid >> 6;
     const int64_t block_first = (int64_t)b * block_docs;
     const int n_local = (int)min((int64_t)block_docs, (int64_t)n_docs - block_first);
     const int q0 = cu_q[q], nt = cu_q[q + 1] - q0;
@@ -227,57 +259,29 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int item,
     }
 
     // ---- scatter: terms in query order, barrier between terms -------------
-    // The postings of (term j, this block) are walked in rounds of SC_THREADS*U
-    // dwords (coalesced: lane-consecutive).  Every load is unconditional (clamped
-    // address, the value of a lane past the end is dropped afterwards): a load behind
-    // a per-lane condition makes the compiler branch around it and drain the counter
-    // (vmcnt(0)) element by element.
-    constexpr int U = 16;
-    constexpr int ROUND = SC_THREADS * U;
-    auto rounds = [&](int jj) { return (int)((hi[jj] - lo[jj] + ROUND - 1) / ROUND); };
-    // wave-uniform base pointer + 32-bit lane offsets (one VGPR per address)
-    auto load_round = [&](int jj, int rr, uint32_t (&r)[U]) {
-        const int64_t b0 = lo[jj] + (int64_t)rr * ROUND;
-        const uint32_t *p = post + b0;
-        const int last = (int)(hi[jj] - 1 - b0);  // >= 0: the round is not empty
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int i = tid + u * SC_THREADS;
-            const uint32_t x = p[min(i, last)];
-            r[u] = i <= last ? x : 0u;
-        }
-    };
-    int j = (ablate & 1) ? nt : 0, rr = 0;  // ablate bit 0: skip the scatter (profiling)
-    while (j < nt && rounds(j) == 0) ++j;
-    // One round = 16 loads per lane in flight, then apply them; the 16 waves of the
-    // CU overlap one another's load latency with their LDS work (a register prefetch
-    // of the next round costs spills and buys nothing: the copy at the back-edge
-    // waits for the loads anyway).
-    while (j < nt) {
-        uint32_t cur[U];
-        load_round(j, rr, cur);
+    // A term's sublist goes in rounds of 16 postings per lane while 16 k remain, then
+    // 4 per lane while more than 1 k remain, then 1: a short tail does not pay for a
+    // full round of issue (loads, LDS reads and writes of masked lanes).  Each round
+    // has all its loads in flight before any is applied; the 16 waves of the CU
+    // overlap one another's load latency with their LDS work.
+    for (int j = (ablate & 1) ? nt : 0; j < nt; ++j) {  // ablate bit 0: skip (profiling)
         const uint32_t first_bits = (uint32_t)(255 - j) << 8;
-        uint32_t w[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) w[u] = sh.acc[(cur[u] >> 8) & (MAX_BLOCK_DOCS - 1)];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const uint32_t v = cur[u] & 255u;  // 0 only for the padding lanes
-            if (v) {
-                const uint32_t x = w[u];
-                sh.acc[(cur[u] >> 8) & (MAX_BLOCK_DOCS - 1)] =
-                    x ? x + (v << 16) : ((v << 16) | first_bits | v);
-            }
+        int64_t pos = lo[j];
+        const int64_t end = hi[j];
+        if (pos >= end) continue;
+        while (end - pos >= 16 * SC_THREADS) {
+            scatter_round<16>(sh.acc, post + pos, 16 * SC_THREADS - 1, tid, first_bits);
+            pos += 16 * SC_THREADS;
         }
-        int jn = j, rn = rr + 1;
-        while (jn < nt && rn >= rounds(jn)) {
-            ++jn;
-            rn = 0;
+        while (end - pos > SC_THREADS) {
+            scatter_round<4>(sh.acc, post + pos, (int)min(end - pos, (int64_t)4 * SC_THREADS) - 1,
+                             tid, first_bits);
+            pos += 4 * SC_THREADS;
         }
-        // term boundary: this round's LDS writes land before any wave reads the next term
-        if (jn != j && jn < nt) __syncthreads();
-        j = jn;
-        rr = rn;
+        if (end - pos > 0)
+            scatter_round<1>(sh.acc, post + pos, (int)(end - pos) - 1, tid, first_bits);
+        // term boundary: this term's LDS writes land before any wave reads the next
+        if (j + 1 < nt) __syncthreads();
     }
     __syncthreads();
 
@@ -291,7 +295,7 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int item,
         if (pos < (uint32_t)k) ck[pos] = ((uint64_t)w << 32) | (uint64_t)(0xFFFFFFFFu - doc);
     };
     auto emit_all_touched = [&]() {
-        const uint32_t n = compact_words(sh, n_local, [](uint32_t w, int) { return w ? 1u : 0u; },
+        const uint32_t n = compact_words(sh, n_local, tid, [](uint32_t w, int) { return w ? 1u : 0u; },
                                          [&](int, uint32_t pos, uint32_t w, int idx) {
                                              cand(pos, w, idx);
                                          });
@@ -303,7 +307,7 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int item,
     if (fast) {
         // ---- fast path: score histogram -> k-th score T -------------------
         uint32_t *hist = sh.u.hist;
-        sweep_words(sh.acc, n_local, [&](uint32_t w, int) {
+        sweep_words(sh.acc, n_local, tid, [&](uint32_t w, int) {
             if (w) atomicAdd(&hist[w >> 16], 1u);
         });
         __syncthreads();
@@ -351,7 +355,7 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int item,
             const bool all_ties = ties == need;
             uint32_t *tl = sh.u.hist;
             compact_words(
-                sh, n_local,
+                sh, n_local, tid,
                 [T, all_ties](uint32_t w, int) -> uint32_t {
                     const uint32_t sc = w >> 16;
                     return (sc > T || (all_ties && sc == T)) ? 1u : (sc == T ? 2u : 0u);
@@ -475,7 +479,7 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int item,
     }
     __syncthreads();
     const uint32_t n = compact_words(
-        sh, n_local,
+        sh, n_local, tid,
         [T, dcut](uint32_t w, int idx) -> uint32_t {
             return (w != 0 && (w > T || (w == T && (0xFFFFu - (uint32_t)idx) >= dcut))) ? 1u : 0u;
         },
@@ -739,6 +743,45 @@ void build_index(di_index *ix, const int64_t *term_off, int64_t n_terms, const u
             uint32_t r = d - doc_lo;
             int b = (int)(r / bd);
             packed[tstart[t] + cur[b]++] = ((r % bd) << 8) | pval[p];
+        }
+    }
+    // pass 3: LDS-bank order inside every (term, block) sublist.  The scorer's lanes
+    // read consecutive postings and update acc[doc_in_block]; a 32-lane group of a
+    // ds_read_b32 / ds_write_b32 conflicts on equal (doc_in_block mod 32).  Dealing
+    // the sublist round-robin from its 32 bank buckets makes every 32 consecutive
+    // postings hit distinct banks while all buckets last.  Any order is exact: a doc
+    // occurs once per term, and its key (first term, value there) does not depend on
+    // the order inside the term.
+    {
+        std::vector<uint32_t> tmp, bucket_cnt(32), bucket_pos(32);
+        for (int64_t t = 0; t < n_terms; ++t) {
+            for (int b = 0; b < nb; ++b) {
+                const int64_t s0 = tstart[t] + boff[t * stride + b];
+                const int64_t s1 = tstart[t] + boff[t * stride + b + 1];
+                if (s1 - s0 <= 1) continue;
+                std::fill(bucket_cnt.begin(), bucket_cnt.end(), 0);
+                for (int64_t i = s0; i < s1; ++i) bucket_cnt[(packed[i] >> 8) & 31]++;
+                uint32_t run = 0;
+                for (int k = 0; k < 32; ++k) {
+                    bucket_pos[k] = run;
+                    run += bucket_cnt[k];
+                }
+                tmp.resize((size_t)(s1 - s0));
+                for (int64_t i = s0; i < s1; ++i) tmp[bucket_pos[(packed[i] >> 8) & 31]++] = packed[i];
+                // bucket k now spans [bucket_pos[k] - bucket_cnt[k], bucket_pos[k])
+                std::vector<uint32_t> &head = bucket_pos;
+                for (int k = 0; k < 32; ++k) head[k] -= bucket_cnt[k];
+                int64_t o = s0;
+                for (bool any = true; any;) {
+                    any = false;
+                    for (int k = 0; k < 32; ++k)
+                        if (bucket_cnt[k]) {
+                            packed[o++] = tmp[head[k]++];
+                            --bucket_cnt[k];
+                            any = true;
+                        }
+                }
+            }
         }
     }
     ix->post.reserve(packed.size() * 4);
