@@ -290,15 +290,32 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int item,
         return;
     }
     const uint64_t doc_base = (uint64_t)doc_lo + (uint64_t)block_first;
+    // Candidates are staged in the unused tail of the accumulator array when they fit
+    // there and copied out coalesced (a lane-scattered 8-byte store per candidate slot
+    // costs a store instruction per slot and wave); else they go straight out.
+    const int n4z = (n_local + 3) >> 2;
+    uint64_t *stage = reinterpret_cast<uint64_t *>(sh.acc + 4 * n4z);
+    const bool staged = 2 * k <= MAX_BLOCK_DOCS - 4 * n4z;
     auto cand = [&](uint32_t pos, uint32_t w, int idx) {
         const uint32_t doc = (uint32_t)(doc_base + (uint64_t)idx);
-        if (pos < (uint32_t)k) ck[pos] = ((uint64_t)w << 32) | (uint64_t)(0xFFFFFFFFu - doc);
+        const uint64_t key = ((uint64_t)w << 32) | (uint64_t)(0xFFFFFFFFu - doc);
+        if (pos < (uint32_t)k) {
+            if (staged)
+                stage[pos] = key;
+            else
+                ck[pos] = key;
+        }
+    };
+    auto flush = [&](uint32_t n_c) {  // after a barrier
+        if (staged)
+            for (uint32_t i = tid; i < n_c; i += SC_THREADS) ck[i] = stage[i];
     };
     auto emit_all_touched = [&]() {
         const uint32_t n = compact_words(sh, n_local, tid, [](uint32_t w, int) { return w ? 1u : 0u; },
                                          [&](int, uint32_t pos, uint32_t w, int idx) {
                                              cand(pos, w, idx);
                                          });
+        flush(min(n & 0xFFFFu, (uint32_t)k));
         if (tid == 0) *cn = (int32_t)min(n & 0xFFFFu, (uint32_t)k);
     };
 
@@ -415,9 +432,11 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int item,
                         cand(pos, (T << 16) | (x >> 16), (int)(0xFFFFu - (x & 0xFFFFu)));
                 }
                 __syncthreads();
+                flush((uint32_t)k);
                 // sh.emit == k by construction; anything else is a selection bug
                 if (tid == 0) *cn = sh.emit == (uint32_t)k ? k : -2;
             } else {
+                flush((uint32_t)k);
                 if (tid == 0) *cn = k;
             }
             return;
@@ -484,6 +503,7 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int item,
             return (w != 0 && (w > T || (w == T && (0xFFFFu - (uint32_t)idx) >= dcut))) ? 1u : 0u;
         },
         [&](int, uint32_t pos, uint32_t w, int idx) { cand(pos, w, idx); });
+    flush((uint32_t)k);
     // exactly k by construction; anything else is a selection bug -> flag it
     if (tid == 0) *cn = (n & 0xFFFFu) == (uint32_t)k ? k : -2;
 }
