@@ -57,6 +57,46 @@ __device__ __forceinline__ f32x2 gelu_erf2(f32x2 x) {
 }
 __device__ __forceinline__ float gelu_erf(float x) { return gelu_erf2(f32x2{x, x}).x; }
 
+// gelu_erf2 on 8 values at once, the four pair chains advanced in lockstep: each
+// Horner step of one pair depends on the previous step, so one chain at a time runs
+// at the dependent-issue latency; four independent chains fill those gaps.
+__device__ __forceinline__ void gelu_erf8(float (&v)[8]) {
+#define DI_C2(c) f32x2{c, c}
+    f32x2 x[4], x2[4], p[4], q[4], h[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const f32x2 xi = f32x2{v[2 * i], v[2 * i + 1]};
+        h[i] = xi * DI_C2(0.5f);
+        x[i] = __builtin_elementwise_min(
+            __builtin_elementwise_max(xi * DI_C2(0.70710678118654752440f), DI_C2(-4.0f)),
+            DI_C2(4.0f));
+        x2[i] = x[i] * x[i];
+        p[i] = DI_C2(-2.72614225801306e-10f);
+        q[i] = DI_C2(-1.45660718464996e-05f);
+    }
+    constexpr float PC[6] = {2.77068142495902e-08f, -2.10102402082508e-06f,
+                             -5.69250639462346e-05f, -7.34990630326855e-04f,
+                             -2.95459980854025e-03f, -1.60960333262415e-02f};
+    constexpr float QC[4] = {-2.13374055278905e-04f, -1.68282697438203e-03f,
+                             -7.37332916720468e-03f, -1.42647390514189e-02f};
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            p[i] = __builtin_elementwise_fma(x2[i], p[i], DI_C2(PC[k]));
+            if (k < 4) q[i] = __builtin_elementwise_fma(x2[i], q[i], DI_C2(QC[k]));
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const f32x2 e = p[i] * x[i] * f32x2{__builtin_amdgcn_rcpf(q[i].x), __builtin_amdgcn_rcpf(q[i].y)};
+        const f32x2 y = __builtin_elementwise_fma(h[i], e, h[i]);
+        v[2 * i] = y.x;
+        v[2 * i + 1] = y.y;
+    }
+#undef DI_C2
+}
+
 // GEMM epilogues
 enum GemmEpi : int {
     EPI_BIAS = 0,        // out(T) = acc + bias

@@ -391,14 +391,7 @@ __global__ void __launch_bounds__(G2_T) gemm256_kernel(GemmArgs g) {
 #pragma unroll
                 for (int e = 0; e < 8; ++e)
                     v[e] = fmaf(ra[mt], acc[mt][2 * h + (e >> 2)][e & 3], fmaf(rb[mt], cs[e], cc[e]));
-                if constexpr (EPI == EPI_FOLD_GELU) {
-#pragma unroll
-                    for (int e = 0; e < 8; e += 2) {
-                        const f32x2 y = gelu_erf2(f32x2{v[e], v[e + 1]});
-                        v[e] = y.x;
-                        v[e + 1] = y.y;
-                    }
-                }
+                if constexpr (EPI == EPI_FOLD_GELU) gelu_erf8(v);
                 bf16x8 ov;
 #pragma unroll
                 for (int e = 0; e < 8; ++e) ov[e] = (bf16)v[e];
@@ -500,14 +493,7 @@ __global__ void __launch_bounds__(G2_T) gemm256_kernel(GemmArgs g) {
             float v[8];
 #pragma unroll
             for (int e = 0; e < 8; ++e) v[e] = acc[mt][2 * h + (e >> 2)][e & 3] + bias_v[h][e];
-            if (EPI == EPI_BIAS_GELU && !(g.ablate & 2)) {  // ablate 2: no GELU (profiling)
-#pragma unroll
-                for (int e = 0; e < 8; e += 2) {
-                    const f32x2 y = gelu_erf2(f32x2{v[e], v[e + 1]});
-                    v[e] = y.x;
-                    v[e + 1] = y.y;
-                }
-            }
+            if (EPI == EPI_BIAS_GELU && !(g.ablate & 2)) gelu_erf8(v);  // ablate 2: no GELU (profiling)
             const int64_t o = (int64_t)row * g.ld_out + col_l + h * 32;
             if constexpr (EPI == EPI_BIAS_RESID || EPI == EPI_BIAS_RESID_LN) {
                 const bf16x8 rv = *reinterpret_cast<const bf16x8 *>(
