@@ -94,6 +94,34 @@ class QueryRelevanceDataset:
         return self.qrels.keys()
 
 
+class Collection:
+    """datasets.py:50-95: pid (str) -> passage of an MS MARCO collection, lines
+    [offset, offset + limit)."""
+
+    def __init__(self, collection_path: Union[str, Path], offset: Optional[int] = None,
+                 limit: Optional[int] = None):
+        offset = 0 if offset is None else offset
+        limit = float("inf") if limit is None else limit
+        self.collection: Dict[str, str] = {}
+        with open(collection_path, encoding="utf-8") as f:
+            for idx, line in enumerate(f):
+                if idx < offset:
+                    continue
+                if idx >= offset + limit:
+                    break
+                pid, passage, = line.strip().split("\t")
+                self.collection[str(pid)] = passage
+
+    def __len__(self):
+        return len(self.collection)
+
+    def __getitem__(self, pid):
+        return self.collection[str(pid)]
+
+    def __iter__(self):
+        return iter(self.collection.items())
+
+
 class RunFile:
     """datasets.py:305-324: qid \\t pid \\t rank \\t score."""
 
@@ -110,3 +138,27 @@ class RunFile:
             for line in f:
                 qid, pid, rank, score = line.strip().split("\t")
                 yield str(qid), str(pid), int(rank), float(score)
+
+
+class TopKRunFile(RunFile):
+    """datasets.py:327-347: qid -> its first k pids by rank."""
+
+    def __init__(self, run_file_path: Union[str, Path], k: int = 2000):
+        super().__init__(run_file_path)
+        top_k: Dict[str, list] = {}
+        for qid, pid, rank, _ in self.read():
+            top_k.setdefault(qid, []).append((rank, pid))
+        for qid in top_k:
+            top_k[qid].sort()
+            top_k[qid] = [v for _, v in top_k[qid][:k]]
+        self.top_k = top_k
+
+    def __len__(self):
+        return len(self.top_k)
+
+    def __getitem__(self, qid):
+        return self.top_k[str(qid)]
+
+    def __iter__(self):
+        for qid in self.top_k:
+            yield qid, self.top_k[qid]

@@ -145,3 +145,38 @@ def test_create_and_rank_cli_match_reference():
             for r, (d, s) in enumerate(ora.score(terms, 1000), start=1):
                 want.append(f"q{i}\t{d}\t{r}\t{s}\n")
         assert (td / "run.tsv").read_text() == "".join(want)
+
+
+def test_reranker_cli_on_the_hip_encoder(small_ckpt):
+    """F3 (reranker.py:13-91): the rerank CLI on the HIP encoder (fp32) scores every
+    candidate as the sum of its query terms' impacts; those equal the fp32 torch
+    oracle's impacts for the same passages within 1e-3 relative."""
+    from improving_learned_index_amd import reranker
+    from improving_learned_index_amd.models import DeepImpact
+
+    fx, path = small_ckpt
+    texts = fx["texts"]
+    with tempfile.TemporaryDirectory() as td:
+        td = Path(td)
+        (td / "coll.tsv").write_text("".join(f"{i}\t{t}\n" for i, t in enumerate(texts)))
+        qs = [" ".join(texts[i].split()[:4]) for i in range(len(texts))]
+        (td / "q.tsv").write_text("".join(f"{i}\t{q}\n" for i, q in enumerate(qs)))
+        (td / "topk.tsv").write_text("".join(
+            f"{q}\t{p}\t{r}\t0\n" for q in range(len(qs))
+            for r, p in enumerate(reversed(range(len(texts))), start=1)))
+        reranker.main(["--checkpoint_path", str(path), "--top_k_run_file_path",
+                       str(td / "topk.tsv"), "--queries_path", str(td / "q.tsv"),
+                       "--collection_path", str(td / "coll.tsv"), "--output_path",
+                       str(td / "out.tsv"), "--tokenizer_path", str(GOLDEN / "tokenizer.json"),
+                       "--precision", "fp32", "--max_length", str(fx["max_length"]),
+                       "--batch_size", "3"])
+        rows = [l.split("\t") for l in (td / "out.tsv").read_text().splitlines()]
+    assert len(rows) == len(qs) * len(texts)
+    # oracle: fp32 torch impacts at each passage's first-token positions
+    want_imp = [dict((t, np.array([b], np.uint32).view(np.float32)[0]) for t, b in d)
+                for d in fx["term_impacts_f32_bits"]]
+    DeepImpact.set_tokenizer(GOLDEN / "tokenizer.json")
+    for q, p, rank, score in rows:
+        terms = DeepImpact.process_query(qs[int(q)])
+        want = sum(float(want_imp[int(p)].get(t, 0)) for t in terms)
+        assert abs(float(score) - want) <= 1e-3 * max(1.0, abs(want)), (q, p, score, want)
