@@ -827,6 +827,9 @@ void enable_big_lds() {
     DI_HIP(hipFuncSetAttribute((const void *)merge_topk_kernel<256>,
                                hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)(sizeof(MergeHead<256>) + MG_LDS_KEYS * 8)));
+    DI_HIP(hipFuncSetAttribute((const void *)merge_topk_kernel<512>,
+                               hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)(sizeof(MergeHead<512>) + MG_LDS_KEYS * 8)));
 }
 
 void launch_merge(const uint64_t *keys, const int32_t *counts, int n_q, int n_lists, int k_in,
@@ -846,9 +849,20 @@ void launch_merge(const uint64_t *keys, const int32_t *counts, int n_q, int n_li
     if (n_lists > 1024 || want > MG_LDS_KEYS) want = k;
     int cap = 64;
     while (cap < want) cap <<= 1;
-    if (cap <= 256) {
+    // workgroup size of the merge (DI_MERGE_THREADS: A/B knob); 512 measured best for
+    // the 4-block x 1000-candidate bench merge (0.68 vs 0.73 ms at 1024, 0.86 at 256)
+    static const int mt = [] {
+        const char *e = std::getenv("DI_MERGE_THREADS");
+        return e ? std::atoi(e) : 512;
+    }();
+    if (cap <= 256 || mt == 256) {
         size_t lds = sizeof(MergeHead<256>) + (size_t)cap * 8;
         hipLaunchKernelGGL(merge_topk_kernel<256>, dim3(n_q), dim3(256), lds, s, keys, counts,
+                           n_lists, k_in, k, ls, cs, qs, cqs, cap, out_key, out_doc, out_score,
+                           out_n, mode);
+    } else if (mt == 512) {
+        size_t lds = sizeof(MergeHead<512>) + (size_t)cap * 8;
+        hipLaunchKernelGGL(merge_topk_kernel<512>, dim3(n_q), dim3(512), lds, s, keys, counts,
                            n_lists, k_in, k, ls, cs, qs, cqs, cap, out_key, out_doc, out_score,
                            out_n, mode);
     } else {
