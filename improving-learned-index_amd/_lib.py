@@ -51,6 +51,7 @@ SIGNATURES = {
     "di_index_search": (ctypes.c_int, [P, P, P, I32, I32, P, P, P, P, U32]),
     "di_index_reserve": (ctypes.c_int, [P, I32, I32]),
     "di_index_info": (ctypes.c_int, [P, P, P, P, P]),
+    "di_index_set_min_impact": (ctypes.c_int, [P, I32]),
     "di_index_set_stream": (ctypes.c_int, [P, P]),
     "di_index_sync": (ctypes.c_int, [P]),
     "di_index_timing": (ctypes.c_int, [P, ctypes.c_char_p, P, ctypes.c_int]),
@@ -196,6 +197,10 @@ class DeviceIndex:
 
     def reserve(self, max_q, k):
         check(lib().di_index_reserve(self._h, max_q, k))
+
+    def set_min_impact(self, min_impact=1):
+        """Score only postings with value >= 2^floor(log2 min_impact) (1 = exact)."""
+        check(lib().di_index_set_min_impact(self._h, int(min_impact)))
 
     def set_stream(self, stream_ptr):
         check(lib().di_index_set_stream(self._h, ctypes.c_void_p(stream_ptr)))

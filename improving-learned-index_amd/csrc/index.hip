@@ -201,7 +201,8 @@ __device__ __forceinline__ void scatter_round(uint32_t *acc, const uint32_t *p, 
 __device__ __forceinline__ void score_item(ScoreShared &sh, int item,
                                            const uint32_t *__restrict__ post,
                                            const int64_t *__restrict__ term_start,
-                                           const uint32_t *__restrict__ blk_off, int nb,
+                                           const uint32_t *__restrict__ blk_off,
+                                           const uint16_t *__restrict__ seg, int min_cls, int nb,
                                            int block_docs, int64_t n_terms, uint32_t n_docs,
                                            uint32_t doc_lo, const uint32_t *__restrict__ q_terms,
                                            const int32_t *__restrict__ cu_q, int k,
@@ -244,7 +245,8 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int item,
         }
         const uint32_t *bo = blk_off + (int64_t)t * (nb + 1) + b;
         lo[j] = term_start[t] + bo[0];
-        hi[j] = term_start[t] + bo[1];
+        hi[j] = min_cls >= 7 ? term_start[t] + bo[1]
+                             : lo[j] + seg[((int64_t)t * nb + b) * 8 + min_cls];
     }
     {
         uint4 *a4 = reinterpret_cast<uint4 *>(sh.acc);
@@ -512,14 +514,16 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int item,
 // workgroup launch cost (16 waves, 150 KiB of LDS) is paid once per CU, not per item.
 __global__ void __launch_bounds__(SC_THREADS)
 score_blocks_kernel(const uint32_t *__restrict__ post, const int64_t *__restrict__ term_start,
-                    const uint32_t *__restrict__ blk_off, int nb, int block_docs, int64_t n_terms,
+                    const uint32_t *__restrict__ blk_off, const uint16_t *__restrict__ seg,
+                    int min_cls, int nb, int block_docs, int64_t n_terms,
                     uint32_t n_docs, uint32_t doc_lo, const uint32_t *__restrict__ q_terms,
                     const int32_t *__restrict__ cu_q, int k, uint64_t *__restrict__ cand_key,
                     int32_t *__restrict__ cand_n, int n_items, int ablate) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     ScoreShared &sh = *reinterpret_cast<ScoreShared *>(smem);
     for (int item = blockIdx.x; item < n_items; item += gridDim.x) {
-        score_item(sh, item, post, term_start, blk_off, nb, block_docs, n_terms, n_docs, doc_lo,
+        score_item(sh, item, post, term_start, blk_off, seg, min_cls, nb, block_docs, n_terms,
+                   n_docs, doc_lo,
                    q_terms, cu_q, k, cand_key, cand_n, ablate);
         __syncthreads();  // every wave is done with the LDS of this item
     }
@@ -679,7 +683,9 @@ struct di_index {
     int64_t n_terms = 0, n_post = 0;
     uint32_t n_docs = 0, doc_lo = 0;  // shard [doc_lo, doc_lo + n_docs)
     int nb = 0, block_docs = 0;
-    DevBuf post, term_start, blk_off;
+    int min_cls = 7;                 // impact-class prefix scored (7 = every posting: exact)
+    std::vector<uint16_t> seg;       // host copy of the class offsets (pass 3)
+    DevBuf post, term_start, blk_off, seg_dev;
     DevBuf ws_q, ws_cu, ws_ck, ws_cn, ws_doc, ws_score, ws_n, ws_key;
     int ablate = 0;  // DI_PROFILE_ABLATE: profiling only (1 no scatter, 2 no selection, 4 stop at the k-th score)
     Timer timer;
@@ -765,41 +771,61 @@ void build_index(di_index *ix, const int64_t *term_off, int64_t n_terms, const u
             packed[tstart[t] + cur[b]++] = ((r % bd) << 8) | pval[p];
         }
     }
-    // pass 3: LDS-bank order inside every (term, block) sublist.  The scorer's lanes
-    // read consecutive postings and update acc[doc_in_block]; a 32-lane group of a
-    // ds_read_b32 / ds_write_b32 conflicts on equal (doc_in_block mod 32).  Dealing
-    // the sublist round-robin from its 32 bank buckets makes every 32 consecutive
-    // postings hit distinct banks while all buckets last.  Any order is exact: a doc
-    // occurs once per term, and its key (first term, value there) does not depend on
-    // the order inside the term.
+    // pass 3: order inside every (term, block) sublist, and the impact-class offsets.
+    // Postings are grouped by impact class c = 7 - floor(log2 value) (class 0 = values
+    // 128..255, ..., class 7 = value 1), classes in order, so that "every posting with
+    // value >= 2^(7-c)" is a prefix of the sublist: seg[(t*nb + b)*8 + c] = its length
+    // (di_index_set_min_impact prunes with it; class 7 = the whole sublist = exact).
+    // Inside a class, postings are dealt round-robin from their 32 LDS bank buckets
+    // (doc_in_block mod 32): the scorer's lanes read consecutive postings and update
+    // acc[doc_in_block], and a 32-lane group of a ds_read_b32 / ds_write_b32 conflicts
+    // on equal banks.  Any order is exact: a doc occurs once per term, and its key
+    // (first term, value there) does not depend on the order inside the term.
+    ix->seg.assign((size_t)std::max<int64_t>(n_terms * nb * 8, 1), 0);
     {
-        std::vector<uint32_t> tmp, bucket_cnt(32), bucket_pos(32);
+        std::vector<uint32_t> tmp, cls_cnt(8), cls_pos(8), bucket_cnt(32), head(32);
+        auto cls_of = [](uint32_t w) { return 7 - (31 - __builtin_clz(w & 255u)); };
         for (int64_t t = 0; t < n_terms; ++t) {
             for (int b = 0; b < nb; ++b) {
                 const int64_t s0 = tstart[t] + boff[t * stride + b];
                 const int64_t s1 = tstart[t] + boff[t * stride + b + 1];
-                if (s1 - s0 <= 1) continue;
-                std::fill(bucket_cnt.begin(), bucket_cnt.end(), 0);
-                for (int64_t i = s0; i < s1; ++i) bucket_cnt[(packed[i] >> 8) & 31]++;
+                uint16_t *sg = &ix->seg[(size_t)(t * nb + b) * 8];
+                std::fill(cls_cnt.begin(), cls_cnt.end(), 0);
+                for (int64_t i = s0; i < s1; ++i) cls_cnt[cls_of(packed[i])]++;
                 uint32_t run = 0;
-                for (int k = 0; k < 32; ++k) {
-                    bucket_pos[k] = run;
-                    run += bucket_cnt[k];
+                for (int c = 0; c < 8; ++c) {
+                    cls_pos[c] = run;
+                    run += cls_cnt[c];
+                    sg[c] = (uint16_t)run;
                 }
+                if (s1 - s0 <= 1) continue;
                 tmp.resize((size_t)(s1 - s0));
-                for (int64_t i = s0; i < s1; ++i) tmp[bucket_pos[(packed[i] >> 8) & 31]++] = packed[i];
-                // bucket k now spans [bucket_pos[k] - bucket_cnt[k], bucket_pos[k])
-                std::vector<uint32_t> &head = bucket_pos;
-                for (int k = 0; k < 32; ++k) head[k] -= bucket_cnt[k];
+                for (int64_t i = s0; i < s1; ++i) tmp[cls_pos[cls_of(packed[i])]++] = packed[i];
+                // tmp: classes in order (stable); deal each class from its bank buckets
                 int64_t o = s0;
-                for (bool any = true; any;) {
-                    any = false;
-                    for (int k = 0; k < 32; ++k)
-                        if (bucket_cnt[k]) {
-                            packed[o++] = tmp[head[k]++];
-                            --bucket_cnt[k];
-                            any = true;
-                        }
+                uint32_t c0 = 0;
+                for (int c = 0; c < 8; ++c) {
+                    const uint32_t c1 = c0 + cls_cnt[c];
+                    std::fill(bucket_cnt.begin(), bucket_cnt.end(), 0);
+                    for (uint32_t i = c0; i < c1; ++i) bucket_cnt[(tmp[i] >> 8) & 31]++;
+                    uint32_t r = 0;
+                    for (int k = 0; k < 32; ++k) {
+                        head[k] = r;
+                        r += bucket_cnt[k];
+                    }
+                    std::vector<uint32_t> bk(c1 - c0);
+                    std::vector<uint32_t> fill = head;
+                    for (uint32_t i = c0; i < c1; ++i) bk[fill[(tmp[i] >> 8) & 31]++] = tmp[i];
+                    for (bool any = true; any;) {
+                        any = false;
+                        for (int k = 0; k < 32; ++k)
+                            if (bucket_cnt[k]) {
+                                packed[o++] = bk[head[k]++];
+                                --bucket_cnt[k];
+                                any = true;
+                            }
+                    }
+                    c0 = c1;
                 }
             }
         }
@@ -810,6 +836,8 @@ void build_index(di_index *ix, const int64_t *term_off, int64_t n_terms, const u
     DI_HIP(hipMemcpy(ix->post.p, packed.data(), packed.size() * 4, hipMemcpyHostToDevice));
     DI_HIP(hipMemcpy(ix->term_start.p, tstart.data(), tstart.size() * 8, hipMemcpyHostToDevice));
     DI_HIP(hipMemcpy(ix->blk_off.p, boff.data(), boff.size() * 4, hipMemcpyHostToDevice));
+    ix->seg_dev.reserve(ix->seg.size() * 2);
+    DI_HIP(hipMemcpy(ix->seg_dev.p, ix->seg.data(), ix->seg.size() * 2, hipMemcpyHostToDevice));
 }
 
 }  // namespace
@@ -1015,7 +1043,8 @@ int di_index_search(di_index *ix, const uint32_t *q_terms, const int32_t *cu_q, 
                 hipLaunchKernelGGL(score_blocks_kernel, dim3(std::min(n_items, n_cu())),
                                    dim3(SC_THREADS), sizeof(ScoreShared), s,
                                    ix->post.as<uint32_t>(), ix->term_start.as<int64_t>(),
-                                   ix->blk_off.as<uint32_t>(), nb, ix->block_docs, ix->n_terms,
+                                   ix->blk_off.as<uint32_t>(), ix->seg_dev.as<uint16_t>(),
+                                   ix->min_cls, nb, ix->block_docs, ix->n_terms,
                                    ix->n_docs, ix->doc_lo, dq, dcu + q0, k,
                                    ix->ws_ck.as<uint64_t>(), ix->ws_cn.as<int32_t>(), n_items,
                                    ix->ablate);
@@ -1055,6 +1084,16 @@ int di_index_info(const di_index *ix, int64_t *n_terms, int64_t *n_postings, uin
         if (n_postings) *n_postings = ix->n_post;
         if (n_docs) *n_docs = ix->n_docs;
         if (n_blocks) *n_blocks = ix->nb;
+    });
+}
+
+int di_index_set_min_impact(di_index *ix, int32_t min_impact) {
+    return guard([&] {
+        DI_REQUIRE(ix, DI_EINVAL, "null handle");
+        DI_REQUIRE(min_impact >= 1 && min_impact <= 255, DI_ERANGE,
+                   "min_impact=%d outside [1, 255]", min_impact);
+        // postings with value >= 2^floor(log2 min_impact): the class prefix
+        ix->min_cls = 7 - (31 - __builtin_clz((unsigned)min_impact));
     });
 }
 

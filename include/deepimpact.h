@@ -108,6 +108,13 @@ int di_index_search(di_index *ix, const uint32_t *q_terms, const int32_t *cu_q, 
 int di_index_reserve(di_index *ix, int32_t max_q, int32_t k);
 int di_index_info(const di_index *ix, int64_t *n_terms, int64_t *n_postings, uint32_t *n_docs,
                   int32_t *n_blocks);
+/* Query-time impact pruning (BASELINE configs[4], the QPS-vs-recall@1000 sweep): score
+ * only the postings with value >= 2^floor(log2 min_impact) -- a prefix of every
+ * (term, block) sublist, which the index keeps grouped by impact class.  1 (the
+ * default) scores every posting: exactly InvertedIndex.score (inverted_index.py:55-62);
+ * anything larger is an approximation whose recall bench tools measure.  No reference
+ * counterpart (the reference scores exhaustively).                                  */
+int di_index_set_min_impact(di_index *ix, int32_t min_impact);
 int di_index_set_stream(di_index *ix, void *hip_stream);
 int di_index_sync(di_index *ix);
 int di_index_timing(di_index *ix, const char *name, di_timing *out, int reset);

@@ -142,3 +142,23 @@ def test_zero_values_stop_term_lists(L):
     pval = np.array([9, 5, 0, 7], np.uint8)
     dev = L.DeviceIndex.from_postings(term_off, pdoc, pval)
     assert dev.search([[0]], 10) == [[(3, 9), (1, 5)]]
+
+
+@pytest.mark.parametrize("min_impact", [2, 5, 64])
+def test_min_impact_pruning_equals_oracle_on_pruned_postings(L, synth, min_impact):
+    """di_index_set_min_impact (BASELINE configs[4] sweep): scoring the postings with
+    value >= 2^floor(log2 min_impact) gives exactly the oracle's ranking over those
+    postings (the first-touch tie rule unchanged); 1 restores the exact search."""
+    term_off, pdoc, pval, ora = synth
+    dev = L.DeviceIndex.from_postings(term_off, pdoc, pval)
+    qs = _queries(5000, 60, seed=min_impact)
+    thr = 1 << (int(min_impact).bit_length() - 1)
+    keep = pval >= thr
+    cnt = np.array([int(keep[term_off[t]:term_off[t + 1]].sum()) for t in range(len(term_off) - 1)])
+    pr = oracle.Index.__new__(oracle.Index)
+    pr.term_off = np.concatenate([[0], np.cumsum(cnt)]).astype(np.int64)
+    pr.pdoc, pr.pval, pr.n_docs = pdoc[keep], pval[keep], ora.n_docs
+    dev.set_min_impact(min_impact)
+    assert dev.search(qs, 1000) == pr.score_ids(qs, 1000, n_threads=8)
+    dev.set_min_impact(1)
+    assert dev.search(qs, 1000) == ora.score_ids(qs, 1000, n_threads=8)
