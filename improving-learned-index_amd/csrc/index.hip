@@ -34,6 +34,7 @@
 #include <memory>
 #include <numeric>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "di_common.h"
@@ -57,7 +58,7 @@ struct ScoreShared {
     uint32_t acc[MAX_BLOCK_DOCS];  // 128 KiB
     union {
         RadixScratch<SC_WAVES> rs;  // general radix path
-        uint32_t hist[HIST_BINS];   // fast path: score histogram, then the tie list
+        uint32_t hist[HIST_BINS + 64];  // fast path: score histogram (+ spare bins), then the tie list
     } u;
     union {
         int64_t bounds[2][MAX_TERMS];  // scatter: sublist [lo, hi) of every query term
@@ -69,7 +70,8 @@ struct ScoreShared {
     uint32_t bad;
     uint32_t thr, above, ties, bin, bin_above;
 };
-static_assert(sizeof(RadixScratch<SC_WAVES>) >= HIST_BINS * 4, "histogram overlays the radix scratch");
+static_assert(sizeof(RadixScratch<SC_WAVES>) >= (HIST_BINS + 64) * 4,
+              "histogram (+ 64 spare bins) overlays the radix scratch");
 
 // One radix pass over the block's words (i-major: lanes read consecutive words,
 // conflict-free).  KeyF: word,index -> key;  Pred: word,index,key -> bool.
@@ -107,9 +109,14 @@ __device__ __forceinline__ void sweep_words(const uint32_t *acc, int n_local, in
         uint4 x[G];
 #pragma unroll
         for (int i = 0; i < G; ++i) {
+            // q4 < 8192 always lies inside the array: load unconditionally (no branch),
+            // then drop what lies past the zeroed range
             const int q4 = (i0 + i) * SC_THREADS + tid;
-            const uint4 y = a4[min(q4, n4 - 1)];
-            x[i] = q4 < n4 ? y : make_uint4(0, 0, 0, 0);
+            const uint4 y = a4[q4];
+            x[i].x = q4 < n4 ? y.x : 0u;
+            x[i].y = q4 < n4 ? y.y : 0u;
+            x[i].z = q4 < n4 ? y.z : 0u;
+            x[i].w = q4 < n4 ? y.w : 0u;
         }
 #pragma unroll
         for (int i = 0; i < G; ++i) {
@@ -127,14 +134,15 @@ __device__ __forceinline__ void sweep_words(const uint32_t *acc, int n_local, in
 // block scan of the packed per-thread counts, one writing sweep calling
 // out(list, pos, w, idx) -- no atomics.  Returns the packed totals (A | B << 16;
 // each list holds at most 32768).  Ends with a barrier.
-template <class Cls, class Out>
+template <class Cls, class Out, class St = void (*)(int)>
 __device__ __forceinline__ uint32_t compact_words(ScoreShared &sh, int n_local, int tid, Cls cls,
-                                                  Out out) {
+                                                  Out out, St st = nullptr) {
     uint32_t cnt = 0;
     sweep_words(sh.acc, n_local, tid, [&](uint32_t w, int idx) {
         const uint32_t c = cls(w, idx);
         cnt += (c & 1u) + ((c & 2u) << 15);
     });
+    if constexpr (!std::is_same<St, void (*)(int)>::value) st(6);
     const int lane = tid & 63, wave = tid >> 6;
     const uint32_t incl = wave_prefix_sum(cnt);
     if (lane == 63) sh.wsum[wave] = incl;
@@ -146,6 +154,7 @@ __device__ __forceinline__ uint32_t compact_words(ScoreShared &sh, int n_local, 
         total += x;
     }
     uint32_t pa = base & 0xFFFFu, pb = base >> 16;
+    if constexpr (!std::is_same<St, void (*)(int)>::value) st(7);
     sweep_words(sh.acc, n_local, tid, [&](uint32_t w, int idx) {
         const uint32_t c = cls(w, idx);
         if (c & 1u) out(0, pa++, w, idx);
@@ -197,6 +206,10 @@ __device__ __forceinline__ void scatter_round(uint32_t *acc, const uint32_t *p, 
     }
 }
 
+// Profiling (DI_PROFILE_ABLATE bit 64): per-phase shader cycles of workgroup 0's items
+// accumulated here and printed by di_index_search.
+__device__ unsigned long long g_sb_phase[8];
+
 // One work item = (query q, doc block b): accumulate, select the block's top-k.
 __device__ __forceinline__ void score_item(ScoreShared &sh, int item,
                                            const uint32_t *__restrict__ post,
@@ -228,6 +241,15 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int item,
         return;
     }
     const bool fast = nt <= FAST_TERMS;
+    const bool stamps = (ablate & 64) && blockIdx.x == 0 && tid == 0;
+    uint64_t t_prev = stamps ? __builtin_amdgcn_s_memtime() : 0;
+    auto stamp = [&](int ph) {
+        if (stamps) {
+            const uint64_t t = __builtin_amdgcn_s_memtime();
+            atomicAdd(&g_sb_phase[ph], (unsigned long long)(t - t_prev));
+            t_prev = t;
+        }
+    };
     if (tid == 0) {
         sh.bad = 0;
         sh.emit = 0;
@@ -253,6 +275,7 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int item,
         const int n4 = (n_local + 3) >> 2;
         for (int i = tid; i < n4; i += SC_THREADS) a4[i] = make_uint4(0, 0, 0, 0);
         if (fast) reinterpret_cast<uint4 *>(sh.u.hist)[tid] = make_uint4(0, 0, 0, 0);
+        // (the 64 spare bins past them are written, never read: no zeroing needed)
     }
     __syncthreads();
     if (sh.bad) {
@@ -260,6 +283,7 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int item,
         return;
     }
 
+    stamp(0);  // setup + zeroing
     // ---- scatter: terms in query order, barrier between terms -------------
     // A term's sublist goes in rounds of 16 postings per lane while 16 k remain, then
     // 4 per lane while more than 1 k remain, then 1: a short tail does not pay for a
@@ -287,6 +311,7 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int item,
     }
     __syncthreads();
 
+    stamp(1);  // scatter
     if (ablate & 2) {  // profiling: skip the selection
         if (tid == 0) *cn = 0;
         return;
@@ -326,8 +351,11 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int item,
     if (fast) {
         // ---- fast path: score histogram -> k-th score T -------------------
         uint32_t *hist = sh.u.hist;
+        // branch-free: an untouched doc (w = 0) counts into a per-lane spare bin past
+        // the 4096 score bins (no same-address conflicts), never read
+        const uint32_t spare = HIST_BINS + (uint32_t)lane;
         sweep_words(sh.acc, n_local, tid, [&](uint32_t w, int) {
-            if (w) atomicAdd(&hist[w >> 16], 1u);
+            atomicAdd(&hist[w ? (w >> 16) : spare], 1u);
         });
         __syncthreads();
         // thread t owns bins 4t..4t+3; s = touched docs with score >= 4t
@@ -360,6 +388,7 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int item,
             sh.ties = hv[e];
         }
         __syncthreads();
+        stamp(2);  // histogram + threshold
         if (ablate & 4) {  // profiling: stop after the threshold
             if (tid == 0) *cn = 0;
             return;
@@ -370,27 +399,82 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int item,
         if (ties == need || ties <= (uint32_t)TIE_CAP) {
             // scores above T are in; the ties at T all go in, or into a list (the
             // histogram is consumed) as (low 16 bits of the word, 0xFFFF - idx):
-            // unique, and larger = first-touch earlier, then doc smaller
+            // unique, and larger = first-touch earlier, then doc smaller.
+            // Compaction: one sweep marks each lane's candidates and ties in two
+            // 32-bit masks over its 32 words (4 per ds_read_b128); a block scan of the
+            // counts gives positions; the write loop visits only the marked words
+            // (~1 per lane), not all 32.
             const bool all_ties = ties == need;
+            const uint32_t thr_a = (all_ties ? T : T + 1) << 16;  // list A: w >= thr_a
             uint32_t *tl = sh.u.hist;
-            compact_words(
-                sh, n_local, tid,
-                [T, all_ties](uint32_t w, int) -> uint32_t {
-                    const uint32_t sc = w >> 16;
-                    return (sc > T || (all_ties && sc == T)) ? 1u : (sc == T ? 2u : 0u);
-                },
-                [&](int list, uint32_t pos, uint32_t w, int idx) {
-                    if (list == 0)
-                        cand(pos, w, idx);
-                    else
-                        tl[pos] = ((w & 0xFFFFu) << 16) | (0xFFFFu - (uint32_t)idx);
-                });
+            uint32_t ma = 0, mb = 0;
+            {
+                const uint4 *a4 = reinterpret_cast<const uint4 *>(sh.acc);
+                const int n4 = (n_local + 3) >> 2;
+#pragma unroll
+                for (int i = 0; i < SC_PER_THREAD / 4; ++i) {
+                    const int q4 = i * SC_THREADS + tid;
+                    const uint4 y = a4[q4];  // q4 < 8192: inside the array
+                    const bool ok = q4 < n4;
+                    const uint32_t wv[4] = {y.x, y.y, y.z, y.w};
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const uint32_t w = ok ? wv[e] : 0u;
+                        ma |= (uint32_t)(w >= thr_a) << (4 * i + e);
+                        mb |= (uint32_t)((w >> 16) == T) << (4 * i + e);
+                    }
+                }
+                if (all_ties) mb = 0;
+            }
+            const uint32_t cnt = (uint32_t)__builtin_popcount(ma) +
+                                 ((uint32_t)__builtin_popcount(mb) << 16);
+            const uint32_t incl = wave_prefix_sum(cnt);
+            if (lane == 63) sh.wsum[wave] = incl;
+            __syncthreads();
+            uint32_t base = incl - cnt;
+            for (int w2 = 0; w2 < wave; ++w2) base += sh.wsum[w2];
+            stamp(6);
+            {
+                uint32_t pa = base & 0xFFFFu, pb = base >> 16;
+                auto idx_of = [&](int bit) { return 4 * ((bit >> 2) * SC_THREADS + tid) + (bit & 3); };
+                while (ma) {
+                    const int bit = __builtin_ctz(ma);
+                    ma &= ma - 1;
+                    const int idx = idx_of(bit);
+                    cand(pa++, sh.acc[idx], idx);
+                }
+                while (mb) {
+                    const int bit = __builtin_ctz(mb);
+                    mb &= mb - 1;
+                    const int idx = idx_of(bit);
+                    tl[pb++] = ((sh.acc[idx] & 0xFFFFu) << 16) | (0xFFFFu - (uint32_t)idx);
+                }
+            }
+            __syncthreads();
+            stamp(3);  // compaction
             if (ablate & 8) {  // profiling: stop after the compaction
                 if (tid == 0) *cn = 0;
                 return;
             }
-            if (!all_ties) {
-                // radix select of the `need` largest tie keys (4 digits, small list)
+            if (!all_ties && ties <= 64) {
+                // few ties (the common case): one wave ranks them -- lane i holds tie
+                // key i and counts the larger keys among all lanes (keys are unique);
+                // the `need` largest go right after the `above` candidates, in rank
+                // order, with no atomics and no further block barrier
+                if (wave == 0) {
+                    const uint32_t x = lane < (int)ties ? tl[lane] : 0u;
+                    uint32_t rank = 0;
+                    for (int j = 0; j < (int)ties; ++j) rank += __shfl(x, j, 64) > x;
+                    if (lane < (int)ties && rank < need)
+                        cand(above + rank, (T << 16) | (x >> 16), (int)(0xFFFFu - (x & 0xFFFFu)));
+                }
+                __syncthreads();
+                stamp(4);  // tie order
+                flush((uint32_t)k);
+                stamp(5);  // copy-out
+                if (tid == 0) *cn = k;
+            } else if (!all_ties) {
+                // radix select of the `need` largest tie keys (4 digits)
                 uint32_t *h = sh.v.h256;
                 uint32_t tp = 0, tm = 0, tneed = need;
                 for (int sft = 24; sft >= 0; sft -= 8) {
@@ -1065,6 +1149,15 @@ int di_index_search(di_index *ix, const uint32_t *q_terms, const int32_t *cu_q, 
             if (out_key)
                 DI_HIP(hipMemcpyAsync(out_key, dkey, (size_t)n_q * k * 8, hipMemcpyDeviceToHost,
                                       s));
+        }
+        if (ix->ablate & 64) {
+            unsigned long long ph[8];
+            DI_HIP(hipStreamSynchronize(s));
+            DI_HIP(hipMemcpyFromSymbol(ph, HIP_SYMBOL(g_sb_phase), sizeof ph));
+            fprintf(stderr, "score_blocks phase cycles (workgroup 0, cumulative): setup %llu "
+                            "scatter %llu hist %llu [count %llu scan %llu] write %llu ties %llu "
+                            "copy %llu\n",
+                    ph[0], ph[1], ph[2], ph[6], ph[7], ph[3], ph[4], ph[5]);
         }
         if (!(flags & DI_F_ASYNC) || !dev) {
             DI_HIP(hipStreamSynchronize(s));
