@@ -184,15 +184,19 @@ __device__ __forceinline__ bool wave_append(bool take, uint32_t *cursor, uint32_
 // and drain vmcnt element by element), then the LDS reads, then the writes.  A doc
 // occurs once per term, so the read-modify-write needs no atomics.
 template <int UU>
-__device__ __forceinline__ void scatter_round(uint32_t *acc, const uint32_t *p, int last, int tid,
-                                              uint32_t first_bits) {
-    uint32_t cur[UU], w[UU];
+__device__ __forceinline__ void scatter_load(const uint32_t *p, int last, int tid,
+                                             uint32_t (&cur)[UU]) {
 #pragma unroll
     for (int u = 0; u < UU; ++u) {
         const int i = tid + u * SC_THREADS;
         const uint32_t x = p[min(i, last)];
         cur[u] = i <= last ? x : 0u;
     }
+}
+template <int UU>
+__device__ __forceinline__ void scatter_apply(uint32_t *acc, const uint32_t (&cur)[UU],
+                                              uint32_t first_bits) {
+    uint32_t w[UU];
 #pragma unroll
     for (int u = 0; u < UU; ++u) w[u] = acc[(cur[u] >> 8) & (MAX_BLOCK_DOCS - 1)];
 #pragma unroll
@@ -290,24 +294,50 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int item,
     // full round of issue (loads, LDS reads and writes of masked lanes).  Each round
     // has all its loads in flight before any is applied; the 16 waves of the CU
     // overlap one another's load latency with their LDS work.
+    // The last round of a term also loads the next term's first 4 k postings, before
+    // the term barrier (a raw one: LDS writes retired, loads left in flight), so the
+    // barrier does not expose a load round trip per term.
+    uint32_t pre[4];
+    bool have_pre = false;
     for (int j = (ablate & 1) ? nt : 0; j < nt; ++j) {  // ablate bit 0: skip (profiling)
         const uint32_t first_bits = (uint32_t)(255 - j) << 8;
         int64_t pos = lo[j];
         const int64_t end = hi[j];
-        if (pos >= end) continue;
-        while (end - pos >= 16 * SC_THREADS) {
-            scatter_round<16>(sh.acc, post + pos, 16 * SC_THREADS - 1, tid, first_bits);
-            pos += 16 * SC_THREADS;
+        if (have_pre) {
+            scatter_apply<4>(sh.acc, pre, first_bits);
+            pos = min(end, pos + (int64_t)4 * SC_THREADS);
+            have_pre = false;
         }
-        while (end - pos > SC_THREADS) {
-            scatter_round<4>(sh.acc, post + pos, (int)min(end - pos, (int64_t)4 * SC_THREADS) - 1,
-                             tid, first_bits);
-            pos += 4 * SC_THREADS;
+        const bool next = j + 1 < nt && hi[j + 1] > lo[j + 1];
+        auto prefetch_next = [&]() {
+            scatter_load<4>(post + lo[j + 1],
+                            (int)min(hi[j + 1] - lo[j + 1], (int64_t)4 * SC_THREADS) - 1, tid, pre);
+            have_pre = true;
+        };
+        while (pos < end) {
+            const int64_t rem = end - pos;
+            if (rem >= 16 * SC_THREADS) {
+                uint32_t r[16];
+                scatter_load<16>(post + pos, 16 * SC_THREADS - 1, tid, r);
+                if (rem == 16 * SC_THREADS && next) prefetch_next();
+                scatter_apply<16>(sh.acc, r, first_bits);
+                pos += 16 * SC_THREADS;
+            } else if (rem > SC_THREADS) {
+                uint32_t r[4];
+                scatter_load<4>(post + pos, (int)min(rem, (int64_t)4 * SC_THREADS) - 1, tid, r);
+                if (rem <= 4 * SC_THREADS && next) prefetch_next();
+                scatter_apply<4>(sh.acc, r, first_bits);
+                pos += 4 * SC_THREADS;
+            } else {
+                uint32_t r[1];
+                scatter_load<1>(post + pos, (int)rem - 1, tid, r);
+                if (next) prefetch_next();
+                scatter_apply<1>(sh.acc, r, first_bits);
+                pos = end;
+            }
         }
-        if (end - pos > 0)
-            scatter_round<1>(sh.acc, post + pos, (int)(end - pos) - 1, tid, first_bits);
         // term boundary: this term's LDS writes land before any wave reads the next
-        if (j + 1 < nt) __syncthreads();
+        if (j + 1 < nt) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     }
     __syncthreads();
 
