@@ -648,13 +648,21 @@ score_blocks_kernel(const uint32_t *__restrict__ post, const int64_t *__restrict
 // ---------------------------------------------------------------------------
 constexpr int MG_LDS_KEYS = 16384;  // fast path: every candidate fits in LDS
 
+// Selection without a sort (fast path, > MG_SEL_MIN candidates, see the kernel):
+// a 4096-bin histogram of the keys' score bits, then counting ranks.
+constexpr int MG_SEL_MIN = 1024;
+constexpr int MG_SEL_BINS = 4096;   // 16 KiB of LDS after the key array
+constexpr int MG_SEL_KEYS = 2048;   // + 16 KiB: up to 2048 selected keys
+constexpr int MG_SEL_CAP = 8192;    // key arrays up to 64 KiB (+32 KiB within the LDS max)
+
 template <int THREADS>
 struct alignas(16) MergeHead {  // 16-byte multiple: the u64 key array follows it
     RadixScratch<THREADS / 64> rs;
     int32_t off[1025];
     uint32_t cnt;
     int32_t bad;
-    uint32_t pad[2];
+    uint32_t thr, above;
+    uint32_t wtot[THREADS / 64];
 };
 
 enum DecodeMode : int { DECODE_QUANT = 0, DECODE_SPARSE = 1, DECODE_NONE = 2 };
@@ -666,7 +674,8 @@ merge_topk_kernel(const uint64_t *__restrict__ keys, const int32_t *__restrict__
                   int n_lists, int k_in, int k, int64_t list_stride, int64_t cnt_stride,
                   int64_t q_stride, int64_t cq_stride, int cap,
                   uint64_t *__restrict__ out_key, uint32_t *__restrict__ out_doc,
-                  uint32_t *__restrict__ out_score, int32_t *__restrict__ out_n, int mode) {
+                  uint32_t *__restrict__ out_score, int32_t *__restrict__ out_n, int mode,
+                  int select) {
     // key i of list l of query q: keys[q*q_stride + l*list_stride + i]
     // its count:                  counts[q*cq_stride + l*cnt_stride]
     constexpr int WAVES = THREADS / 64;
@@ -717,10 +726,28 @@ merge_topk_kernel(const uint64_t *__restrict__ keys, const int32_t *__restrict__
     const int take = (int)min<int64_t>(total, k);
     uint64_t *ok = out_key ? out_key + (int64_t)q * k : nullptr;
     if (fast_lists && total <= cap) {
-        for (int l = 0; l < n_lists; ++l) {
-            const int o = sh.off[l], c = sh.off[l + 1] - o;
-            const uint64_t *s = src0 + (int64_t)l * list_stride;
-            for (int i = tid; i < c; i += THREADS) lk[o + i] = s[i];
+        // flattened over the lists, 8 loads per lane in flight (clamped addresses:
+        // unconditional loads), list of key i by binary search over the offsets
+        constexpr int U = 8;
+        const int tot = (int)total;
+        for (int base = 0; base < tot; base += U * THREADS) {
+            uint64_t v[U];
+#pragma unroll
+            for (int j = 0; j < U; ++j) {
+                const int i = min(base + j * THREADS + tid, tot - 1);
+                int lo = 0, hi = n_lists - 1;  // last list with off[l] <= i
+                while (lo < hi) {
+                    const int mid = (lo + hi + 1) >> 1;
+                    if (sh.off[mid] <= i) lo = mid;
+                    else hi = mid - 1;
+                }
+                v[j] = src0[(int64_t)lo * list_stride + (i - sh.off[lo])];
+            }
+#pragma unroll
+            for (int j = 0; j < U; ++j) {
+                const int i = base + j * THREADS + tid;
+                if (i < tot) lk[i] = v[j];
+            }
         }
         __syncthreads();
     } else {
@@ -764,13 +791,7 @@ merge_topk_kernel(const uint64_t *__restrict__ keys, const int32_t *__restrict__
         __syncthreads();
         total = take;
     }
-    int n2 = 64;
-    while (n2 < total) n2 <<= 1;
-    for (int i = (int)total + tid; i < n2; i += THREADS) lk[i] = 0;
-    __syncthreads();
-    bitonic_sort_desc<THREADS>(lk, n2);
-    for (int i = tid; i < take; i += THREADS) {
-        uint64_t x = lk[i];
+    auto emit = [&](int i, uint64_t x) {  // output rank i
         if (ok) ok[i] = x;
         if (mode == DECODE_QUANT) {
             out_doc[(int64_t)q * k + i] = 0xFFFFFFFFu - (uint32_t)x;
@@ -779,7 +800,75 @@ merge_topk_kernel(const uint64_t *__restrict__ keys, const int32_t *__restrict__
             out_doc[(int64_t)q * k + i] = 0xFFFFFFu - (uint32_t)(x & 0xFFFFFFu);
             out_score[(int64_t)q * k + i] = (uint32_t)(x >> 32);  // f32 bits
         }
+    };
+    if (select && fast_lists && total > MG_SEL_MIN && cap <= MG_SEL_CAP && take < total) {
+        // Selection by counting instead of a sort.  Every key below 2^60 (score <
+        // 4096)?  Then bin = key bits 48..59 (the score) orders the keys up to ties
+        // inside a bin: a histogram gives the bin T of the take-th largest key and
+        // every bin's start rank; the keys of bins >= T are placed bin by bin, and a
+        // key's rank is its bin's start + the keys of its own bin that are larger.
+        bool big = false;
+        for (int i = tid; i < total; i += THREADS) big |= (lk[i] >> 60) != 0;
+        if (!__syncthreads_or(big)) {
+            uint32_t *hist = reinterpret_cast<uint32_t *>(lk + cap);
+            uint64_t *out = reinterpret_cast<uint64_t *>(hist + MG_SEL_BINS);
+            auto bin = [](uint64_t x) { return (uint32_t)(x >> 48) & (MG_SEL_BINS - 1); };
+            for (int i = tid; i < MG_SEL_BINS; i += THREADS) hist[i] = 0;
+            __syncthreads();
+            for (int i = tid; i < total; i += THREADS) atomicAdd(&hist[bin(lk[i])], 1u);
+            __syncthreads();
+            // thread t owns BPT consecutive bins from the top, in descending order
+            constexpr int BPT = MG_SEL_BINS / THREADS;
+            const int top = MG_SEL_BINS - 1 - tid * BPT;
+            uint32_t hc[BPT], c = 0;
+#pragma unroll
+            for (int j = 0; j < BPT; ++j) c += (hc[j] = hist[top - j]);
+            const uint32_t incl = wave_prefix_sum(c);
+            const int lane = tid & 63, w = tid >> 6;
+            if (lane == 63) sh.wtot[w] = incl;
+            __syncthreads();
+            uint32_t run = incl - c;
+            for (int v = 0; v < w; ++v) run += sh.wtot[v];
+            // counts -> start ranks (keys in higher bins); T = the take-th key's bin
+#pragma unroll
+            for (int j = 0; j < BPT; ++j) {
+                if (run < (uint32_t)take && run + hc[j] >= (uint32_t)take) {
+                    sh.thr = (uint32_t)(top - j);
+                    sh.above = run + hc[j];  // keys in bins >= T
+                }
+                hist[top - j] = run;
+                run += hc[j];
+            }
+            __syncthreads();
+            const uint32_t T = sh.thr, n_sel = sh.above;
+            if (n_sel <= (uint32_t)MG_SEL_KEYS) {
+                // place (hist[b] becomes the end of bin b = the start of bin b - 1)
+                for (int i = tid; i < total; i += THREADS) {
+                    const uint64_t x = lk[i];
+                    const uint32_t b = bin(x);
+                    if (b >= T) out[atomicAdd(&hist[b], 1u)] = x;
+                }
+                __syncthreads();
+                for (int p = tid; p < (int)n_sel; p += THREADS) {
+                    const uint64_t x = out[p];
+                    const uint32_t b = bin(x);
+                    const uint32_t lo = b == MG_SEL_BINS - 1 ? 0u : hist[b + 1], hi = hist[b];
+                    uint32_t r = lo;
+                    for (uint32_t j = lo; j < hi; ++j) r += out[j] > x;
+                    if (r < (uint32_t)take) emit((int)r, x);
+                }
+                if (tid == 0) out_n[q] = take;
+                return;
+            }
+            __syncthreads();  // (the sort below reuses nothing of this)
+        }
     }
+    int n2 = 64;
+    while (n2 < total) n2 <<= 1;
+    for (int i = (int)total + tid; i < n2; i += THREADS) lk[i] = 0;
+    __syncthreads();
+    bitonic_sort_desc<THREADS>(lk, n2);
+    for (int i = tid; i < take; i += THREADS) emit(i, lk[i]);
     if (tid == 0) out_n[q] = take;
 }
 
@@ -997,21 +1086,28 @@ void launch_merge(const uint64_t *keys, const int32_t *counts, int n_q, int n_li
         const char *e = std::getenv("DI_MERGE_THREADS");
         return e ? std::atoi(e) : 512;
     }();
+    // score-histogram selection before the sort (DI_MERGE_SELECT=0: sort everything)
+    static const int select = [] {
+        const char *e = std::getenv("DI_MERGE_SELECT");
+        return e && e[0] == '0' ? 0 : 1;
+    }();
+    // (the histogram follows the keys; only for cap <= MG_SEL_CAP, inside the attribute's max)
+    const size_t sel_lds = cap > MG_SEL_MIN && cap <= MG_SEL_CAP ? (size_t)MG_SEL_BINS * 4 + MG_SEL_KEYS * 8 : 0;
     if (cap <= 256 || mt == 256) {
-        size_t lds = sizeof(MergeHead<256>) + (size_t)cap * 8;
+        size_t lds = sizeof(MergeHead<256>) + (size_t)cap * 8 + sel_lds;
         hipLaunchKernelGGL(merge_topk_kernel<256>, dim3(n_q), dim3(256), lds, s, keys, counts,
                            n_lists, k_in, k, ls, cs, qs, cqs, cap, out_key, out_doc, out_score,
-                           out_n, mode);
+                           out_n, mode, select);
     } else if (mt == 512) {
-        size_t lds = sizeof(MergeHead<512>) + (size_t)cap * 8;
+        size_t lds = sizeof(MergeHead<512>) + (size_t)cap * 8 + sel_lds;
         hipLaunchKernelGGL(merge_topk_kernel<512>, dim3(n_q), dim3(512), lds, s, keys, counts,
                            n_lists, k_in, k, ls, cs, qs, cqs, cap, out_key, out_doc, out_score,
-                           out_n, mode);
+                           out_n, mode, select);
     } else {
-        size_t lds = sizeof(MergeHead<1024>) + (size_t)cap * 8;
+        size_t lds = sizeof(MergeHead<1024>) + (size_t)cap * 8 + sel_lds;
         hipLaunchKernelGGL(merge_topk_kernel<1024>, dim3(n_q), dim3(1024), lds, s, keys,
                            counts, n_lists, k_in, k, ls, cs, qs, cqs, cap, out_key, out_doc,
-                           out_score, out_n, mode);
+                           out_score, out_n, mode, select);
     }
     check_launch("merge_topk");
 }
