@@ -19,7 +19,7 @@ import time
 from pathlib import Path
 
 from .datasets import COLLECTION_TYPES, CollectionParser
-from .indexer import Indexer
+from .indexer import Indexer, TokenizerPool, pool_supported, resolve_tokenizer
 from .models import DeepImpact
 
 BATCH_SIZE = 32  # src/utils/defaults.py:15
@@ -34,10 +34,27 @@ def run(collection_path, collection_type, output_file_path, model_checkpoint_pat
     if pairwise:
         raise NotImplementedError("DeepPairwiseImpact is outside this build (SURVEY §8f F4)")
     start = time.time()
-    model = DeepImpact.load(model_checkpoint_path, tokenizer_path=tokenizer_path,
-                            precision=precision, device=device, variant=variant,
-                            max_length=max_length)
-    indexer = Indexer(model, model_batch_size=model_batch_size, num_processes=num_processes)
+    # the tokenizer workers start before the GPU is initialised (DeepImpact.load)
+    tok = resolve_tokenizer(model_checkpoint_path, tokenizer_path)
+    pool = None
+    if num_processes > 1 and tok is not None and pool_supported():
+        pool = TokenizerPool(num_processes, tok, max_length or DeepImpact.max_length,
+                             "bert_legacy" if variant == "bert" else "word_ids")
+    try:
+        model = DeepImpact.load(model_checkpoint_path, tokenizer_path=tokenizer_path,
+                                precision=precision, device=device, variant=variant,
+                                max_length=max_length)
+        indexer = Indexer(model, model_batch_size=model_batch_size,
+                          num_processes=num_processes, pool=pool)
+        return _index_file(indexer, collection_path, collection_type, output_file_path,
+                           process_batch_size, doc_range, start)
+    finally:
+        if pool is not None:
+            pool.close()
+
+
+def _index_file(indexer, collection_path, collection_type, output_file_path,
+                process_batch_size, doc_range, start):
     lo, hi = (0, None) if doc_range is None else doc_range
     with open(collection_path) as f, open(output_file_path, "w") as out:
         batch = []

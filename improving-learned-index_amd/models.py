@@ -198,8 +198,8 @@ class DeepImpact:
                 (Path(checkpoint_path) / "tokenizer.json").exists():
             tok = Path(checkpoint_path) / "tokenizer.json"
         model = cls(enc, tok, max_length)
-        if variant == "bert":
-            model.term_mapping = "bert_legacy"
+        # class-level, like the tokenizer: process_document(s) are classmethods
+        cls.term_mapping = "bert_legacy" if variant == "bert" else "word_ids"
         return model
 
     # ------------------------------------------------------------------ forward
@@ -228,17 +228,29 @@ class DeepImpact:
         proc = self.process_documents(documents, max_length or self.max_length)
         return self.encode_processed(proc, round3)
 
-    def encode_processed(self, proc, round3=False):
+    @staticmethod
+    def pack_processed(proc):
+        """process_documents output -> the packed batch of the C ABI: token ids and
+        their offsets, the kept terms (flat) with their first-token index and offsets."""
         lens = np.array([len(e.ids) for e, _ in proc], np.int64)
         cu = np.zeros(len(proc) + 1, np.int32)
         cu[1:] = np.cumsum(lens)
         ids = np.fromiter((i for e, _ in proc for i in e.ids), np.int32, count=int(cu[-1]))
-        tt = np.fromiter((t for _, m in proc for t in m.values()), np.int32,
-                         count=sum(len(m) for _, m in proc))
+        terms = [t for _, m in proc for t in m]
+        tt = np.fromiter((t for _, m in proc for t in m.values()), np.int32, count=len(terms))
         ct = np.zeros(len(proc) + 1, np.int32)
         ct[1:] = np.cumsum([len(m) for _, m in proc])
+        return ids, cu, terms, tt, ct
+
+    def encode_packed_terms(self, packed, round3=False):
+        """Encode a pack_processed batch: per document its (term, impact) list."""
+        ids, cu, terms, tt, ct = packed
         imp = self.encoder.encode_packed(ids, cu, tt, ct, round3=round3)
-        return [list(zip(m.keys(), imp[ct[i]:ct[i + 1]])) for i, (_, m) in enumerate(proc)]
+        return [list(zip(terms[ct[i]:ct[i + 1]], imp[ct[i]:ct[i + 1]]))
+                for i in range(len(ct) - 1)]
+
+    def encode_processed(self, proc, round3=False):
+        return self.encode_packed_terms(self.pack_processed(proc), round3)
 
     def get_impact_scores(self, document: str) -> List[Tuple[str, np.float32]]:
         """xlmr_original.py:227-241."""

@@ -1,0 +1,116 @@
+"""Host hot loop #1 in worker processes, and the BERT variant's term
+mapping.  The TokenizerPool (the reference's 8-process Pool, indexer.py:29,41) must
+give the in-process bytes; the BERT variant maps terms with the upstream
+soyuj/deeper-impact logic (reference original.py:155-177, a commented block there:
+every token after [CLS] not starting with '##' opens the next term), restated on a
+locally built WordPiece tokenizer -- parity unpinned beyond that restatement."""
+import json
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+
+
+class _FakeModel:
+    """process_documents of the real class; encode_processed = deterministic impacts
+    (a function of the term's first token id), rounded like DI_F_ROUND3."""
+
+    max_length = 512
+
+    def __init__(self):
+        from improving_learned_index_amd import models
+
+        self.process_documents = models.DeepImpact.process_documents
+
+    def encode_packed_terms(self, packed, round3=False):
+        ids, cu, terms, tt, ct = packed
+        out = []
+        for d in range(len(ct) - 1):
+            out.append([(terms[j], np.float32(np.rint(
+                np.float32(ids[cu[d] + tt[j]] % 977 / 97.0) * 1000) / 1000))
+                for j in range(ct[d], ct[d + 1])])
+        return out
+
+    def encode_processed(self, proc, round3=False):
+        from improving_learned_index_amd import models
+
+        return self.encode_packed_terms(models.DeepImpact.pack_processed(proc), round3)
+
+
+@pytest.fixture
+def restore_class():
+    from improving_learned_index_amd import models
+
+    saved = (models.DeepImpact.tokenizer, models.DeepImpact.term_mapping)
+    yield models
+    models.DeepImpact.tokenizer, models.DeepImpact.term_mapping = saved
+
+
+def test_pool_indexer_writes_the_in_process_bytes(tmp_path, restore_class):
+    from improving_learned_index_amd import indexer
+
+    restore_class.DeepImpact.set_tokenizer(GOLDEN / "tokenizer.json")
+    texts = json.loads((GOLDEN / "encoder_xlmr_small.json").read_text())["texts"]
+    batch = [texts[i % len(texts)] + f" doc{i}" for i in range(600)]  # 3 chunks of <= 256
+    fake = _FakeModel()
+    with open(tmp_path / "a.tsv", "w") as f:
+        indexer.Indexer(fake, 32).index(batch, f)
+    with indexer.TokenizerPool(2, GOLDEN / "tokenizer.json", 512) as pool:
+        with open(tmp_path / "b.tsv", "w") as f:
+            indexer.Indexer(fake, 32, num_processes=2, pool=pool).index(batch, f)
+    a = (tmp_path / "a.tsv").read_bytes()
+    assert a == (tmp_path / "b.tsv").read_bytes()
+    assert a.count(b"\n") == len(batch) and b"doc599: " in a
+
+
+def _bert_tokenizer():
+    from tokenizers import Tokenizer, models, normalizers, pre_tokenizers, processors
+
+    vocab = {t: i for i, t in enumerate(
+        ["[PAD]", "[UNK]", "[CLS]", "[SEP]", "hello", "world", "again", ",", "un",
+         "##believ", "##able", "the"])}
+    tok = Tokenizer(models.WordPiece(vocab, unk_token="[UNK]"))
+    tok.normalizer = normalizers.BertNormalizer(lowercase=True)
+    tok.pre_tokenizer = pre_tokenizers.BertPreTokenizer()
+    tok.post_processor = processors.TemplateProcessing(
+        single="[CLS] $A [SEP]", special_tokens=[("[CLS]", 2), ("[SEP]", 3)])
+    return tok
+
+
+def _legacy_restatement(tokens, terms, punct):
+    """original.py:162-177 (commented block)."""
+    t2t, counter = {}, 0
+    for i, token in enumerate(tokens[1:], start=1):
+        if token.startswith("##"):
+            continue
+        t2t[counter] = i
+        counter += 1
+    out = {}
+    for i, term in enumerate(terms):
+        if term not in out and term not in punct and i in t2t:
+            out[term] = t2t[i]
+    return out
+
+
+@pytest.mark.parametrize("max_length", [4, 6, 512])
+def test_bert_legacy_term_mapping(restore_class, max_length):
+    M = restore_class
+    tok = _bert_tokenizer()
+    M.DeepImpact.tokenizer = tok
+    M.DeepImpact.term_mapping = "bert_legacy"
+    doc = "Hello world, unbelievable the world again!"
+    (enc, tmap), = M.DeepImpact.process_documents([doc], max_length)
+    tok.no_padding()
+    tok.enable_truncation(max_length)
+    terms = [x[0] for x in tok.pre_tokenizer.pre_tokenize_str(tok.normalizer.normalize_str(doc))]
+    e = tok.encode(terms, is_pretokenized=True)
+    assert tmap == _legacy_restatement(e.tokens, terms, M.PUNCTUATION)
+    if max_length == 4:  # [CLS] hello world [SEP]: the legacy counter maps ',' -> [SEP]
+        assert tmap == {"hello": 1, "world": 2}
+    if max_length == 6:  # [CLS] hello world , un [SEP]: 'unbelievable' -> 'un', 'the' -> [SEP]
+        assert tmap == {"hello": 1, "world": 2, "unbelievable": 4, "the": 5}
+    M.DeepImpact.term_mapping = "word_ids"
+    (_, wmap), = M.DeepImpact.process_documents([doc], max_length)
+    if max_length == 6:
+        assert wmap == {"hello": 1, "world": 2, "unbelievable": 4}
