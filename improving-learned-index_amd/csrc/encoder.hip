@@ -413,8 +413,20 @@ void forward_folded(di_encoder *e, const int32_t *d_ids, const int32_t *d_cu, in
                               e->emb_b.as<float>(), c.layer_norm_eps, pos_offset, c.vocab_size,
                               c.max_positions, X, e->err.as<int32_t>(), s);
     }
+    // A/B knobs of the 256-tile GEMMs (tools / bench experiments): first-tile delay
+    // of every other CU (shader cycles) and the tile-order group size
+    static const int stagger = [] {
+        const char *v = std::getenv("DI_GEMM_STAGGER");
+        return v ? std::atoi(v) : 0;
+    }();
+    static const int tune_gm = [] {
+        const char *v = std::getenv("DI_GEMM_GM");
+        return v ? std::atoi(v) : 0;
+    }();
     auto base = [&]() {
         GemmArgs g{};
+        g.stagger = stagger;
+        g.tune_gm = tune_gm;
         g.M = (int)M;
         g.a_rows = e->cap_rows;
         g.hidden = H;
