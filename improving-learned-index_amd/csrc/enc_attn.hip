@@ -633,12 +633,24 @@ attention_v3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
     // pending load, so it neither waits nor drains the K/V prefetch for them), into the
     // register set not in use; the wait at the top of the pair retires it.  The two
     // sets are used in turn (the loop is unrolled by two: no register copies).
+    // Query tiles (16 queries) of a document are dealt to the 8 waves in contiguous
+    // runs whose lengths differ by at most one (wave w: tiles [t_first, t_first + t_cnt));
+    // a wave takes its run two tiles at a time (K / V fragments shared) and an odd last
+    // tile alone, so a pair costs ceil(tiles / 8) tile-steps instead of whole 32-query
+    // blocks dealt round robin.
+    auto tiles_of = [&](int nn, int &t_first, int &t_cnt) {
+        const int n_t = (nn + 15) >> 4, base = n_t / ATT3_WAVES, extra = n_t % ATT3_WAVES;
+        t_cnt = base + (wave < extra ? 1 : 0);
+        t_first = wave * base + min(wave, extra);
+    };
     auto load_q = [&](int pp, uint4 (&qd)[2][QTB][2]) {
         const int dd = pp / n_heads, hh = pp % n_heads;
         const int t0 = cu_seqlens[dd], nn = cu_seqlens[dd + 1] - t0;
+        int t_first, t_cnt;
+        tiles_of(nn, t_first, t_cnt);
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
-            const int q_base = (wave + i * ATT3_WAVES) * 16 * QTB;
+            const int q_base = (t_first + 2 * i) * 16;
 #pragma unroll
             for (int qt = 0; qt < QTB; ++qt) {
                 const int qrow = t0 + min(q_base + 16 * qt + c, nn - 1);
@@ -667,7 +679,8 @@ attention_v3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
         __syncthreads();
         const int doc = p / n_heads, h = p % n_heads;
         const int tok0 = cu_seqlens[doc], n = cu_seqlens[doc + 1] - tok0;
-        const int n_qb = (n + 16 * QTB - 1) / (16 * QTB);
+        int t_first, t_cnt;
+        tiles_of(n, t_first, t_cnt);
         if (p + (int)gridDim.x < n_pairs) {
             load_q(p + gridDim.x, qn);
             if (DB) stage(p + gridDim.x, b ^ 1);
@@ -677,9 +690,9 @@ attention_v3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
         const uint32_t vim = kim + Att3<DB>::ROWS * 128;
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
-            const int qb = wave + i * ATT3_WAVES;
-            if (qb >= n_qb) continue;  // (not break: keeps the loop unrolled, qf[i] static)
-            const int q_base = qb * 16 * QTB;
+            if (2 * i >= t_cnt) continue;  // (not break: keeps the loop unrolled, qf[i] static)
+            const int nqt = min(QTB, t_cnt - 2 * i);  // tiles in this step (1 or 2)
+            const int q_base = (t_first + 2 * i) * 16;
             float m[QTB], msc[QTB];
             f32x4 o[QTB][4], l[QTB];
 #pragma unroll
@@ -723,6 +736,7 @@ attention_v3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
                 const bool tail = key0 + 32 > n;
 #pragma unroll
                 for (int qt = 0; qt < QTB; ++qt) {
+                    if (qt >= nqt) continue;  // (wave-uniform)
                     f32x4 s[2];
 #pragma unroll
                     for (int t = 0; t < 2; ++t) {
@@ -751,7 +765,7 @@ attention_v3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
             for (int qt = 0; qt < QTB; ++qt) {
                 const float inv = 1.0f / l[qt][0];
                 const int q = q_base + 16 * qt + c;
-                if (q < n) {
+                if (qt < nqt && q < n) {
                     bf16 *out = ctx + (int64_t)(tok0 + q) * H + h * ATT_D + 4 * g;
 #pragma unroll
                     for (int dt = 0; dt < 4; ++dt) {
