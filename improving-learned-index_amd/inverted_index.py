@@ -36,12 +36,20 @@ class InvertedIndex:
     """
 
     def __init__(self, index_path: Union[str, Path], device: int = 0, doc_lo: int = 0,
-                 doc_hi: int = 0):
+                 doc_hi: int = 0, min_impact: int = 1):
         self.index_path = Path(index_path)
         self.vocab = self._load_vocab()
         self.device = device
         self.doc_lo, self.doc_hi = doc_lo, doc_hi
         self._dev = DeviceIndex.from_reference_dir(self.index_path, doc_lo, doc_hi, device)
+        self.set_min_impact(min_impact)
+
+    def set_min_impact(self, min_impact: int) -> None:
+        """Query-time impact pruning (config 5): score only postings of value >= the
+        largest power of two <= min_impact (1 = every posting = the reference's exact
+        ranking).  Recall trade-off: DESIGN.md §4."""
+        self.min_impact = int(min_impact)
+        self._dev.set_min_impact(self.min_impact)
 
     def _load_vocab(self):
         vocab = dict()

@@ -23,7 +23,8 @@ class Ranker:
                  output_path: Union[str, Path], num_workers: int = 4,
                  qrels_path: Optional[Union[str, Path]] = None, pairwise: bool = False,
                  dataset_type: Optional[str] = COLLECTION_TYPES[0], tokenizer_path=None,
-                 device: int = 0, top_k: int = 1000, batch_queries: int = 8192):
+                 device: int = 0, top_k: int = 1000, batch_queries: int = 8192,
+                 min_impact: int = 1):
         if pairwise:
             raise NotImplementedError("pairwise terms are outside this build (SURVEY §8f F4)")
         if tokenizer_path is not None:
@@ -32,7 +33,7 @@ class Ranker:
         self.query_iterator = list(self.queries.keys())
         if qrels_path is not None:  # ranker.py:34-35
             self.query_iterator = list(QueryRelevanceDataset(qrels_path=qrels_path).keys())
-        self.index = InvertedIndex(index_path=index_path, device=device)
+        self.index = InvertedIndex(index_path=index_path, device=device, min_impact=min_impact)
         self.run_file = RunFile(run_file_path=output_path)
         self.top_k = top_k
         self.batch_queries = batch_queries
@@ -61,9 +62,14 @@ def main(argv=None):
     p.add_argument("--pairwise", action="store_true")
     p.add_argument("--tokenizer_path", type=str, required=True)
     p.add_argument("--device", type=int, default=0)
+    p.add_argument("--top_k", type=int, default=1000)
+    p.add_argument("--min_impact", type=int, default=1,
+                   help="query-time pruning: score postings with value >= this (rounded down "
+                        "to a power of two); 1 = exact")
     a = p.parse_args(argv)
     Ranker(a.index_path, a.queries_path, a.output_path, a.num_workers, a.qrels_path, a.pairwise,
-           a.dataset_type, a.tokenizer_path, a.device).run()
+           a.dataset_type, a.tokenizer_path, a.device, top_k=a.top_k,
+           min_impact=a.min_impact).run()
 
 
 if __name__ == "__main__":

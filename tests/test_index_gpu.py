@@ -162,3 +162,27 @@ def test_min_impact_pruning_equals_oracle_on_pruned_postings(L, synth, min_impac
     assert dev.search(qs, 1000) == pr.score_ids(qs, 1000, n_threads=8)
     dev.set_min_impact(1)
     assert dev.search(qs, 1000) == ora.score_ids(qs, 1000, n_threads=8)
+
+
+def test_inverted_index_min_impact_matches_pruned_oracle(L):
+    """The Python drop-in carries the config-5 knob (InvertedIndex(min_impact=...),
+    rank --min_impact): on the reference-format golden index it ranks exactly like
+    the oracle over the postings it keeps; set_min_impact(1) is the exact ranking."""
+    from improving_learned_index_amd.inverted_index import InvertedIndex
+
+    fx = json.loads((GOLDEN / "score.json").read_text())
+    ora = oracle.Index(GOLDEN / "index")
+    qids = [ora.term_ids(q) for q in fx["queries"]]
+    ix = InvertedIndex(GOLDEN / "index", min_impact=6)  # -> values >= 4
+    keep = ora.pval >= 4
+    cnt = np.array([int(keep[ora.term_off[t]:ora.term_off[t + 1]].sum())
+                    for t in range(len(ora.term_off) - 1)])
+    pr = oracle.Index.__new__(oracle.Index)
+    pr.term_off = np.concatenate([[0], np.cumsum(cnt)]).astype(np.int64)
+    pr.pdoc, pr.pval, pr.n_docs = ora.pdoc[keep], ora.pval[keep], ora.n_docs
+    assert keep.sum() < keep.size  # the knob prunes something here
+    assert ix.score_batch(fx["queries"], 1000) == pr.score_ids(qids, 1000)
+    ix.set_min_impact(1)
+    assert [[list(x) for x in g] for g in ix.score_batch(fx["queries"], 1000)] == fx["top1000"]
+    with pytest.raises(Exception):
+        ix.set_min_impact(0)
