@@ -205,6 +205,75 @@ ln_vec_kernel(const T *__restrict__ pre, int M, const float *__restrict__ gamma,
     if (head_w) head_out(hs, head_b, act, impact, row);
 }
 
+// embed_ln for H = 256 NC (XLM-R / BERT base and large): one workgroup per document,
+// so the position is the row's offset in the document (no per-token search over the
+// document offsets), 4 waves x 2 rows in flight, lane holds 4 consecutive columns of
+// each 256-column chunk (8-byte loads, the ln_vec_kernel layout and arithmetic).
+template <typename T, int NC>
+__global__ void __launch_bounds__(256)
+embed_ln_vec_kernel(const int32_t *__restrict__ ids, const int32_t *__restrict__ cu,
+                    const T *__restrict__ word, const T *__restrict__ pos,
+                    const T *__restrict__ type0, const float *__restrict__ gamma,
+                    const float *__restrict__ beta, float eps, int pos_offset, int vocab,
+                    int max_pos, T *__restrict__ out, int32_t *__restrict__ err) {
+    constexpr int H = 256 * NC, RB = 2;
+    const int d = blockIdx.x, wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int r0 = cu[d], n = cu[d + 1] - r0;
+    float gm[NC][4], bt[NC][4], ty[NC][4];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+        ld4<float>(gamma + 256 * c + 4 * lane, gm[c]);
+        ld4<float>(beta + 256 * c + 4 * lane, bt[c]);
+        ld4<T>(type0 + 256 * c + 4 * lane, ty[c]);
+    }
+    for (int i0 = wave * RB; i0 < n; i0 += 4 * RB) {
+        float v[RB][NC][4];
+#pragma unroll
+        for (int r = 0; r < RB; ++r) {
+            const int i = min(i0 + r, n - 1);  // clamped: loads stay unconditional
+            const int p = i + pos_offset;
+            int id = ids[r0 + i];
+            if (id < 0 || id >= vocab || p >= max_pos) {
+                if (lane == 0) atomicOr(err, 1);
+                id = min(max(id, 0), vocab - 1);
+            }
+            const T *wr = word + (int64_t)id * H + 4 * lane;
+            const T *pr = pos + (int64_t)min(p, max_pos - 1) * H + 4 * lane;
+#pragma unroll
+            for (int c = 0; c < NC; ++c) {
+                float w4[4], p4[4];
+                ld4<T>(wr + 256 * c, w4);
+                ld4<T>(pr + 256 * c, p4);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) v[r][c][j] = w4[j] + p4[j] + ty[c][j];
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < RB; ++r) {
+            if (i0 + r >= n) break;
+            float s = 0.f;
+#pragma unroll
+            for (int c = 0; c < NC; ++c) s += (v[r][c][0] + v[r][c][1]) + (v[r][c][2] + v[r][c][3]);
+            const float mean = wave_sum_f(s) / (float)H;
+            float q = 0.f;
+#pragma unroll
+            for (int c = 0; c < NC; ++c)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const float dd = v[r][c][j] - mean;
+                    q += dd * dd;
+                }
+            const float rstd = 1.0f / sqrtf(wave_sum_f(q) / (float)H + eps);
+#pragma unroll
+            for (int c = 0; c < NC; ++c) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) v[r][c][j] = (v[r][c][j] - mean) * rstd * gm[c][j] + bt[c][j];
+                st4(out + (int64_t)(r0 + i0 + r) * H + 256 * c + 4 * lane, v[r][c]);
+            }
+        }
+    }
+}
+
 // LayerNorm folding: per-row (rstd, -rstd * mean) from the row-statistics partials
 // of the producing GEMM (biased variance as torch layer_norm; fixed summation order).
 __global__ void row_ln_kernel(const float4 *__restrict__ st, int ld, int n_part, int M, int H,
@@ -292,6 +361,18 @@ void launch_embed_ln(const int32_t *ids, const int32_t *cu, int n_docs, int M, i
                      const float *beta, float eps, int pos_offset, int vocab, int max_pos, T *out,
                      int32_t *err, hipStream_t s) {
     if (M == 0) return;
+    if (H == 768 || H == 1024) {  // one workgroup per document
+        if (H == 768)
+            hipLaunchKernelGGL((embed_ln_vec_kernel<T, 3>), dim3(n_docs), dim3(256), 0, s, ids, cu,
+                               word, pos, type0, gamma, beta, eps, pos_offset, vocab, max_pos,
+                               out, err);
+        else
+            hipLaunchKernelGGL((embed_ln_vec_kernel<T, 4>), dim3(n_docs), dim3(256), 0, s, ids, cu,
+                               word, pos, type0, gamma, beta, eps, pos_offset, vocab, max_pos,
+                               out, err);
+        check_launch("embed_ln");
+        return;
+    }
     dim3 grid((M + 3) / 4);
     if (H <= 256)
         hipLaunchKernelGGL((embed_ln_kernel<T, 4>), grid, dim3(256), 0, s, ids, cu, n_docs, M, H,
