@@ -55,6 +55,19 @@ constexpr int G2_PAR_ROW = 0, G2_PAR_C0 = 2048, G2_PAR_C1 = 3072, G2_PAR_C2 = 40
               G2_PAR_C3 = 5120;
 constexpr int G2_LDS = 2 * G2_BUF + 6144;
 
+// Epilogue row store (16 B per lane).  DI_NT_STORE (experiment builds only): the
+// non-temporal form, so the streamed output does not evict the operand panels.
+__device__ __forceinline__ void g2_store(bf16 *p, const bf16x8 &v) {
+#ifdef DI_NT_STORE
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    u32x4 u;
+    __builtin_memcpy(&u, &v, 16);
+    __builtin_nontemporal_store(u, reinterpret_cast<u32x4 *>(p));
+#else
+    *reinterpret_cast<bf16x8 *>(p) = v;
+#endif
+}
+
 #define G2_BAR() asm volatile("s_barrier" ::: "memory")
 
 template <int EPI>
@@ -395,8 +408,7 @@ __global__ void __launch_bounds__(G2_T) gemm256_kernel(GemmArgs g) {
                 bf16x8 ov;
 #pragma unroll
                 for (int e = 0; e < 8; ++e) ov[e] = (bf16)v[e];
-                *reinterpret_cast<bf16x8 *>(static_cast<bf16 *>(g.out) + (int64_t)row * g.ld_out +
-                                            col_l + h * 32) = ov;
+                g2_store(static_cast<bf16 *>(g.out) + (int64_t)row * g.ld_out + col_l + h * 32, ov);
             }
         }
     } else if constexpr (EPI == EPI_RESID_STATS) {
@@ -450,8 +462,7 @@ __global__ void __launch_bounds__(G2_T) gemm256_kernel(GemmArgs g) {
                     sq[mt] = fmaf(yb, yb, sq[mt]);
                     sd[mt] = fmaf(yb, wg[e], sd[mt]);
                 }
-                *reinterpret_cast<bf16x8 *>(static_cast<bf16 *>(g.out) + (int64_t)row * g.ld_out +
-                                            col_l + h * 32) = ov;
+                g2_store(static_cast<bf16 *>(g.out) + (int64_t)row * g.ld_out + col_l + h * 32, ov);
             }
         }
         // partials: the 4 lane groups (lanes l, l^16, l^32, l^48 share a row), then
@@ -509,7 +520,7 @@ __global__ void __launch_bounds__(G2_T) gemm256_kernel(GemmArgs g) {
                 __builtin_memcpy(&u, &ov, 16);
                 asm volatile("" ::"v"(u.x), "v"(u.y), "v"(u.z), "v"(u.w));
             } else {
-                *reinterpret_cast<bf16x8 *>(static_cast<bf16 *>(g.out) + o) = ov;
+                g2_store(static_cast<bf16 *>(g.out) + o, ov);
             }
         }
     }
