@@ -55,7 +55,7 @@ constexpr int HIST_BINS = 4096;
 constexpr int TIE_CAP = HIST_BINS;
 
 struct ScoreShared {
-    uint32_t acc[MAX_BLOCK_DOCS];  // 128 KiB
+    uint32_t acc[MAX_BLOCK_DOCS + 4];  // 128 KiB (+ the scatter's dummy word)
     union {
         RadixScratch<SC_WAVES> rs;  // general radix path
         uint32_t hist[HIST_BINS + 64];  // fast path: score histogram (+ spare bins), then the tie list
@@ -178,35 +178,44 @@ __device__ __forceinline__ bool wave_append(bool take, uint32_t *cursor, uint32_
     return take;
 }
 
-// One scatter round over postings p[0..last] (lane-consecutive, U per lane): all
-// loads first (unconditional: clamped address, a lane past the end drops its value
-// afterwards -- a load behind a per-lane condition makes the compiler branch around it
-// and drain vmcnt element by element), then the LDS reads, then the writes.  A doc
-// occurs once per term, so the read-modify-write needs no atomics.
+// Device posting words are ((doc_in_block << 8) | value) XOR POST_X.  A buffer load
+// past the descriptor's range returns 0, which decodes to doc MAX_BLOCK_DOCS -- the
+// dummy accumulator word after the block -- with value 0: the padding lanes of a
+// round need no clamp, no select and no branch (their update lands in the dummy).
+constexpr uint32_t POST_X = (uint32_t)MAX_BLOCK_DOCS << 8;
+
+// One scatter round over postings p[0 .. min(avail, UU * SC_THREADS)) (lane-
+// consecutive, UU per lane; p and avail wave-uniform): all loads first -- buffer loads
+// bounds-checked by the hardware, a 32-bit lane offset and no per-posting address
+// arithmetic -- then the LDS reads, then the writes.  A doc occurs once per term, so
+// the read-modify-write needs no atomics.
 template <int UU>
-__device__ __forceinline__ void scatter_load(const uint32_t *p, int last, int tid,
+__device__ __forceinline__ void scatter_load(const uint32_t *p, int64_t avail, int tid,
                                              uint32_t (&cur)[UU]) {
+    const uint64_t pa = reinterpret_cast<uint64_t>(p);
+    const uint32_t lo32 = __builtin_amdgcn_readfirstlane((uint32_t)pa);
+    const uint32_t hi32 = __builtin_amdgcn_readfirstlane((uint32_t)(pa >> 32));
+    const int bytes = __builtin_amdgcn_readfirstlane(
+        (int)(min(avail, (int64_t)UU * SC_THREADS) * 4));
+    void *base = reinterpret_cast<void *>(((uint64_t)hi32 << 32) | lo32);
+    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(base, (short)0, bytes, 0x00020000);
 #pragma unroll
-    for (int u = 0; u < UU; ++u) {
-        const int i = tid + u * SC_THREADS;
-        const uint32_t x = p[min(i, last)];
-        cur[u] = i <= last ? x : 0u;
-    }
+    for (int u = 0; u < UU; ++u)
+        cur[u] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, (tid + u * SC_THREADS) * 4, 0, 0);
 }
 template <int UU>
 __device__ __forceinline__ void scatter_apply(uint32_t *acc, const uint32_t (&cur)[UU],
                                               uint32_t first_bits) {
-    uint32_t w[UU];
-#pragma unroll
-    for (int u = 0; u < UU; ++u) w[u] = acc[(cur[u] >> 8) & (MAX_BLOCK_DOCS - 1)];
+    uint32_t w[UU], a[UU];
 #pragma unroll
     for (int u = 0; u < UU; ++u) {
-        const uint32_t v = cur[u] & 255u;  // 0 only for the padding lanes
-        if (v) {
-            const uint32_t x = w[u];
-            acc[(cur[u] >> 8) & (MAX_BLOCK_DOCS - 1)] =
-                x ? x + (v << 16) : ((v << 16) | first_bits | v);
-        }
+        a[u] = (cur[u] ^ POST_X) >> 8;
+        w[u] = acc[a[u]];
+    }
+#pragma unroll
+    for (int u = 0; u < UU; ++u) {
+        const uint32_t v = cur[u] & 255u, vs = v << 16;
+        acc[a[u]] = w[u] ? w[u] + vs : (vs | first_bits | v);
     }
 }
 
@@ -310,27 +319,26 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int item,
         }
         const bool next = j + 1 < nt && hi[j + 1] > lo[j + 1];
         auto prefetch_next = [&]() {
-            scatter_load<4>(post + lo[j + 1],
-                            (int)min(hi[j + 1] - lo[j + 1], (int64_t)4 * SC_THREADS) - 1, tid, pre);
+            scatter_load<4>(post + lo[j + 1], hi[j + 1] - lo[j + 1], tid, pre);
             have_pre = true;
         };
         while (pos < end) {
             const int64_t rem = end - pos;
             if (rem >= 16 * SC_THREADS) {
                 uint32_t r[16];
-                scatter_load<16>(post + pos, 16 * SC_THREADS - 1, tid, r);
+                scatter_load<16>(post + pos, rem, tid, r);
                 if (rem == 16 * SC_THREADS && next) prefetch_next();
                 scatter_apply<16>(sh.acc, r, first_bits);
                 pos += 16 * SC_THREADS;
             } else if (rem > SC_THREADS) {
                 uint32_t r[4];
-                scatter_load<4>(post + pos, (int)min(rem, (int64_t)4 * SC_THREADS) - 1, tid, r);
+                scatter_load<4>(post + pos, rem, tid, r);
                 if (rem <= 4 * SC_THREADS && next) prefetch_next();
                 scatter_apply<4>(sh.acc, r, first_bits);
                 pos += 4 * SC_THREADS;
             } else {
                 uint32_t r[1];
-                scatter_load<1>(post + pos, (int)rem - 1, tid, r);
+                scatter_load<1>(post + pos, rem, tid, r);
                 if (next) prefetch_next();
                 scatter_apply<1>(sh.acc, r, first_bits);
                 pos = end;
@@ -1033,6 +1041,7 @@ void build_index(di_index *ix, const int64_t *term_off, int64_t n_terms, const u
             }
         }
     }
+    for (auto &w : packed) w ^= POST_X;  // device encoding (see POST_X)
     ix->post.reserve(packed.size() * 4);
     ix->term_start.reserve(tstart.size() * 8);
     ix->blk_off.reserve(boff.size() * 4);
