@@ -206,16 +206,27 @@ __device__ __forceinline__ void scatter_load(const uint32_t *p, int64_t avail, i
 template <int UU>
 __device__ __forceinline__ void scatter_apply(uint32_t *acc, const uint32_t (&cur)[UU],
                                               uint32_t first_bits) {
+    // LDS byte addresses formed here and the accesses in inline asm (the compiler's own
+    // form adds the array's zero base once more per posting); the reads are retired by
+    // the explicit wait, the writes by the caller's term barrier / final wait.
+    // (acc is the first member of the kernel's only LDS object, the dynamic segment at
+    // LDS address 0: score_blocks_kernel checks that once)
+    (void)acc;
     uint32_t w[UU], a[UU];
 #pragma unroll
     for (int u = 0; u < UU; ++u) {
-        a[u] = (cur[u] ^ POST_X) >> 8;
-        w[u] = acc[a[u]];
+        a[u] = ((cur[u] ^ POST_X) >> 8) << 2;
+        asm volatile("ds_read_b32 %0, %1" : "=v"(w[u]) : "v"(a[u]) : "memory");
     }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
     for (int u = 0; u < UU; ++u) {
-        const uint32_t v = cur[u] & 255u, vs = v << 16;
-        acc[a[u]] = w[u] ? w[u] + vs : (vs | first_bits | v);
+        // touched: w + (v << 16); first touch: (v << 16) | first_bits | v -- both one
+        // 24-bit multiply-add (v < 256, first_bits = (255 - j) << 8: no carries)
+        const uint32_t v = cur[u] & 255u;
+        const uint32_t t = __umul24(v, 0x10000u) + w[u];
+        const uint32_t f = __umul24(v, 0x10001u) + first_bits;
+        asm volatile("ds_write_b32 %0, %1" ::"v"(a[u]), "v"(w[u] ? t : f) : "memory");
     }
 }
 
@@ -347,6 +358,7 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int item,
         // term boundary: this term's LDS writes land before any wave reads the next
         if (j + 1 < nt) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the asm LDS writes
     __syncthreads();
 
     stamp(1);  // scatter
@@ -643,6 +655,13 @@ score_blocks_kernel(const uint32_t *__restrict__ post, const int64_t *__restrict
                     int32_t *__restrict__ cand_n, int n_items, int ablate) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     ScoreShared &sh = *reinterpret_cast<ScoreShared *>(smem);
+    if ((uint32_t)(uintptr_t)((__attribute__((address_space(3))) unsigned char *)smem) != 0) {
+        // scatter_apply addresses the accumulators from LDS address 0 (folded away when
+        // the segment starts there, as it does): otherwise fail every item loudly
+        for (int item = blockIdx.x; item < n_items; item += gridDim.x)
+            if (threadIdx.x == 0) cand_n[item] = -1;
+        return;
+    }
     for (int item = blockIdx.x; item < n_items; item += gridDim.x) {
         score_item(sh, item, post, term_start, blk_off, seg, min_cls, nb, block_docs, n_terms,
                    n_docs, doc_lo,
