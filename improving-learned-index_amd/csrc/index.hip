@@ -47,6 +47,12 @@ constexpr int SC_THREADS = 1024;
 constexpr int SC_WAVES = SC_THREADS / 64;
 constexpr int SC_PER_THREAD = MAX_BLOCK_DOCS / SC_THREADS;  // 32
 constexpr int MAX_TERMS = DI_MAX_QUERY_TERMS;
+// Long sublists (>= WLONG_MIN postings in a block) carry a per-wave layout (build pass
+// 3): wave w scatters only the docs of its segment, and runs of long terms need no
+// barrier.  Queries with more than WTERMS terms use the all-wave form only.
+constexpr int WSEG = SC_WAVES;
+constexpr int WLONG_MIN = 1024;
+constexpr int WTERMS = 64;
 // Fast selection: with at most 16 query terms every score is below 255 * 16 < 4096,
 // so one pass of a 4096-bin score histogram finds the k-th score; the docs tied at
 // that score (a few, typically) are ordered from a compact list in LDS.
@@ -69,6 +75,8 @@ struct ScoreShared {
     uint32_t n_tie;  // tie-list cursor
     uint32_t bad;
     uint32_t thr, above, ties, bin, bin_above;
+    uint32_t lmask[WTERMS / 32];      // terms (j < WTERMS) with a per-wave layout in this block
+    uint32_t wtab[WTERMS][WSEG];      // their per-wave runs: start << 16 | end (in the sublist)
 };
 static_assert(sizeof(RadixScratch<SC_WAVES>) >= (HIST_BINS + 64) * 4,
               "histogram (+ 64 spare bins) overlays the radix scratch");
@@ -189,19 +197,19 @@ constexpr uint32_t POST_X = (uint32_t)MAX_BLOCK_DOCS << 8;
 // bounds-checked by the hardware, a 32-bit lane offset and no per-posting address
 // arithmetic -- then the LDS reads, then the writes.  A doc occurs once per term, so
 // the read-modify-write needs no atomics.
-template <int UU>
+template <int UU, int NT = SC_THREADS>
 __device__ __forceinline__ void scatter_load(const uint32_t *p, int64_t avail, int tid,
                                              uint32_t (&cur)[UU]) {
     const uint64_t pa = reinterpret_cast<uint64_t>(p);
     const uint32_t lo32 = __builtin_amdgcn_readfirstlane((uint32_t)pa);
     const uint32_t hi32 = __builtin_amdgcn_readfirstlane((uint32_t)(pa >> 32));
     const int bytes = __builtin_amdgcn_readfirstlane(
-        (int)(min(avail, (int64_t)UU * SC_THREADS) * 4));
+        (int)(min(avail, (int64_t)UU * NT) * 4));
     void *base = reinterpret_cast<void *>(((uint64_t)hi32 << 32) | lo32);
     const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(base, (short)0, bytes, 0x00020000);
 #pragma unroll
     for (int u = 0; u < UU; ++u)
-        cur[u] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, (tid + u * SC_THREADS) * 4, 0, 0);
+        cur[u] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, (tid + u * NT) * 4, 0, 0);
 }
 template <int UU>
 __device__ __forceinline__ void scatter_apply(uint32_t *acc, const uint32_t (&cur)[UU],
@@ -219,6 +227,11 @@ __device__ __forceinline__ void scatter_apply(uint32_t *acc, const uint32_t (&cu
         asm volatile("ds_read_b32 %0, %1" : "=v"(w[u]) : "v"(a[u]) : "memory");
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    // the compiler sees the asm reads' results as ready at once: redefine them after
+    // the wait, and fence the scheduler, so that no use is hoisted above it
+#pragma unroll
+    for (int u = 0; u < UU; ++u) asm volatile("" : "+v"(w[u]));
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int u = 0; u < UU; ++u) {
         // touched: w + (v << 16); first touch: (v << 16) | first_bits | v -- both one
@@ -239,7 +252,9 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int item,
                                            const uint32_t *__restrict__ post,
                                            const int64_t *__restrict__ term_start,
                                            const uint32_t *__restrict__ blk_off,
-                                           const uint16_t *__restrict__ seg, int min_cls, int nb,
+                                           const uint16_t *__restrict__ seg,
+                                           const uint32_t *__restrict__ lid,
+                                           const uint16_t *__restrict__ wmeta, int min_cls, int nb,
                                            int block_docs, int64_t n_terms, uint32_t n_docs,
                                            uint32_t doc_lo, const uint32_t *__restrict__ q_terms,
                                            const int32_t *__restrict__ cu_q, int k,
@@ -278,21 +293,50 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int item,
         sh.bad = 0;
         sh.emit = 0;
         sh.n_tie = 0;
+        for (int i = 0; i < WTERMS / 32; ++i) sh.lmask[i] = 0;
     }
     __syncthreads();
 
-    // sublist bounds for this block, zero the accumulators (and the fast histogram)
-    for (int j = tid; j < nt; j += SC_THREADS) {
-        const uint32_t t = q_terms[q0 + j];
-        if (t >= n_terms) {  // invalid id (device-pointer callers are not pre-checked)
-            sh.bad = 1;
-            lo[j] = hi[j] = 0;
-            continue;
-        }
+    // sublist bounds for this block and, with the per-wave layout, the long terms' runs
+    // (one pass: the loads of both depend only on the term id, so they overlap);
+    // ablate bit 128: all-wave form only
+    const bool wl = nt <= WTERMS && !(ablate & 128);
+    auto bounds = [&](int j, uint32_t t) {
         const uint32_t *bo = blk_off + (int64_t)t * (nb + 1) + b;
         lo[j] = term_start[t] + bo[0];
         hi[j] = min_cls >= 7 ? term_start[t] + bo[1]
                              : lo[j] + seg[((int64_t)t * nb + b) * 8 + min_cls];
+    };
+    if (wl) {
+        for (int e = tid; e < nt * WSEG; e += SC_THREADS) {
+            const int j = e / WSEG, w = e % WSEG;
+            const uint32_t t = q_terms[q0 + j];
+            if (t >= n_terms) {  // invalid id (device-pointer callers are not pre-checked)
+                if (w == 0) {
+                    sh.bad = 1;
+                    lo[j] = hi[j] = 0;
+                }
+                continue;
+            }
+            const uint32_t id = lid[(int64_t)t * nb + b];
+            if (w == 0) bounds(j, t);
+            if (id == 0xFFFFFFFFu) continue;
+            const uint16_t *m = wmeta + (int64_t)id * (WSEG * 8);
+            const uint32_t s0 = w ? m[(w - 1) * 8 + 7] : 0u;
+            const uint32_t e0 = m[w * 8 + min(min_cls, 7)];
+            sh.wtab[j][w] = (s0 << 16) | e0;
+            if (w == 0) atomicOr(&sh.lmask[j >> 5], 1u << (j & 31));
+        }
+    } else {
+        for (int j = tid; j < nt; j += SC_THREADS) {
+            const uint32_t t = q_terms[q0 + j];
+            if (t >= n_terms) {
+                sh.bad = 1;
+                lo[j] = hi[j] = 0;
+                continue;
+            }
+            bounds(j, t);
+        }
     }
     {
         uint4 *a4 = reinterpret_cast<uint4 *>(sh.acc);
@@ -317,10 +361,47 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int item,
     // The last round of a term also loads the next term's first 4 k postings, before
     // the term barrier (a raw one: LDS writes retired, loads left in flight), so the
     // barrier does not expose a load round trip per term.
+    // A long term (per-wave layout) is scattered by each wave over its own doc segment,
+    // rounds of up to 16 postings per lane: no other wave touches those docs, so a run
+    // of long terms needs no barrier between its terms, only at its ends.
     uint32_t pre[4];
     bool have_pre = false;
+    auto is_long = [&](int j) { return wl && ((sh.lmask[j >> 5] >> (j & 31)) & 1u); };
     for (int j = (ablate & 1) ? nt : 0; j < nt; ++j) {  // ablate bit 0: skip (profiling)
         const uint32_t first_bits = (uint32_t)(255 - j) << 8;
+        const bool lj = is_long(j);
+        if (lj) {
+            const uint32_t se = sh.wtab[j][wave];
+            int64_t pos = lo[j] + (se >> 16);
+            const int64_t end = lo[j] + (se & 0xFFFFu);
+            while (pos < end) {
+                const int64_t rem = end - pos;
+                if (rem > 8 * 64) {
+                    uint32_t r[16];
+                    scatter_load<16, 64>(post + pos, rem, lane, r);
+                    scatter_apply<16>(sh.acc, r, first_bits);
+                    pos += 16 * 64;
+                } else if (rem > 4 * 64) {
+                    uint32_t r[8];
+                    scatter_load<8, 64>(post + pos, rem, lane, r);
+                    scatter_apply<8>(sh.acc, r, first_bits);
+                    pos = end;
+                } else if (rem > 64) {
+                    uint32_t r[4];
+                    scatter_load<4, 64>(post + pos, rem, lane, r);
+                    scatter_apply<4>(sh.acc, r, first_bits);
+                    pos = end;
+                } else {
+                    uint32_t r[1];
+                    scatter_load<1, 64>(post + pos, rem, lane, r);
+                    scatter_apply<1>(sh.acc, r, first_bits);
+                    pos = end;
+                }
+            }
+            if (j + 1 < nt && !is_long(j + 1))
+                asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+            continue;
+        }
         int64_t pos = lo[j];
         const int64_t end = hi[j];
         if (have_pre) {
@@ -328,7 +409,7 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int item,
             pos = min(end, pos + (int64_t)4 * SC_THREADS);
             have_pre = false;
         }
-        const bool next = j + 1 < nt && hi[j + 1] > lo[j + 1];
+        const bool next = j + 1 < nt && hi[j + 1] > lo[j + 1] && !is_long(j + 1);
         auto prefetch_next = [&]() {
             scatter_load<4>(post + lo[j + 1], hi[j + 1] - lo[j + 1], tid, pre);
             have_pre = true;
@@ -649,6 +730,7 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int item,
 __global__ void __launch_bounds__(SC_THREADS)
 score_blocks_kernel(const uint32_t *__restrict__ post, const int64_t *__restrict__ term_start,
                     const uint32_t *__restrict__ blk_off, const uint16_t *__restrict__ seg,
+                    const uint32_t *__restrict__ lid, const uint16_t *__restrict__ wmeta,
                     int min_cls, int nb, int block_docs, int64_t n_terms,
                     uint32_t n_docs, uint32_t doc_lo, const uint32_t *__restrict__ q_terms,
                     const int32_t *__restrict__ cu_q, int k, uint64_t *__restrict__ cand_key,
@@ -663,7 +745,8 @@ score_blocks_kernel(const uint32_t *__restrict__ post, const int64_t *__restrict
         return;
     }
     for (int item = blockIdx.x; item < n_items; item += gridDim.x) {
-        score_item(sh, item, post, term_start, blk_off, seg, min_cls, nb, block_docs, n_terms,
+        score_item(sh, item, post, term_start, blk_off, seg, lid, wmeta, min_cls, nb, block_docs,
+                   n_terms,
                    n_docs, doc_lo,
                    q_terms, cu_q, k, cand_key, cand_n, ablate);
         __syncthreads();  // every wave is done with the LDS of this item
@@ -915,7 +998,9 @@ struct di_index {
     int nb = 0, block_docs = 0;
     int min_cls = 7;                 // impact-class prefix scored (7 = every posting: exact)
     std::vector<uint16_t> seg;       // host copy of the class offsets (pass 3)
-    DevBuf post, term_start, blk_off, seg_dev;
+    std::vector<uint32_t> lid;       // long-sublist ids (pass 3)
+    std::vector<uint16_t> wmeta;     // per-wave class ends of the long sublists
+    DevBuf post, term_start, blk_off, seg_dev, lid_dev, wmeta_dev;
     DevBuf ws_q, ws_cu, ws_ck, ws_cn, ws_doc, ws_score, ws_n, ws_key;
     int ablate = 0;  // DI_PROFILE_ABLATE: profiling only (1 no scatter, 2 no selection, 4 stop at the k-th score)
     Timer timer;
@@ -1012,50 +1097,90 @@ void build_index(di_index *ix, const int64_t *term_off, int64_t n_terms, const u
     // on equal banks.  Any order is exact: a doc occurs once per term, and its key
     // (first term, value there) does not depend on the order inside the term.
     ix->seg.assign((size_t)std::max<int64_t>(n_terms * nb * 8, 1), 0);
+    // Long sublists (>= WLONG_MIN postings) are laid out by wave segment first: wave w
+    // of the scorer owns the block's docs [w S, (w + 1) S), S = ceil(bd / 16), and
+    // its postings of the sublist form one run (classes in order, bank-dealt inside),
+    // so that consecutive long terms need no barrier (no two waves touch one doc).
+    // wmeta[lid * 128 + 8 w + c] = end of class c of segment w (offset in the
+    // sublist), lid[t * nb + b] = the sublist's long id (0xFFFFFFFF: short).
+    ix->lid.assign((size_t)std::max<int64_t>(n_terms * nb, 1), 0xFFFFFFFFu);
+    ix->wmeta.clear();
     {
-        std::vector<uint32_t> tmp, cls_cnt(8), cls_pos(8), bucket_cnt(32), head(32);
         auto cls_of = [](uint32_t w) { return 7 - (31 - __builtin_clz(w & 255u)); };
+        const uint32_t S = (bd + WSEG - 1) / WSEG;
+        static const int64_t wlong_min = [] {  // A/B: DI_WLONG_MIN (postings)
+            const char *e = std::getenv("DI_WLONG_MIN");
+            return e ? (int64_t)std::atoll(e) : (int64_t)WLONG_MIN;
+        }();
+        std::vector<uint32_t> grp, tmp, bk, cls_cnt(8), cls_pos(8), bucket_cnt(32), head(32),
+            fill(32);
+        // one group (any order in): classes in order (stable), each dealt round-robin
+        // from its 32 LDS bank buckets (doc_in_block mod 32) into packed[o..];
+        // cum[c] = end of class c relative to the sublist start s0
+        auto emit_group = [&](const uint32_t *in, size_t n, int64_t &o, int64_t s0,
+                              uint16_t *cum) {
+            std::fill(cls_cnt.begin(), cls_cnt.end(), 0);
+            for (size_t i = 0; i < n; ++i) cls_cnt[cls_of(in[i])]++;
+            uint32_t run = 0;
+            for (int c = 0; c < 8; ++c) {
+                cls_pos[c] = run;
+                run += cls_cnt[c];
+            }
+            tmp.resize(n);
+            for (size_t i = 0; i < n; ++i) tmp[cls_pos[cls_of(in[i])]++] = in[i];
+            uint32_t c0 = 0;
+            for (int c = 0; c < 8; ++c) {
+                const uint32_t c1 = c0 + cls_cnt[c];
+                std::fill(bucket_cnt.begin(), bucket_cnt.end(), 0);
+                for (uint32_t i = c0; i < c1; ++i) bucket_cnt[(tmp[i] >> 8) & 31]++;
+                uint32_t r = 0;
+                for (int k = 0; k < 32; ++k) {
+                    head[k] = r;
+                    r += bucket_cnt[k];
+                }
+                bk.resize(c1 - c0);
+                fill = head;
+                for (uint32_t i = c0; i < c1; ++i) bk[fill[(tmp[i] >> 8) & 31]++] = tmp[i];
+                for (bool any = true; any;) {
+                    any = false;
+                    for (int k = 0; k < 32; ++k)
+                        if (bucket_cnt[k]) {
+                            packed[o++] = bk[head[k]++];
+                            --bucket_cnt[k];
+                            any = true;
+                        }
+                }
+                if (cum) cum[c] = (uint16_t)(o - s0);
+                c0 = c1;
+            }
+        };
         for (int64_t t = 0; t < n_terms; ++t) {
             for (int b = 0; b < nb; ++b) {
                 const int64_t s0 = tstart[t] + boff[t * stride + b];
                 const int64_t s1 = tstart[t] + boff[t * stride + b + 1];
                 uint16_t *sg = &ix->seg[(size_t)(t * nb + b) * 8];
-                std::fill(cls_cnt.begin(), cls_cnt.end(), 0);
-                for (int64_t i = s0; i < s1; ++i) cls_cnt[cls_of(packed[i])]++;
-                uint32_t run = 0;
-                for (int c = 0; c < 8; ++c) {
-                    cls_pos[c] = run;
-                    run += cls_cnt[c];
-                    sg[c] = (uint16_t)run;
-                }
-                if (s1 - s0 <= 1) continue;
-                tmp.resize((size_t)(s1 - s0));
-                for (int64_t i = s0; i < s1; ++i) tmp[cls_pos[cls_of(packed[i])]++] = packed[i];
-                // tmp: classes in order (stable); deal each class from its bank buckets
+                grp.assign(packed.begin() + s0, packed.begin() + s1);
                 int64_t o = s0;
-                uint32_t c0 = 0;
-                for (int c = 0; c < 8; ++c) {
-                    const uint32_t c1 = c0 + cls_cnt[c];
-                    std::fill(bucket_cnt.begin(), bucket_cnt.end(), 0);
-                    for (uint32_t i = c0; i < c1; ++i) bucket_cnt[(tmp[i] >> 8) & 31]++;
-                    uint32_t r = 0;
-                    for (int k = 0; k < 32; ++k) {
-                        head[k] = r;
-                        r += bucket_cnt[k];
-                    }
-                    std::vector<uint32_t> bk(c1 - c0);
-                    std::vector<uint32_t> fill = head;
-                    for (uint32_t i = c0; i < c1; ++i) bk[fill[(tmp[i] >> 8) & 31]++] = tmp[i];
-                    for (bool any = true; any;) {
-                        any = false;
-                        for (int k = 0; k < 32; ++k)
-                            if (bucket_cnt[k]) {
-                                packed[o++] = bk[head[k]++];
-                                --bucket_cnt[k];
-                                any = true;
-                            }
-                    }
-                    c0 = c1;
+                if (s1 - s0 < wlong_min) {
+                    emit_group(grp.data(), grp.size(), o, s0, sg);
+                    continue;
+                }
+                {  // whole-sublist class counts (seg), then the per-wave layout
+                    uint32_t run = 0, cc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+                    for (uint32_t x : grp) cc[cls_of(x)]++;
+                    for (int c = 0; c < 8; ++c) sg[c] = (uint16_t)(run += cc[c]);
+                }
+                const uint32_t id = (uint32_t)(ix->wmeta.size() / (WSEG * 8));
+                ix->lid[(size_t)(t * nb + b)] = id;
+                ix->wmeta.resize(ix->wmeta.size() + WSEG * 8);
+                std::vector<uint32_t> seg_in;
+                for (int w = 0; w < WSEG; ++w) {
+                    seg_in.clear();
+                    for (uint32_t x : grp)
+                        if (std::min<uint32_t>((x >> 8) / S, WSEG - 1) == (uint32_t)w)
+                            seg_in.push_back(x);
+                    emit_group(seg_in.data(), seg_in.size(), o, s0,
+                               &ix->wmeta[(size_t)id * WSEG * 8 + w * 8]);
                 }
             }
         }
@@ -1069,6 +1194,11 @@ void build_index(di_index *ix, const int64_t *term_off, int64_t n_terms, const u
     DI_HIP(hipMemcpy(ix->blk_off.p, boff.data(), boff.size() * 4, hipMemcpyHostToDevice));
     ix->seg_dev.reserve(ix->seg.size() * 2);
     DI_HIP(hipMemcpy(ix->seg_dev.p, ix->seg.data(), ix->seg.size() * 2, hipMemcpyHostToDevice));
+    ix->lid_dev.reserve(ix->lid.size() * 4);
+    DI_HIP(hipMemcpy(ix->lid_dev.p, ix->lid.data(), ix->lid.size() * 4, hipMemcpyHostToDevice));
+    if (ix->wmeta.empty()) ix->wmeta.assign(WSEG * 8, 0);
+    ix->wmeta_dev.reserve(ix->wmeta.size() * 2);
+    DI_HIP(hipMemcpy(ix->wmeta_dev.p, ix->wmeta.data(), ix->wmeta.size() * 2, hipMemcpyHostToDevice));
 }
 
 }  // namespace
@@ -1161,6 +1291,8 @@ int di_index_create(const int64_t *term_off, int64_t n_terms, const uint32_t *pd
         ix->own_stream = true;
         enable_big_lds();
         if (const char *ab = std::getenv("DI_PROFILE_ABLATE")) ix->ablate = std::atoi(ab);
+        if (const char *sw = std::getenv("DI_SCATTER_WAVE"))  // A/B: 0 = all-wave scatter only
+            if (sw[0] == '0') ix->ablate |= 128;
         build_index(ix.get(), term_off, n_terms, pdoc, pval, doc_lo, doc_hi);
         *out = ix.release();
     });
@@ -1282,6 +1414,7 @@ int di_index_search(di_index *ix, const uint32_t *q_terms, const int32_t *cu_q, 
                                    dim3(SC_THREADS), sizeof(ScoreShared), s,
                                    ix->post.as<uint32_t>(), ix->term_start.as<int64_t>(),
                                    ix->blk_off.as<uint32_t>(), ix->seg_dev.as<uint16_t>(),
+                                   ix->lid_dev.as<uint32_t>(), ix->wmeta_dev.as<uint16_t>(),
                                    ix->min_cls, nb, ix->block_docs, ix->n_terms,
                                    ix->n_docs, ix->doc_lo, dq, dcu + q0, k,
                                    ix->ws_ck.as<uint64_t>(), ix->ws_cn.as<int32_t>(), n_items,
