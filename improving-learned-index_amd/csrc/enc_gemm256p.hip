@@ -364,6 +364,8 @@ __global__ void __launch_bounds__(GP_T) gemm256p_kernel(GemmArgs g) {
                     asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(pr[mt]) : "v"(prow), "i"(mt * 128));
                 GP_SYNC_READS();
 #pragma unroll
+                for (int mt = 0; mt < 8; ++mt) asm volatile("" : "+v"(pr[mt]));
+#pragma unroll
                 for (int mt = 0; mt < 8; ++mt) {
                     ra8[mt] = __uint_as_float(pr[mt].x);
                     rb8[mt] = __uint_as_float(pr[mt].y);
@@ -377,6 +379,7 @@ __global__ void __launch_bounds__(GP_T) gemm256p_kernel(GemmArgs g) {
         GP_LD(p0_, pcol, (off) + (h) * 128);                                                   \
         GP_LD(p1_, pcol, (off) + (h) * 128 + 16);                                              \
         GP_SYNC_READS();                                                                       \
+        asm volatile("" : "+v"(p0_), "+v"(p1_)); /* results exist only after the wait */       \
         as8(p0_, p1_, v);                                                                      \
     } while (0)
         auto as8 = [](const uint4 &a, const uint4 &b, float (&v)[8]) {
@@ -513,6 +516,8 @@ __global__ void __launch_bounds__(GP_T) gemm256p_kernel(GemmArgs g) {
                     for (int w = 0; w < 4; ++w)
                         asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(p[w]) : "v"(part_rd), "i"(w * 4096));
                     GP_SYNC_READS();
+#pragma unroll
+                    for (int w = 0; w < 4; ++w) asm volatile("" : "+v"(p[w]));
                     float4 t = make_float4(p[0].x, p[0].y, p[0].z, 0.f);
 #pragma unroll
                     for (int w = 1; w < 4; ++w) {
