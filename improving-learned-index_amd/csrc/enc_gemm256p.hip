@@ -364,7 +364,7 @@ __global__ void __launch_bounds__(GP_T) gemm256p_kernel(GemmArgs g) {
                     asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(pr[mt]) : "v"(prow), "i"(mt * 128));
                 GP_SYNC_READS();
 #pragma unroll
-                for (int mt = 0; mt < 8; ++mt) asm volatile("" : "+v"(pr[mt]));
+                for (int mt = 0; mt < 8; ++mt) asm volatile("" : "+v"(pr[mt].x), "+v"(pr[mt].y));
 #pragma unroll
                 for (int mt = 0; mt < 8; ++mt) {
                     ra8[mt] = __uint_as_float(pr[mt].x);
@@ -379,7 +379,8 @@ __global__ void __launch_bounds__(GP_T) gemm256p_kernel(GemmArgs g) {
         GP_LD(p0_, pcol, (off) + (h) * 128);                                                   \
         GP_LD(p1_, pcol, (off) + (h) * 128 + 16);                                              \
         GP_SYNC_READS();                                                                       \
-        asm volatile("" : "+v"(p0_), "+v"(p1_)); /* results exist only after the wait */       \
+        asm volatile("" : "+v"(p0_.x), "+v"(p0_.y), "+v"(p0_.z), "+v"(p0_.w), "+v"(p1_.x),      \
+                     "+v"(p1_.y), "+v"(p1_.z), "+v"(p1_.w)); /* results exist after the wait */ \
         as8(p0_, p1_, v);                                                                      \
     } while (0)
         auto as8 = [](const uint4 &a, const uint4 &b, float (&v)[8]) {
