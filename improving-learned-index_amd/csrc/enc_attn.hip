@@ -717,22 +717,37 @@ attention_v3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
                                      : "v"(kim + r * 128 + (((ch * 4 + g) ^ (r & 7)) << 4)));
                 }
                 // V^T fragments: d-tile dt, halves h2 = keys 8g + 4h2 + (0..3)
-                bf16x8 vf[4];
+                uint2 hv[4][2];
 #pragma unroll
-                for (int dt = 0; dt < 4; ++dt) {
-                    uint2 hv[2];
+                for (int dt = 0; dt < 4; ++dt)
 #pragma unroll
                     for (int h2 = 0; h2 < 2; ++h2) {
                         const int r = key0 + 8 * g + 4 * h2 + tq;
                         const int chv = 2 * dt + (tp >> 1);
-                        hv[h2] = ds_read_tr_b16(vim + r * 128 + ((chv ^ (r & 7)) << 4) +
-                                                8 * (tp & 1));
+                        hv[dt][h2] = ds_read_tr_b16(vim + r * 128 + ((chv ^ (r & 7)) << 4) +
+                                                    8 * (tp & 1));
                     }
-                    const uint4 v4 = make_uint4(hv[0].x, hv[0].y, hv[1].x, hv[1].y);
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                // the asm reads' results exist only from here: redefine them after the
+                // wait (no use or copy hoisted above it), then fence the scheduler
+#pragma unroll
+                for (int t = 0; t < 2; ++t)
+#pragma unroll
+                    for (int ch = 0; ch < 2; ++ch)
+                        asm volatile("" : "+v"(kf[t][ch].x), "+v"(kf[t][ch].y), "+v"(kf[t][ch].z),
+                                     "+v"(kf[t][ch].w));
+#pragma unroll
+                for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+                    for (int h2 = 0; h2 < 2; ++h2)
+                        asm volatile("" : "+v"(hv[dt][h2].x), "+v"(hv[dt][h2].y));
+                __builtin_amdgcn_sched_barrier(0);  // no MFMA above the wait (rule 18)
+                bf16x8 vf[4];
+#pragma unroll
+                for (int dt = 0; dt < 4; ++dt) {
+                    const uint4 v4 = make_uint4(hv[dt][0].x, hv[dt][0].y, hv[dt][1].x, hv[dt][1].y);
                     __builtin_memcpy(&vf[dt], &v4, 16);
                 }
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                __builtin_amdgcn_sched_barrier(0);  // no MFMA above the wait (rule 18)
                 const bool tail = key0 + 32 > n;
 #pragma unroll
                 for (int qt = 0; qt < QTB; ++qt) {
