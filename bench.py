@@ -368,7 +368,7 @@ def main():
     ap.add_argument("--k", type=int, default=1000)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--docs", type=int, default=4096, help="docs encoded per step per GPU (1024: -2%%; the 256-row GEMM tiles quantize less on 256 CUs at 4096)")
+    ap.add_argument("--docs", type=int, default=8192, help="docs encoded per step per GPU (1024: -3%%, 4096: -1%%: the 256-row GEMM tiles quantize less on 256 CUs with more rows)")
     ap.add_argument("--max-len", type=int, default=300)
     ap.add_argument("--legs", default="encode,retrieve")
     args = ap.parse_args()

@@ -426,7 +426,9 @@ void forward_folded(di_encoder *e, const int32_t *d_ids, const int32_t *d_cu, in
     auto base = [&]() {
         GemmArgs g{};
         g.stagger = stagger;
-        g.tune_gm = tune_gm;
+        // tile-order group: 8 M-tiles (measured +4% QKV, +1% O / FFN1 over 4); FFN2
+        // (K = 3072, N = 768) keeps 4
+        g.tune_gm = tune_gm ? tune_gm : 8;
         g.M = (int)M;
         g.a_rows = e->cap_rows;
         g.hidden = H;
@@ -511,6 +513,7 @@ void forward_folded(di_encoder *e, const int32_t *d_ids, const int32_t *d_cu, in
         g.N = H;
         g.K = F;
         g.ld_out = H;
+        if (tune_gm == 0) g.tune_gm = 4;
         g.row_ln = rl1;
         g.res_gamma = L.ln1_g.as<float>();
         g.res_beta = L.ln1_b.as<float>();
