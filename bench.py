@@ -209,10 +209,22 @@ def synthetic_docs_tokens(n_docs, vocab, seed, max_len=300):
     return ids, cu, lens, np.array(term_tok, np.int32), np.array(cu_terms, np.int32)
 
 
-def flops_per_doc(n, H=768, L=12):
-    """sum over layers (24 n H^2 + 4 n^2 H) + 2 n H (real tokens only)."""
+def flops_per_doc(n, H=768, L=12, t=None):
+    """sum over layers (24 n H^2 + 4 n^2 H) + 2 n H (real tokens only).
+    With t (kept terms per doc): the FLOPs executed when the last layer runs its
+    attention queries and its O / FFN GEMMs on the t term rows only (the pruned last
+    layer; the QKV projection still covers every row)."""
     n = np.asarray(n, np.float64)
-    return L * (24.0 * n * H * H + 4.0 * n * n * H) + 2.0 * n * H
+    f = L * (24.0 * n * H * H + 4.0 * n * n * H) + 2.0 * n * H
+    if t is not None:
+        t = np.asarray(t, np.float64)
+        f = f - (18.0 * H * H * (n - t) + 4.0 * (n - t) * n * H)
+    return f
+
+
+def prune_last_layer():
+    """The library's DI_PRUNE_LAST default (on) for the term-output encode."""
+    return os.environ.get("DI_PRUNE_LAST", "1")[:1] != "0"
 
 
 def encode_leg(args, rank, world, dev):
@@ -266,8 +278,13 @@ def encode_leg(args, rank, world, dev):
         ms, n = enc.timing(name)
         kernels[name] = {"ms_per_step": ms / max(args.steps, 1), "launches": n}
     M, H, F, L = float(cu[-1]), cfg.hidden, cfg.intermediate, cfg.layers
-    gemm_flops = {"gemm_qkv": 2 * M * H * 3 * H, "gemm_o": 2 * M * H * H,
-                  "gemm_ffn1": 2 * M * H * F, "gemm_ffn2": 2 * M * F * H}
+    # rows per launch, averaged over the L launches of a step: the pruned last layer runs
+    # O / FFN1 / FFN2 on the T term rows (QKV on all M)
+    T = float(ct[-1])
+    prune = prune_last_layer()
+    Mp = ((L - 1) * M + T) / L if prune else M
+    gemm_flops = {"gemm_qkv": 2 * M * H * 3 * H, "gemm_o": 2 * Mp * H * H,
+                  "gemm_ffn1": 2 * Mp * H * F, "gemm_ffn2": 2 * Mp * F * H}
     per_launch = {}
     for k, f in gemm_flops.items():
         ms, n = enc.timing(k)
@@ -280,7 +297,8 @@ def encode_leg(args, rank, world, dev):
     pmc_name = {"gemm_qkv": "gemm256_kernel<5>", "gemm_ffn1": "gemm256_kernel<6>",
                 "gemm_o": "gemm256_kernel<7>", "gemm_ffn2": "gemm256_kernel<7>"}[dom]
     traffic, src = load_pmc_traffic(pmc_name)
-    model_flops = float(flops_per_doc(lens).sum())
+    # executed FLOPs (the pruned last layer skips the rows no output reads)
+    model_flops = float(flops_per_doc(lens, t=np.diff(ct) if prune else None).sum())
     docs_per_s = world * args.docs * args.steps / el
     res = {
         "value": docs_per_s,
@@ -410,7 +428,11 @@ def main():
                    "docs_per_step_per_gpu": args.docs, "max_length": args.max_len,
                    "docs_per_shard": DOCS_PER_SHARD, "queries": args.queries, "k": args.k,
                    "parallelism": f"doc-sharded x{world} (encode: no collective; retrieve: "
-                                  f"RCCL all-gather of per-shard top-k)"},
+                                  f"RCCL all-gather of per-shard top-k)",
+                   "encode_output": "term impacts (A8/A9 gather + round3); the last layer "
+                                    "computes only the rows the gather reads -- bit-identical "
+                                    "impacts, DESIGN.md §3" if prune_last_layer() else
+                                    "term impacts (A8/A9 gather + round3), every row computed"},
         "roofline": primary["roofline"],
         "cpu_baseline": None,
     }

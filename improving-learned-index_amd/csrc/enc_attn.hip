@@ -591,7 +591,11 @@ __device__ __forceinline__ uint2 ds_read_tr_b16(uint32_t addr) {
 template <bool DB>
 __global__ void __launch_bounds__(64 * ATT3_WAVES, 1)
 attention_v3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu_seqlens, int H,
-                    int n_heads, int n_pairs, bf16 *__restrict__ ctx) {
+                    int n_heads, int n_pairs, bf16 *__restrict__ ctx,
+                    const int32_t *__restrict__ qsel, const int32_t *__restrict__ cu_qsel) {
+    // qsel (optional): only the query rows qsel[cu_qsel[d] ..) (doc-local token
+    // indices) of document d are computed, into ctx rows cu_qsel[d] + i (the encoder's
+    // last layer: only the rows the term gather reads); keys are always every token.
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     typedef __attribute__((address_space(3))) void lds_void;
     constexpr int QTB = 2;
@@ -646,14 +650,18 @@ attention_v3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
     auto load_q = [&](int pp, uint4 (&qd)[2][QTB][2]) {
         const int dd = pp / n_heads, hh = pp % n_heads;
         const int t0 = cu_seqlens[dd], nn = cu_seqlens[dd + 1] - t0;
+        const int qs0 = qsel ? cu_qsel[dd] : 0, nq = qsel ? cu_qsel[dd + 1] - qs0 : nn;
         int t_first, t_cnt;
-        tiles_of(nn, t_first, t_cnt);
+        tiles_of(nq, t_first, t_cnt);
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
             const int q_base = (t_first + 2 * i) * 16;
 #pragma unroll
             for (int qt = 0; qt < QTB; ++qt) {
-                const int qrow = t0 + min(q_base + 16 * qt + c, nn - 1);
+                const int qi = max(min(q_base + 16 * qt + c, nq - 1), 0);
+                const int qloc = qsel ? (nq > 0 ? min(max(qsel[qs0 + qi], 0), max(nn - 1, 0)) : 0)
+                                      : qi;
+                const int qrow = t0 + qloc;
 #pragma unroll
                 for (int ch = 0; ch < 2; ++ch) {
                     const bf16 *src = qkv + (int64_t)qrow * ld + hh * ATT_D + ch * 32 + 8 * g;
@@ -679,8 +687,10 @@ attention_v3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
         __syncthreads();
         const int doc = p / n_heads, h = p % n_heads;
         const int tok0 = cu_seqlens[doc], n = cu_seqlens[doc + 1] - tok0;
+        const int qs0 = qsel ? cu_qsel[doc] : 0, nq = qsel ? cu_qsel[doc + 1] - qs0 : n;
+        const int out0 = qsel ? qs0 : tok0;  // ctx row of query 0
         int t_first, t_cnt;
-        tiles_of(n, t_first, t_cnt);
+        tiles_of(nq, t_first, t_cnt);
         if (p + (int)gridDim.x < n_pairs) {
             load_q(p + gridDim.x, qn);
             if (DB) stage(p + gridDim.x, b ^ 1);
@@ -780,8 +790,8 @@ attention_v3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
             for (int qt = 0; qt < QTB; ++qt) {
                 const float inv = 1.0f / l[qt][0];
                 const int q = q_base + 16 * qt + c;
-                if (qt < nqt && q < n) {
-                    bf16 *out = ctx + (int64_t)(tok0 + q) * H + h * ATT_D + 4 * g;
+                if (qt < nqt && q < nq) {
+                    bf16 *out = ctx + (int64_t)(out0 + q) * H + h * ATT_D + 4 * g;
 #pragma unroll
                     for (int dt = 0; dt < 4; ++dt) {
                         bf16x4 v;
@@ -814,7 +824,8 @@ attention_v3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
 bool attention_v3_ok(int max_len, int H) { return max_len <= 512 && H % ATT_D == 0; }
 
 void launch_attention_v3(const bf16 *qkv, const int32_t *cu_seqlens, int n_docs, int max_len,
-                         int H, bf16 *ctx, hipStream_t s) {
+                         int H, bf16 *ctx, hipStream_t s, const int32_t *qsel,
+                         const int32_t *cu_qsel) {
     DI_REQUIRE(attention_v3_ok(max_len, H), DI_EINVAL, "attention v3: max_len %d > 512", max_len);
     if (n_docs == 0 || max_len == 0) return;
     static int n_cu = [] {
@@ -829,12 +840,14 @@ void launch_attention_v3(const bf16 *qkv, const int32_t *cu_seqlens, int n_docs,
         DI_HIP(hipFuncSetAttribute((const void *)attention_v3_kernel<true>,
                                    hipFuncAttributeMaxDynamicSharedMemorySize, Att3<true>::LDS));
         hipLaunchKernelGGL(attention_v3_kernel<true>, dim3(grid), dim3(64 * ATT3_WAVES),
-                           Att3<true>::LDS, s, qkv, cu_seqlens, H, n_heads, n_pairs, ctx);
+                           Att3<true>::LDS, s, qkv, cu_seqlens, H, n_heads, n_pairs, ctx, qsel,
+                           cu_qsel);
     } else {
         DI_HIP(hipFuncSetAttribute((const void *)attention_v3_kernel<false>,
                                    hipFuncAttributeMaxDynamicSharedMemorySize, Att3<false>::LDS));
         hipLaunchKernelGGL(attention_v3_kernel<false>, dim3(grid), dim3(64 * ATT3_WAVES),
-                           Att3<false>::LDS, s, qkv, cu_seqlens, H, n_heads, n_pairs, ctx);
+                           Att3<false>::LDS, s, qkv, cu_seqlens, H, n_heads, n_pairs, ctx, qsel,
+                           cu_qsel);
     }
     check_launch("attention_v3");
 }

@@ -350,9 +350,38 @@ __global__ void gather_terms_kernel(const float *__restrict__ impact,
     if (tok < 0 || tok >= len) {
         atomicOr(err, 2);
     } else {
-        v = impact[cu_seq[d] + tok];
+        // pruned: the last layer computed only the terms' rows, row i = term i
+        v = impact[do_round & 2 ? i : cu_seq[d] + tok];
     }
-    out[i] = do_round ? round3(v) : v;
+    out[i] = (do_round & 1) ? round3(v) : v;
+}
+
+// The encoder's pruned last layer: the layer-input rows (and their LayerNorm row
+// parameters) of the terms' first tokens, packed in term order.  One workgroup per
+// document, one wave per row, 8-byte copies.
+__global__ void __launch_bounds__(256)
+gather_term_rows_kernel(const bf16 *__restrict__ X, const float2 *__restrict__ rl,
+                        const int32_t *__restrict__ cu_seq, const int32_t *__restrict__ cu_terms,
+                        const int32_t *__restrict__ term_tok, int H, bf16 *__restrict__ Xg,
+                        float2 *__restrict__ rlg) {
+    const int d = blockIdx.x, wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int t0 = cu_seq[d], n = cu_seq[d + 1] - t0;
+    for (int j = cu_terms[d] + wave; j < cu_terms[d + 1]; j += 4) {
+        const int row = t0 + min(max(term_tok[j], 0), max(n - 1, 0));  // (checked by the gather)
+        const uint2 *src = reinterpret_cast<const uint2 *>(X + (int64_t)row * H);
+        uint2 *dst = reinterpret_cast<uint2 *>(Xg + (int64_t)j * H);
+        for (int c = lane; c < H / 4; c += 64) dst[c] = src[c];
+        if (rl && lane == 0) rlg[j] = rl[row];
+    }
+}
+
+void launch_gather_term_rows(const bf16 *X, const float2 *rl, const int32_t *cu_seq,
+                             const int32_t *cu_terms, const int32_t *term_tok, int n_docs, int H,
+                             bf16 *Xg, float2 *rlg, hipStream_t s) {
+    if (n_docs == 0) return;
+    hipLaunchKernelGGL(gather_term_rows_kernel, dim3(n_docs), dim3(256), 0, s, X, rl, cu_seq,
+                       cu_terms, term_tok, H, Xg, rlg);
+    check_launch("gather_term_rows");
 }
 
 template <typename T>

@@ -46,7 +46,11 @@ void launch_row_ln(const float4 *st, int ld, int n_part, int M, int H, float eps
                    hipStream_t s);
 int gemm_stats_cols();
 void launch_attention_v3(const bf16 *qkv, const int32_t *cu_seqlens, int n_docs, int max_len,
-                         int H, bf16 *ctx, hipStream_t s);
+                         int H, bf16 *ctx, hipStream_t s, const int32_t *qsel = nullptr,
+                         const int32_t *cu_qsel = nullptr);
+void launch_gather_term_rows(const bf16 *X, const float2 *rl, const int32_t *cu_seq,
+                             const int32_t *cu_terms, const int32_t *term_tok, int n_docs, int H,
+                             bf16 *Xg, float2 *rlg, hipStream_t s);
 int vt_ld(int64_t M, int n_docs);
 void launch_gather_terms(const float *impact, const int32_t *cu_seq, const int32_t *cu_terms,
                          int n_docs, const int32_t *term_tok, int n_terms, int do_round,
@@ -396,8 +400,16 @@ void forward(di_encoder *e, const int32_t *d_ids, const int32_t *d_cu, int n_doc
 // activations.  Buffers: X holds the layer input (the normalised embeddings, then
 // the un-normalised FFN output P2 of the previous layer), X1 the attention-block
 // output P1; stats2 / stats1 their row-statistics partials.
+// Pruned last layer (d_tt != nullptr): the term gather reads only the rows of the
+// terms' first tokens, and every operation after the last layer's QKV projection is
+// row-independent (attention per query row, the GEMMs and the LayerNorms per row), so
+// that layer computes the attention for those query rows only (keys: every token) and
+// the O / FFN GEMMs, row statistics and head on the packed term rows -- the same
+// arithmetic per kept row (bit-identical impacts), ~4/5 fewer rows at the bench shape.
 void forward_folded(di_encoder *e, const int32_t *d_ids, const int32_t *d_cu, int n_docs,
-                    int64_t M, int max_len, bool timing, hipStream_t s) {
+                    int64_t M, int max_len, bool timing, hipStream_t s,
+                    const int32_t *d_tt = nullptr, const int32_t *d_ct = nullptr,
+                    int64_t n_terms = 0) {
     const auto &c = e->cfg;
     const int H = c.hidden, F = c.intermediate;
     const int pos_offset = (c.variant == DI_VARIANT_XLMR) ? c.pad_id + 1 : 0;
@@ -460,23 +472,40 @@ void forward_folded(di_encoder *e, const int32_t *d_ids, const int32_t *d_cu, in
             TimedLaunch tl(e->timer, timing, "gemm_qkv", s);
             launch_gemm<bf16>(P ? EPI_FOLD : EPI_BIAS, g, s);
         }
+        const bool prune = last && d_tt != nullptr;
+        const int64_t Mr = prune ? n_terms : M;  // rows from here on
+        bf16 *Xr = X;                             // the O GEMM's residual rows
+        const float2 *rl2r = rl2;
         {
             TimedLaunch tl(e->timer, timing, "attention", s);
-            launch_attention_v3(e->qk.as<bf16>(), d_cu, n_docs, max_len, H, e->ctx.as<bf16>(), s);
+            launch_attention_v3(e->qk.as<bf16>(), d_cu, n_docs, max_len, H, e->ctx.as<bf16>(), s,
+                                prune ? d_tt : nullptr, prune ? d_ct : nullptr);
         }
+        if (prune) {  // the terms' residual rows (and LN2 parameters), packed: Hff / rl1
+            TimedLaunch tl(e->timer, timing, "gather_rows", s);  // are free until later
+            Xr = e->Hff.as<bf16>();
+            launch_gather_term_rows(X, P ? rl2 : nullptr, d_cu, d_ct, d_tt, n_docs, H, Xr,
+                                    rl1, s);
+            rl2r = rl1;
+        }
+        auto base_r = [&]() {
+            GemmArgs gr = base();
+            gr.M = (int)Mr;
+            return gr;
+        };
         // O: P1 = ctx W_o^T + b_o + LN2(l-1)(X)  (plain X on layer 0) -> X1, stats1
-        g = base();
+        g = base_r();
         g.A = e->ctx.p;
         g.B = L.w_o.p;
         g.bias = L.b_o.as<float>();
-        g.resid = X;
+        g.resid = Xr;
         g.out = X1;
         g.N = H;
         g.K = H;
         g.ld_out = H;
         g.stats_out = st1;
         if (P) {
-            g.row_ln = rl2;
+            g.row_ln = rl2r;
             g.res_gamma = P->ln2_g.as<float>();
             g.res_beta = P->ln2_b.as<float>();
         }
@@ -486,10 +515,10 @@ void forward_folded(di_encoder *e, const int32_t *d_ids, const int32_t *d_cu, in
         }
         {
             TimedLaunch tl(e->timer, timing, "row_ln", s);
-            launch_row_ln(st1, ld, n_part, (int)M, H, c.layer_norm_eps, rl1, s);
+            launch_row_ln(st1, ld, n_part, (int)Mr, H, c.layer_norm_eps, rl1, s);
         }
         // FFN1 on LN1(P1), folded
-        g = base();
+        g = base_r();
         g.A = X1;
         g.B = L.w_i.p;
         g.out = e->Hff.p;
@@ -504,7 +533,7 @@ void forward_folded(di_encoder *e, const int32_t *d_ids, const int32_t *d_cu, in
             launch_gemm<bf16>(EPI_FOLD_GELU, g, s);
         }
         // FFN2: P2 = Hff W_out^T + b_out + LN1(P1) -> X, stats2 (+ head dot, last layer)
-        g = base();
+        g = base_r();
         g.A = e->Hff.p;
         g.B = L.w_out.p;
         g.bias = L.b_out.as<float>();
@@ -530,7 +559,8 @@ void forward_folded(di_encoder *e, const int32_t *d_ids, const int32_t *d_cu, in
     }
     {
         TimedLaunch tl(e->timer, timing, "head", s);
-        launch_head_from_stats(st2, ld, n_part, (int)M, H, c.layer_norm_eps, e->head_sw,
+        launch_head_from_stats(st2, ld, n_part, (int)(d_tt ? n_terms : M), H, c.layer_norm_eps,
+                               e->head_sw,
                                e->head_cw, c.activation, e->impact.as<float>(), s);
     }
 }
@@ -720,10 +750,23 @@ int di_encode(di_encoder *e, const int32_t *tok_ids, const int32_t *cu_seqlens, 
         const int32_t *d_cu =
             (const int32_t *)stage_in(cu_seqlens, (size_t)(n_docs + 1) * 4, dev, e->cu, s);
         DI_HIP(hipMemsetAsync(e->err.p, 0, 4, s));
+        const int32_t *d_tt = nullptr, *d_cut = nullptr;
+        if (!token_out) {
+            d_tt = (const int32_t *)stage_in(term_tok, (size_t)n_terms * 4, dev, e->tt, s);
+            d_cut = (const int32_t *)stage_in(cu_terms, (size_t)(n_docs + 1) * 4, dev, e->cut, s);
+        }
+        // pruned last layer (bf16 folded path, term output; DI_PRUNE_LAST=0: off)
+        static const bool prune_env = [] {
+            const char *v = std::getenv("DI_PRUNE_LAST");
+            return !(v && v[0] == '0');
+        }();
+        const bool prune = prune_env && !token_out && e->esz == 2 && e->folded &&
+                           n_terms <= n_tokens;  // (packed term rows fit the row buffers)
         if (n_tokens > 0) {
             if (e->esz == 2)
                 if (e->folded)
-                    forward_folded(e, d_ids, d_cu, n_docs, n_tokens, max_len, timing, s);
+                    forward_folded(e, d_ids, d_cu, n_docs, n_tokens, max_len, timing, s,
+                                   prune ? d_tt : nullptr, prune ? d_cut : nullptr, n_terms);
                 else
                     forward<bf16>(e, d_ids, d_cu, n_docs, n_tokens, max_len, timing, s);
             else
@@ -739,10 +782,6 @@ int di_encode(di_encoder *e, const int32_t *tok_ids, const int32_t *cu_seqlens, 
                 DI_HIP(hipMemcpyAsync(out, e->impact.p, (size_t)n_tokens * 4,
                                       hipMemcpyDeviceToHost, s));
         } else {
-            const int32_t *d_tt =
-                (const int32_t *)stage_in(term_tok, (size_t)n_terms * 4, dev, e->tt, s);
-            const int32_t *d_cut =
-                (const int32_t *)stage_in(cu_terms, (size_t)(n_docs + 1) * 4, dev, e->cut, s);
             if (!dev) {
                 tmp.reserve((size_t)std::max<int64_t>(n_terms, 1) * 4);
                 d_out = tmp.as<float>();
@@ -750,8 +789,9 @@ int di_encode(di_encoder *e, const int32_t *tok_ids, const int32_t *cu_seqlens, 
             {
                 TimedLaunch tl(e->timer, timing, "gather_terms", s);
                 launch_gather_terms(e->impact.as<float>(), d_cu, d_cut, n_docs, d_tt,
-                                    (int)n_terms, (flags & DI_F_ROUND3) ? 1 : 0, d_out,
-                                    e->err.as<int32_t>(), s);
+                                    (int)n_terms,
+                                    ((flags & DI_F_ROUND3) ? 1 : 0) | (prune && n_tokens > 0 ? 2 : 0),
+                                    d_out, e->err.as<int32_t>(), s);
             }
             if (!dev && n_terms)
                 DI_HIP(hipMemcpyAsync(out, d_out, (size_t)n_terms * 4, hipMemcpyDeviceToHost,

@@ -157,6 +157,37 @@ def test_bf16_close_to_fp32_reference_base_shape(E):
     assert float(np.median(err / np.maximum(np.abs(w), 1e-3))) < 1e-2
 
 
+def test_bf16_pruned_last_layer_is_bitexact(E):
+    """Term output (di_encode with term arrays) computes the last layer only for the
+    terms' first-token rows; every row's arithmetic is unchanged, so its impacts must
+    equal the full per-token forward gathered at those rows, bit for bit -- with
+    ragged documents, a document without terms, terms in any order and repeated."""
+    fx, sd = _fixture("xlmr_base")
+    enc = E.DeviceEncoder(sd, _cfg(E, fx, "xlmr", "softplus"), precision="bf16")
+    rng = np.random.default_rng(11)
+    lens = np.array([300, 250, 2, 64, 9, 180, 120, 33])
+    pad, mask = _random_batch(rng, len(lens), 300, 250002, lens)
+    ids, cu = _pack(pad.tolist(), mask.tolist())
+    tok = enc.encode_packed(ids, cu, token_impacts=True)
+    tt, ct = [], [0]
+    for d, n in enumerate(lens):
+        k = 0 if d == 2 else int(rng.integers(1, n + 1))
+        pos = rng.choice(n, size=k, replace=False)
+        if d == 3:
+            pos = np.concatenate([pos, pos[:2]])  # repeated token positions
+        tt += pos.tolist()
+        ct.append(len(tt))
+    tt, ct = np.array(tt, np.int32), np.array(ct, np.int32)
+    want = np.array([tok[cu[d] + tt[j]] for d in range(len(lens)) for j in range(ct[d], ct[d + 1])],
+                    np.float32)
+    got = enc.encode_packed(ids, cu, tt, ct)
+    np.testing.assert_array_equal(got, want)
+    from improving_learned_index_amd import synthetic
+
+    np.testing.assert_array_equal(enc.encode_packed(ids, cu, tt, ct, round3=True),
+                                  synthetic.round3_f32(want))
+
+
 def test_encoder_rejects_bad_input(E):
     from improving_learned_index_amd import _lib
 

@@ -20,7 +20,8 @@ void launch_attention(const T *qk, const T *vt, const int32_t *cu_seqlens, int n
                       int max_len, int H, int ld_v, T *ctx, hipStream_t s);
 void launch_vt_cols(const int32_t *cu, int n_docs, int M, int32_t *vcol, hipStream_t s);
 void launch_attention_v3(const bf16 *qkv, const int32_t *cu_seqlens, int n_docs, int max_len,
-                         int H, bf16 *ctx, hipStream_t s);
+                         int H, bf16 *ctx, hipStream_t s, const int32_t *qsel = nullptr,
+                         const int32_t *cu_qsel = nullptr);
 int vt_ld(int64_t M, int n_docs);
 }  // namespace di
 using namespace di;
