@@ -61,7 +61,7 @@ constexpr int HIST_BINS = 4096;
 constexpr int TIE_CAP = HIST_BINS;
 
 struct ScoreShared {
-    uint32_t acc[MAX_BLOCK_DOCS + 4];  // 128 KiB (+ the scatter's dummy word)
+    uint32_t acc[MAX_BLOCK_DOCS + 64];  // 128 KiB (+ the scatter's dummy words)
     union {
         RadixScratch<SC_WAVES> rs;  // general radix path
         uint32_t hist[HIST_BINS + 64];  // fast path: score histogram (+ spare bins), then the tie list
@@ -243,6 +243,32 @@ __device__ __forceinline__ void scatter_apply(uint32_t *acc, const uint32_t (&cu
     }
 }
 
+// scatter_apply restricted to the docs [dlo, dhi) of one wave (a short term, whose
+// sublist every wave reads in full): the other postings (and the padding) update a
+// per-lane dummy word past the block instead.
+template <int UU>
+__device__ __forceinline__ void scatter_apply_own(const uint32_t (&cur)[UU], uint32_t first_bits,
+                                                  uint32_t dlo, uint32_t dn, uint32_t dummy) {
+    uint32_t w[UU], a[UU];
+#pragma unroll
+    for (int u = 0; u < UU; ++u) {
+        const uint32_t d = (cur[u] ^ POST_X) >> 8;
+        a[u] = (d - dlo < dn) ? d << 2 : dummy;
+        asm volatile("ds_read_b32 %0, %1" : "=v"(w[u]) : "v"(a[u]) : "memory");
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int u = 0; u < UU; ++u) asm volatile("" : "+v"(w[u]));
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int u = 0; u < UU; ++u) {
+        const uint32_t v = cur[u] & 255u;
+        const uint32_t t = __umul24(v, 0x10000u) + w[u];
+        const uint32_t f = __umul24(v, 0x10001u) + first_bits;
+        asm volatile("ds_write_b32 %0, %1" ::"v"(a[u]), "v"(w[u] ? t : f) : "memory");
+    }
+}
+
 // Profiling (DI_PROFILE_ABLATE bit 64): per-phase shader cycles of workgroup 0's items
 // accumulated here and printed by di_index_search.
 __device__ unsigned long long g_sb_phase[8];
@@ -367,6 +393,13 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int item,
     uint32_t pre[4];
     bool have_pre = false;
     auto is_long = [&](int j) { return wl && ((sh.lmask[j >> 5] >> (j & 31)) & 1u); };
+    // with the per-wave layout, short terms too are scattered by each wave over its own
+    // docs (ablate bit 256: the barrier form for them): then no term needs a barrier
+    const bool own_short = wl && !(ablate & 256);
+    const uint32_t wseg = ((uint32_t)block_docs + WSEG - 1) / WSEG;
+    const uint32_t wdlo = (uint32_t)wave * wseg;
+    const uint32_t wdn = wave == WSEG - 1 ? 0x7FFFFFFFu - wdlo : wseg;  // last: the rest
+    const uint32_t wdummy = (uint32_t)(MAX_BLOCK_DOCS + lane) << 2;
     for (int j = (ablate & 1) ? nt : 0; j < nt; ++j) {  // ablate bit 0: skip (profiling)
         const uint32_t first_bits = (uint32_t)(255 - j) << 8;
         const bool lj = is_long(j);
@@ -398,8 +431,37 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int item,
                     pos = end;
                 }
             }
-            if (j + 1 < nt && !is_long(j + 1))
+            if (!own_short && j + 1 < nt && !is_long(j + 1))
                 asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+            continue;
+        }
+        if (own_short) {
+            // a short term (< WLONG_MIN postings in the block): every wave reads the whole
+            // sublist and applies the postings of its own doc segment -- no barrier
+            for (int64_t pos = lo[j], end = hi[j]; pos < end;) {
+                const int64_t rem = end - pos;
+                if (rem > 8 * 64) {
+                    uint32_t r[16];
+                    scatter_load<16, 64>(post + pos, rem, lane, r);
+                    scatter_apply_own<16>(r, first_bits, wdlo, wdn, wdummy);
+                    pos += 16 * 64;
+                } else if (rem > 4 * 64) {
+                    uint32_t r[8];
+                    scatter_load<8, 64>(post + pos, rem, lane, r);
+                    scatter_apply_own<8>(r, first_bits, wdlo, wdn, wdummy);
+                    pos = end;
+                } else if (rem > 64) {
+                    uint32_t r[4];
+                    scatter_load<4, 64>(post + pos, rem, lane, r);
+                    scatter_apply_own<4>(r, first_bits, wdlo, wdn, wdummy);
+                    pos = end;
+                } else {
+                    uint32_t r[1];
+                    scatter_load<1, 64>(post + pos, rem, lane, r);
+                    scatter_apply_own<1>(r, first_bits, wdlo, wdn, wdummy);
+                    pos = end;
+                }
+            }
             continue;
         }
         int64_t pos = lo[j];
@@ -1293,6 +1355,8 @@ int di_index_create(const int64_t *term_off, int64_t n_terms, const uint32_t *pd
         if (const char *ab = std::getenv("DI_PROFILE_ABLATE")) ix->ablate = std::atoi(ab);
         if (const char *sw = std::getenv("DI_SCATTER_WAVE"))  // A/B: 0 = all-wave scatter only
             if (sw[0] == '0') ix->ablate |= 128;
+        if (const char *ss = std::getenv("DI_SCATTER_SHORT"))  // A/B: 0 = barrier form for
+            if (ss[0] == '0') ix->ablate |= 256;                  // the short terms
         build_index(ix.get(), term_off, n_terms, pdoc, pval, doc_lo, doc_hi);
         *out = ix.release();
     });
