@@ -274,6 +274,47 @@ __device__ __forceinline__ void softmax_step(f32x4 (&s)[2], float &m, float &msc
     }
 }
 
+// softmax_step split in its three parts (same arithmetic), so that the merged key
+// loop of attention_v3_kernel<., true> can test every query tile of a step with one
+// branch and keep the common path of both tiles in one basic block.
+__device__ __forceinline__ bool softmax_need(const f32x4 (&s)[2], float m) {
+    constexpr float sc = 0.125f * 1.4426950408889634f;
+    const float lim = m + 8.0f / sc;
+    bool need = false;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) need |= s[t][r] > lim;
+    return need;
+}
+__device__ __forceinline__ void softmax_rescale(const f32x4 (&s)[2], float &m, float &msc,
+                                                f32x4 (&o)[4], f32x4 &l) {
+    constexpr float sc = 0.125f * 1.4426950408889634f;
+    float cmax = fmaxf(fmaxf(fmaxf(s[0][0], s[0][1]), fmaxf(s[0][2], s[0][3])),
+                       fmaxf(fmaxf(s[1][0], s[1][1]), fmaxf(s[1][2], s[1][3])));
+    const auto p16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(cmax),
+                                                      __float_as_uint(cmax), false, false);
+    cmax = fmaxf(__uint_as_float(p16[0]), __uint_as_float(p16[1]));
+    const auto p32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(cmax),
+                                                      __float_as_uint(cmax), false, false);
+    cmax = fmaxf(__uint_as_float(p32[0]), __uint_as_float(p32[1]));
+    const float m_new = fmaxf(m, cmax);
+    const float alpha = exp2f((m - m_new) * sc);  // 0 on the first chunk
+    m = m_new;
+    msc = m_new * sc;
+    l *= alpha;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) o[dt] *= alpha;
+}
+__device__ __forceinline__ void softmax_p(const f32x4 (&s)[2], float msc, bf16x8 &pb) {
+    constexpr float sc = 0.125f * 1.4426950408889634f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        pb[r] = (bf16)__builtin_amdgcn_exp2f(fmaf(s[0][r], sc, -msc));
+        pb[4 + r] = (bf16)__builtin_amdgcn_exp2f(fmaf(s[1][r], sc, -msc));
+    }
+}
+
 // bf16 fast path.  Same swapped-product structure as attention_kernel, with the
 // softmax VALU work cut down (the f32/bf16 kernel above is VALU-issue-bound):
 //  * exp argument is one FMA on the raw score: p = exp2(s * c - m * c);
@@ -588,7 +629,12 @@ __device__ __forceinline__ uint2 ds_read_tr_b16(uint32_t addr) {
     return r;
 }
 
-template <bool DB>
+// MERGED = true (default): the key loop is instantiated per tile count (1 or 2) and
+// runs both tiles' S^T products, one shared rescale test (a branch only into the
+// rare path) and both tiles' exp / O^T products as one basic block, so that one
+// tile's softmax VALU overlaps the other tile's MFMAs; same arithmetic as the
+// per-tile loop (MERGED = false, DI_ATTN_V3_MERGED=0), bit-identical outputs.
+template <bool DB, bool MERGED>
 __global__ void __launch_bounds__(64 * ATT3_WAVES, 1)
 attention_v3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu_seqlens, int H,
                     int n_heads, int n_pairs, bf16 *__restrict__ ctx,
@@ -698,6 +744,144 @@ attention_v3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
 
         const uint32_t kim = lds_base + b * Att3<DB>::BUF;
         const uint32_t vim = kim + Att3<DB>::ROWS * 128;
+        // K fragments (2 S^T tiles x 2 head-dim chunks) and V^T fragments of the
+        // 32-key chunk at key0, read from the LDS images (asm: see below)
+        // The 12 reads and their lgkmcnt(0) are ONE asm statement: its outputs exist
+        // only after the wait, so no copy of a register still being loaded can be
+        // scheduled above it (separate asm reads plus "+v" redefinitions after the
+        // wait do not guarantee that: the compiler may copy a tied input early).
+        auto read_kv = [&](int key0, uint4 (&kf)[2][2], bf16x8 (&vf)[4]) {
+            uint32_t ka[2][2], va[4][2];
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+                const int r = min(key0 + krel + 4 * t, n - 1);
+#pragma unroll
+                for (int ch = 0; ch < 2; ++ch) ka[t][ch] = kim + r * 128 + (((ch * 4 + g) ^ (r & 7)) << 4);
+            }
+#pragma unroll
+            for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+                for (int h2 = 0; h2 < 2; ++h2) {
+                    const int r = key0 + 8 * g + 4 * h2 + tq;
+                    const int chv = 2 * dt + (tp >> 1);
+                    va[dt][h2] = vim + r * 128 + ((chv ^ (r & 7)) << 4) + 8 * (tp & 1);
+                }
+            uint2 hv[4][2];
+            asm volatile(
+                "ds_read_b128 %0, %12\n\t"
+                "ds_read_b128 %1, %13\n\t"
+                "ds_read_b128 %2, %14\n\t"
+                "ds_read_b128 %3, %15\n\t"
+                "ds_read_b64_tr_b16 %4, %16\n\t"
+                "ds_read_b64_tr_b16 %5, %17\n\t"
+                "ds_read_b64_tr_b16 %6, %18\n\t"
+                "ds_read_b64_tr_b16 %7, %19\n\t"
+                "ds_read_b64_tr_b16 %8, %20\n\t"
+                "ds_read_b64_tr_b16 %9, %21\n\t"
+                "ds_read_b64_tr_b16 %10, %22\n\t"
+                "ds_read_b64_tr_b16 %11, %23\n\t"
+                "s_waitcnt lgkmcnt(0)"
+                : "=&v"(kf[0][0]), "=&v"(kf[0][1]), "=&v"(kf[1][0]), "=&v"(kf[1][1]),
+                  "=&v"(hv[0][0]), "=&v"(hv[0][1]), "=&v"(hv[1][0]), "=&v"(hv[1][1]),
+                  "=&v"(hv[2][0]), "=&v"(hv[2][1]), "=&v"(hv[3][0]), "=&v"(hv[3][1])
+                : "v"(ka[0][0]), "v"(ka[0][1]), "v"(ka[1][0]), "v"(ka[1][1]), "v"(va[0][0]),
+                  "v"(va[0][1]), "v"(va[1][0]), "v"(va[1][1]), "v"(va[2][0]), "v"(va[2][1]),
+                  "v"(va[3][0]), "v"(va[3][1])
+                : "memory");
+            __builtin_amdgcn_sched_barrier(0);  // no MFMA above the wait (rule 18)
+#pragma unroll
+            for (int dt = 0; dt < 4; ++dt) {
+                const uint4 v4 = make_uint4(hv[dt][0].x, hv[dt][0].y, hv[dt][1].x, hv[dt][1].y);
+                __builtin_memcpy(&vf[dt], &v4, 16);
+            }
+        };
+        // merged key loop over NQ (1 or 2) query tiles starting at q_base
+        auto key_loop = [&](auto nq_c, const uint4 (&qf)[QTB][2], int q_base) {
+            constexpr int NQ = decltype(nq_c)::value;
+            float m[NQ], msc[NQ];
+            f32x4 o[NQ][4], l[NQ];
+#pragma unroll
+            for (int qt = 0; qt < NQ; ++qt) {
+                m[qt] = -INFINITY;
+                msc[qt] = -INFINITY;
+                l[qt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int dt = 0; dt < 4; ++dt) o[qt][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+            }
+            for (int key0 = 0; key0 < n; key0 += 32) {
+                uint4 kf[2][2];
+                bf16x8 vf[4];
+                read_kv(key0, kf, vf);
+                f32x4 s[NQ][2];
+#pragma unroll
+                for (int qt = 0; qt < NQ; ++qt)
+#pragma unroll
+                    for (int t = 0; t < 2; ++t) s[qt][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int ch = 0; ch < 2; ++ch)  // independent chains adjacent
+#pragma unroll
+                    for (int qt = 0; qt < NQ; ++qt)
+#pragma unroll
+                        for (int t = 0; t < 2; ++t) mma_chunk(kf[t][ch], qf[qt][ch], s[qt][t], bf16{});
+                if (key0 + 32 > n) {
+#pragma unroll
+                    for (int qt = 0; qt < NQ; ++qt)
+#pragma unroll
+                        for (int t = 0; t < 2; ++t)
+#pragma unroll
+                            for (int r = 0; r < 4; ++r)
+                                if (key0 + 8 * g + 4 * t + r >= n) s[qt][t][r] = -INFINITY;
+                }
+                bool need[NQ], need_any = false;
+#pragma unroll
+                for (int qt = 0; qt < NQ; ++qt) {
+                    need[qt] = softmax_need(s[qt], m[qt]);
+                    need_any |= need[qt];
+                }
+                if (__any(need_any)) {  // rare after the first chunk
+#pragma unroll
+                    for (int qt = 0; qt < NQ; ++qt)
+                        if (__any(need[qt])) softmax_rescale(s[qt], m[qt], msc[qt], o[qt], l[qt]);
+                }
+                bf16x8 pb[NQ];
+#pragma unroll
+                for (int qt = 0; qt < NQ; ++qt) softmax_p(s[qt], msc[qt], pb[qt]);
+#pragma unroll
+                for (int qt = 0; qt < NQ; ++qt) {
+#pragma unroll
+                    for (int dt = 0; dt < 4; ++dt)
+                        o[qt][dt] =
+                            __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf[dt], pb[qt], o[qt][dt], 0, 0, 0);
+                    l[qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pb[qt], l[qt], 0, 0, 0);
+                }
+            }
+#pragma unroll
+            for (int qt = 0; qt < NQ; ++qt) {
+                const float inv = 1.0f / l[qt][0];
+                const int q = q_base + 16 * qt + c;
+                if (q < nq) {
+                    bf16 *out = ctx + (int64_t)(out0 + q) * H + h * ATT_D + 4 * g;
+#pragma unroll
+                    for (int dt = 0; dt < 4; ++dt) {
+                        bf16x4 v;
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) v[r] = (bf16)(o[qt][dt][r] * inv);
+                        *reinterpret_cast<bf16x4 *>(out + dt * 16) = v;
+                    }
+                }
+            }
+        };
+        if constexpr (MERGED) {
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                if (2 * i >= t_cnt) continue;
+                const int q_base = (t_first + 2 * i) * 16;
+                if (t_cnt - 2 * i >= 2)
+                    key_loop(std::integral_constant<int, 2>{}, qc[i], q_base);
+                else
+                    key_loop(std::integral_constant<int, 1>{}, qc[i], q_base);
+            }
+        } else {
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
             if (2 * i >= t_cnt) continue;  // (not break: keeps the loop unrolled, qf[i] static)
@@ -714,50 +898,9 @@ attention_v3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
                 for (int dt = 0; dt < 4; ++dt) o[qt][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
             }
             for (int key0 = 0; key0 < n; key0 += 32) {
-                // inline-asm LDS reads: the compiler cannot see them, so it does not
-                // drain the in-flight LDS-DMA prefetch (vmcnt(0)) in front of them
                 uint4 kf[2][2];
-#pragma unroll
-                for (int t = 0; t < 2; ++t) {
-                    const int r = min(key0 + krel + 4 * t, n - 1);
-#pragma unroll
-                    for (int ch = 0; ch < 2; ++ch)
-                        asm volatile("ds_read_b128 %0, %1"
-                                     : "=v"(kf[t][ch])
-                                     : "v"(kim + r * 128 + (((ch * 4 + g) ^ (r & 7)) << 4)));
-                }
-                // V^T fragments: d-tile dt, halves h2 = keys 8g + 4h2 + (0..3)
-                uint2 hv[4][2];
-#pragma unroll
-                for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-                    for (int h2 = 0; h2 < 2; ++h2) {
-                        const int r = key0 + 8 * g + 4 * h2 + tq;
-                        const int chv = 2 * dt + (tp >> 1);
-                        hv[dt][h2] = ds_read_tr_b16(vim + r * 128 + ((chv ^ (r & 7)) << 4) +
-                                                    8 * (tp & 1));
-                    }
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                // the asm reads' results exist only from here: redefine them after the
-                // wait (no use or copy hoisted above it), then fence the scheduler
-#pragma unroll
-                for (int t = 0; t < 2; ++t)
-#pragma unroll
-                    for (int ch = 0; ch < 2; ++ch)
-                        asm volatile("" : "+v"(kf[t][ch].x), "+v"(kf[t][ch].y), "+v"(kf[t][ch].z),
-                                     "+v"(kf[t][ch].w));
-#pragma unroll
-                for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-                    for (int h2 = 0; h2 < 2; ++h2)
-                        asm volatile("" : "+v"(hv[dt][h2].x), "+v"(hv[dt][h2].y));
-                __builtin_amdgcn_sched_barrier(0);  // no MFMA above the wait (rule 18)
                 bf16x8 vf[4];
-#pragma unroll
-                for (int dt = 0; dt < 4; ++dt) {
-                    const uint4 v4 = make_uint4(hv[dt][0].x, hv[dt][0].y, hv[dt][1].x, hv[dt][1].y);
-                    __builtin_memcpy(&vf[dt], &v4, 16);
-                }
+                read_kv(key0, kf, vf);
                 const bool tail = key0 + 32 > n;
 #pragma unroll
                 for (int qt = 0; qt < QTB; ++qt) {
@@ -802,6 +945,7 @@ attention_v3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
                 }
             }
         }
+        }  // !MERGED
         __syncthreads();  // every wave is done with buffer b before it is restaged
     };
     uint4 qa[2][QTB][2], qb2[2][QTB][2];
@@ -836,18 +980,27 @@ void launch_attention_v3(const bf16 *qkv, const int32_t *cu_seqlens, int n_docs,
     }();
     const int n_heads = H / ATT_D, n_pairs = n_docs * n_heads;
     const int grid = std::min(n_pairs, n_cu);
+    // A/B knob: DI_ATTN_V3_MERGED=0 runs the per-tile key loop (bit-identical)
+    static const bool merged = [] {
+        const char *e = std::getenv("DI_ATTN_V3_MERGED");
+        return !(e && std::atoi(e) == 0);
+    }();
+    auto launch = [&](auto kern, int lds_bytes) {
+        DI_HIP(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   lds_bytes));
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * ATT3_WAVES), lds_bytes, s, qkv, cu_seqlens,
+                           H, n_heads, n_pairs, ctx, qsel, cu_qsel);
+    };
     if (max_len <= Att3<true>::ROWS) {
-        DI_HIP(hipFuncSetAttribute((const void *)attention_v3_kernel<true>,
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, Att3<true>::LDS));
-        hipLaunchKernelGGL(attention_v3_kernel<true>, dim3(grid), dim3(64 * ATT3_WAVES),
-                           Att3<true>::LDS, s, qkv, cu_seqlens, H, n_heads, n_pairs, ctx, qsel,
-                           cu_qsel);
+        if (merged)
+            launch(attention_v3_kernel<true, true>, Att3<true>::LDS);
+        else
+            launch(attention_v3_kernel<true, false>, Att3<true>::LDS);
     } else {
-        DI_HIP(hipFuncSetAttribute((const void *)attention_v3_kernel<false>,
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, Att3<false>::LDS));
-        hipLaunchKernelGGL(attention_v3_kernel<false>, dim3(grid), dim3(64 * ATT3_WAVES),
-                           Att3<false>::LDS, s, qkv, cu_seqlens, H, n_heads, n_pairs, ctx, qsel,
-                           cu_qsel);
+        if (merged)
+            launch(attention_v3_kernel<false, true>, Att3<false>::LDS);
+        else
+            launch(attention_v3_kernel<false, false>, Att3<false>::LDS);
     }
     check_launch("attention_v3");
 }
