@@ -1,0 +1,80 @@
+"""Static check of the hand-scheduled LDS reads (developer tool + CPU test).
+
+Several kernels read LDS fragments with inline-asm ds_read instructions (so that
+the compiler does not drain an in-flight LDS-DMA prefetch with vmcnt(0)) and wait
+for them with an explicit s_waitcnt lgkmcnt.  The compiler sees an asm output as
+defined when the asm statement ends, so it may legally schedule a copy or a use of
+such a register ABOVE the wait -- reading a register the LDS is still writing.
+This scans the gfx950 assembly of a source file and reports every instruction
+that touches a destination register of an inline-asm ds_read before the next
+lgkmcnt wait.
+
+    python tools/asm_wait_scan.py improving-learned-index_amd/csrc/enc_attn.hip
+"""
+import re
+import subprocess
+import sys
+import tempfile
+from pathlib import Path
+
+HIPCC = "/opt/rocm/bin/hipcc"
+
+
+def _regs(s):
+    out = set()
+    for m in re.finditer(r"v\[(\d+):(\d+)\]", s):
+        out |= set(range(int(m.group(1)), int(m.group(2)) + 1))
+    for m in re.finditer(r"\bv(\d+)\b", s):
+        out.add(int(m.group(1)))
+    return out
+
+
+def scan_asm(text):
+    """[(function, instruction)] touching a pending asm ds_read destination."""
+    hits, fn, pending, in_asm = [], None, set(), False
+    for ln in text.split("\n"):
+        if re.match(r"^_Z\S+:", ln):
+            fn, pending = ln.split(":")[0], set()
+        t = ln.strip()
+        if t.startswith(";;#ASMSTART"):
+            in_asm = True
+            continue
+        if t.startswith(";;#ASMEND"):
+            in_asm = False
+            continue
+        if in_asm and t.startswith("ds_read"):
+            pending |= _regs(t.split()[1].rstrip(","))
+        elif "s_waitcnt" in t and "lgkmcnt" in t:
+            pending = set()
+        elif pending and not in_asm and re.match(r"(v_|global_|buffer_|ds_|flat_)", t):
+            ops = t.split(None, 1)[1].split(",") if " " in t else []
+            touched = set()
+            for o in ops:
+                touched |= _regs(o)
+            if touched & pending:
+                hits.append((fn, t))
+    return hits
+
+
+def compile_asm(src, arch="gfx950"):
+    with tempfile.TemporaryDirectory() as d:
+        out = Path(d) / "k.s"
+        subprocess.run([HIPCC, f"--offload-arch={arch}", "-O3", "-std=c++17", "--cuda-device-only",
+                        "-I", str(Path(src).resolve().parent), "-S", "-o", str(out), str(src)],
+                       check=True, capture_output=True)
+        return out.read_text()
+
+
+def main(argv):
+    bad = 0
+    for src in argv:
+        hits = scan_asm(compile_asm(src))
+        print(f"{src}: {len(hits)} early touch(es) of pending asm LDS reads")
+        for fn, ins in hits[:10]:
+            print("   ", fn[:70], "|", ins)
+        bad += len(hits)
+    return 1 if bad else 0
+
+
+if __name__ == "__main__":
+    sys.exit(main(sys.argv[1:]))
