@@ -693,7 +693,8 @@ attention_v3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
         t_cnt = base + (wave < extra ? 1 : 0);
         t_first = wave * base + min(wave, extra);
     };
-    auto load_q = [&](int pp, uint4 (&qd)[2][QTB][2]) {
+    // Q row addresses of pair pp for this wave's tiles: [i][qt][ch]
+    auto q_srcs = [&](int pp, const bf16 *(&src)[2][QTB][2]) {
         const int dd = pp / n_heads, hh = pp % n_heads;
         const int t0 = cu_seqlens[dd], nn = cu_seqlens[dd + 1] - t0;
         const int qs0 = qsel ? cu_qsel[dd] : 0, nq = qsel ? cu_qsel[dd + 1] - qs0 : nn;
@@ -709,18 +710,53 @@ attention_v3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
                                       : qi;
                 const int qrow = t0 + qloc;
 #pragma unroll
-                for (int ch = 0; ch < 2; ++ch) {
-                    const bf16 *src = qkv + (int64_t)qrow * ld + hh * ATT_D + ch * 32 + 8 * g;
-                    asm volatile("global_load_dwordx4 %0, %1, off"
-                                 : "=v"(qd[i][qt][ch])
-                                 : "v"(src)
-                                 : "memory");
-                }
+                for (int ch = 0; ch < 2; ++ch)
+                    src[i][qt][ch] = qkv + (int64_t)qrow * ld + hh * ATT_D + ch * 32 + 8 * g;
             }
         }
     };
+    auto load_q = [&](int pp, uint4 (&qd)[2][QTB][2]) {  // DB: one pair ahead
+        const bf16 *src[2][QTB][2];
+        q_srcs(pp, src);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int qt = 0; qt < QTB; ++qt)
+#pragma unroll
+                for (int ch = 0; ch < 2; ++ch)
+                    asm volatile("global_load_dwordx4 %0, %1, off"
+                                 : "=v"(qd[i][qt][ch])
+                                 : "v"(src[i][qt][ch])
+                                 : "memory");
+    };
+    // !DB: this pair's Q, loaded together with the wait for them and the K / V
+    // staging (one asm statement: the outputs exist only after the wait, so no copy
+    // of a register still being loaded can be scheduled above it)
+    auto load_q_wait = [&](int pp, uint4 (&qd)[2][QTB][2]) {
+        static_assert(QTB == 2, "load_q_wait: 8 loads");
+        const bf16 *src[2][QTB][2];
+        q_srcs(pp, src);
+        asm volatile(
+            "global_load_dwordx4 %0, %8, off\n\t"
+            "global_load_dwordx4 %1, %9, off\n\t"
+            "global_load_dwordx4 %2, %10, off\n\t"
+            "global_load_dwordx4 %3, %11, off\n\t"
+            "global_load_dwordx4 %4, %12, off\n\t"
+            "global_load_dwordx4 %5, %13, off\n\t"
+            "global_load_dwordx4 %6, %14, off\n\t"
+            "global_load_dwordx4 %7, %15, off\n\t"
+            "s_waitcnt vmcnt(0)"
+            : "=&v"(qd[0][0][0]), "=&v"(qd[0][0][1]), "=&v"(qd[0][1][0]), "=&v"(qd[0][1][1]),
+              "=&v"(qd[1][0][0]), "=&v"(qd[1][0][1]), "=&v"(qd[1][1][0]), "=&v"(qd[1][1][1])
+            : "v"(src[0][0][0]), "v"(src[0][0][1]), "v"(src[0][1][0]), "v"(src[0][1][1]),
+              "v"(src[1][0][0]), "v"(src[1][0][1]), "v"(src[1][1][0]), "v"(src[1][1][1])
+            : "memory");
+    };
     auto run_pair = [&](int p, int b, uint4 (&qc)[2][QTB][2], uint4 (&qn)[2][QTB][2]) {
-        if (!DB) stage(p, 0);
+        if (!DB) {
+            stage(p, 0);
+            load_q_wait(p, qc);  // (also retires the staging)
+        }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // K/V and Q of this pair
 #pragma unroll
         for (int i = 0; i < 2; ++i)
@@ -737,9 +773,9 @@ attention_v3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
         const int out0 = qsel ? qs0 : tok0;  // ctx row of query 0
         int t_first, t_cnt;
         tiles_of(nq, t_first, t_cnt);
-        if (p + (int)gridDim.x < n_pairs) {
+        if (DB && p + (int)gridDim.x < n_pairs) {
             load_q(p + gridDim.x, qn);
-            if (DB) stage(p + gridDim.x, b ^ 1);
+            stage(p + gridDim.x, b ^ 1);
         }
 
         const uint32_t kim = lds_base + b * Att3<DB>::BUF;
@@ -950,8 +986,8 @@ attention_v3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
     };
     uint4 qa[2][QTB][2], qb2[2][QTB][2];
     int p = blockIdx.x, b = 0;
-    if (p < n_pairs) {
-        if (DB) stage(p, 0);
+    if (DB && p < n_pairs) {
+        stage(p, 0);
         load_q(p, qa);
     }
     while (p < n_pairs) {

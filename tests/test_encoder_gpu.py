@@ -188,6 +188,36 @@ def test_bf16_pruned_last_layer_is_bitexact(E):
                                   synthetic.round3_f32(want))
 
 
+def test_bf16_long_documents_single_buffer_attention(E):
+    """Documents longer than 320 tokens (XLM-R's default max_length is 512) take the
+    single-buffer attention variant (K / V of one (doc, head) pair at a time, Q loaded
+    with the pair): bf16 close to the fp32 oracle, and the pruned term output equal to
+    the per-token output at the term rows, bit for bit."""
+    fx, sd = _fixture("xlmr_base")
+    enc = E.DeviceEncoder(sd, _cfg(E, fx, "xlmr", "softplus"), precision="bf16")
+    rng = np.random.default_rng(21)
+    lens = np.array([512, 400, 321, 40, 3, 333])
+    pad, mask = _random_batch(rng, len(lens), 512, 250002, lens)
+    with torch.no_grad():
+        want = encoder_ref.forward(sd, fx["config"], torch.from_numpy(pad),
+                                   torch.from_numpy(mask), "xlmr", "softplus").numpy()
+    ids, cu = _pack(pad.tolist(), mask.tolist())
+    tok = enc.encode_packed(ids, cu, token_impacts=True)
+    w = want[mask.astype(bool)]
+    err = np.abs(tok - w)
+    assert (err <= 0.05 + 0.05 * np.abs(w)).all(), float(err.max())
+    assert float(np.median(err / np.maximum(np.abs(w), 1e-3))) < 1e-2
+    tt, ct = [], [0]
+    for n in lens:
+        tt += np.sort(rng.choice(n, size=int(rng.integers(1, n + 1)), replace=False)).tolist()
+        ct.append(len(tt))
+    tt, ct = np.array(tt, np.int32), np.array(ct, np.int32)
+    got = enc.encode_packed(ids, cu, tt, ct)
+    np.testing.assert_array_equal(
+        got, np.array([tok[cu[d] + tt[j]] for d in range(len(lens))
+                       for j in range(ct[d], ct[d + 1])], np.float32))
+
+
 def test_encoder_rejects_bad_input(E):
     from improving_learned_index_amd import _lib
 

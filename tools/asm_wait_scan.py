@@ -6,8 +6,8 @@ for them with an explicit s_waitcnt lgkmcnt.  The compiler sees an asm output as
 defined when the asm statement ends, so it may legally schedule a copy or a use of
 such a register ABOVE the wait -- reading a register the LDS is still writing.
 This scans the gfx950 assembly of a source file and reports every instruction
-that touches a destination register of an inline-asm ds_read before the next
-lgkmcnt wait.
+that touches a destination register of an inline-asm ds_read (global / buffer
+load) before the next lgkmcnt (vmcnt) wait.
 
     python tools/asm_wait_scan.py improving-learned-index_amd/csrc/enc_attn.hip
 """
@@ -31,10 +31,10 @@ def _regs(s):
 
 def scan_asm(text):
     """[(function, instruction)] touching a pending asm ds_read destination."""
-    hits, fn, pending, in_asm = [], None, set(), False
+    hits, fn, pending, pending_vm, in_asm = [], None, set(), set(), False
     for ln in text.split("\n"):
         if re.match(r"^_Z\S+:", ln):
-            fn, pending = ln.split(":")[0], set()
+            fn, pending, pending_vm = ln.split(":")[0], set(), set()
         t = ln.strip()
         if t.startswith(";;#ASMSTART"):
             in_asm = True
@@ -44,14 +44,19 @@ def scan_asm(text):
             continue
         if in_asm and t.startswith("ds_read"):
             pending |= _regs(t.split()[1].rstrip(","))
-        elif "s_waitcnt" in t and "lgkmcnt" in t:
-            pending = set()
-        elif pending and not in_asm and re.match(r"(v_|global_|buffer_|ds_|flat_)", t):
+        elif in_asm and re.match(r"(global_load|buffer_load)", t) and "lds" not in t:
+            pending_vm |= _regs(t.split()[1].rstrip(","))
+        elif "s_waitcnt" in t and ("lgkmcnt" in t or "vmcnt" in t):
+            if "lgkmcnt" in t:
+                pending = set()
+            if "vmcnt" in t:
+                pending_vm = set()
+        elif (pending or pending_vm) and not in_asm and re.match(r"(v_|global_|buffer_|ds_|flat_)", t):
             ops = t.split(None, 1)[1].split(",") if " " in t else []
             touched = set()
             for o in ops:
                 touched |= _regs(o)
-            if touched & pending:
+            if touched & (pending | pending_vm):
                 hits.append((fn, t))
     return hits
 
@@ -69,7 +74,7 @@ def main(argv):
     bad = 0
     for src in argv:
         hits = scan_asm(compile_asm(src))
-        print(f"{src}: {len(hits)} early touch(es) of pending asm LDS reads")
+        print(f"{src}: {len(hits)} early touch(es) of pending asm loads")
         for fn, ins in hits[:10]:
             print("   ", fn[:70], "|", ins)
         bad += len(hits)
