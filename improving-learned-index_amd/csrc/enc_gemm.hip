@@ -23,8 +23,6 @@ namespace di {
 
 bool gemm256_ok(int epi, const GemmArgs &g);
 void launch_gemm256(int epi, const GemmArgs &g, hipStream_t s);
-bool gemm2x_ok(int epi, const GemmArgs &g);
-void launch_gemm2x(int epi, const GemmArgs &g, hipStream_t s);
 
 constexpr int GB_M = 128, GB_N = 128, G_THREADS = 256;
 constexpr int ROW_BYTES = 128;                 // bytes of one row per K step
@@ -273,10 +271,6 @@ void launch_gemm(int epi, const GemmArgs &g, hipStream_t s) {
                "GEMM K=%d must be a multiple of %d", g.K, ROW_BYTES / (int)sizeof(T));
     if (g.M == 0) return;
     if constexpr (std::is_same<T, bf16>::value) {
-        if (!force_gemm128() && gemm2x_ok(epi, g)) {
-            launch_gemm2x(epi, g, s);
-            return;
-        }
         if (!force_gemm128() && gemm256_ok(epi, g)) {
             launch_gemm256(epi, g, s);
             return;

@@ -660,15 +660,12 @@ bool gemm256_ok(int epi, const GemmArgs &g) {
            (epi != EPI_BIAS_RESID_LN || (g.N <= 1024 && g.ld_out == g.N));
 }
 
-bool gemm256p_ok(int epi);
-void launch_gemm256p(int epi, const GemmArgs &g, hipStream_t s);
+// column width of one partial-statistics slot of the residual epilogues (the
+// encoder sizes its statistics buffers by it)
+int gemm_stats_cols() { return G2_TILE; }
 
 void launch_gemm256(int epi, const GemmArgs &g, hipStream_t s) {
     static_assert(G2_LDS <= 160 * 1024, "LDS");
-    if (gemm256p_ok(epi)) {  // persistent form (enc_gemm256p.hip)
-        launch_gemm256p(epi, g, s);
-        return;
-    }
     dim3 grid(epi == EPI_BIAS_RESID_LN ? 1 : g.N / G2_TILE, (g.M + G2_TILE - 1) / G2_TILE);
     switch (epi) {
 #define G2_CASE(E)                                                                             \
