@@ -1,4 +1,4 @@
-"""The default-path kernels' inline-asm LDS reads are never touched before their
+"""Every library kernel source's inline-asm loads are never touched before their
 lgkmcnt wait in the compiled gfx950 code (tools/asm_wait_scan.py).  A compiler copy
 of a register that an asm ds_read is still writing reads stale data; this happened
 in attention_v3 before its reads and wait became one asm statement."""
@@ -17,7 +17,8 @@ CSRC = ROOT / "improving-learned-index_amd" / "csrc"
 
 @pytest.mark.skipif(not Path(asm_wait_scan.HIPCC).exists() and shutil.which("hipcc") is None,
                     reason="hipcc not available")
-@pytest.mark.parametrize("src", ["enc_attn.hip", "enc_gemm256.hip", "index.hip"])
+@pytest.mark.parametrize("src", ["enc_attn.hip", "enc_gemm256.hip", "enc_gemm.hip", "enc_misc.hip",
+                                 "encoder.hip", "index.hip", "sparse.hip"])
 def test_no_early_use_of_asm_lds_reads(src):
     hits = asm_wait_scan.scan_asm(asm_wait_scan.compile_asm(CSRC / src))
     assert hits == [], hits[:5]
