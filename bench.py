@@ -227,16 +227,19 @@ def prune_last_layer():
     return os.environ.get("DI_PRUNE_LAST", "1")[:1] != "0"
 
 
-def encode_leg(args, rank, world, dev):
+def encode_leg(args, rank, world, dev, precision="bf16"):
+    """precision "bf16": the throughput mode configs[1] names; "bf16x3": the
+    fp32-faithful mode (split-bf16 GEMMs, f32 attention / LayerNorm; impacts within
+    1e-3 of the fp32 reference -- tests/test_encoder_bf16x3_gpu.py)."""
     from improving_learned_index_amd.encoder import DeviceEncoder, EncoderConfig
 
     t0 = time.time()
     cfg = EncoderConfig.xlmr_base()
     sd = synthetic_state_dict(cfg, seed=0)
-    enc = DeviceEncoder(sd, cfg, precision="bf16", device=dev)
+    enc = DeviceEncoder(sd, cfg, precision=precision, device=dev)
     ids, cu, lens, tt, ct = synthetic_docs_tokens(args.docs, cfg.vocab_size, seed=100 + rank,
                                                   max_len=args.max_len)
-    log(f"[rank {rank}] encoder ready in {time.time() - t0:.1f}s: {args.docs} docs, "
+    log(f"[rank {rank}] {precision} encoder ready in {time.time() - t0:.1f}s: {args.docs} docs, "
         f"{int(cu[-1])} tokens, {int(ct[-1])} terms per step")
     stream = torch.cuda.current_stream()
     enc.set_stream(stream.cuda_stream)
@@ -281,7 +284,8 @@ def encode_leg(args, rank, world, dev):
     # rows per launch, averaged over the L launches of a step: the pruned last layer runs
     # O / FFN1 / FFN2 on the T term rows (QKV on all M)
     T = float(ct[-1])
-    prune = prune_last_layer()
+    split = precision == "bf16x3"
+    prune = prune_last_layer() and not split  # the split forward computes every row
     Mp = ((L - 1) * M + T) / L if prune else M
     gemm_flops = {"gemm_qkv": 2 * M * H * 3 * H, "gemm_o": 2 * Mp * H * H,
                   "gemm_ffn1": 2 * Mp * H * F, "gemm_ffn2": 2 * Mp * F * H}
@@ -296,7 +300,13 @@ def encode_leg(args, rank, world, dev):
     # QKV, 6 = folded FFN1 + GELU, 7 = residual + row statistics (O and FFN2 share it)
     pmc_name = {"gemm_qkv": "gemm256_kernel<5>", "gemm_ffn1": "gemm256_kernel<6>",
                 "gemm_o": "gemm256_kernel<7>", "gemm_ffn2": "gemm256_kernel<7>"}[dom]
+    if split:  # gemm256_kernel<EPI, true>: EPI 3 = QKV, 1 = bias + GELU, 2 = residual
+        pmc_name = {"gemm_qkv": "gemm256_kernel<3, true>", "gemm_ffn1": "gemm256_kernel<1, true>",
+                    "gemm_o": "gemm256_kernel<2, true>", "gemm_ffn2": "gemm256_kernel<2, true>"}[dom]
     traffic, src = load_pmc_traffic(pmc_name)
+    # bf16x3: algorithmic (fp32) FLOPs against the split scheme's own peak -- three
+    # bf16 MFMA products per fp32 product, 2500 / 3 TF/s (the f32 MFMA peak is 157.3)
+    peak = MFMA_BF16_PEAK_TFLOPS / 3.0 if split else MFMA_BF16_PEAK_TFLOPS
     # executed FLOPs (the pruned last layer skips the rows no output reads)
     model_flops = float(flops_per_doc(lens, t=np.diff(ct) if prune else None).sum())
     docs_per_s = world * args.docs * args.steps / el
@@ -307,10 +317,10 @@ def encode_leg(args, rank, world, dev):
         "kernels": kernels,
         "gemm_tflops": {k: round(v[2], 1) for k, v in per_launch.items()},
         "model_tflops": round(model_flops * args.steps / el / 1e12 * 1.0, 1),
-        "model_flops_frac": round(model_flops * args.steps / el / 1e12 / MFMA_BF16_PEAK_TFLOPS, 4),
+        "model_flops_frac": round(model_flops * args.steps / el / 1e12 / peak, 4),
         "roofline": {"kernel": f"{pmc_name} ({dom})", "bound": "mfma",
-                     "achieved": round(tf, 1), "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": round(tf / MFMA_BF16_PEAK_TFLOPS, 4), "traffic": traffic,
+                     "achieved": round(tf, 1), "peak": round(peak, 1), "unit": "TFLOP/s",
+                     "frac": round(tf / peak, 4), "traffic": traffic,
                      "traffic_source": src, "algorithmic_flops_per_launch": f, "avg_launch_ms": round(avg * 1000, 4),
                      "launches": enc.timing(dom)[1]},
     }
@@ -388,7 +398,8 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--docs", type=int, default=8192, help="docs encoded per step per GPU (1024: -3%%, 4096: -1%%: the 256-row GEMM tiles quantize less on 256 CUs with more rows)")
     ap.add_argument("--max-len", type=int, default=300)
-    ap.add_argument("--legs", default="encode,retrieve")
+    ap.add_argument("--legs", default="encode,encode_x3,retrieve",
+                    help="encode (bf16, configs[1]), encode_x3 (fp32-faithful bf16x3), retrieve")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -403,15 +414,18 @@ def main():
 
     legs = set(args.legs.split(","))
     enc_res = ret_res = None
+    x3_res = None
     if "encode" in legs:
         enc_res, enc_ctx = encode_leg(args, rank, world, dev)
+    if "encode_x3" in legs:
+        x3_res, _ = encode_leg(args, rank, world, dev, precision="bf16x3")
     if "retrieve" in legs:
         ret_res, ret_ctx = retrieve_leg(args, rank, world, dev)
-    primary = enc_res if enc_res is not None else ret_res
+    primary = enc_res if enc_res is not None else (x3_res if x3_res is not None else ret_res)
     out = {
         "metric": "docs/sec encoded + queries/sec@top-1000, MS MARCO passage, 1/2/4/8 MI355X",
         "value": round(primary["value"], 2),
-        "unit": "docs/s" if enc_res is not None else "queries/s",
+        "unit": "queries/s" if primary is ret_res else "docs/s",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
@@ -419,7 +433,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "bf16" if enc_res is not None else "u8",
+        "dtype": "bf16" if enc_res is not None else ("bf16x3" if x3_res is not None else "u8"),
         "data": "synthetic (seeded generators of BASELINE.md §2 / SURVEY §8d); random-init "
                 "xlm-roberta-base weights",
         "config": {"workload": "configs[1]: MS MARCO passage 100k-doc slice shape, bf16 encode "
@@ -439,6 +453,15 @@ def main():
     if enc_res is not None:
         out["encode"] = {k: enc_res[k] for k in ("tokens_per_step", "kernels", "gemm_tflops",
                                                  "model_tflops", "model_flops_frac")}
+    if x3_res is not None:
+        out["encode_fp32_faithful"] = {
+            "value": round(x3_res["value"], 2), "unit": "docs/s", "dtype": "bf16x3",
+            "precision": "split-bf16 GEMMs (A_hi W_hi + A_hi W_lo + A_lo W_hi, f32 accumulate), "
+                         "f32 MFMA attention, f32 LayerNorm: impacts within 1e-3 relative of "
+                         "the fp32 reference (tests/test_encoder_bf16x3_gpu.py)",
+            "ms_per_step": round(x3_res["ms_per_step"], 4),
+            **{k: x3_res[k] for k in ("kernels", "gemm_tflops", "model_tflops",
+                                      "model_flops_frac", "roofline")}}
     if ret_res is not None:
         out["retrieve"] = {"value": round(ret_res["value"], 2), "unit": "queries/s",
                            "ms_per_step": round(ret_res["ms_per_step"], 4),

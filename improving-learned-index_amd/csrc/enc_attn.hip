@@ -67,7 +67,9 @@ template <typename T>
 __global__ void __launch_bounds__(64)
 attention_kernel(const T *__restrict__ qk, const T *__restrict__ vt,
                  const int32_t *__restrict__ cu_seqlens, int H, int ld_v, int n_qb, int n_heads,
-                 int n_pairs, T *__restrict__ ctx) {
+                 int n_pairs, T *__restrict__ ctx, bf16 *__restrict__ ctx_split) {
+    // ctx_split (f32 kernel, fp32-faithful mode): the output as split-bf16 rows
+    // [hi(H) | lo(H)] for the next split GEMM, instead of ctx
     constexpr int KC = AttnOps<T>::KC, EPC = AttnOps<T>::EPC;
     constexpr int NCH = ATT_D / KC;  // k chunks over the head dim
     // 1-D grid, XCD-grouped (speed only): the QB query blocks of one (doc, head)
@@ -215,7 +217,17 @@ attention_kernel(const T *__restrict__ qk, const T *__restrict__ vt,
         l += __shfl_xor(l, 32, 64);
         const float inv = 1.0f / l;
         const int q = q_base + 16 * qt + c;
-        if (q < n) {
+        if (q < n && ctx_split) {
+            bf16 *out = ctx_split + (int64_t)(tok0 + q) * 2 * H + h * ATT_D + 4 * g;
+#pragma unroll
+            for (int dt = 0; dt < 4; ++dt) {
+                bf16x4 hv, lv;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) hv[r] = split_hi(o[qt][dt][r] * inv), lv[r] = split_lo(o[qt][dt][r] * inv);
+                *reinterpret_cast<bf16x4 *>(out + dt * 16) = hv;
+                *reinterpret_cast<bf16x4 *>(out + H + dt * 16) = lv;
+            }
+        } else if (q < n) {
             T *out = ctx + (int64_t)(tok0 + q) * H + h * ATT_D + 4 * g;
 #pragma unroll
             for (int dt = 0; dt < 4; ++dt) {
@@ -1070,8 +1082,9 @@ int vt_ld(int64_t M, int n_docs) {
 
 template <typename T>
 void launch_attention(const T *qk, const T *vt, const int32_t *cu_seqlens, int n_docs,
-                      int max_len, int H, int ld_v, T *ctx, hipStream_t s) {
+                      int max_len, int H, int ld_v, T *ctx, hipStream_t s, bf16 *ctx_split) {
     DI_REQUIRE(H % ATT_D == 0, DI_EINVAL, "hidden %d is not a multiple of the head dim 64", H);
+    DI_REQUIRE(!ctx_split || sizeof(T) == 4, DI_EINVAL, "split output: f32 attention only");
     if (n_docs == 0 || max_len == 0) return;
     const int n_heads = H / ATT_D, n_pairs = n_docs * n_heads;
     if constexpr (std::is_same<T, bf16>::value) {
@@ -1113,13 +1126,13 @@ void launch_attention(const T *qk, const T *vt, const int32_t *cu_seqlens, int n
     const int64_t blocks = (int64_t)((n_pairs + 7) / 8) * 8 * n_qb;
     DI_REQUIRE(blocks < (1ll << 31), DI_ERANGE, "attention grid too large");
     hipLaunchKernelGGL(attention_kernel<T>, dim3((unsigned)blocks), dim3(64), 0, s, qk, vt,
-                       cu_seqlens, H, ld_v, n_qb, n_heads, n_pairs, ctx);
+                       cu_seqlens, H, ld_v, n_qb, n_heads, n_pairs, ctx, ctx_split);
     check_launch("attention");
 }
 
 template void launch_attention<bf16>(const bf16 *, const bf16 *, const int32_t *, int, int, int,
-                                     int, bf16 *, hipStream_t);
+                                     int, bf16 *, hipStream_t, bf16 *);
 template void launch_attention<float>(const float *, const float *, const int32_t *, int, int,
-                                      int, int, float *, hipStream_t);
+                                      int, int, float *, hipStream_t, bf16 *);
 
 }  // namespace di

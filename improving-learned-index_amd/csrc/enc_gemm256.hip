@@ -70,7 +70,7 @@ __device__ __forceinline__ void g2_store(bf16 *p, const bf16x8 &v) {
 
 #define G2_BAR() asm volatile("s_barrier" ::: "memory")
 
-template <int EPI>
+template <int EPI, bool SPLIT>
 __global__ void __launch_bounds__(G2_T) gemm256_kernel(GemmArgs g) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const int tid = threadIdx.x, lane = tid & 63;
@@ -102,7 +102,12 @@ __global__ void __launch_bounds__(G2_T) gemm256_kernel(GemmArgs g) {
     const int gsz = min(GM, n_tm - first_m);
     const int in = bid % (GM * n_tn);
     const int M = g.M, N = g.N, K = g.K;
-    const int nk = K / 64;
+    // SPLIT: virtual K tiles t < nkl read (A_hi, B_hi), nkl..2nkl-1 (A_hi, B_lo),
+    // 2nkl.. (A_lo, B_hi): A's physical tile is t - nkl past the first nkl
+    const int nkl = K / 64;
+    const int nk = SPLIT ? 3 * nkl : nkl;
+    const int lda = SPLIT ? 2 * K : K, ldb = SPLIT ? 3 * K : K;
+#define G2_AT(t) ((SPLIT && (t) >= nkl) ? (t) - nkl : (t))
     // EPI_BIAS_RESID_LN: one block owns 256 whole rows (grid 1 x n_tm) and walks
     // their N/256 column tiles, so that the LayerNorm of its rows needs no other block
     constexpr bool LN = EPI == EPI_BIAS_RESID_LN;
@@ -124,7 +129,7 @@ __global__ void __launch_bounds__(G2_T) gemm256_kernel(GemmArgs g) {
     int m0s = m0;
     asm volatile("" : "+s"(A_p), "+s"(B_p), "+s"(m0s));
     const bf16 *a_src = static_cast<const bf16 *>(A_p) +
-                        (int64_t)(m0s + wave * 8 + (lane >> 3)) * K + chunk;
+                        (int64_t)(m0s + wave * 8 + (lane >> 3)) * lda + chunk;
     // B rows are stored permuted inside each 32-column group: LDS row q = sub*16 +
     // g*4 + r holds column g*8 + sub*4 + r, so that MFMA fragment nt (rows sub*16..+15
     // of half nt>>1) gives, in the C^T layout below, every lane 8 consecutive output
@@ -132,17 +137,17 @@ __global__ void __launch_bounds__(G2_T) gemm256_kernel(GemmArgs g) {
     const int qb = (wave & 3) * 8 + (lane >> 3);  // LDS row within the 32-column group
     const int b_col = ((qb >> 2) & 3) * 8 + (qb >> 4) * 4 + (qb & 3);
     const bf16 *b_src = static_cast<const bf16 *>(B_p) +
-                        (int64_t)(n0 + (wave >> 2) * 64 + b_col) * K + chunk;
-    const int64_t a_h = (int64_t)64 * K, a_j = (int64_t)128 * K;
-    const int64_t b_h = (int64_t)32 * K, b_j = (int64_t)128 * K;
+                        (int64_t)(n0 + (wave >> 2) * 64 + b_col) * ldb + chunk;
+    const int64_t a_h = (int64_t)64 * lda, a_j = (int64_t)128 * lda;
+    const int64_t b_h = (int64_t)32 * ldb, b_j = (int64_t)128 * ldb;
     typedef __attribute__((address_space(3))) void lds_void;
 #define G2_STAGE_A(buf, h, t)                                                                  \
     do {                                                                                       \
-        __builtin_amdgcn_global_load_lds((const void *)(a_src + (h) * a_h + (t) * 64),         \
+        __builtin_amdgcn_global_load_lds((const void *)(a_src + (h) * a_h + G2_AT(t) * 64),    \
                                          (lds_void *)(lds + (buf) * G2_BUF + (h) * 16384 +     \
                                                       wave * 1024),                            \
                                          16, 0, 0);                                            \
-        __builtin_amdgcn_global_load_lds((const void *)(a_src + (h) * a_h + a_j + (t) * 64),   \
+        __builtin_amdgcn_global_load_lds((const void *)(a_src + (h) * a_h + a_j + G2_AT(t) * 64), \
                                          (lds_void *)(lds + (buf) * G2_BUF + (h) * 16384 +     \
                                                       8192 + wave * 1024),                     \
                                          16, 0, 0);                                            \
@@ -324,6 +329,7 @@ __global__ void __launch_bounds__(G2_T) gemm256_kernel(GemmArgs g) {
     if (wr == 0) G2_BAR();  // re-align the two groups (every barrier is matched)
 #undef G2_STAGE_A
 #undef G2_STAGE_B
+#undef G2_AT
 #undef G2_LD
 #undef G2_READ_A
 #undef G2_READ_B
@@ -365,7 +371,8 @@ __global__ void __launch_bounds__(G2_T) gemm256_kernel(GemmArgs g) {
     par8(G2_PAR_C0, 1, bias_v[1]);
     if constexpr (EPI == EPI_QKV) {
         if (n0 >= 2 * g.hidden) {  // V columns: transposed element stores into V^T
-            bf16 *vt = static_cast<bf16 *>(g.out2) + (int64_t)(col_l - 2 * g.hidden) * g.ld_v;
+            typedef typename std::conditional<SPLIT, float, bf16>::type VT;  // SPLIT: f32 V^T
+            VT *vt = static_cast<VT *>(g.out2) + (int64_t)(col_l - 2 * g.hidden) * g.ld_v;
 #pragma unroll
             for (int mt = 0; mt < 8; ++mt) {
                 const int row = row_l + mt * 16;
@@ -376,7 +383,7 @@ __global__ void __launch_bounds__(G2_T) gemm256_kernel(GemmArgs g) {
 #pragma unroll
                         for (int e = 0; e < 8; ++e)
                             vt[(int64_t)(h * 32 + e) * g.ld_v + vc] =
-                                (bf16)(acc[mt][2 * h + (e >> 2)][e & 3] + bias_v[h][e]);
+                                (VT)(acc[mt][2 * h + (e >> 2)][e & 3] + bias_v[h][e]);
                 }
             }
             return;
@@ -513,10 +520,33 @@ __global__ void __launch_bounds__(G2_T) gemm256_kernel(GemmArgs g) {
             if (EPI == EPI_BIAS_GELU && !(g.ablate & 2)) gelu_erf8(v);  // ablate 2: no GELU (profiling)
             const int64_t o = (int64_t)row * g.ld_out + col_l + h * 32;
             if constexpr (EPI == EPI_BIAS_RESID || EPI == EPI_BIAS_RESID_LN) {
-                const bf16x8 rv = *reinterpret_cast<const bf16x8 *>(
-                    static_cast<const bf16 *>(g.resid) + (int64_t)row * N + col_l + h * 32);
+                if constexpr (SPLIT) {  // residual rows [hi | lo]
+                    const bf16 *rp = static_cast<const bf16 *>(g.resid) + (int64_t)row * 2 * N +
+                                     col_l + h * 32;
+                    const bf16x8 rh = *reinterpret_cast<const bf16x8 *>(rp);
+                    const bf16x8 rl = *reinterpret_cast<const bf16x8 *>(rp + N);
 #pragma unroll
-                for (int e = 0; e < 8; ++e) v[e] += (float)rv[e];
+                    for (int e = 0; e < 8; ++e) v[e] += (float)rh[e] + (float)rl[e];
+                } else {
+                    const bf16x8 rv = *reinterpret_cast<const bf16x8 *>(
+                        static_cast<const bf16 *>(g.resid) + (int64_t)row * N + col_l + h * 32);
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) v[e] += (float)rv[e];
+                }
+            }
+            if constexpr (SPLIT) {
+                if constexpr (EPI == EPI_QKV || EPI == EPI_BIAS_RESID) {  // f32 rows
+                    float *op = static_cast<float *>(g.out) + o;
+                    *reinterpret_cast<float4 *>(op) = make_float4(v[0], v[1], v[2], v[3]);
+                    *reinterpret_cast<float4 *>(op + 4) = make_float4(v[4], v[5], v[6], v[7]);
+                } else {  // split rows: hi at o, lo at o + N (ld_out = 2N)
+                    bf16x8 hv, lv;
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) hv[e] = split_hi(v[e]), lv[e] = split_lo(v[e]);
+                    g2_store(static_cast<bf16 *>(g.out) + o, hv);
+                    g2_store(static_cast<bf16 *>(g.out) + o + N, lv);
+                }
+                continue;
             }
             bf16x8 ov;
 #pragma unroll
@@ -661,6 +691,9 @@ __global__ void __launch_bounds__(G2_T) gemm256_kernel(GemmArgs g) {
 // Shapes the 8-phase kernel takes; everything else goes to the 128x128 kernel.
 bool gemm256_ok(int epi, const GemmArgs &g) {
     const int64_t m_pad = ((int64_t)g.M + G2_TILE - 1) / G2_TILE * G2_TILE;
+    if (g.split && !(epi == EPI_BIAS || epi == EPI_BIAS_GELU || epi == EPI_BIAS_RESID ||
+                     epi == EPI_QKV))
+        return false;
     return g.N % G2_TILE == 0 && g.K % 128 == 0 && g.K >= 128 && g.a_rows >= m_pad &&
            (epi != EPI_QKV || (2 * g.hidden) % G2_TILE == 0) &&
            (epi != EPI_BIAS_RESID_LN || (g.N <= 1024 && g.ld_out == g.N));
@@ -673,12 +706,32 @@ int gemm_stats_cols() { return G2_TILE; }
 void launch_gemm256(int epi, const GemmArgs &g, hipStream_t s) {
     static_assert(G2_LDS <= 160 * 1024, "LDS");
     dim3 grid(epi == EPI_BIAS_RESID_LN ? 1 : g.N / G2_TILE, (g.M + G2_TILE - 1) / G2_TILE);
+    DI_REQUIRE(gemm256_ok(epi, g), DI_EINVAL, "gemm256: unsupported shape / epilogue");
+    if (g.split) {
+        switch (epi) {
+#define G2_SCASE(E)                                                                            \
+    case E:                                                                                    \
+        DI_HIP(hipFuncSetAttribute((const void *)gemm256_kernel<E, true>,                      \
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, G2_LDS));       \
+        hipLaunchKernelGGL((gemm256_kernel<E, true>), grid, dim3(G2_T), G2_LDS, s, g);         \
+        break;
+            G2_SCASE(EPI_BIAS)
+            G2_SCASE(EPI_BIAS_GELU)
+            G2_SCASE(EPI_BIAS_RESID)
+            G2_SCASE(EPI_QKV)
+#undef G2_SCASE
+            default:
+                fail(DI_EINVAL, "bad split GEMM epilogue");
+        }
+        check_launch("gemm256_split");
+        return;
+    }
     switch (epi) {
 #define G2_CASE(E)                                                                             \
     case E:                                                                                    \
-        DI_HIP(hipFuncSetAttribute((const void *)gemm256_kernel<E>,                            \
+        DI_HIP(hipFuncSetAttribute((const void *)gemm256_kernel<E, false>,                     \
                                    hipFuncAttributeMaxDynamicSharedMemorySize, G2_LDS));       \
-        hipLaunchKernelGGL((gemm256_kernel<E>), grid, dim3(G2_T), G2_LDS, s, g);               \
+        hipLaunchKernelGGL((gemm256_kernel<E, false>), grid, dim3(G2_T), G2_LDS, s, g);        \
         break;
         G2_CASE(EPI_BIAS)
         G2_CASE(EPI_BIAS_GELU)

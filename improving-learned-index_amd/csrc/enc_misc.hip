@@ -5,6 +5,7 @@
 
 #include <algorithm>
 #include <cstring>
+#include <type_traits>
 
 #include "di_common.h"
 #include "enc_common.h"
@@ -160,11 +161,32 @@ __device__ __forceinline__ void st4(bf16 *p, const float (&f)[4]) {
 __device__ __forceinline__ void st4(float *p, const float (&f)[4]) {
     *reinterpret_cast<float4 *>(p) = make_float4(f[0], f[1], f[2], f[3]);
 }
+// split-bf16 row store (fp32-faithful mode): hi at p, lo at p + H
+__device__ __forceinline__ void st4_split(bf16 *p, int H, const float (&f)[4]) {
+    bf16x4 hi, lo;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) hi[j] = split_hi(f[j]), lo[j] = split_lo(f[j]);
+    *reinterpret_cast<bf16x4 *>(p) = hi;
+    *reinterpret_cast<bf16x4 *>(p + H) = lo;
+}
+// row store of the LayerNorm kernels: OUT = T (plain rows) or split rows of 2H bf16
+template <typename T, bool SPLIT>
+struct LnOut {
+    typedef typename std::conditional<SPLIT, bf16, T>::type type;
+};
+template <bool SPLIT, typename O>
+__device__ __forceinline__ void st4_row(O *out, int64_t row, int H, int col, const float (&f)[4]) {
+    if constexpr (SPLIT)
+        st4_split(out + row * 2 * H + col, H, f);
+    else
+        st4(out + row * H + col, f);
+}
 
-template <typename T, int NC>
+template <typename T, int NC, bool SPLIT = false>
 __global__ void __launch_bounds__(256)
 ln_vec_kernel(const T *__restrict__ pre, int M, const float *__restrict__ gamma,
-              const float *__restrict__ beta, float eps, T *__restrict__ out,
+              const float *__restrict__ beta, float eps,
+              typename LnOut<T, SPLIT>::type *__restrict__ out,
               const float *__restrict__ head_w, float head_b, int act, float *__restrict__ impact) {
     constexpr int H = 256 * NC;
     const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -194,7 +216,7 @@ ln_vec_kernel(const T *__restrict__ pre, int M, const float *__restrict__ gamma,
         ld4<float>(beta + 256 * c + 4 * lane, bt);
 #pragma unroll
         for (int j = 0; j < 4; ++j) v[c][j] = (v[c][j] - mean) * rstd * gm[j] + bt[j];
-        if (out) st4(out + (int64_t)row * H + 256 * c + 4 * lane, v[c]);
+        if (out) st4_row<SPLIT>(out, row, H, 256 * c + 4 * lane, v[c]);
         if (head_w) {
             float w[4];
             ld4<float>(head_w + 256 * c + 4 * lane, w);
@@ -209,13 +231,14 @@ ln_vec_kernel(const T *__restrict__ pre, int M, const float *__restrict__ gamma,
 // so the position is the row's offset in the document (no per-token search over the
 // document offsets), 4 waves x 2 rows in flight, lane holds 4 consecutive columns of
 // each 256-column chunk (8-byte loads, the ln_vec_kernel layout and arithmetic).
-template <typename T, int NC>
+template <typename T, int NC, bool SPLIT = false>
 __global__ void __launch_bounds__(256)
 embed_ln_vec_kernel(const int32_t *__restrict__ ids, const int32_t *__restrict__ cu,
                     const T *__restrict__ word, const T *__restrict__ pos,
                     const T *__restrict__ type0, const float *__restrict__ gamma,
                     const float *__restrict__ beta, float eps, int pos_offset, int vocab,
-                    int max_pos, T *__restrict__ out, int32_t *__restrict__ err) {
+                    int max_pos, typename LnOut<T, SPLIT>::type *__restrict__ out,
+                    int32_t *__restrict__ err) {
     constexpr int H = 256 * NC, RB = 2;
     const int d = blockIdx.x, wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int r0 = cu[d], n = cu[d + 1] - r0;
@@ -268,7 +291,7 @@ embed_ln_vec_kernel(const int32_t *__restrict__ ids, const int32_t *__restrict__
             for (int c = 0; c < NC; ++c) {
 #pragma unroll
                 for (int j = 0; j < 4; ++j) v[r][c][j] = (v[r][c][j] - mean) * rstd * gm[c][j] + bt[c][j];
-                st4(out + (int64_t)(r0 + i0 + r) * H + 256 * c + 4 * lane, v[r][c]);
+                st4_row<SPLIT>(out, (int64_t)(r0 + i0 + r), H, 256 * c + 4 * lane, v[r][c]);
             }
         }
     }
@@ -439,6 +462,39 @@ void launch_ln(const T *pre, int M, int H, const float *gamma, const float *beta
         hipLaunchKernelGGL((ln_kernel<T, LN_MAX_PER_LANE>), grid, dim3(256), 0, s, pre, M, H,
                            gamma, beta, eps, out, head_w, head_b, act, impact);
     check_launch("ln");
+}
+
+// fp32-faithful (split-bf16) mode: f32 tables / pre-LN rows in, split rows out
+void launch_embed_ln_split(const int32_t *ids, const int32_t *cu, int n_docs, int M, int H,
+                           const float *word, const float *pos, const float *type0,
+                           const float *gamma, const float *beta, float eps, int pos_offset,
+                           int vocab, int max_pos, bf16 *out, int32_t *err, hipStream_t s) {
+    if (M == 0) return;
+    DI_REQUIRE(H == 768 || H == 1024, DI_EINVAL, "split mode: hidden %d (768 / 1024)", H);
+    if (H == 768)
+        hipLaunchKernelGGL((embed_ln_vec_kernel<float, 3, true>), dim3(n_docs), dim3(256), 0, s,
+                           ids, cu, word, pos, type0, gamma, beta, eps, pos_offset, vocab, max_pos,
+                           out, err);
+    else
+        hipLaunchKernelGGL((embed_ln_vec_kernel<float, 4, true>), dim3(n_docs), dim3(256), 0, s,
+                           ids, cu, word, pos, type0, gamma, beta, eps, pos_offset, vocab, max_pos,
+                           out, err);
+    check_launch("embed_ln_split");
+}
+
+void launch_ln_split(const float *pre, int M, int H, const float *gamma, const float *beta,
+                     float eps, bf16 *out, const float *head_w, float head_b, int act,
+                     float *impact, hipStream_t s) {
+    if (M == 0) return;
+    DI_REQUIRE(H == 768 || H == 1024, DI_EINVAL, "split mode: hidden %d (768 / 1024)", H);
+    dim3 grid((M + 3) / 4);
+    if (H == 768)
+        hipLaunchKernelGGL((ln_vec_kernel<float, 3, true>), grid, dim3(256), 0, s, pre, M, gamma,
+                           beta, eps, out, head_w, head_b, act, impact);
+    else
+        hipLaunchKernelGGL((ln_vec_kernel<float, 4, true>), grid, dim3(256), 0, s, pre, M, gamma,
+                           beta, eps, out, head_w, head_b, act, impact);
+    check_launch("ln_split");
 }
 
 void launch_gather_terms(const float *impact, const int32_t *cu_seq, const int32_t *cu_terms,

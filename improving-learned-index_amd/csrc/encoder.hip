@@ -28,7 +28,16 @@ template <typename T>
 void launch_gemm(int epi, const GemmArgs &g, hipStream_t s);
 template <typename T>
 void launch_attention(const T *qk, const T *vt, const int32_t *cu_seqlens, int n_docs,
-                      int max_len, int H, int ld_v, T *ctx, hipStream_t s);
+                      int max_len, int H, int ld_v, T *ctx, hipStream_t s,
+                      bf16 *ctx_split = nullptr);
+void launch_gemm256(int epi, const GemmArgs &g, hipStream_t s);
+void launch_embed_ln_split(const int32_t *ids, const int32_t *cu, int n_docs, int M, int H,
+                           const float *word, const float *pos, const float *type0,
+                           const float *gamma, const float *beta, float eps, int pos_offset,
+                           int vocab, int max_pos, bf16 *out, int32_t *err, hipStream_t s);
+void launch_ln_split(const float *pre, int M, int H, const float *gamma, const float *beta,
+                     float eps, bf16 *out, const float *head_w, float head_b, int act,
+                     float *impact, hipStream_t s);
 template <typename T>
 void launch_embed_ln(const int32_t *ids, const int32_t *cu, int n_docs, int M, int H,
                      const T *word, const T *pos, const T *type0, const float *gamma,
@@ -71,6 +80,9 @@ struct di_encoder {
     hipStream_t stream = nullptr;
     bool own_stream = false;
     size_t esz = 2;  // bytes per activation/weight element (bf16 or f32)
+    // fp32-faithful split-bf16 mode (DI_PREC_BF16X3): esz = 4 sizes the workspace (a
+    // split row of 2H bf16 = an f32 row), f32 tables, GEMM weights [N][3K] bf16
+    bool split = false;
     DevBuf word, pos, type0, emb_g, emb_b, head_w;
     float head_b = 0.f;
     std::vector<std::unique_ptr<Layer>> layers;
@@ -205,6 +217,32 @@ void upload(DevBuf &dst, const std::vector<const HostTensor *> &parts, int64_t r
         }
         DI_HIP(hipMemcpy(dst.p, h.data(), (size_t)n * 2, hipMemcpyHostToDevice));
     }
+}
+
+// split-bf16 GEMM weight (fp32-faithful mode): each [K] row of W becomes
+// [hi(K) | lo(K) | hi(K)], hi = bf16(w), lo = bf16(w - hi), so that the 3K-long
+// K loop of the split GEMM (A rows [hi | lo]) sums A_hi W_hi + A_hi W_lo + A_lo W_hi.
+void upload_split3(DevBuf &dst, const std::vector<const HostTensor *> &parts, int K) {
+    int64_t rows = 0;
+    for (auto *p : parts) rows += p->numel() / K;
+    std::vector<uint16_t> h((size_t)(rows * 3 * K));
+    int64_t r = 0;
+    for (auto *p : parts) {
+        const int64_t pr = p->numel() / K;
+        for (int64_t i = 0; i < pr; ++i, ++r) {
+            uint16_t *o = &h[(size_t)(r * 3 * K)];
+            for (int k = 0; k < K; ++k) {
+                const float w = p->at(i * K + k);
+                const uint16_t hi = f32_to_bf16_bits(w);
+                const uint16_t lo = f32_to_bf16_bits(w - bf16_bits_to_f32(hi));
+                o[k] = hi;
+                o[K + k] = lo;
+                o[2 * K + k] = hi;
+            }
+        }
+    }
+    dst.reserve(h.size() * 2);
+    DI_HIP(hipMemcpy(dst.p, h.data(), h.size() * 2, hipMemcpyHostToDevice));
 }
 
 void ensure_workspace(di_encoder *e, int64_t M, int n_docs, int64_t n_terms) {
@@ -565,6 +603,112 @@ void forward_folded(di_encoder *e, const int32_t *d_ids, const int32_t *d_cu, in
     }
 }
 
+// fp32-faithful forward (DI_PREC_BF16X3): the unfolded post-LN structure of
+// forward<T> with every GEMM a split-bf16 256-tile GEMM (3 bf16 MFMA products per
+// fp32 product, f32 accumulate: ~2^-17 relative per product), attention in exact f32
+// MFMA, LayerNorms in f32 from f32 pre-LN rows.  Activations that feed a GEMM are
+// split rows [hi | lo]; Q | K and V^T are f32; the pre-LN rows are f32.
+void forward_split(di_encoder *e, const int32_t *d_ids, const int32_t *d_cu, int n_docs,
+                   int64_t M, int max_len, bool timing, hipStream_t s) {
+    const auto &c = e->cfg;
+    const int H = c.hidden, F = c.intermediate;
+    const int pos_offset = (c.variant == DI_VARIANT_XLMR) ? c.pad_id + 1 : 0;
+    bf16 *X = e->X.as<bf16>(), *X1 = e->X1.as<bf16>(), *ctx = e->ctx.as<bf16>();
+    float *pre = e->pre.as<float>();
+    {
+        TimedLaunch tl(e->timer, timing, "embed_ln", s);
+        launch_embed_ln_split(d_ids, d_cu, n_docs, (int)M, H, e->word.as<float>(),
+                              e->pos.as<float>(), e->type0.as<float>(), e->emb_g.as<float>(),
+                              e->emb_b.as<float>(), c.layer_norm_eps, pos_offset, c.vocab_size,
+                              c.max_positions, X, e->err.as<int32_t>(), s);
+    }
+    launch_vt_cols(d_cu, n_docs, (int)M, e->vcol.as<int32_t>(), s);
+    auto base = [&]() {
+        GemmArgs g{};
+        g.M = (int)M;
+        g.a_rows = e->cap_rows;
+        g.hidden = H;
+        g.tune_gm = 8;
+        g.split = 1;
+        return g;
+    };
+    for (size_t l = 0; l < e->layers.size(); ++l) {
+        Layer &L = *e->layers[l];
+        const bool last = l + 1 == e->layers.size();
+        GemmArgs g = base();
+        g.A = X;
+        g.B = L.w_qkv.p;
+        g.bias = L.b_qkv.as<float>();
+        g.out = e->qk.p;  // f32 Q | K rows
+        g.out2 = e->vt.p; // f32 V^T
+        g.N = 3 * H;
+        g.K = H;
+        g.ld_out = 2 * H;
+        g.ld_v = e->ld_v;
+        g.vcol = e->vcol.as<int32_t>();
+        {
+            TimedLaunch tl(e->timer, timing, "gemm_qkv", s);
+            launch_gemm256(EPI_QKV, g, s);
+        }
+        {
+            TimedLaunch tl(e->timer, timing, "attention", s);
+            launch_attention<float>(e->qk.as<float>(), e->vt.as<float>(), d_cu, n_docs, max_len,
+                                    H, e->ld_v, nullptr, s, ctx);
+        }
+        g = base();
+        g.A = ctx;
+        g.B = L.w_o.p;
+        g.bias = L.b_o.as<float>();
+        g.resid = X;
+        g.out = pre;
+        g.N = H;
+        g.K = H;
+        g.ld_out = H;
+        {
+            TimedLaunch tl(e->timer, timing, "gemm_o", s);
+            launch_gemm256(EPI_BIAS_RESID, g, s);
+        }
+        {
+            TimedLaunch tl(e->timer, timing, "ln", s);
+            launch_ln_split(pre, (int)M, H, L.ln1_g.as<float>(), L.ln1_b.as<float>(),
+                            c.layer_norm_eps, X1, nullptr, 0.f, c.activation, nullptr, s);
+        }
+        g = base();
+        g.A = X1;
+        g.B = L.w_i.p;
+        g.bias = L.b_i.as<float>();
+        g.out = e->Hff.p;
+        g.N = F;
+        g.K = H;
+        g.ld_out = 2 * F;
+        {
+            TimedLaunch tl(e->timer, timing, "gemm_ffn1", s);
+            launch_gemm256(EPI_BIAS_GELU, g, s);
+        }
+        g = base();
+        g.A = e->Hff.p;
+        g.B = L.w_out.p;
+        g.bias = L.b_out.as<float>();
+        g.resid = X1;
+        g.out = pre;
+        g.N = H;
+        g.K = F;
+        g.ld_out = H;
+        g.tune_gm = 4;
+        {
+            TimedLaunch tl(e->timer, timing, "gemm_ffn2", s);
+            launch_gemm256(EPI_BIAS_RESID, g, s);
+        }
+        {
+            TimedLaunch tl(e->timer, timing, "ln", s);
+            launch_ln_split(pre, (int)M, H, L.ln2_g.as<float>(), L.ln2_b.as<float>(),
+                            c.layer_norm_eps, last ? nullptr : X,
+                            last ? e->head_w.as<float>() : nullptr, e->head_b, c.activation,
+                            last ? e->impact.as<float>() : nullptr, s);
+        }
+    }
+}
+
 }  // namespace
 
 extern "C" {
@@ -582,8 +726,12 @@ int di_encoder_create(const di_encoder_cfg *cfg, const di_tensor *w, int32_t n_w
                    "bad variant");
         DI_REQUIRE(c.activation == DI_ACT_SOFTPLUS || c.activation == DI_ACT_RELU, DI_EINVAL,
                    "bad activation");
-        DI_REQUIRE(c.precision == DI_PREC_BF16 || c.precision == DI_PREC_FP32, DI_EINVAL,
-                   "bad precision");
+        DI_REQUIRE(c.precision == DI_PREC_BF16 || c.precision == DI_PREC_FP32 ||
+                       c.precision == DI_PREC_BF16X3,
+                   DI_EINVAL, "bad precision");
+        DI_REQUIRE(c.precision != DI_PREC_BF16X3 ||
+                       ((c.hidden == 768 || c.hidden == 1024) && c.intermediate % 256 == 0),
+                   DI_EINVAL, "bf16x3 mode: hidden 768 / 1024 and intermediate %% 256");
         DI_REQUIRE(c.hidden > 0 && c.hidden % 64 == 0 && c.hidden <= 1024, DI_EINVAL,
                    "hidden=%d must be a multiple of 64, <= 1024", c.hidden);
         DI_REQUIRE(c.heads > 0 && c.hidden / c.heads == 64 && c.hidden % c.heads == 0,
@@ -597,6 +745,7 @@ int di_encoder_create(const di_encoder_cfg *cfg, const di_tensor *w, int32_t n_w
         e->cfg = c;
         e->device = device;
         e->esz = c.precision == DI_PREC_BF16 ? 2 : 4;
+        e->split = c.precision == DI_PREC_BF16X3;
         DI_HIP(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
         e->own_stream = true;
 
@@ -662,25 +811,36 @@ int di_encoder_create(const di_encoder_cfg *cfg, const di_tensor *w, int32_t n_w
             const std::vector<const HostTensor *> bqkv = {
                 get(p + "attention.self.query.bias", {H}), get(p + "attention.self.key.bias", {H}),
                 get(p + "attention.self.value.bias", {H})};
-            if (e->folded && l > 0)  // layer 0 reads the (normalised) embedding output
+            if (e->split)
+                upload_split3(L->w_qkv, wqkv, (int)H);
+            else if (e->folded && l > 0)  // layer 0 reads the (normalised) embedding output
                 fold_upload(L->w_qkv, L->s_qkv, L->c_qkv, wqkv, bqkv, H, prev_g2, prev_b2);
             else
                 upload(L->w_qkv, wqkv, 0, false, e->esz);
             upload(L->b_qkv, bqkv, 0, true, 4);
-            upload(L->w_o, {get(p + "attention.output.dense.weight", {H, H})}, 0, false, e->esz);
+            if (e->split)
+                upload_split3(L->w_o, {get(p + "attention.output.dense.weight", {H, H})}, (int)H);
+            else
+                upload(L->w_o, {get(p + "attention.output.dense.weight", {H, H})}, 0, false,
+                       e->esz);
             upload(L->b_o, {get(p + "attention.output.dense.bias", {H})}, 0, true, 4);
             upload(L->ln1_g, {get(p + "attention.output.LayerNorm.weight", {H})}, 0, true, 4);
             upload(L->ln1_b, {get(p + "attention.output.LayerNorm.bias", {H})}, 0, true, 4);
             const HostTensor *wi = get(p + "intermediate.dense.weight", {F, H});
             const HostTensor *bi = get(p + "intermediate.dense.bias", {F});
-            if (e->folded)
+            if (e->split)
+                upload_split3(L->w_i, {wi}, (int)H);
+            else if (e->folded)
                 fold_upload(L->w_i, L->s_i, L->c_i, {wi}, {bi}, H,
                             get(p + "attention.output.LayerNorm.weight", {H}),
                             get(p + "attention.output.LayerNorm.bias", {H}));
             else
                 upload(L->w_i, {wi}, 0, false, e->esz);
             upload(L->b_i, {bi}, 0, true, 4);
-            upload(L->w_out, {get(p + "output.dense.weight", {H, F})}, 0, false, e->esz);
+            if (e->split)
+                upload_split3(L->w_out, {get(p + "output.dense.weight", {H, F})}, (int)F);
+            else
+                upload(L->w_out, {get(p + "output.dense.weight", {H, F})}, 0, false, e->esz);
             upload(L->b_out, {get(p + "output.dense.bias", {H})}, 0, true, 4);
             prev_g2 = get(p + "output.LayerNorm.weight", {H});
             prev_b2 = get(p + "output.LayerNorm.bias", {H});
@@ -763,7 +923,9 @@ int di_encode(di_encoder *e, const int32_t *tok_ids, const int32_t *cu_seqlens, 
         const bool prune = prune_env && !token_out && e->esz == 2 && e->folded &&
                            n_terms <= n_tokens;  // (packed term rows fit the row buffers)
         if (n_tokens > 0) {
-            if (e->esz == 2)
+            if (e->split)
+                forward_split(e, d_ids, d_cu, n_docs, n_tokens, max_len, timing, s);
+            else if (e->esz == 2)
                 if (e->folded)
                     forward_folded(e, d_ids, d_cu, n_docs, n_tokens, max_len, timing, s,
                                    prune ? d_tt : nullptr, prune ? d_cut : nullptr, n_terms);

@@ -17,7 +17,11 @@ from ._lib import check, lib, ptr
 
 DI_VARIANT_XLMR, DI_VARIANT_BERT = 0, 1
 DI_ACT_SOFTPLUS, DI_ACT_RELU = 0, 1
-DI_PREC_BF16, DI_PREC_FP32 = 0, 1
+DI_PREC_BF16, DI_PREC_FP32, DI_PREC_BF16X3 = 0, 1, 2
+# "bf16": bf16 MFMA (throughput mode, not fp32-faithful); "fp32": f32 MFMA throughout;
+# "bf16x3": split-bf16 GEMMs (3 bf16 products per fp32 product) + f32 attention /
+# LayerNorm -- fp32-faithful (impacts within 1e-3 relative of the reference) and fast
+PRECISIONS = {"bf16": DI_PREC_BF16, "fp32": DI_PREC_FP32, "bf16x3": DI_PREC_BF16X3}
 DI_DTYPE_F32, DI_DTYPE_BF16 = 0, 1
 DI_F_ROUND3 = 0x10
 DI_F_TOKEN_IMPACTS = 0x20
@@ -105,7 +109,9 @@ class EncoderConfig:
         c = di_encoder_cfg()
         c.variant = DI_VARIANT_XLMR if self.variant == "xlmr" else DI_VARIANT_BERT
         c.activation = DI_ACT_SOFTPLUS if self.activation == "softplus" else DI_ACT_RELU
-        c.precision = DI_PREC_BF16 if precision == "bf16" else DI_PREC_FP32
+        if precision not in PRECISIONS:
+            raise ValueError(f"precision {precision!r}: one of {sorted(PRECISIONS)}")
+        c.precision = PRECISIONS[precision]
         for f in ("vocab_size", "hidden", "layers", "heads", "intermediate", "max_positions",
                   "type_vocab", "pad_id"):
             setattr(c, f, getattr(self, f))
@@ -132,6 +138,8 @@ class DeviceEncoder:
     """Weights resident on one GPU; encode() runs the whole forward there."""
 
     def __init__(self, state_dict: Mapping, cfg: EncoderConfig, precision="bf16", device=0):
+        if precision == "bf16x3" and not (cfg.hidden in (768, 1024) and cfg.intermediate % 256 == 0):
+            precision = "fp32"  # split-bf16 kernels take base / large shapes; f32 MFMA otherwise
         self.cfg, self.precision, self.device = cfg, precision, device
         keep, tens = [], []
         for k, v in state_dict.items():

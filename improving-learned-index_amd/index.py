@@ -29,7 +29,7 @@ logger = logging.getLogger("index")
 
 def run(collection_path, collection_type, output_file_path, model_checkpoint_path,
         num_processes=8, process_batch_size=50 * BATCH_SIZE, model_batch_size=BATCH_SIZE,
-        tokenizer_path=None, max_length=None, precision="bf16", device=0, variant="xlmr",
+        tokenizer_path=None, max_length=None, precision="bf16x3", device=0, variant="xlmr",
         doc_range=None, pairwise=False):
     if pairwise:
         raise NotImplementedError("DeepPairwiseImpact is outside this build (SURVEY §8f F4)")
@@ -88,7 +88,9 @@ def main(argv=None):
     p.add_argument("--pairwise", action="store_true")
     p.add_argument("--tokenizer_path", type=str, default=None)
     p.add_argument("--max_length", type=int, default=None)
-    p.add_argument("--precision", choices=["bf16", "fp32"], default="bf16")
+    p.add_argument("--precision", choices=["bf16x3", "fp32", "bf16"], default="bf16x3",
+                   help="bf16x3 (default): fp32-faithful split-bf16; fp32: f32 MFMA; "
+                        "bf16: throughput mode, NOT fp32-faithful (different round3 text)")
     p.add_argument("--device", type=int, default=0)
     p.add_argument("--variant", choices=["xlmr", "bert"], default="xlmr")
     p.add_argument("--doc_range", type=str, default=None, help="start:end line range (shard)")

@@ -183,7 +183,7 @@ class DeepImpact:
     @classmethod
     def load(cls, checkpoint_path: Optional[Union[str, Path]] = None, *,
              config: Optional[EncoderConfig] = None, tokenizer_path=None,
-             precision: str = "bf16", device: int = 0, variant: str = "xlmr",
+             precision: str = "bf16x3", device: int = 0, variant: str = "xlmr",
              max_length: Optional[int] = None) -> "DeepImpact":
         """Replaces DeepImpact.load (xlmr_original.py:191-203) + .to(cuda).eval().
 

@@ -26,7 +26,7 @@ class ReRanker:
     def __init__(self, checkpoint_path: Union[str, Path, None], top_k_run_file_path,
                  queries_path, collection_path, output_path, batch_size: int = 128,
                  num_processes: int = 4, model: Optional[DeepImpact] = None,
-                 tokenizer_path=None, precision: str = "bf16", device: int = 0,
+                 tokenizer_path=None, precision: str = "bf16x3", device: int = 0,
                  variant: str = "xlmr", max_length: Optional[int] = None):
         self.top_k = TopKRunFile(run_file_path=top_k_run_file_path)
         self.queries = Queries(queries_path=queries_path)
@@ -79,7 +79,9 @@ def main(argv=None):
     p.add_argument("--batch_size", type=int, default=128)
     p.add_argument("--num_processes", type=int, default=4)
     p.add_argument("--tokenizer_path", type=str, default=None)
-    p.add_argument("--precision", choices=["bf16", "fp32"], default="bf16")
+    p.add_argument("--precision", choices=["bf16x3", "fp32", "bf16"], default="bf16x3",
+                   help="bf16x3 (default): fp32-faithful split-bf16; fp32: f32 MFMA; "
+                        "bf16: throughput mode, NOT fp32-faithful (different round3 text)")
     p.add_argument("--device", type=int, default=0)
     p.add_argument("--variant", choices=["xlmr", "bert"], default="xlmr")
     p.add_argument("--max_length", type=int, default=None)

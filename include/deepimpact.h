@@ -165,6 +165,9 @@ typedef struct di_encoder di_encoder;
 #define DI_ACT_RELU 1     /* nn.ReLU() head (original.py:44-47)                        */
 #define DI_PREC_BF16 0    /* bf16 MFMA, f32 accumulate/softmax/LayerNorm (fast)        */
 #define DI_PREC_FP32 1    /* f32 MFMA throughout (parity with the f32 reference)       */
+#define DI_PREC_BF16X3 2  /* fp32-faithful fast mode: split-bf16 GEMMs (3 bf16 MFMA
+                             products per f32 product, f32 accumulate), f32 attention
+                             and LayerNorm; hidden 768 / 1024                           */
 #define DI_DTYPE_F32 0
 #define DI_DTYPE_BF16 1
 

@@ -1,0 +1,231 @@
+"""GPU parity of the fp32-faithful fast encode mode (precision "bf16x3", DI_PREC_BF16X3).
+
+Every GEMM runs as split-bf16 (A = A_hi + A_lo, W = W_hi + W_lo; three bf16 MFMA
+products A_hi W_hi + A_hi W_lo + A_lo W_hi, f32 accumulate, ~2^-17 relative per
+product), attention in exact f32 MFMA, LayerNorms in f32 -- the reference computes in
+fp32 (src/deep_impact/indexing/indexer.py:46, no autocast).  Checked against:
+  * the reference's own DeepImpact (XLM-R) forward on the full xlm-roberta-base shape
+    (tests/golden/encoder_xlmr_base.json, made by tests/golden/make_golden.py);
+  * the plain PyTorch fp32 restatement oracle/encoder_ref.py on ragged batches up to
+    512 tokens, and with outlier LayerNorm channels (large |mean| / sigma rows, the
+    regime of trained RoBERTa-family checkpoints);
+  * end to end through the reference's text path: round(., 3) (indexer.py:62-68) ->
+    quantize (quantize.py:13-47) -> index (create.py) -> top-1000 (inverted_index.py:55-62)
+    -> MRR@10 / Recall (metrics.py:26-57), against the fp32 oracle's impacts.
+Tolerance (north star): float impacts within 1e-3 relative of the fp32 reference.
+"""
+import json
+
+import numpy as np
+import pytest
+import torch
+
+import encoder_ref
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+RTOL = 1e-3  # north star: float scores within 1e-3 relative
+
+
+@pytest.fixture(scope="module")
+def E():
+    from improving_learned_index_amd import _lib, encoder
+
+    if _lib.device_count() < 1:
+        pytest.fail("no HIP device visible (GPU test run without a GPU)")
+    return encoder
+
+
+@pytest.fixture(scope="module")
+def base():
+    fx = json.loads((GOLDEN / "encoder_xlmr_base.json").read_text())
+    sd = encoder_ref.seeded_state_dict(fx["state_dict_shapes"], fx["seed"], fx["std"])
+    return fx, sd
+
+
+def _cfg(E, fx):
+    c = fx["config"]
+    return E.EncoderConfig(variant="xlmr", activation="softplus", vocab_size=c["vocab_size"],
+                           hidden=c["hidden_size"], layers=c["num_hidden_layers"],
+                           heads=c["num_attention_heads"], intermediate=c["intermediate_size"],
+                           max_positions=c["max_position_embeddings"],
+                           type_vocab=c["type_vocab_size"], pad_id=c["pad_token_id"],
+                           layer_norm_eps=c["layer_norm_eps"])
+
+
+def _pack(input_ids, mask):
+    ids, cu = [], [0]
+    for row, m in zip(input_ids, mask):
+        n = int(sum(m))
+        ids += list(row[:n])
+        cu.append(cu[-1] + n)
+    return np.array(ids, np.int32), np.array(cu, np.int32)
+
+
+def _random_batch(rng, lens, vocab):
+    ids = [rng.integers(5, vocab, n).astype(np.int64) for n in lens]
+    for a in ids:
+        a[0] = 0
+    pad = np.ones((len(lens), max(lens)), np.int64)
+    mask = np.zeros_like(pad)
+    for i, a in enumerate(ids):
+        pad[i, :len(a)] = a
+        mask[i, :len(a)] = 1
+    return pad, mask
+
+
+def _oracle(sd, fx, pad, mask):
+    with torch.no_grad():
+        return encoder_ref.forward(sd, fx["config"], torch.from_numpy(pad),
+                                   torch.from_numpy(mask), "xlmr", "softplus").numpy()
+
+
+def test_bf16x3_term_impacts_match_reference_class(E, base):
+    fx, sd = base
+    enc = E.DeviceEncoder(sd, _cfg(E, fx), precision="bf16x3")
+    ids, cu = _pack(fx["input_ids"], fx["attention_mask"])
+    maps = fx["term_maps"]
+    tt = np.array([tok for m in maps for _, tok in m], np.int32)
+    ct = np.cumsum([0] + [len(m) for m in maps]).astype(np.int32)
+    got = enc.encode_packed(ids, cu, tt, ct)
+    want = np.array([b for d in fx["term_impacts_f32_bits"] for _, b in d],
+                    np.uint32).view(np.float32)
+    np.testing.assert_allclose(got, want, rtol=RTOL, atol=1e-6)
+
+
+@pytest.mark.parametrize("lens", [[300, 250, 180, 64, 9, 120], [512, 400, 321, 40, 3, 1]])
+def test_bf16x3_ragged_batches_match_torch_oracle(E, base, lens):
+    fx, sd = base
+    enc = E.DeviceEncoder(sd, _cfg(E, fx), precision="bf16x3")
+    rng = np.random.default_rng(sum(lens))
+    pad, mask = _random_batch(rng, lens, 250002)
+    want = _oracle(sd, fx, pad, mask)[mask.astype(bool)]
+    ids, cu = _pack(pad.tolist(), mask.tolist())
+    got = enc.encode_packed(ids, cu, token_impacts=True)
+    np.testing.assert_allclose(got, want, rtol=RTOL, atol=1e-6)
+
+
+def _outlier_sd(sd):
+    """Outlier LayerNorm channels in every LayerNorm: large beta and gamma on three
+    channels, so the residual stream carries rows with |mean| / sigma >> 1."""
+    sd = dict(sd)
+    ch = [5, 77, 300]
+    beta = torch.tensor([6.0, -8.0, 12.0])
+    for k in list(sd):
+        if k.endswith("LayerNorm.bias"):
+            v = sd[k].clone()
+            v[ch] = beta
+            sd[k] = v
+        elif k.endswith("LayerNorm.weight"):
+            v = sd[k].clone()
+            v[ch] = 4.0
+            sd[k] = v
+    return sd
+
+
+def test_layernorm_outlier_channels(E, base, monkeypatch):
+    """bf16x3 stays inside the 1e-3 bar with outlier channels; the bf16 throughput
+    mode with LayerNorm folding (residual rounded to bf16 before normalisation) is
+    compared with the unfolded bf16 path (DI_NO_LN_FOLD) against the same oracle, and
+    folding must not be materially worse than not folding."""
+    fx, sd = base
+    sd = _outlier_sd(sd)
+    rng = np.random.default_rng(5)
+    lens = [200, 150, 77, 31]
+    pad, mask = _random_batch(rng, lens, 250002)
+    want = _oracle(sd, fx, pad, mask)[mask.astype(bool)]
+    ids, cu = _pack(pad.tolist(), mask.tolist())
+    enc = E.DeviceEncoder(sd, _cfg(E, fx), precision="bf16x3")
+    got = enc.encode_packed(ids, cu, token_impacts=True)
+    np.testing.assert_allclose(got, want, rtol=RTOL, atol=1e-6)
+    rel = lambda y: np.abs(y - want) / np.maximum(np.abs(want), 1e-3)  # noqa: E731
+    folded = E.DeviceEncoder(sd, _cfg(E, fx), precision="bf16")
+    r_fold = rel(folded.encode_packed(ids, cu, token_impacts=True))
+    del folded
+    monkeypatch.setenv("DI_NO_LN_FOLD", "1")
+    plain = E.DeviceEncoder(sd, _cfg(E, fx), precision="bf16")
+    r_plain = rel(plain.encode_packed(ids, cu, token_impacts=True))
+    print(f"bf16x3 max rel {rel(got).max():.2e}; bf16 folded max/median rel "
+          f"{r_fold.max():.2e}/{np.median(r_fold):.2e}; unfolded {r_plain.max():.2e}/"
+          f"{np.median(r_plain):.2e}")
+    assert np.median(r_fold) <= 2.0 * np.median(r_plain) + 1e-3
+    assert r_fold.max() <= 2.0 * r_plain.max() + 1e-2
+
+
+def _pipeline(impacts_per_doc, terms_per_doc, queries, max_val=None):
+    """Reference text path: round3 + repr text -> quantize -> index -> top-1000."""
+    import oracle
+
+    lines = [oracle.impact_line(t, v) for t, v in zip(terms_per_doc, impacts_per_doc)]
+    q, used = oracle.quantize_lines(lines, max_val)
+    docs = [dict((p.split(": ")[0], float(p.split(": ")[1])) for p in l.split(", ")) if l else {}
+            for l in q]
+    vocab, term_off, pdoc, pval = oracle.build_index(docs)
+    ix = oracle.Index.__new__(oracle.Index)
+    ix.vocab = {t: i for i, t in enumerate(vocab)}
+    ix.term_off, ix.pdoc, ix.pval = term_off, pdoc, pval
+    ix.n_docs = len(docs)
+    runs = ix.score_ids([ix.term_ids(sorted(qq)) for qq in queries], 1000)
+    return lines, q, runs, used
+
+
+def test_bf16x3_end_to_end_quantized_and_metrics(E, base):
+    """Impacts -> impact TSV text -> 8-bit quantized integers -> index -> top-1000 ->
+    MRR@10 / Recall: the bf16x3 run must give the fp32 oracle's metrics, with
+    quantized-integer flips (terms whose integer differs) at most 2e-3 of all terms;
+    the bf16 throughput mode's flip rate is reported beside it."""
+    import oracle
+
+    fx, sd = base
+    rng = np.random.default_rng(7)
+    lens = rng.integers(24, 128, 32).tolist()
+    pad, mask = _random_batch(rng, lens, 250002)
+    ids, cu = _pack(pad.tolist(), mask.tolist())
+    # terms: first occurrence of each token id (term string = "t<id>"), every 2nd token
+    terms, toks = [], []
+    for d, n in enumerate(lens):
+        seen, tt, tk = set(), [], []
+        for i in range(1, n - 1, 2):
+            t = f"t{int(pad[d, i])}"
+            if t not in seen:
+                seen.add(t)
+                tt.append(t)
+                tk.append(i)
+        terms.append(tt)
+        toks.append(tk)
+    tt = np.array([i for tk in toks for i in tk], np.int32)
+    ct = np.cumsum([0] + [len(tk) for tk in toks]).astype(np.int32)
+    want_tok = _oracle(sd, fx, pad, mask)
+    want = [want_tok[d, toks[d]].astype(np.float32) for d in range(len(lens))]
+    queries, qrels = [], {}
+    for qi in range(64):
+        d = int(rng.integers(0, len(lens)))
+        k = min(len(terms[d]), int(rng.integers(2, 7)))
+        queries.append(set(rng.choice(terms[d], size=k, replace=False).tolist()))
+        qrels[qi] = {d}
+    l_ref, q_ref, run_ref, _ = _pipeline(want, terms, queries)
+
+    def evaluate(run):
+        trip = [(qi, doc, r + 1) for qi, res in enumerate(run) for r, (doc, _) in enumerate(res)]
+        return oracle.mrr_recall(trip, qrels)
+
+    m_ref = evaluate(run_ref)
+    res = {}
+    for prec in ("bf16x3", "bf16"):
+        enc = E.DeviceEncoder(sd, _cfg(E, fx), precision=prec)
+        got = enc.encode_packed(ids, cu, tt, ct)
+        del enc
+        per_doc = [got[ct[d]:ct[d + 1]] for d in range(len(lens))]
+        l_got, q_got, run_got, _ = _pipeline(per_doc, terms, queries)
+        qa = [p for l in q_ref for p in (l.split(", ") if l else [])]
+        qb = [p for l in q_got for p in (l.split(", ") if l else [])]
+        text_flip = np.mean([a != b for a, b in zip(
+            [p for l in l_ref for p in l.split(", ")], [p for l in l_got for p in l.split(", ")])])
+        q_flip = (sum(a != b for a, b in zip(qa, qb)) + abs(len(qa) - len(qb))) / max(len(qa), 1)
+        res[prec] = (text_flip, q_flip, evaluate(run_got))
+    print({k: (f"text flips {v[0]:.2e}", f"quantized flips {v[1]:.2e}", v[2][0]) for k, v in
+           res.items()})
+    text_flip, q_flip, m = res["bf16x3"]
+    assert q_flip <= 2e-3, q_flip
+    assert m == m_ref
