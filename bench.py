@@ -56,18 +56,30 @@ def load_pmc_traffic(name):
     return None, None
 
 
-def retrieve_leg(args, rank, world, dev):
+def retrieve_leg(args, rank, world, dev, n_docs=DOCS_PER_SHARD, check_queries=0):
+    """One doc-id shard of n_docs per rank.  100k docs: the numpy generator
+    (synthetic.msmarco_like_docs, one doc at a time); larger shards: the same
+    distribution from the library's threaded generator (synthetic.synth_postings).
+    check_queries > 0: the first that many queries are checked against the oracle's
+    C scorer right after the timed loop."""
     t0 = time.time()
-    cu, term, imp = S.msmarco_like_docs(DOCS_PER_SHARD, V_TERMS, seed=1234 + rank)
-    q, _ = S.quantize_like_reference(imp)
-    term_off, pdoc, pval = S.postings_reference_order(cu, term, q, V_TERMS)
-    doc_lo = rank * DOCS_PER_SHARD
-    pdoc = pdoc + np.uint32(doc_lo)
-    ix = _lib.DeviceIndex.from_postings(term_off, pdoc, pval, doc_lo, doc_lo + DOCS_PER_SHARD,
+    if n_docs == DOCS_PER_SHARD:
+        cu, term, imp = S.msmarco_like_docs(DOCS_PER_SHARD, V_TERMS, seed=1234 + rank)
+        q, _ = S.quantize_like_reference(imp)
+        term_off, pdoc, pval = S.postings_reference_order(cu, term, q, V_TERMS)
+        del cu, term, imp, q
+    else:
+        term_off, pdoc, pval, _ = S.synth_postings(n_docs, V_TERMS, seed=4321 + rank)
+    t_gen = time.time() - t0
+    doc_lo = rank * n_docs
+    if doc_lo:
+        pdoc = pdoc + np.uint32(doc_lo)
+    ix = _lib.DeviceIndex.from_postings(term_off, pdoc, pval, doc_lo, doc_lo + n_docs,
                                         device=dev)
     queries = S.msmarco_like_queries(args.queries, V_TERMS, seed=1234)
     flat, cuq = _lib.csr(queries)
-    log(f"[rank {rank}] shard index: {ix.info()} built in {time.time() - t0:.1f}s")
+    log(f"[rank {rank}] shard index: {ix.info()} generated in {t_gen:.1f}s, built in "
+        f"{time.time() - t0 - t_gen:.1f}s")
 
     stream = torch.cuda.current_stream()
     ix.set_stream(stream.cuda_stream)
@@ -114,6 +126,21 @@ def retrieve_leg(args, rank, world, dev):
     ix.sync()
     ms_sb, n_sb = ix.timing("score_blocks")
     ms_mg, n_mg = ix.timing("merge_topk")
+    if check_queries and rank == 0:
+        sys.path.insert(0, str(ROOT / "oracle"))
+        import oracle
+
+        ora = oracle.Index.__new__(oracle.Index)
+        ora.term_off, ora.pdoc, ora.pval = term_off, pdoc - np.uint32(doc_lo), pval
+        ora.n_docs = n_docs
+        want = ora.score_ids(queries[:check_queries], k, n_threads=min(16, os.cpu_count() or 1))
+        od, osc, on = out_doc.cpu().numpy(), out_score.cpu().numpy(), out_n.cpu().numpy()
+        for i in range(check_queries):
+            got = list(zip((od[i * k:i * k + on[i]] - doc_lo).tolist(),
+                           osc[i * k:i * k + on[i]].tolist()))
+            if got != want[i]:
+                raise SystemExit(f"bench parity check failed on query {i} ({n_docs} docs)")
+        log(f"[rank 0] {n_docs}-doc shard: the first {check_queries} queries equal the oracle")
     if world > 1:
         t = torch.tensor([el], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -127,12 +154,22 @@ def retrieve_leg(args, rank, world, dev):
         "value": nq * args.steps / el,
         "ms_per_step": 1000.0 * el / args.steps,
         "postings_per_query": post_per_launch / nq,
+        "docs": n_docs, "postings": int(ix.info()["n_postings"]), "blocks": ix.info()["n_blocks"],
         "kernel_ms": {"score_blocks": ms_sb / max(n_sb, 1), "merge_topk": ms_mg / max(n_mg, 1)},
+        "kernel_ms_per_step": {"score_blocks": ms_sb / max(args.steps, 1),
+                               "merge_topk": ms_mg / max(args.steps, 1)},
+        "launches_per_step": n_sb / max(args.steps, 1),
     }
-    bytes_per_launch = 4.0 * post_per_launch  # packed u32 posting: (doc_in_block << 8) | value
-    avg_s = (ms_sb / max(n_sb, 1)) / 1000.0
+    # algorithmic bytes of one step (every query's postings, 4 B each: the packed u32
+    # posting (doc_in_block << 8) | value) over the score_blocks time of one step -- a
+    # step is several launches when the candidate workspace splits the queries into
+    # chunks (nb * k * 8 bytes per query, <= 1 GiB per chunk)
+    bytes_per_launch = 4.0 * post_per_launch
+    avg_s = (ms_sb / max(args.steps, 1)) / 1000.0  # score_blocks time per step
     achieved = bytes_per_launch / avg_s / 1e9 if avg_s > 0 else 0.0
-    traffic, src = load_pmc_traffic("score_blocks_kernel")
+    # PMC traffic: the committed summary was measured on the 100k-doc shard only
+    traffic, src = (load_pmc_traffic("score_blocks_kernel") if n_docs == DOCS_PER_SHARD
+                    else (None, None))
     res["roofline"] = {
         "kernel": "score_blocks_kernel",
         "bound": "hbm",
@@ -141,8 +178,8 @@ def retrieve_leg(args, rank, world, dev):
         "unit": "GB/s",
         "frac": round(achieved / HBM_PEAK_GBS, 4),
         "traffic": traffic,
-        "algorithmic_bytes_per_launch": bytes_per_launch,
-        "avg_launch_ms": round(avg_s * 1000.0, 4),
+        "algorithmic_bytes_per_step": bytes_per_launch,
+        "score_blocks_ms_per_step": round(avg_s * 1000.0, 4),
         "launches": n_sb,
         "traffic_source": src,
     }
@@ -398,8 +435,10 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--docs", type=int, default=8192, help="docs encoded per step per GPU (1024: -3%%, 4096: -1%%: the 256-row GEMM tiles quantize less on 256 CUs with more rows)")
     ap.add_argument("--max-len", type=int, default=300)
-    ap.add_argument("--legs", default="encode,encode_x3,retrieve",
-                    help="encode (bf16, configs[1]), encode_x3 (fp32-faithful bf16x3), retrieve")
+    ap.add_argument("--legs", default="encode,encode_x3,retrieve,retrieve_shard",
+                    help="encode (bf16, configs[1]), encode_x3 (fp32-faithful bf16x3), retrieve "
+                         "(100k-doc shard, configs[1]), retrieve_shard (1.1M docs: one 8-way shard "
+                         "of configs[2]), retrieve_full (8.8M docs on one GPU, configs[2])")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -421,6 +460,11 @@ def main():
         x3_res, _ = encode_leg(args, rank, world, dev, precision="bf16x3")
     if "retrieve" in legs:
         ret_res, ret_ctx = retrieve_leg(args, rank, world, dev)
+    big = {}
+    for leg, nd in (("retrieve_shard", 1_100_000), ("retrieve_full", 8_800_000)):
+        if leg in legs:
+            big[leg], _ = retrieve_leg(args, rank, world, dev, n_docs=nd, check_queries=20)
+            torch.cuda.empty_cache()
     primary = enc_res if enc_res is not None else (x3_res if x3_res is not None else ret_res)
     out = {
         "metric": "docs/sec encoded + queries/sec@top-1000, MS MARCO passage, 1/2/4/8 MI355X",
@@ -468,6 +512,13 @@ def main():
                            "postings_per_query": round(ret_res["postings_per_query"], 1),
                            "kernel_ms": ret_res["kernel_ms"], "roofline": ret_res["roofline"],
                            "cpu_baseline": None}
+    for leg, r in big.items():
+        out[leg] = {"value": round(r["value"], 2), "unit": "queries/s",
+                    "docs_per_shard": r["docs"], "postings": r["postings"], "blocks": r["blocks"],
+                    "ms_per_step": round(r["ms_per_step"], 4),
+                    "postings_per_query": round(r["postings_per_query"], 1),
+                    "kernel_ms": r["kernel_ms"], "kernel_ms_per_step": r["kernel_ms_per_step"],
+                    "launches_per_step": r["launches_per_step"], "roofline": r["roofline"]}
     if rank == 0 and world == 1 and not args.no_cpu:
         if enc_res is not None:
             out["cpu_baseline"] = cpu_baseline_encode(args, *enc_ctx)

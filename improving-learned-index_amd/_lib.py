@@ -73,6 +73,8 @@ SIGNATURES = {
     "di_sparse_info": (ctypes.c_int, [P, P, P, P, P]),
     "di_sparse_timing": (ctypes.c_int, [P, ctypes.c_char_p, P, ctypes.c_int]),
     "di_sparse_destroy": (ctypes.c_int, [P]),
+    "di_synth_postings": (ctypes.c_int, [I64, I32, U64, I32, I32, ctypes.c_double, P, P, P, I64,
+                                         P, P]),
 }
 
 _LIB = None

@@ -5,11 +5,14 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdarg>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <map>
 #include <string>
+#include <thread>
 #include <utility>
 #include <vector>
 
@@ -25,6 +28,31 @@ int n_cu();  // compute units of the current device
 struct Error {
     int code;
 };
+
+// Host worker threads of the library's host-side passes (index build, synthetic
+// collections): DI_HOST_THREADS, else OMP_NUM_THREADS (16 on the GPU box), else the
+// hardware count; at most 64.
+inline int host_threads() {
+    const char *e = std::getenv("DI_HOST_THREADS");
+    if (!e) e = std::getenv("OMP_NUM_THREADS");
+    const int t = e ? std::atoi(e) : (int)std::thread::hardware_concurrency();
+    return std::max(1, std::min(t > 0 ? t : 1, 64));
+}
+
+// f(lo, hi, thread) over [0, n) split in host_threads() contiguous ranges.  f must not
+// throw (a worker has no one to report to): collect failures and check them after.
+template <class F>
+void parallel_for(int64_t n, F &&f) {
+    const int T = (int)std::min<int64_t>(host_threads(), std::max<int64_t>(n, 1));
+    if (T == 1) {
+        f((int64_t)0, n, 0);
+        return;
+    }
+    std::vector<std::thread> th;
+    th.reserve((size_t)T);
+    for (int t = 0; t < T; ++t) th.emplace_back([&, t] { f(n * t / T, n * (t + 1) / T, t); });
+    for (auto &x : th) x.join();
+}
 
 [[noreturn]] inline void fail(int code, const char *msg) {
     set_error("%s", msg);

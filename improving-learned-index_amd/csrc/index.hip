@@ -59,6 +59,7 @@ constexpr int WTERMS = 64;
 constexpr int FAST_TERMS = 16;
 constexpr int HIST_BINS = 4096;
 constexpr int TIE_CAP = HIST_BINS;
+constexpr int QH_BINS = 4096;  // per-query candidate-score histogram (shared threshold)
 
 struct ScoreShared {
     uint32_t acc[MAX_BLOCK_DOCS + 64];  // 128 KiB (+ the scatter's dummy words)
@@ -75,6 +76,7 @@ struct ScoreShared {
     uint32_t n_tie;  // tie-list cursor
     uint32_t bad;
     uint32_t thr, above, ties, bin, bin_above;
+    uint32_t tq;  // the query's shared threshold as this item read it
     uint32_t lmask[WTERMS / 32];      // terms (j < WTERMS) with a per-wave layout in this block
     uint32_t wtab[WTERMS][WSEG];      // their per-wave runs: start << 16 | end (in the sublist)
 };
@@ -274,7 +276,7 @@ __device__ __forceinline__ void scatter_apply_own(const uint32_t (&cur)[UU], uin
 __device__ unsigned long long g_sb_phase[8];
 
 // One work item = (query q, doc block b): accumulate, select the block's top-k.
-__device__ __forceinline__ void score_item(ScoreShared &sh, int item,
+__device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
                                            const uint32_t *__restrict__ post,
                                            const int64_t *__restrict__ term_start,
                                            const uint32_t *__restrict__ blk_off,
@@ -285,11 +287,10 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int item,
                                            uint32_t doc_lo, const uint32_t *__restrict__ q_terms,
                                            const int32_t *__restrict__ cu_q, int k,
                                            uint64_t *__restrict__ cand_key,
-                                           int32_t *__restrict__ cand_n, int ablate) {
+                                           int32_t *__restrict__ cand_n,
+                                           uint32_t *__restrict__ qhist, int ablate) {
     int64_t *lo = sh.v.bounds[0], *hi = sh.v.bounds[1];
 
-    const int b = item % nb;
-    const int q = item / nb;
     // opaque per item: keeps the per-thread index arithmetic of the sweeps from being
     // hoisted out of the persistent item loop (it spilled there)
     int tid = threadIdx.x;
@@ -526,9 +527,15 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int item,
                 ck[pos] = key;
         }
     };
-    auto flush = [&](uint32_t n_c) {  // after a barrier
-        if (staged)
-            for (uint32_t i = tid; i < n_c; i += SC_THREADS) ck[i] = stage[i];
+    // final candidates: copied out (staged) and counted into the query's score
+    // histogram (qhist, see below); called once per item, after a barrier
+    uint32_t *qh = qhist ? qhist + (int64_t)q * QH_BINS : nullptr;
+    auto flush = [&](uint32_t n_c) {
+        for (uint32_t i = tid; i < n_c; i += SC_THREADS) {
+            const uint64_t key = staged ? stage[i] : ck[i];
+            if (staged) ck[i] = key;
+            if (qh) atomicAdd(&qh[min((uint32_t)(key >> 48), (uint32_t)QH_BINS - 1)], 1u);
+        }
     };
     auto emit_all_touched = [&]() {
         const uint32_t n = compact_words(sh, n_local, tid, [](uint32_t w, int) { return w ? 1u : 0u; },
@@ -538,6 +545,55 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int item,
         flush(min(n & 0xFFFFu, (uint32_t)k));
         if (tid == 0) *cn = (int32_t)min(n & 0xFFFFu, (uint32_t)k);
     };
+
+    // Shared per-query threshold.  qhist[q] (when given) counts the scores of every
+    // candidate the query's finished blocks emitted (distinct docs, full scores; bin
+    // 4095 = 4095 and above).  Tq = the largest s with >= k counted candidates scoring
+    // >= s: at least k docs score >= Tq, so the final k-th score is >= Tq and a doc
+    // below Tq cannot be in the query's top-k.  When at most k of this block's docs
+    // reach Tq they are its only candidates (no histogram, no tie order -- the merge
+    // orders them by key); else the full selection below runs.  Items run block-major
+    // (all queries' block 0 first), so Tq is close to the final k-th score after the
+    // first blocks and the later blocks emit few candidates.  A stale (smaller) count
+    // still gives a valid lower bound.
+    uint32_t Tq = 0;
+    if (qh) {
+        // thread t: bins 4t..4t+3 (relaxed atomic loads: other CUs add to them)
+        uint32_t hv[4], c = 0;
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+            c += (hv[e] = __hip_atomic_load(&qh[4 * tid + e], __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_AGENT));
+        uint32_t sfx = wave_suffix_sum(c);
+        if (lane == 0) sh.wsum[wave] = sfx;
+        if (tid == 0) sh.tq = 0;
+        __syncthreads();
+        for (int w2 = wave + 1; w2 < SC_WAVES; ++w2) sfx += sh.wsum[w2];
+        // one thread holds the crossing: count(>= 4t + e) >= k > count(>= 4t + e + 1)
+        if (sfx >= (uint32_t)k && sfx - c < (uint32_t)k) {
+            uint32_t above = sfx - c;
+            int e = 3;
+            for (; e > 0; --e) {
+                if (above + hv[e] >= (uint32_t)k) break;
+                above += hv[e];
+            }
+            sh.tq = (uint32_t)(4 * tid + e);
+        }
+        __syncthreads();
+        Tq = sh.tq;
+        if (Tq > 0) {
+            const uint32_t thr_w = Tq << 16;
+            const uint32_t n = compact_words(
+                sh, n_local, tid, [thr_w](uint32_t w, int) { return w >= thr_w ? 1u : 0u; },
+                [&](int, uint32_t pos, uint32_t w, int idx) { cand(pos, w, idx); });
+            const uint32_t na = n & 0xFFFFu;
+            if (na <= (uint32_t)k) {
+                flush(na);
+                if (tid == 0) *cn = (int32_t)na;
+                return;
+            }
+        }
+    }
 
     uint32_t prefix = 0, mask = 0, need = (uint32_t)k;
     int shift = 24;  // next digit of the general radix path
@@ -588,6 +644,7 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int item,
         }
         const uint32_t T = sh.thr, ties = sh.ties;  // T >= 1: every touched score is
         const uint32_t above = sh.above;             // nonzero
+
         need -= above;
         if (ties == need || ties <= (uint32_t)TIE_CAP) {
             // scores above T are in; the ties at T all go in, or into a list (the
@@ -756,6 +813,7 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int item,
     }
     const uint32_t T = prefix;
     const uint32_t ties = sh.u.rs.tot[sh.u.rs.bin];
+
     // doc-order cut among the ties: the `need` smallest doc indices
     // (all ties when exactly `need` of them exist)
     uint32_t dcut = 0;
@@ -796,7 +854,8 @@ score_blocks_kernel(const uint32_t *__restrict__ post, const int64_t *__restrict
                     int min_cls, int nb, int block_docs, int64_t n_terms,
                     uint32_t n_docs, uint32_t doc_lo, const uint32_t *__restrict__ q_terms,
                     const int32_t *__restrict__ cu_q, int k, uint64_t *__restrict__ cand_key,
-                    int32_t *__restrict__ cand_n, int n_items, int ablate) {
+                    int32_t *__restrict__ cand_n, int n_items, int n_q,
+                    uint32_t *__restrict__ qhist, int ablate) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     ScoreShared &sh = *reinterpret_cast<ScoreShared *>(smem);
     if ((uint32_t)(uintptr_t)((__attribute__((address_space(3))) unsigned char *)smem) != 0) {
@@ -806,11 +865,11 @@ score_blocks_kernel(const uint32_t *__restrict__ post, const int64_t *__restrict
             if (threadIdx.x == 0) cand_n[item] = -1;
         return;
     }
+    // items block-major: item = b * n_q + q (the shared threshold, see score_item)
     for (int item = blockIdx.x; item < n_items; item += gridDim.x) {
-        score_item(sh, item, post, term_start, blk_off, seg, lid, wmeta, min_cls, nb, block_docs,
-                   n_terms,
-                   n_docs, doc_lo,
-                   q_terms, cu_q, k, cand_key, cand_n, ablate);
+        score_item(sh, item % n_q, item / n_q, post, term_start, blk_off, seg, lid, wmeta,
+                   min_cls, nb, block_docs, n_terms, n_docs, doc_lo, q_terms, cu_q, k, cand_key,
+                   cand_n, qhist, ablate);
         __syncthreads();  // every wave is done with the LDS of this item
     }
 }
@@ -865,16 +924,32 @@ merge_topk_kernel(const uint64_t *__restrict__ keys, const int32_t *__restrict__
     int64_t total = 0;
     const bool fast_lists = n_lists <= 1024;
     if (fast_lists) {
-        for (int l = tid; l < n_lists; l += THREADS) {
-            int c = cnt(l);
-            if (c < 0) sh.bad = 1;
-            sh.off[l + 1] = min(max(c, 0), k_in);
+        // list offsets by a block scan (thread t owns lists LPT t .. LPT t + LPT - 1):
+        // a serial scan by one thread cost ~10 us per query at 269 lists
+        constexpr int LPT = (1024 + THREADS - 1) / THREADS;
+        int c[LPT];
+        uint32_t run = 0;
+#pragma unroll
+        for (int j = 0; j < LPT; ++j) {
+            const int l = tid * LPT + j;
+            c[j] = l < n_lists ? cnt(l) : 0;
+            if (c[j] < 0) sh.bad = 1;
+            c[j] = min(max(c[j], 0), k_in);
+            run += (uint32_t)c[j];
         }
+        const uint32_t incl = wave_prefix_sum(run);
+        const int lane = tid & 63, w = tid >> 6;
+        if (lane == 63) sh.wtot[w] = incl;
         __syncthreads();
-        if (tid == 0) {
-            sh.off[0] = 0;
-            for (int l = 0; l < n_lists; ++l) sh.off[l + 1] += sh.off[l];
+        uint32_t base = incl - run;
+        for (int v = 0; v < w; ++v) base += sh.wtot[v];
+#pragma unroll
+        for (int j = 0; j < LPT; ++j) {
+            const int l = tid * LPT + j;
+            base += (uint32_t)c[j];
+            if (l < n_lists) sh.off[l + 1] = (int32_t)base;
         }
+        if (tid == 0) sh.off[0] = 0;
         __syncthreads();
         total = sh.off[n_lists];
     } else {
@@ -1063,7 +1138,11 @@ struct di_index {
     std::vector<uint32_t> lid;       // long-sublist ids (pass 3)
     std::vector<uint16_t> wmeta;     // per-wave class ends of the long sublists
     DevBuf post, term_start, blk_off, seg_dev, lid_dev, wmeta_dev;
-    DevBuf ws_q, ws_cu, ws_ck, ws_cn, ws_doc, ws_score, ws_n, ws_key;
+    DevBuf ws_q, ws_cu, ws_ck, ws_cn, ws_doc, ws_score, ws_n, ws_key, ws_thr;
+    // per-query threshold shared across blocks: -1 = auto (on from 8 blocks: at 4 blocks it
+    // measured 2.31 vs 2.14 ms per 6980-query batch, at 34 / 269 blocks 16.9 vs 19.5 and
+    // 130 vs 161 ms, merge 0.5 vs 7.1 and 1.4 vs 74 ms); DI_SCORE_THRESHOLD=0 / 1 forces
+    int shared_thr = -1;
     int ablate = 0;  // DI_PROFILE_ABLATE: profiling only (1 no scatter, 2 no selection, 4 stop at the k-th score)
     Timer timer;
 };
@@ -1113,41 +1192,49 @@ void build_index(di_index *ix, const int64_t *term_off, int64_t n_terms, const u
     const int64_t stride = nb + 1;
     std::vector<int64_t> tstart(std::max<int64_t>(n_terms, 1), 0);
     std::vector<uint32_t> boff((size_t)std::max<int64_t>(n_terms * stride, 1), 0);
+    // The three passes run over term ranges on host_threads() threads (every term owns
+    // disjoint output ranges); the result does not depend on the thread count.
     // pass 1: per (term, block) counts of kept postings
+    parallel_for(n_terms, [&](int64_t t0, int64_t t1, int) {
+        std::vector<uint32_t> cnt(stride);
+        for (int64_t t = t0; t < t1; ++t) {
+            std::fill(cnt.begin(), cnt.end(), 0);
+            for (int64_t p = term_off[t]; p < term_off[t + 1]; ++p) {
+                if (pval[p] == 0) break;  // inverted_index.py:50-51
+                uint32_t d = pdoc[p];
+                if (d < doc_lo || d >= doc_hi) continue;
+                cnt[(d - doc_lo) / bd]++;
+            }
+            uint32_t run = 0;
+            for (int b = 0; b < nb; ++b) {
+                boff[t * stride + b] = run;
+                run += cnt[b];
+            }
+            boff[t * stride + nb] = run;
+        }
+    });
     int64_t total = 0;
-    std::vector<uint32_t> cnt(stride);
     for (int64_t t = 0; t < n_terms; ++t) {
-        std::fill(cnt.begin(), cnt.end(), 0);
-        for (int64_t p = term_off[t]; p < term_off[t + 1]; ++p) {
-            if (pval[p] == 0) break;  // inverted_index.py:50-51
-            uint32_t d = pdoc[p];
-            if (d < doc_lo || d >= doc_hi) continue;
-            cnt[(d - doc_lo) / bd]++;
-        }
         tstart[t] = total;
-        uint32_t run = 0;
-        for (int b = 0; b < nb; ++b) {
-            boff[t * stride + b] = run;
-            run += cnt[b];
-        }
-        boff[t * stride + nb] = run;
-        total += run;
+        total += boff[t * stride + nb];
     }
     ix->n_post = total;
     std::vector<uint32_t> packed((size_t)std::max<int64_t>(total, 4));
     // pass 2: place (stable: keeps value-desc/doc-asc inside each block)
-    std::vector<uint32_t> cur(stride);
-    for (int64_t t = 0; t < n_terms; ++t) {
-        for (int b = 0; b <= nb; ++b) cur[b] = boff[t * stride + b];
-        for (int64_t p = term_off[t]; p < term_off[t + 1]; ++p) {
-            if (pval[p] == 0) break;
-            uint32_t d = pdoc[p];
-            if (d < doc_lo || d >= doc_hi) continue;
-            uint32_t r = d - doc_lo;
-            int b = (int)(r / bd);
-            packed[tstart[t] + cur[b]++] = ((r % bd) << 8) | pval[p];
+    parallel_for(n_terms, [&](int64_t t0, int64_t t1, int) {
+        std::vector<uint32_t> cur(stride);
+        for (int64_t t = t0; t < t1; ++t) {
+            for (int b = 0; b <= nb; ++b) cur[b] = boff[t * stride + b];
+            for (int64_t p = term_off[t]; p < term_off[t + 1]; ++p) {
+                if (pval[p] == 0) break;
+                uint32_t d = pdoc[p];
+                if (d < doc_lo || d >= doc_hi) continue;
+                uint32_t r = d - doc_lo;
+                int b = (int)(r / bd);
+                packed[tstart[t] + cur[b]++] = ((r % bd) << 8) | pval[p];
+            }
         }
-    }
+    });
     // pass 3: order inside every (term, block) sublist, and the impact-class offsets.
     // Postings are grouped by impact class c = 7 - floor(log2 value) (class 0 = values
     // 128..255, ..., class 7 = value 1), classes in order, so that "every posting with
@@ -1164,88 +1251,94 @@ void build_index(di_index *ix, const int64_t *term_off, int64_t n_terms, const u
     // its postings of the sublist form one run (classes in order, bank-dealt inside),
     // so that consecutive long terms need no barrier (no two waves touch one doc).
     // wmeta[lid * 128 + 8 w + c] = end of class c of segment w (offset in the
-    // sublist), lid[t * nb + b] = the sublist's long id (0xFFFFFFFF: short).
+    // sublist), lid[t * nb + b] = the sublist's long id (0xFFFFFFFF: short), ids in
+    // (term, block) order.
     ix->lid.assign((size_t)std::max<int64_t>(n_terms * nb, 1), 0xFFFFFFFFu);
-    ix->wmeta.clear();
     {
-        auto cls_of = [](uint32_t w) { return 7 - (31 - __builtin_clz(w & 255u)); };
-        const uint32_t S = (bd + WSEG - 1) / WSEG;
         static const int64_t wlong_min = [] {  // A/B: DI_WLONG_MIN (postings)
             const char *e = std::getenv("DI_WLONG_MIN");
             return e ? (int64_t)std::atoll(e) : (int64_t)WLONG_MIN;
         }();
-        std::vector<uint32_t> grp, tmp, bk, cls_cnt(8), cls_pos(8), bucket_cnt(32), head(32),
-            fill(32);
-        // one group (any order in): classes in order (stable), each dealt round-robin
-        // from its 32 LDS bank buckets (doc_in_block mod 32) into packed[o..];
-        // cum[c] = end of class c relative to the sublist start s0
-        auto emit_group = [&](const uint32_t *in, size_t n, int64_t &o, int64_t s0,
-                              uint16_t *cum) {
-            std::fill(cls_cnt.begin(), cls_cnt.end(), 0);
-            for (size_t i = 0; i < n; ++i) cls_cnt[cls_of(in[i])]++;
-            uint32_t run = 0;
-            for (int c = 0; c < 8; ++c) {
-                cls_pos[c] = run;
-                run += cls_cnt[c];
+        uint32_t n_long = 0;
+        for (int64_t t = 0; t < n_terms; ++t)
+            for (int b = 0; b < nb; ++b)
+                if ((int64_t)(boff[t * stride + b + 1] - boff[t * stride + b]) >= wlong_min)
+                    ix->lid[(size_t)(t * nb + b)] = n_long++;
+        ix->wmeta.assign((size_t)n_long * WSEG * 8, 0);
+        auto cls_of = [](uint32_t w) { return 7 - (31 - __builtin_clz(w & 255u)); };
+        const uint32_t S = (bd + WSEG - 1) / WSEG;
+        parallel_for(n_terms, [&](int64_t t0, int64_t t1, int) {
+            std::vector<uint32_t> grp, tmp, bk, seg_in, cls_cnt(8), cls_pos(8), bucket_cnt(32),
+                head(32), fill(32);
+            // one group (any order in): classes in order (stable), each dealt round-robin
+            // from its 32 LDS bank buckets (doc_in_block mod 32) into packed[o..];
+            // cum[c] = end of class c relative to the sublist start s0
+            auto emit_group = [&](const uint32_t *in, size_t n, int64_t &o, int64_t s0,
+                                  uint16_t *cum) {
+                std::fill(cls_cnt.begin(), cls_cnt.end(), 0);
+                for (size_t i = 0; i < n; ++i) cls_cnt[cls_of(in[i])]++;
+                uint32_t run = 0;
+                for (int c = 0; c < 8; ++c) {
+                    cls_pos[c] = run;
+                    run += cls_cnt[c];
+                }
+                tmp.resize(n);
+                for (size_t i = 0; i < n; ++i) tmp[cls_pos[cls_of(in[i])]++] = in[i];
+                uint32_t c0 = 0;
+                for (int c = 0; c < 8; ++c) {
+                    const uint32_t c1 = c0 + cls_cnt[c];
+                    std::fill(bucket_cnt.begin(), bucket_cnt.end(), 0);
+                    for (uint32_t i = c0; i < c1; ++i) bucket_cnt[(tmp[i] >> 8) & 31]++;
+                    uint32_t r = 0;
+                    for (int k = 0; k < 32; ++k) {
+                        head[k] = r;
+                        r += bucket_cnt[k];
+                    }
+                    bk.resize(c1 - c0);
+                    fill = head;
+                    for (uint32_t i = c0; i < c1; ++i) bk[fill[(tmp[i] >> 8) & 31]++] = tmp[i];
+                    for (bool any = true; any;) {
+                        any = false;
+                        for (int k = 0; k < 32; ++k)
+                            if (bucket_cnt[k]) {
+                                packed[o++] = bk[head[k]++];
+                                --bucket_cnt[k];
+                                any = true;
+                            }
+                    }
+                    if (cum) cum[c] = (uint16_t)(o - s0);
+                    c0 = c1;
+                }
+            };
+            for (int64_t t = t0; t < t1; ++t) {
+                for (int b = 0; b < nb; ++b) {
+                    const int64_t s0 = tstart[t] + boff[t * stride + b];
+                    const int64_t s1 = tstart[t] + boff[t * stride + b + 1];
+                    if (s1 == s0) continue;
+                    uint16_t *sg = &ix->seg[(size_t)(t * nb + b) * 8];
+                    grp.assign(packed.begin() + s0, packed.begin() + s1);
+                    int64_t o = s0;
+                    const uint32_t id = ix->lid[(size_t)(t * nb + b)];
+                    if (id == 0xFFFFFFFFu) {
+                        emit_group(grp.data(), grp.size(), o, s0, sg);
+                        continue;
+                    }
+                    {  // whole-sublist class counts (seg), then the per-wave layout
+                        uint32_t run = 0, cc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+                        for (uint32_t x : grp) cc[cls_of(x)]++;
+                        for (int c = 0; c < 8; ++c) sg[c] = (uint16_t)(run += cc[c]);
+                    }
+                    for (int w = 0; w < WSEG; ++w) {
+                        seg_in.clear();
+                        for (uint32_t x : grp)
+                            if (std::min<uint32_t>((x >> 8) / S, WSEG - 1) == (uint32_t)w)
+                                seg_in.push_back(x);
+                        emit_group(seg_in.data(), seg_in.size(), o, s0,
+                                   &ix->wmeta[(size_t)id * WSEG * 8 + w * 8]);
+                    }
+                }
             }
-            tmp.resize(n);
-            for (size_t i = 0; i < n; ++i) tmp[cls_pos[cls_of(in[i])]++] = in[i];
-            uint32_t c0 = 0;
-            for (int c = 0; c < 8; ++c) {
-                const uint32_t c1 = c0 + cls_cnt[c];
-                std::fill(bucket_cnt.begin(), bucket_cnt.end(), 0);
-                for (uint32_t i = c0; i < c1; ++i) bucket_cnt[(tmp[i] >> 8) & 31]++;
-                uint32_t r = 0;
-                for (int k = 0; k < 32; ++k) {
-                    head[k] = r;
-                    r += bucket_cnt[k];
-                }
-                bk.resize(c1 - c0);
-                fill = head;
-                for (uint32_t i = c0; i < c1; ++i) bk[fill[(tmp[i] >> 8) & 31]++] = tmp[i];
-                for (bool any = true; any;) {
-                    any = false;
-                    for (int k = 0; k < 32; ++k)
-                        if (bucket_cnt[k]) {
-                            packed[o++] = bk[head[k]++];
-                            --bucket_cnt[k];
-                            any = true;
-                        }
-                }
-                if (cum) cum[c] = (uint16_t)(o - s0);
-                c0 = c1;
-            }
-        };
-        for (int64_t t = 0; t < n_terms; ++t) {
-            for (int b = 0; b < nb; ++b) {
-                const int64_t s0 = tstart[t] + boff[t * stride + b];
-                const int64_t s1 = tstart[t] + boff[t * stride + b + 1];
-                uint16_t *sg = &ix->seg[(size_t)(t * nb + b) * 8];
-                grp.assign(packed.begin() + s0, packed.begin() + s1);
-                int64_t o = s0;
-                if (s1 - s0 < wlong_min) {
-                    emit_group(grp.data(), grp.size(), o, s0, sg);
-                    continue;
-                }
-                {  // whole-sublist class counts (seg), then the per-wave layout
-                    uint32_t run = 0, cc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-                    for (uint32_t x : grp) cc[cls_of(x)]++;
-                    for (int c = 0; c < 8; ++c) sg[c] = (uint16_t)(run += cc[c]);
-                }
-                const uint32_t id = (uint32_t)(ix->wmeta.size() / (WSEG * 8));
-                ix->lid[(size_t)(t * nb + b)] = id;
-                ix->wmeta.resize(ix->wmeta.size() + WSEG * 8);
-                std::vector<uint32_t> seg_in;
-                for (int w = 0; w < WSEG; ++w) {
-                    seg_in.clear();
-                    for (uint32_t x : grp)
-                        if (std::min<uint32_t>((x >> 8) / S, WSEG - 1) == (uint32_t)w)
-                            seg_in.push_back(x);
-                    emit_group(seg_in.data(), seg_in.size(), o, s0,
-                               &ix->wmeta[(size_t)id * WSEG * 8 + w * 8]);
-                }
-            }
-        }
+        });
     }
     for (auto &w : packed) w ^= POST_X;  // device encoding (see POST_X)
     ix->post.reserve(packed.size() * 4);
@@ -1296,8 +1389,10 @@ void launch_merge(const uint64_t *keys, const int32_t *counts, int n_q, int n_li
     }
     // LDS key capacity: all candidates when they fit, else the k survivors of the
     // slow path's radix select
+    // (many lists: the score_blocks shared threshold leaves ~k + a few candidates per
+    // query, so an 8192-key array -- the selection path's maximum -- usually holds them)
     int64_t want = (int64_t)n_lists * k_in;
-    if (n_lists > 1024 || want > MG_LDS_KEYS) want = k;
+    if (n_lists > 1024 || want > MG_LDS_KEYS) want = std::max<int64_t>(k, MG_SEL_CAP);
     int cap = 64;
     while (cap < want) cap <<= 1;
     // workgroup size of the merge (DI_MERGE_THREADS: A/B knob); 512 measured best for
@@ -1357,6 +1452,8 @@ int di_index_create(const int64_t *term_off, int64_t n_terms, const uint32_t *pd
             if (sw[0] == '0') ix->ablate |= 128;
         if (const char *ss = std::getenv("DI_SCATTER_SHORT"))  // A/B: 0 = barrier form for
             if (ss[0] == '0') ix->ablate |= 256;                  // the short terms
+        if (const char *st = std::getenv("DI_SCORE_THRESHOLD"))  // (tested both ways)
+            ix->shared_thr = st[0] != '0' ? 1 : 0;
         build_index(ix.get(), term_off, n_terms, pdoc, pval, doc_lo, doc_hi);
         *out = ix.release();
     });
@@ -1448,6 +1545,7 @@ int di_index_search(di_index *ix, const uint32_t *q_terms, const int32_t *cu_q, 
         const int chunk = (int)std::max<int64_t>(1, std::min<int64_t>(n_q, (1ll << 30) / per_q));
         ix->ws_ck.reserve((size_t)chunk * per_q);
         ix->ws_cn.reserve((size_t)chunk * nb * 4);
+        ix->ws_thr.reserve((size_t)chunk * QH_BINS * 4);
         const uint32_t *dq = (const uint32_t *)stage_in(
             q_terms, (size_t)nterms_total * 4, dev, ix->ws_q, s);
         const int32_t *dcu =
@@ -1472,6 +1570,8 @@ int di_index_search(di_index *ix, const uint32_t *q_terms, const int32_t *cu_q, 
             if (ix->nb == 0) {
                 DI_HIP(hipMemsetAsync(ix->ws_cn.p, 0, (size_t)nq * nb * 4, s));
             } else {
+                const bool thr = nb > 1 && (ix->shared_thr < 0 ? nb >= 8 : ix->shared_thr == 1);
+                if (thr) DI_HIP(hipMemsetAsync(ix->ws_thr.p, 0, (size_t)nq * QH_BINS * 4, s));
                 TimedLaunch tl(ix->timer, timing, "score_blocks", s);
                 const int n_items = nq * nb;
                 hipLaunchKernelGGL(score_blocks_kernel, dim3(std::min(n_items, n_cu())),
@@ -1482,7 +1582,7 @@ int di_index_search(di_index *ix, const uint32_t *q_terms, const int32_t *cu_q, 
                                    ix->min_cls, nb, ix->block_docs, ix->n_terms,
                                    ix->n_docs, ix->doc_lo, dq, dcu + q0, k,
                                    ix->ws_ck.as<uint64_t>(), ix->ws_cn.as<int32_t>(), n_items,
-                                   ix->ablate);
+                                   nq, thr ? ix->ws_thr.as<uint32_t>() : nullptr, ix->ablate);
                 check_launch("score_blocks");
             }
             {

@@ -70,3 +70,25 @@ def msmarco_like_queries(n_q, v_terms=200_000, seed=1234, draws=6):
         z = np.minimum(rng.zipf(1.3, draws), v_terms) - 1
         out.append(list(dict.fromkeys(int(x) for x in z)))
     return out
+
+
+def synth_postings(n_docs, v_terms=200_000, seed=1234, max_terms=100, draws=200, zipf_a=1.2):
+    """The same generator at full scale, in the HIP library's host code (threads over
+    doc chunks, a counter-based stream per doc): reference-order postings
+    (term_off, pdoc u32, pval u8) of the quantized collection and the fp64 max impact.
+    Same distribution as msmarco_like_docs -> quantize_like_reference ->
+    postings_reference_order; a different random stream (seconds at 8.8 M docs)."""
+    import ctypes
+
+    from ._lib import check, lib, ptr
+
+    term_off = np.zeros(v_terms + 1, np.int64)
+    cap = int(n_docs) * int(max_terms)
+    pdoc = np.empty(max(cap, 1), np.uint32)
+    pval = np.empty(max(cap, 1), np.uint8)
+    n = ctypes.c_int64(0)
+    m = ctypes.c_double(0.0)
+    check(lib().di_synth_postings(int(n_docs), int(v_terms), int(seed), int(max_terms),
+                                  int(draws), float(zipf_a), ptr(term_off), ptr(pdoc), ptr(pval),
+                                  cap, ctypes.byref(n), ctypes.byref(m)))
+    return term_off, pdoc[:n.value], pval[:n.value], m.value

@@ -245,6 +245,19 @@ int di_format_impact_lines(const char *terms, const int64_t *term_off, const flo
                            const int64_t *cu_doc_terms, int32_t n_docs, char *out,
                            int64_t out_cap, int64_t *out_len);
 
+/* ======================================================================
+ * Bench / test data (not a reference interface)
+ * ====================================================================== */
+/* Seeded MS MARCO-shaped quantized collection (SURVEY §8d generator: per doc the
+ * first max_terms unique values of `draws` draws of min(zipf(zipf_a), v_terms),
+ * impacts float32(softplus(N(-0.5, 1.5))), round3 + fp64 8-bit quantize, zeros
+ * dropped), returned as reference-order postings (term_off[v_terms + 1], then per
+ * term value desc / doc asc, create.py:41).  pdoc / pval may be null (sizes only);
+ * else cap >= *n_post.  Host threads: DI_HOST_THREADS or OMP_NUM_THREADS. */
+int di_synth_postings(int64_t n_docs, int32_t v_terms, uint64_t seed, int32_t max_terms,
+                      int32_t draws, double zipf_a, int64_t *term_off, uint32_t *pdoc,
+                      uint8_t *pval, int64_t cap, int64_t *n_post, double *max_impact);
+
 /* Decoding of a quantized-index merge key. */
 static inline uint32_t di_key_doc(uint64_t key) { return 0xFFFFFFFFu - (uint32_t)key; }
 static inline uint32_t di_key_score(uint64_t key) { return (uint32_t)(key >> 48); }

@@ -186,3 +186,43 @@ def test_inverted_index_min_impact_matches_pruned_oracle(L):
     assert [[list(x) for x in g] for g in ix.score_batch(fx["queries"], 1000)] == fx["top1000"]
     with pytest.raises(Exception):
         ix.set_min_impact(0)
+
+
+def test_shared_threshold_off_equals_oracle(L, synth, monkeypatch):
+    """The per-query threshold shared across blocks (default) and the plain per-block
+    top-k (DI_SCORE_THRESHOLD=0) both rank exactly as the oracle."""
+    term_off, pdoc, pval, ora = synth
+    qs = _queries(5000, 80, seed=3, long_every=20)
+    want = ora.score_ids(qs, 1000, n_threads=8)
+    monkeypatch.setenv("DI_SCORE_THRESHOLD", "0")
+    off = L.DeviceIndex.from_postings(term_off, pdoc, pval)
+    assert off.search(qs, 1000) == want
+    monkeypatch.setenv("DI_SCORE_THRESHOLD", "1")
+    on = L.DeviceIndex.from_postings(term_off, pdoc, pval)
+    assert on.search(qs, 1000) == want
+    assert on.search(qs, 7) == ora.score_ids(qs, 7, n_threads=8)
+
+
+@pytest.fixture(scope="module")
+def million():
+    """One 8-way shard of configs[2] (full MS MARCO: 8.8 M docs): 1.1 M docs, 34 LDS
+    blocks, ~100 M postings (the library's threaded generator, same distribution as
+    the 100k bench shard)."""
+    from improving_learned_index_amd import synthetic as S
+
+    term_off, pdoc, pval, _ = S.synth_postings(1_100_000, 200_000, seed=99)
+    ora = oracle.Index.__new__(oracle.Index)
+    ora.term_off, ora.pdoc, ora.pval = term_off, pdoc, pval
+    ora.n_docs = 1_100_000
+    return term_off, pdoc, pval, ora
+
+
+@pytest.mark.parametrize("k", [10, 1000])
+def test_million_doc_shard_matches_oracle(L, million, k):
+    from improving_learned_index_amd import synthetic as S
+
+    term_off, pdoc, pval, ora = million
+    dev = L.DeviceIndex.from_postings(term_off, pdoc, pval, 0, ora.n_docs)
+    assert dev.info()["n_blocks"] == 34
+    qs = S.msmarco_like_queries(24, 200_000, seed=k) + _queries(200_000, 8, seed=k)
+    assert dev.search(qs, k) == ora.score_ids(qs, k, n_threads=16)
