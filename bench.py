@@ -42,10 +42,12 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def load_pmc_traffic(name):
+def load_pmc_traffic(name, leg=None):
     """Per-launch HBM bytes of kernel `name` from the committed rocprofv3 PMC
-    summary (profiles/*pmc*.json, produced by tools/pmc_summary.py), or None."""
-    for p in sorted((ROOT / "profiles").glob("*pmc*.json"), reverse=True):
+    summaries (tools/pmc_legs.sh -> profiles/<round>_pmc_<leg>.json for a bench leg;
+    profiles/*pmc_summary*.json from tools/pmc.sh), newest first, or None."""
+    pats = ([f"*pmc_{leg}.json"] if leg else []) + ["*pmc_summary*.json"]
+    for p in [q for pat in pats for q in sorted((ROOT / "profiles").glob(pat), reverse=True)]:
         try:
             d = json.loads(p.read_text())
         except Exception:
@@ -167,9 +169,13 @@ def retrieve_leg(args, rank, world, dev, n_docs=DOCS_PER_SHARD, check_queries=0)
     bytes_per_launch = 4.0 * post_per_launch
     avg_s = (ms_sb / max(args.steps, 1)) / 1000.0  # score_blocks time per step
     achieved = bytes_per_launch / avg_s / 1e9 if avg_s > 0 else 0.0
-    # PMC traffic: the committed summary was measured on the 100k-doc shard only
-    traffic, src = (load_pmc_traffic("score_blocks_kernel") if n_docs == DOCS_PER_SHARD
-                    else (None, None))
+    # PMC traffic (beyond-L2 bytes: FETCH_SIZE counts Infinity-Cache hits too) of the
+    # leg's own summary, per launch -> per step
+    leg = {DOCS_PER_SHARD: "retrieve", 1_100_000: "retrieve_shard",
+           8_800_000: "retrieve_full"}.get(n_docs)
+    traffic, src = load_pmc_traffic("score_blocks_kernel", leg) if leg else (None, None)
+    if traffic is not None:
+        traffic *= n_sb / max(args.steps, 1)
     res["roofline"] = {
         "kernel": "score_blocks_kernel",
         "bound": "hbm",
@@ -338,9 +344,9 @@ def encode_leg(args, rank, world, dev, precision="bf16"):
     pmc_name = {"gemm_qkv": "gemm256_kernel<5>", "gemm_ffn1": "gemm256_kernel<6>",
                 "gemm_o": "gemm256_kernel<7>", "gemm_ffn2": "gemm256_kernel<7>"}[dom]
     if split:  # gemm256_kernel<EPI, true>: EPI 3 = QKV, 1 = bias + GELU, 2 = residual
-        pmc_name = {"gemm_qkv": "gemm256_kernel<3, true>", "gemm_ffn1": "gemm256_kernel<1, true>",
-                    "gemm_o": "gemm256_kernel<2, true>", "gemm_ffn2": "gemm256_kernel<2, true>"}[dom]
-    traffic, src = load_pmc_traffic(pmc_name)
+        pmc_name = {"gemm_qkv": "gemm256_kernel<3,true>", "gemm_ffn1": "gemm256_kernel<1,true>",
+                    "gemm_o": "gemm256_kernel<2,true>", "gemm_ffn2": "gemm256_kernel<2,true>"}[dom]
+    traffic, src = load_pmc_traffic(pmc_name, "encode_x3" if split else "encode")
     # bf16x3: algorithmic (fp32) FLOPs against the split scheme's own peak -- three
     # bf16 MFMA products per fp32 product, 2500 / 3 TF/s (the f32 MFMA peak is 157.3)
     peak = MFMA_BF16_PEAK_TFLOPS / 3.0 if split else MFMA_BF16_PEAK_TFLOPS
@@ -465,11 +471,14 @@ def main():
         if leg in legs:
             big[leg], _ = retrieve_leg(args, rank, world, dev, n_docs=nd, check_queries=20)
             torch.cuda.empty_cache()
-    primary = enc_res if enc_res is not None else (x3_res if x3_res is not None else ret_res)
+    primary = next((r for r in (enc_res, x3_res, ret_res) + tuple(big.values())
+                    if r is not None), None)
+    if primary is None:
+        raise SystemExit("no bench leg selected")
     out = {
         "metric": "docs/sec encoded + queries/sec@top-1000, MS MARCO passage, 1/2/4/8 MI355X",
         "value": round(primary["value"], 2),
-        "unit": "queries/s" if primary is ret_res else "docs/s",
+        "unit": "docs/s" if primary is enc_res or primary is x3_res else "queries/s",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,

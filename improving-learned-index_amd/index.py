@@ -64,7 +64,10 @@ def _index_file(indexer, collection_path, collection_type, output_file_path,
                 break
             if i - 1 < lo:
                 continue
-            if i % process_batch_size == 0:  # index.py:35 (first batch one short)
+            # index.py:35 (first batch one short); a shard never flushes an empty batch
+            # (its flush points need not fall inside it: an empty flush would write a
+            # stray empty line and shift every later doc id of the joined file)
+            if i % process_batch_size == 0 and (doc_range is None or batch):
                 indexer.index(batch, out)
                 logger.info(f"Indexed {i} passages [Rate: {i / (time.time() - start):.2f} "
                             f"passages/s]")
@@ -72,7 +75,8 @@ def _index_file(indexer, collection_path, collection_type, output_file_path,
             doc_id, passage = CollectionParser.parse(passage, collection_type)
             batch.append(passage)
             n += 1
-        indexer.index(batch, out)
+        if doc_range is None or batch:
+            indexer.index(batch, out)
     return n
 
 

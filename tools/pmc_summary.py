@@ -12,7 +12,8 @@ from collections import defaultdict
 from pathlib import Path
 
 
-_TARGS = [(r"DF16b", "bf16"), (r"f", "f32"), (r"Li(\d+)E", None), (r"j", "u32"), (r"i", "i32")]
+_TARGS = [(r"DF16b", "bf16"), (r"f", "f32"), (r"Li(\d+)E", None), (r"Lb1E", "true"),
+          (r"Lb0E", "false"), (r"j", "u32"), (r"i", "i32")]
 
 
 def _short_mangled(name):
