@@ -457,6 +457,11 @@ def main():
         torch.cuda.set_device(0)
     dev = torch.cuda.current_device()
 
+    # every leg runs on one real torch stream (torch's default stream has the null
+    # handle, which the library's set_stream takes as "own stream": RCCL collectives
+    # and the merge would not be ordered after the scorer)
+    main_stream = torch.cuda.Stream()
+    torch.cuda.set_stream(main_stream)
     legs = set(args.legs.split(","))
     enc_res = ret_res = None
     x3_res = None

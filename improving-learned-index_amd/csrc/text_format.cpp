@@ -67,7 +67,7 @@ std::string read_all(const char *path) {
 extern "C" int di_quantize_file(const char *input_path, const char *output_path, double max_val,
                                 int32_t bits, int device, double *max_used) {
     return guard([&] {
-        DI_REQUIRE(input_path && output_path, DI_EINVAL, "null argument");
+        DI_REQUIRE(input_path, DI_EINVAL, "null argument");
         std::string buf = read_all(input_path);
         std::vector<std::string_view> terms;
         std::vector<double> vals;
@@ -112,6 +112,10 @@ extern "C" int di_quantize_file(const char *input_path, const char *output_path,
         (void)hipSetDevice(prev);
         double m;
         std::memcpy(&m, &mb, 8);
+        if (!output_path) {  // max only (find_max_value, quantize.py:17-24; 0 if no term)
+            if (max_used) *max_used = m;
+            return;
+        }
         if (!(max_val > 0.0)) {
             DI_REQUIRE(m > 0.0, DI_EINVAL,
                        "max impact is 0: the reference divides by zero (quantize.py:37)");

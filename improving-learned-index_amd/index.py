@@ -9,7 +9,10 @@ Same flags as the reference plus --tokenizer_path / --max_length / --precision /
 --device / --variant (the reference hard-wires a hub tokenizer and 512 tokens).
 Output bytes are those of the reference (one line per input line, in order).
 Multi-GPU: --doc_range start:end encodes one doc-id shard; concatenating the
-shard outputs in order gives the single-GPU file.
+shard outputs in order gives the single-GPU file.  Under torchrun
+(--nproc-per-node N) every rank encodes doc-id shard r on its GPU and rank 0 joins
+the parts into --output_file_path (the reference's DataParallel over every visible
+GPU, indexer.py:25-26, as one process per GPU).
 """
 from __future__ import annotations
 
@@ -18,6 +21,7 @@ import logging
 import time
 from pathlib import Path
 
+from . import parallel
 from .datasets import COLLECTION_TYPES, CollectionParser
 from .indexer import Indexer, TokenizerPool, pool_supported, resolve_tokenizer
 from .models import DeepImpact
@@ -101,9 +105,23 @@ def main(argv=None):
     a = p.parse_args(argv)
     dr = tuple(int(x) for x in a.doc_range.split(":")) if a.doc_range else None
     logging.basicConfig(level=logging.INFO)
-    run(a.collection_path, a.collection_type, a.output_file_path, a.model_checkpoint_path,
+    world, rank, local = parallel.dist_env()
+    out, device = a.output_file_path, a.device
+    if world > 1:
+        import torch.distributed as dist
+
+        parallel.init_group("gloo")  # host barriers only: encode needs no collective
+        dr = parallel.shard_range(parallel.count_lines(a.collection_path), world, rank)
+        out, device = parallel.part_path(a.output_file_path, rank), parallel.rank_device(local)
+    run(a.collection_path, a.collection_type, out, a.model_checkpoint_path,
         a.num_processes, a.process_batch_size, a.model_batch_size, a.tokenizer_path,
-        a.max_length, a.precision, a.device, a.variant, dr, a.pairwise)
+        a.max_length, a.precision, device, a.variant, dr, a.pairwise)
+    if world > 1:
+        dist.barrier()
+        if rank == 0:
+            parallel.concat_parts([parallel.part_path(a.output_file_path, r) for r in range(world)],
+                                  a.output_file_path)
+        dist.barrier()
 
 
 if __name__ == "__main__":

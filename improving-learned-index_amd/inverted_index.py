@@ -80,6 +80,19 @@ class InvertedIndex:
         return self._dev
 
 
+def reference_n_docs(index_path: Union[str, Path]) -> int:
+    """Docs of a reference-format index: the largest doc id in inverted_index.dat + 1
+    (doc id = collection line index, create.py:41-47)."""
+    dat = Path(index_path) / INVERTED_INDEX_DATA
+    if dat.stat().st_size == 0:
+        return 0
+    rec = np.memmap(dat, dtype=[("doc", "<u4"), ("val", "u1")], mode="r")
+    m = 0
+    for s in range(0, rec.shape[0], 1 << 26):
+        m = max(m, int(rec["doc"][s:s + (1 << 26)].max()))
+    return m + 1
+
+
 def create_index(deep_impact_collection_path: Union[str, Path],
                  output_path: Union[str, Path]) -> None:
     """InvertedIndexCreator.run (create.py:53-55), byte-identical output."""

@@ -65,6 +65,56 @@ def ndcg_at_k(qrels: Dict[str, Dict[str, int]], results: Dict[str, Dict[str, flo
     return sum(vals) / len(vals) if vals else 0.0
 
 
+def _trec_ranked(run: Dict[str, float]):
+    """trec_eval's document order: score descending, ties by doc id descending."""
+    return [d for d, _ in sorted(run.items(), key=lambda x: (x[1], x[0]), reverse=True)]
+
+
+def evaluate_retrieval(qrels: Dict[str, Dict[str, int]], results: Dict[str, Dict[str, float]],
+                       k_values=(10, 100, 1000), ignore_identical_ids: bool = True):
+    """beir EvaluateRetrieval.evaluate (called at nano_beir_evaluator.py:230-231) restated
+    on trec_eval's measures (pytrec_eval is absent here -- parity unpinned):
+    ndcg_cut.k (gain = relevance, log2(rank + 1) discount), map_cut.k (AP truncated at
+    k over the query's relevant count), recall.k, P.k (over k); per-query values are
+    averaged over the queries of `results` that have judgments, then rounded to 5
+    places.  Returns the (NDCG, MAP, Recall, P) dicts beir returns; with
+    ignore_identical_ids (beir's default) a doc whose id equals the query id is
+    dropped first."""
+    ndcg = {f"NDCG@{k}": 0.0 for k in k_values}
+    _map = {f"MAP@{k}": 0.0 for k in k_values}
+    recall = {f"Recall@{k}": 0.0 for k in k_values}
+    prec = {f"P@{k}": 0.0 for k in k_values}
+    n = 0
+    for qid, run in results.items():
+        rels = qrels.get(qid)
+        if rels is None:
+            continue
+        n += 1
+        if ignore_identical_ids and qid in run:
+            run = {d: s for d, s in run.items() if d != qid}
+        ranked = _trec_ranked(run)
+        n_rel = sum(1 for g in rels.values() if g > 0)
+        ideal = sorted((g for g in rels.values() if g > 0), reverse=True)
+        for k in k_values:
+            top = ranked[:k]
+            dcg = sum(rels.get(d, 0) / math.log2(i + 2) for i, d in enumerate(top)
+                      if rels.get(d, 0) > 0)
+            idcg = sum(g / math.log2(i + 2) for i, g in enumerate(ideal[:k]))
+            ndcg[f"NDCG@{k}"] += dcg / idcg if idcg > 0 else 0.0
+            hits, ap = 0, 0.0
+            for i, d in enumerate(top):
+                if rels.get(d, 0) > 0:
+                    hits += 1
+                    ap += hits / (i + 1)
+            _map[f"MAP@{k}"] += ap / n_rel if n_rel else 0.0
+            recall[f"Recall@{k}"] += hits / n_rel if n_rel else 0.0
+            prec[f"P@{k}"] += hits / k
+    for m in (ndcg, _map, recall, prec):
+        for key in m:
+            m[key] = round(m[key] / n, 5) if n else 0.0
+    return ndcg, _map, recall, prec
+
+
 def main(argv=None):
     p = argparse.ArgumentParser("Evaluate a DeepImpact run file.")
     p.add_argument("--run_file_path", type=Path, required=True)

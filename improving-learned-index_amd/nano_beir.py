@@ -23,7 +23,7 @@ from typing import Dict, Optional
 import numpy as np
 
 from ._lib import DeviceSparseIndex, csr
-from .metrics import ndcg_at_k
+from .metrics import evaluate_retrieval, ndcg_at_k  # noqa: F401
 
 
 class SparseSearch:
@@ -97,16 +97,99 @@ def _read_local(path: Path):
     return corpus, queries, qrels
 
 
+# nano_beir_evaluator.py:30-60: the 13 NanoBEIR datasets (hub ids zeta-alpha-ai/Nano*)
+MAPPING_DATASET_NAME_TO_HUMAN_READABLE = {
+    "climatefever": "ClimateFEVER", "dbpedia": "DBPedia", "fever": "FEVER",
+    "fiqa2018": "FiQA2018", "hotpotqa": "HotpotQA", "msmarco": "MSMARCO",
+    "nfcorpus": "NFCorpus", "nq": "NQ", "quoraretrieval": "QuoraRetrieval",
+    "scidocs": "SCIDOCS", "arguana": "ArguAna", "scifact": "SciFact",
+    "touche2020": "Touche2020",
+}
+MAPPING_DATASET_NAME_TO_ID = {k: f"zeta-alpha-ai/Nano{v}"
+                              for k, v in MAPPING_DATASET_NAME_TO_HUMAN_READABLE.items()}
+K_VALUES = (10, 100, 1000)  # nano_beir_evaluator.py:231
+
+
 class NanoBEIREvaluator:
-    """evaluate_dataset on local data: (corpus, queries, qrels) dicts or a directory."""
+    """nano_beir_evaluator.py:153-232 on local data.  A dataset is a (corpus, queries,
+    qrels) tuple of dicts or a directory with corpus.jsonl / queries.jsonl / qrels.tsv
+    (the hub's NanoBEIR files); ``evaluate_all`` walks ``data_dir``/Nano<Name> for the
+    13 datasets (those present) and adds their average as metrics["avg"]."""
 
-    def __init__(self, batch_size=16, verbose=False, device=0):
+    def __init__(self, batch_size=16, verbose=False, device=0, data_dir=None):
         self.batch_size, self.verbose, self.device = batch_size, verbose, device
+        self.data_dir = Path(data_dir) if data_dir is not None else None
 
-    def evaluate_dataset(self, model, dataset, k_values=(10, 100, 1000)):
-        corpus, queries, qrels = _read_local(Path(dataset)) if isinstance(
-            dataset, (str, Path)) else dataset
+    def _load_dataset(self, dataset):
+        if isinstance(dataset, (str, Path)):
+            p = Path(dataset)
+            if not p.exists() and self.data_dir is not None:
+                name = MAPPING_DATASET_NAME_TO_HUMAN_READABLE.get(str(dataset), str(dataset))
+                p = self.data_dir / f"Nano{name}"
+            return _read_local(p)
+        return dataset
+
+    def search(self, model, dataset, k=1000):
+        corpus, queries, qrels = self._load_dataset(dataset)
         searcher = SparseSearch(model, batch_size=self.batch_size, verbose=self.verbose,
                                 device=self.device)
-        results = searcher.search(queries, corpus, k=1000)
-        return {f"NDCG@{k}": ndcg_at_k(qrels, results, k) for k in k_values}, results
+        return searcher.search(queries, corpus, k=k), qrels
+
+    def evaluate_dataset(self, model, dataset):
+        """(NDCG, MAP, Recall, P) dicts at k = 10, 100, 1000 (beir's evaluate)."""
+        results, qrels = self.search(model, dataset, k=1000)
+        return evaluate_retrieval(qrels, results, K_VALUES)
+
+    def evaluate_all(self, model, data_dir=None):
+        root = Path(data_dir) if data_dir is not None else self.data_dir
+        if root is None:
+            raise ValueError("evaluate_all needs data_dir (the hub is unreachable offline)")
+        metrics = {}
+        for name, human in MAPPING_DATASET_NAME_TO_HUMAN_READABLE.items():
+            d = root / f"Nano{human}"
+            if not d.is_dir():
+                continue
+            if self.verbose:
+                print(f"Evaluating dataset {name}...")
+            metrics[name] = self.evaluate_dataset(model, d)
+            if self.verbose:
+                print(f"Metrics for {name}: {metrics[name]}")
+        if not metrics:
+            raise FileNotFoundError(f"no Nano<Name> dataset directory under {root}")
+        metrics["avg"] = tuple(
+            {key: sum(metrics[n][i][key] for n in metrics) / len(metrics) for key in m}
+            for i, m in enumerate(next(iter(metrics.values()))))
+        return metrics
+
+
+def main(argv=None):
+    """nano_beir_evaluator.py:236-243 (the reference loads soyuj/deeper-impact from the
+    hub; here a local checkpoint + tokenizer and local NanoBEIR directories)."""
+    import argparse
+
+    from .models import DeepImpact
+
+    p = argparse.ArgumentParser("NanoBEIR evaluation of a DeepImpact checkpoint.")
+    p.add_argument("--data_dir", type=Path, required=True,
+                   help="directory holding Nano<Name>/{corpus.jsonl,queries.jsonl,qrels.tsv}")
+    p.add_argument("--model_checkpoint_path", type=str, required=True)
+    p.add_argument("--tokenizer_path", type=str, default=None)
+    p.add_argument("--variant", choices=["xlmr", "bert"], default="bert")
+    p.add_argument("--precision", choices=["bf16x3", "fp32", "bf16"], default="bf16x3")
+    p.add_argument("--max_length", type=int, default=None)
+    p.add_argument("--batch_size", type=int, default=16)
+    p.add_argument("--device", type=int, default=0)
+    p.add_argument("--dataset", type=str, default=None, help="one dataset name only")
+    a = p.parse_args(argv)
+    model = DeepImpact.load(a.model_checkpoint_path, tokenizer_path=a.tokenizer_path,
+                            precision=a.precision, device=a.device, variant=a.variant,
+                            max_length=a.max_length)
+    ev = NanoBEIREvaluator(batch_size=a.batch_size, verbose=True, device=a.device,
+                           data_dir=a.data_dir)
+    out = ev.evaluate_dataset(model, a.dataset) if a.dataset else ev.evaluate_all(model)
+    print(out)
+    return out
+
+
+if __name__ == "__main__":
+    main()

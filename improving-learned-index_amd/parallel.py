@@ -14,9 +14,78 @@ MI355X and over gloo in the CPU tests (tests/test_distributed_cpu.py).
 """
 from __future__ import annotations
 
+import os
+import shutil
+from pathlib import Path
 from typing import Callable, List, Optional, Sequence, Tuple
 
 import numpy as np
+
+
+def dist_env() -> Tuple[int, int, int]:
+    """(world, rank, local_rank) from the torchrun environment (1, 0, 0 without it)."""
+    return (int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0")),
+            int(os.environ.get("LOCAL_RANK", "0")))
+
+
+def init_group(backend: str, local_rank: int = 0):
+    """Process group of a torchrun-launched CLI: "nccl" (RCCL over xGMI; every rank
+    owns GPU local_rank) for the retrieval exchange, "gloo" for the host-only
+    barriers / scalars of the sharded index and quantize CLIs."""
+    import torch
+    import torch.distributed as dist
+
+    if dist.is_initialized():
+        return
+    if backend == "nccl":
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    else:
+        dist.init_process_group("gloo")
+
+
+def rank_device(local_rank: int) -> int:
+    """GPU of a local rank: one per GPU on an 8-GPU node; ranks share the devices when
+    there are more ranks than GPUs (the 1-GPU test box)."""
+    import torch
+
+    # (torch's count: it does not initialise the GPU; torch's HIP runtime must come up
+    # before the library's, see Ranker)
+    return local_rank % max(1, torch.cuda.device_count())
+
+
+def exchange_backend(world: int) -> str:
+    """RCCL (nccl) when every rank owns its GPU, else gloo over host tensors
+    (DI_DIST_BACKEND overrides)."""
+    import torch
+
+    return os.environ.get("DI_DIST_BACKEND") or (
+        "nccl" if world <= torch.cuda.device_count() else "gloo")
+
+
+def concat_parts(parts: Sequence[Path], out_path: Path) -> None:
+    """Rank 0: the shard outputs in rank order -> the single-process file."""
+    with open(out_path, "wb") as out:
+        for p in parts:
+            with open(p, "rb") as f:
+                shutil.copyfileobj(f, out, 1 << 24)
+    for p in parts:
+        os.unlink(p)
+
+
+def part_path(path, rank: int) -> Path:
+    path = Path(path)
+    return path.with_name(f"{path.name}.part{rank:05d}")
+
+
+def count_lines(path) -> int:
+    """Lines as Python's file iteration sees them (a last line without '\\n' counts)."""
+    n, last = 0, b"\n"
+    with open(path, "rb") as f:
+        for blk in iter(lambda: f.read(1 << 24), b""):
+            n += blk.count(b"\n")
+            last = blk[-1:]
+    return n + (last != b"\n")
 
 
 def shard_range(n_items: int, world: int, rank: int) -> Tuple[int, int]:
@@ -39,6 +108,38 @@ def decode_quant_keys(keys: np.ndarray, n: int) -> List[Tuple[int, int]]:
     docs = (np.uint64(0xFFFFFFFF) - (k & np.uint64(0xFFFFFFFF))).astype(np.int64)
     scores = (k >> np.uint64(48)).astype(np.int64)
     return list(zip(docs.tolist(), scores.tolist()))
+
+
+def quantize_sharded(input_path, output_path, max_val, world: int, rank: int,
+                     shard_max: Callable, shard_quantize: Callable) -> float:
+    """Doc-sharded quantize (quantize.py:27-47 over `world` ranks): every rank takes a
+    contiguous line range of the impact TSV, the global max is the all_reduce(MAX) of
+    the shard maxima (find_max_value, quantize.py:17-24), every rank quantizes its
+    lines with it, and rank 0 joins the parts: the single-process bytes.
+    shard_max(path) -> float and shard_quantize(in, out, max) are the per-shard
+    kernels (the HIP di_quantize_file by default in quantize.py)."""
+    import torch.distributed as dist
+
+    with open(input_path, "rb") as f:
+        lines = f.readlines()
+    lo, hi = shard_range(len(lines), world, rank)
+    part_in = Path(f"{part_path(output_path, rank)}.in")
+    with open(part_in, "wb") as f:
+        f.writelines(lines[lo:hi])
+    del lines
+    if max_val is None:
+        m = global_max(shard_max(part_in) if hi > lo else 0.0)
+        if not m > 0.0:
+            raise ZeroDivisionError("float division by zero")  # quantize.py:37
+    else:
+        m = float(max_val)
+    shard_quantize(part_in, part_path(output_path, rank), m)
+    os.unlink(part_in)
+    dist.barrier()
+    if rank == 0:
+        concat_parts([part_path(output_path, r) for r in range(world)], Path(output_path))
+    dist.barrier()
+    return m
 
 
 class ShardedRetriever:
@@ -82,6 +183,65 @@ class ShardedRetriever:
     def search(self, queries) -> List[List[Tuple[int, int]]]:
         mk, mn = self.search_keys(queries)
         return [decode_quant_keys(mk[i], int(mn[i])) for i in range(len(mn))]
+
+
+def exchange_merge_device(index, queries, k: int, device: int, flags: int = 0):
+    """The rank CLI's retrieval step on one doc-id shard: score every query
+    on this rank's DeviceIndex shard into device tensors, all_gather the (key, count)
+    lists -- RCCL over xGMI under the nccl backend; host tensors under gloo -- and merge
+    them on the GPU with di_topk_merge (DI_F_LISTS_MAJOR: the gathered rank-major
+    layout, no transpose).  Returns host (keys [n_q, k] uint64, counts [n_q])."""
+    import torch
+    import torch.distributed as dist
+
+    from . import _lib
+
+    dev = torch.device("cuda", device)
+    # one real stream for the scorer, the collectives and the merge (torch's default
+    # stream has the null handle, which di_index_set_stream takes as "own stream": the
+    # all_gather would then not be ordered after the scorer)
+    stream = torch.cuda.Stream(dev)
+    with torch.cuda.stream(stream):
+        index.set_stream(stream.cuda_stream)
+        return _exchange_merge(index, queries, k, device, dev, stream, flags)
+
+
+def _exchange_merge(index, queries, k, device, dev, stream, flags):
+    import torch
+    import torch.distributed as dist
+
+    from . import _lib
+
+    world = dist.get_world_size()
+    gpu_exchange = dist.get_backend() == "nccl"
+    flat, cu = _lib.csr(queries)
+    nq = len(queries)
+    f = _lib.DI_F_DEVICE_PTRS | _lib.DI_F_ASYNC | flags
+    d_terms = torch.from_numpy(flat.astype(np.int32)).to(dev)
+    d_cu = torch.from_numpy(cu).to(dev)
+    out_doc = torch.empty(max(nq * k, 1), dtype=torch.int32, device=dev)
+    out_score = torch.empty_like(out_doc)
+    out_n = torch.empty(max(nq, 1), dtype=torch.int32, device=dev)
+    out_key = torch.empty(max(nq * k, 1), dtype=torch.int64, device=dev)
+    if nq:
+        index.search_device(d_terms, d_cu, nq, k, out_doc, out_score, out_n, out_key, f)
+    key, cnt = (out_key, out_n) if gpu_exchange else (out_key.cpu(), out_n.cpu())
+    if not gpu_exchange:
+        torch.cuda.synchronize(dev)
+    g_key = torch.empty(world * key.numel(), dtype=key.dtype, device=key.device)
+    g_n = torch.empty(world * cnt.numel(), dtype=cnt.dtype, device=cnt.device)
+    dist.all_gather_into_tensor(g_key, key)
+    dist.all_gather_into_tensor(g_n, cnt)
+    if nq == 0:
+        return np.zeros((0, k), np.uint64), np.zeros(0, np.int32)
+    m_key = torch.empty(nq * k, dtype=torch.int64, device=dev)
+    m_n = torch.empty(nq, dtype=torch.int32, device=dev)
+    if not gpu_exchange:  # gathered on the host: back to the device for the merge
+        g_key, g_n = g_key.to(dev), g_n.to(dev)
+    _lib.topk_merge_device(g_key, g_n, nq, world, k, m_key, m_n, device=device,
+                           stream=stream.cuda_stream, flags=f | _lib.DI_F_LISTS_MAJOR)
+    keys = m_key.cpu().numpy().view(np.uint64).reshape(nq, k)
+    return keys, m_n.cpu().numpy()
 
 
 def device_shard_search(index, k: int):

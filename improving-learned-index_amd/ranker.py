@@ -6,6 +6,12 @@ time, ranker.py:44-46); here every query of the file is scored by one batched
 GPU launch sequence (di_index_search).  The run file holds the same lines; the
 reference writes queries in imap_unordered completion order, this writes them
 in input order (a valid completion order of the reference).
+
+Multi-GPU (torchrun --nproc-per-node N -m improving_learned_index_amd.rank ...): rank r
+loads doc-id shard r of the index on its GPU, every rank scores every query, the
+per-shard top-k keys are all-gathered over RCCL and merged on the GPU
+(parallel.exchange_merge_device); rank 0 writes the run file -- the same lines as one
+process (the keys totally order score, first touch and doc).
 """
 from __future__ import annotations
 
@@ -13,8 +19,9 @@ import argparse
 from pathlib import Path
 from typing import Optional, Union
 
+from . import parallel
 from .datasets import COLLECTION_TYPES, Queries, QueryRelevanceDataset, RunFile
-from .inverted_index import InvertedIndex
+from .inverted_index import InvertedIndex, reference_n_docs
 from .models import DeepImpact
 
 
@@ -33,8 +40,21 @@ class Ranker:
         self.query_iterator = list(self.queries.keys())
         if qrels_path is not None:  # ranker.py:34-35
             self.query_iterator = list(QueryRelevanceDataset(qrels_path=qrels_path).keys())
-        self.index = InvertedIndex(index_path=index_path, device=device, min_impact=min_impact)
-        self.run_file = RunFile(run_file_path=output_path)
+        self.world, self.rank, local = parallel.dist_env()
+        lo = hi = 0
+        if self.world > 1:
+            import torch
+
+            device = parallel.rank_device(local)
+            # torch's HIP runtime first: the exchange uses torch device tensors, and torch
+            # cannot initialise the GPU after the library's (newer) runtime has
+            torch.cuda.set_device(device)
+            parallel.init_group(parallel.exchange_backend(self.world), device)
+            lo, hi = parallel.shard_range(reference_n_docs(index_path), self.world, self.rank)
+        self.device = device
+        self.index = InvertedIndex(index_path=index_path, device=device, doc_lo=lo, doc_hi=hi,
+                                   min_impact=min_impact)
+        self.run_file = RunFile(run_file_path=output_path) if self.rank == 0 else None
         self.top_k = top_k
         self.batch_queries = batch_queries
 
@@ -45,10 +65,24 @@ class Ranker:
         qids = self.query_iterator
         for s in range(0, len(qids), self.batch_queries):
             chunk = qids[s:s + self.batch_queries]
-            results = self.index.score_batch([self.get_query_terms(q) for q in chunk],
-                                             self.top_k)
-            for qid, scores in zip(chunk, results):
-                self.run_file.writelines(qid, scores)
+            terms = [self.get_query_terms(q) for q in chunk]
+            if self.world > 1:
+                # every shard must apply the terms in one order (the first-touch tie key):
+                # process_query returns a set whose iteration order follows the process's
+                # hash seed, so rank 0's order is broadcast to all ranks
+                import torch.distributed as dist
+
+                ids = [[self.index.term_ids(t) for t in terms]]
+                dist.broadcast_object_list(ids, src=0)
+                keys, n = parallel.exchange_merge_device(
+                    self.index.device_index, ids[0], self.top_k, self.device)
+                results = [parallel.decode_quant_keys(keys[i], int(n[i]))
+                           for i in range(len(chunk))]
+            else:
+                results = self.index.score_batch(terms, self.top_k)
+            if self.run_file is not None:
+                for qid, scores in zip(chunk, results):
+                    self.run_file.writelines(qid, scores)
 
 
 def main(argv=None):

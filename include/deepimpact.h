@@ -229,7 +229,9 @@ int di_quantize(const float *impacts, int64_t n, double max_val, int32_t bits, i
 /* quantize_file (quantize.py:27-47) end to end: parse the impact TSV exactly as
  * the reference (line.strip().split(', '), t.strip().split(': '), float()),
  * quantize on the GPU in fp64, write the quantized TSV.  Empty / malformed
- * lines fail with DI_EFORMAT where the reference raises ValueError. */
+ * lines fail with DI_EFORMAT where the reference raises ValueError.
+ * output_path NULL: only *max_used = the file's max impact (find_max_value,
+ * quantize.py:17-24) -- the doc-sharded quantizer all-reduces it (MAX) across ranks. */
 int di_quantize_file(const char *input_path, const char *output_path, double max_val,
                      int32_t bits, int device, double *max_used);
 

@@ -147,3 +147,52 @@ def test_sharded_search_golden_index():
     assert out[0][0] == out[1][0]
     # the reference's own ranking (InvertedIndex.score, set-iteration tie order)
     assert [[[int(d), int(s)] for d, s in qq] for qq in out[0][0]] == gold["top1000"]
+
+
+def _quant_worker(rank, world, port, src, out, max_val, q):
+    try:
+        import torch.distributed as dist
+
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+
+        def shard_max(path):
+            with open(path, encoding="utf-8") as f:
+                vals = [float(s) for line in f for _, s in oracle.parse_impact_line(line)]
+            return max([0.0] + vals)
+
+        m = parallel.quantize_sharded(src, out, max_val, world, rank, shard_max,
+                                      lambda i, o, mm: oracle.quantize_file(i, o, mm))
+        dist.destroy_process_group()
+        q.put((rank, m))
+    except Exception:
+        q.put((rank, traceback.format_exc()))
+
+
+@pytest.mark.parametrize("world,max_val", [(2, None), (3, None), (2, 7.0)])
+def test_quantize_sharded_equals_single(tmp_path, world, max_val):
+    """parallel.quantize_sharded (the quantize CLI under torchrun): all_reduce(MAX) of
+    the shard maxima, per-shard quantize, rank-0 join == the reference file (golden
+    q254 fixture: maxima where int(max * 255 / max) = 254)."""
+    from conftest import GOLDEN
+
+    src = GOLDEN / "q254.index"
+    out = tmp_path / "q.out"
+    ctx = mp.get_context("fork")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_quant_worker, args=(r, world, port, src, out, max_val, q))
+          for r in range(world)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=120) for _ in ps]
+    for p in ps:
+        p.join(timeout=60)
+    for r, m in res:
+        assert not isinstance(m, str), m
+    if max_val is None:
+        assert out.read_bytes() == (GOLDEN / "q254.quantized").read_bytes()
+    else:
+        want = tmp_path / "want"
+        oracle.quantize_file(src, want, max_val)
+        assert out.read_bytes() == want.read_bytes()

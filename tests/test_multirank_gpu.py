@@ -1,0 +1,119 @@
+"""Doc-sharded CLIs end to end on the GPU: the index, quantize and rank
+CLIs launched by torchrun with 2 ranks produce byte-identical files to one process.
+The test box has one GPU, so both ranks share it and the retrieval exchange runs
+over gloo host tensors (parallel.exchange_backend); on an 8-GPU node every rank owns
+its GPU and the same code path all-gathers over RCCL.  The merge is di_topk_merge on
+the GPU either way."""
+import json
+import os
+import socket
+import subprocess
+import sys
+import tempfile
+from pathlib import Path
+
+import pytest
+import torch
+
+import encoder_ref
+from conftest import GOLDEN, ROOT
+
+pytestmark = pytest.mark.gpu
+
+
+def _port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _torchrun(module, args, world=2, timeout=240):
+    """world > 0: torchrun with `world` ranks; 0: one plain process.  PYTHONHASHSEED is
+    fixed: query terms are a set (process_query), whose iteration order -- the
+    reference's first-touch tie order -- follows the hash seed."""
+    env = dict(os.environ, PYTHONPATH=str(ROOT), OMP_NUM_THREADS="4", PYTHONHASHSEED="0")
+    run = ([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+            f"--nproc-per-node={world}", "--master-addr", "127.0.0.1",
+            f"--master-port={_port()}"] if world else [sys.executable])
+    cmd = run + ["-m", f"improving_learned_index_amd.{module}"] + args
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=timeout)
+    assert r.returncode == 0, "\n".join(l for l in r.stderr.splitlines()
+                                         if "[rank" in l or "Error" in l)[-8000:]
+
+
+@pytest.fixture(scope="module")
+def ckpt(tmp_path_factory):
+    from improving_learned_index_amd import _lib
+
+    if _lib.device_count() < 1:
+        pytest.fail("no HIP device visible (GPU test run without a GPU)")
+    fx = json.loads((GOLDEN / "encoder_xlmr_small.json").read_text())
+    sd = encoder_ref.seeded_state_dict(fx["state_dict_shapes"], fx["seed"], fx["std"])
+    path = tmp_path_factory.mktemp("ckpt") / "DeepImpact_latest.pt"
+    torch.save({"model_state_dict": sd, "optimizer_state_dict": {}, "step": 0,
+                "batch_size": 0}, path)
+    return fx, path
+
+
+def test_index_cli_two_ranks_equals_one(ckpt):
+    from improving_learned_index_amd import index as index_cli
+
+    fx, path = ckpt
+    texts = [t for t in fx["texts"] if t] * 3  # 21 passages: shards of 10 and 11
+    with tempfile.TemporaryDirectory() as td:
+        td = Path(td)
+        coll = td / "collection.tsv"
+        coll.write_text("".join(f"{i}\t{t}\n" for i, t in enumerate(texts)))
+        common = ["--collection_path", str(coll), "--model_checkpoint_path", str(path),
+                  "--tokenizer_path", str(GOLDEN / "tokenizer.json"), "--max_length",
+                  str(fx["max_length"]), "--precision", "fp32", "--process_batch_size", "4",
+                  "--num_processes", "1"]
+        index_cli.main(common + ["--output_file_path", str(td / "one.index")])
+        _torchrun("index", common + ["--output_file_path", str(td / "two.index")])
+        assert (td / "two.index").read_bytes() == (td / "one.index").read_bytes()
+        assert not list(td.glob("*.part*"))
+
+
+def test_quantize_cli_two_ranks_equals_one():
+    from improving_learned_index_amd.quantize import quantize_file
+
+    src = GOLDEN / "q254.index"
+    with tempfile.TemporaryDirectory() as td:
+        td = Path(td)
+        quantize_file(src, td / "one")
+        _torchrun("quantize", ["-i", str(src), "-o", str(td / "two")])
+        assert (td / "two").read_bytes() == (td / "one").read_bytes() == \
+            (GOLDEN / "q254.quantized").read_bytes()
+        _torchrun("quantize", ["-i", str(src), "-o", str(td / "two7"), "-m", "7"], world=3)
+        quantize_file(src, td / "one7", max_val=7.0)
+        assert (td / "two7").read_bytes() == (td / "one7").read_bytes()
+
+
+def _same_run(got: str, want: str):
+    g, w = got.splitlines(), want.splitlines()
+    for i, (a, b) in enumerate(zip(g, w)):
+        assert a == b, (i, a, b, len(g), len(w))
+    assert len(g) == len(w), (len(g), len(w))
+
+
+def test_rank_cli_two_ranks_equals_one():
+    from improving_learned_index_amd.inverted_index import InvertedIndexCreator
+
+    fx = json.loads((GOLDEN / "score.json").read_text())
+    with tempfile.TemporaryDirectory() as td:
+        td = Path(td)
+        InvertedIndexCreator(GOLDEN / "collection.quantized", td / "index").run()
+        qf = td / "queries.tsv"
+        texts = [" ".join(t.lstrip("▁") for t in q) for q in fx["queries"]]
+        texts = [t for t in texts if t.strip()]  # (an empty query line does not parse)
+        qf.write_text("".join(f"q{i}\t{t}\n" for i, t in enumerate(texts)))
+        args = ["--index_path", str(td / "index"), "--queries_path", str(qf),
+                "--tokenizer_path", str(GOLDEN / "tokenizer.json")]
+        _torchrun("rank", args + ["--output_path", str(td / "one.tsv")], world=0)
+        _torchrun("rank", args + ["--output_path", str(td / "two.tsv")])
+        _same_run((td / "two.tsv").read_text(), (td / "one.tsv").read_text())
+        _torchrun("rank", args + ["--output_path", str(td / "three.tsv"), "--top_k", "7"],
+                  world=3)
+        _torchrun("rank", args + ["--output_path", str(td / "one7.tsv"), "--top_k", "7"],
+                  world=0)
+        _same_run((td / "three.tsv").read_text(), (td / "one7.tsv").read_text())
