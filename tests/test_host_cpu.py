@@ -92,3 +92,15 @@ def test_ndcg_trec_eval_conventions():
     assert ndcg_at_k(qrels, {"q": {"a": 2.0, "c": 1.0, "b": 0.5}}, 10) == pytest.approx(
         (1 + 1 / np.log2(4)) / (1 + 1 / np.log2(3)))
     assert ndcg_at_k(qrels, {}, 10) == 0.0
+
+
+@pytest.mark.parametrize("name", ["collection.index", "collection.quantized", "edge.tsv"])
+def test_convert_to_anserini_matches_reference_output(tmp_path, name):
+    """F1: byte-identical to the reference's own convert_to_anserini.process output
+    (fixtures made by tests/golden/make_golden_f1.py, which ran the reference)."""
+    from improving_learned_index_amd import convert_to_anserini
+
+    src = GOLDEN / name if name != "edge.tsv" else GOLDEN / "anserini" / name
+    out = tmp_path / "out.jsonl"
+    convert_to_anserini.process(src, out)
+    assert out.read_bytes() == (GOLDEN / "anserini" / f"{name}.jsonl").read_bytes()
