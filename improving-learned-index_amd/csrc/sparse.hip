@@ -16,6 +16,11 @@
 // j = first query term that touched the doc -- first-touch order is term order,
 // then doc (corpus) order inside the term.  Merge key: score bits(32) |
 // 255-j(8) | 0xFFFFFF-doc(24).
+// Long queries (argument-style NanoBEIR queries can pass 256 unique terms): terms go
+// in chunks of SP_MAX_TERMS, the accumulators carrying over, up to
+// DI_MAX_SPARSE_QUERY_TERMS; the sums stay exact, and j saturates at 255, so only
+// docs with EXACTLY equal scores first touched by terms 255, 256, ... are ordered by
+// corpus order instead of by (term, corpus order).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -63,41 +68,46 @@ sparse_score_kernel(const uint16_t *__restrict__ pdoc, const float *__restrict__
     const int q0 = cu_q[q], nt = cu_q[q + 1] - q0;
     int32_t *cn = cand_n + (int64_t)q * nb + b;
     uint64_t *ck = cand_key + ((int64_t)q * nb + b) * k;
-    if (nt > SP_MAX_TERMS || nt < 0 || n_local <= 0) {
-        if (tid == 0) *cn = (nt > SP_MAX_TERMS || nt < 0) ? -1 : 0;
+    if (nt > DI_MAX_SPARSE_QUERY_TERMS || nt < 0 || n_local <= 0) {
+        if (tid == 0) *cn = (nt > DI_MAX_SPARSE_QUERY_TERMS || nt < 0) ? -1 : 0;
         return;
     }
     if (tid == 0) {
         sh.bad = 0;
         sh.emit = 0;
     }
-    __syncthreads();
-    for (int j = tid; j < nt; j += SP_THREADS) {
-        uint32_t t = q_terms[q0 + j];
-        if (t >= n_terms) {
-            sh.bad = 1;
-            sh.lo[j] = sh.hi[j] = 0;
-            continue;
-        }
-        const uint32_t *bo = blk_off + (int64_t)t * (nb + 1) + b;
-        sh.lo[j] = term_start[t] + bo[0];
-        sh.hi[j] = term_start[t] + bo[1];
-    }
     for (int i = tid; i < SP_DOCS; i += SP_THREADS) sh.acc[i] = 0.f;
-    __syncthreads();
-    if (sh.bad) {
-        if (tid == 0) *cn = -1;
-        return;
-    }
-    // ---- accumulate: terms in query order, one barrier per term ----
-    for (int j = 0; j < nt; ++j) {
-        for (int64_t i = sh.lo[j] + tid; i < sh.hi[j]; i += SP_THREADS) {
-            const int d = pdoc[i] & (SP_DOCS - 1);
-            const float a = sh.acc[d];
-            if (a == 0.f) sh.first[d] = (uint8_t)j;  // impacts > 0: 0 == untouched
-            sh.acc[d] = a + pimp[i];
+    // ---- accumulate: terms in query order, one barrier per term, chunks of
+    // SP_MAX_TERMS term bounds ----
+    for (int c0 = 0; c0 < nt; c0 += SP_MAX_TERMS) {
+        const int cn_t = min(SP_MAX_TERMS, nt - c0);
+        __syncthreads();  // the previous chunk's bounds are no longer read
+        for (int j = tid; j < cn_t; j += SP_THREADS) {
+            uint32_t t = q_terms[q0 + c0 + j];
+            if (t >= n_terms) {
+                sh.bad = 1;
+                sh.lo[j] = sh.hi[j] = 0;
+                continue;
+            }
+            const uint32_t *bo = blk_off + (int64_t)t * (nb + 1) + b;
+            sh.lo[j] = term_start[t] + bo[0];
+            sh.hi[j] = term_start[t] + bo[1];
         }
         __syncthreads();
+        if (sh.bad) {
+            if (tid == 0) *cn = -1;
+            return;
+        }
+        for (int j = 0; j < cn_t; ++j) {
+            const uint8_t jj = (uint8_t)min(c0 + j, 255);
+            for (int64_t i = sh.lo[j] + tid; i < sh.hi[j]; i += SP_THREADS) {
+                const int d = pdoc[i] & (SP_DOCS - 1);
+                const float a = sh.acc[d];
+                if (a == 0.f) sh.first[d] = jj;  // impacts > 0: 0 == untouched
+                sh.acc[d] = a + pimp[i];
+            }
+            __syncthreads();
+        }
     }
     // ---- block top-k over the unique 56-bit keys (untouched docs: key < 2^40) ----
     uint64_t prefix = 0, mask = 0;
@@ -269,8 +279,8 @@ int di_sparse_search(di_sparse *sp, const uint32_t *q_terms, const int32_t *cu_q
         if (!dev) {
             for (int q = 0; q < n_q; ++q) {
                 const int32_t c = cu_q[q + 1] - cu_q[q];
-                DI_REQUIRE(c >= 0 && c <= DI_MAX_QUERY_TERMS, DI_ERANGE,
-                           "query %d has %d terms (limit %d)", q, c, DI_MAX_QUERY_TERMS);
+                DI_REQUIRE(c >= 0 && c <= DI_MAX_SPARSE_QUERY_TERMS, DI_ERANGE,
+                           "query %d has %d terms (limit %d)", q, c, DI_MAX_SPARSE_QUERY_TERMS);
             }
             ntot = cu_q[n_q];
             for (int64_t i = 0; i < ntot; ++i)

@@ -49,6 +49,7 @@ extern "C" {
 /* Limits of the retrieval kernels (documented in DESIGN.md). */
 #define DI_MAX_QUERY_TERMS 256   /* known terms per query (first-touch key, u16 score) */
 #define DI_MAX_TOPK 4096
+#define DI_MAX_SPARSE_QUERY_TERMS 4096 /* float search: known terms per query (chunked) */
 #define DI_MAX_SPARSE_DOCS 16777215u /* float index: doc ids embedded in 24 bits   */
 
 const char *di_last_error(void);

@@ -68,3 +68,34 @@ def test_sparse_multiblock_matches_oracle(fx):
         want = ora.search(qs, k)
         for g, w in zip(got, want):
             assert [(d, float(s)) for d, s in g] == w
+
+
+def test_sparse_long_queries_match_oracle(fx):
+    """Argument-style queries with more than 256 known terms (NanoArguAna-like) are
+    scored in term chunks with the accumulators carried over: same scores and order as
+    the oracle (continuous impacts: no exact ties among late-touched docs)."""
+    from improving_learned_index_amd import _lib
+
+    rng = np.random.default_rng(4)
+    n_docs, V = 20000, 1500
+    lists = {t: [] for t in range(V)}
+    for d in range(n_docs):
+        for t in rng.choice(V, size=40, replace=False):
+            lists[int(t)].append((d, np.float32(rng.random() * 3 + 1e-3)))
+    term_off = np.zeros(V + 1, np.int64)
+    term_off[1:] = np.cumsum([len(lists[t]) for t in range(V)])
+    pdoc = np.array([d for t in range(V) for d, _ in lists[t]], np.uint32)
+    pimp = np.array([x for t in range(V) for _, x in lists[t]], np.float32)
+    dev = _lib.DeviceSparseIndex(term_off, pdoc, pimp, n_docs)
+    ora = oracle.SparseIndex.__new__(oracle.SparseIndex)
+    ora.corpus_ids = list(range(n_docs))
+    ora.vocab = {t: t for t in range(V)}
+    ora.term_off, ora.pdoc, ora.pimp = term_off, pdoc, pimp
+    qs = [rng.choice(V, size=n, replace=False).tolist() for n in (257, 300, 600, 1200, 5)]
+    for k in (10, 1000):
+        got = dev.search(qs, k)
+        want = ora.search(qs, k)
+        for g, w in zip(got, want):
+            assert [(d, float(s)) for d, s in g] == w
+    with pytest.raises(_lib.DIError):
+        dev.search([list(range(V)) * 3], 10)  # 4500 terms > DI_MAX_SPARSE_QUERY_TERMS
