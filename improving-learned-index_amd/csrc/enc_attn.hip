@@ -246,6 +246,174 @@ attention_kernel(const T *__restrict__ qk, const T *__restrict__ vt,
     }
 }
 
+// fp32-faithful attention (precision bf16x3): attention_kernel's register-direct
+// structure on the f32 Q | K rows and f32 V^T of the split QKV GEMM, with every
+// product as split bf16 (x = x_hi + x_lo, three 16x16x32 bf16 MFMAs per f32 product:
+// hi*hi + lo*hi + hi*lo, f32 accumulate, ~2^-17 relative per product) instead of
+// f32 MFMA (1/16 of the bf16 rate): S^T = K Q^T from split K and Q, O^T = V^T P^T
+// from split V^T and the split probabilities; softmax and the row sums in f32.
+// Output: split-bf16 ctx rows [hi(H) | lo(H)] for the O GEMM.
+__device__ __forceinline__ void split8(const float4 &a, const float4 &b, bf16x8 &hi,
+                                       bf16x8 &lo) {
+    const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        hi[e] = split_hi(v[e]);
+        lo[e] = split_lo(v[e]);
+    }
+}
+
+__device__ __forceinline__ f32x4 mma_x3(const bf16x8 &ah, const bf16x8 &al, const bf16x8 &bh,
+                                        const bf16x8 &bl, f32x4 acc) {
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh, acc, 0, 0, 0);
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl, acc, 0, 0, 0);
+}
+
+__global__ void __launch_bounds__(64)
+attention_x3_kernel(const float *__restrict__ qk, const float *__restrict__ vt,
+                    const int32_t *__restrict__ cu_seqlens, int H, int ld_v, int n_qb,
+                    int n_heads, int n_pairs, bf16 *__restrict__ ctx_split) {
+    const int id = blockIdx.x, x = id & 7, j = id >> 3;  // XCD-grouped, as attention_kernel
+    const int pair = (j / n_qb) * 8 + x;
+    const int qb = j % n_qb;
+    if (pair >= n_pairs) return;
+    const int doc = pair / n_heads, h = pair % n_heads;
+    const int lane = threadIdx.x;
+    const int g = lane >> 4, c = lane & 15;
+    const int tok0 = cu_seqlens[doc], n = cu_seqlens[doc + 1] - tok0;
+    const int q_base = qb * (16 * QT);
+    if (q_base >= n) return;
+    const int ldqk = 2 * H;
+
+    // B operands Q^T, lane (g, c): Q[q_base + 16 qt + c][32 ch + 8 g + e]
+    bf16x8 qh[QT][2], ql[QT][2];
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt) {
+        const int qrow = tok0 + min(q_base + 16 * qt + c, n - 1);
+#pragma unroll
+        for (int ch = 0; ch < 2; ++ch) {
+            const float *src = qk + (int64_t)qrow * ldqk + h * ATT_D + ch * 32 + 8 * g;
+            split8(*reinterpret_cast<const float4 *>(src),
+                   *reinterpret_cast<const float4 *>(src + 4), qh[qt][ch], ql[qt][ch]);
+        }
+    }
+    const float sc = 0.125f * 1.4426950408889634f;  // 1/sqrt(64) * log2(e)
+    float m[QT], lsum[QT];
+    f32x4 o[QT][4];
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt) {
+        m[qt] = -INFINITY;
+        lsum[qt] = 0.f;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) o[qt][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    const float *kbase = qk + H + h * ATT_D;
+    const float *vbase = vt + (int64_t)(h * ATT_D) * ld_v + vt_base(doc, tok0);
+
+    for (int key0 = 0; key0 < n; key0 += 32) {
+        // A operands K (two 16-key tiles), lane (g, c): K[key0 + 16 t + c][32 ch + 8 g + e]
+        bf16x8 kh[2][2], kl[2][2];
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            const int krow = tok0 + min(key0 + 16 * t + c, n - 1);
+#pragma unroll
+            for (int ch = 0; ch < 2; ++ch) {
+                const float *src = kbase + (int64_t)krow * ldqk + ch * 32 + 8 * g;
+                split8(*reinterpret_cast<const float4 *>(src),
+                       *reinterpret_cast<const float4 *>(src + 4), kh[t][ch], kl[t][ch]);
+            }
+        }
+        // A operands V^T, lane (g, c) of d-tile dt: d = 16 dt + c, keys key0 + 4 g..+3
+        // then key0 + 16 + 4 g..+3 (the P^T k permutation, as the bf16 path)
+        bf16x8 vh[4], vl[4];
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) {
+            const float *vrow = vbase + (int64_t)(dt * 16 + c) * ld_v + key0 + 4 * g;
+            split8(*reinterpret_cast<const float4 *>(vrow),
+                   *reinterpret_cast<const float4 *>(vrow + 16), vh[dt], vl[dt]);
+        }
+#pragma unroll
+        for (int qt = 0; qt < QT; ++qt) {
+            f32x4 s[2];
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+                s[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int ch = 0; ch < 2; ++ch)
+                    s[t] = mma_x3(kh[t][ch], kl[t][ch], qh[qt][ch], ql[qt][ch], s[t]);
+            }
+            // lane holds S^T[key0 + 16 t + 4 g + r][q_base + 16 qt + c]
+            float cmax = -INFINITY;
+#pragma unroll
+            for (int t = 0; t < 2; ++t)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int key = key0 + 16 * t + 4 * g + r;
+                    const float v = (key < n) ? s[t][r] * sc : -INFINITY;
+                    s[t][r] = v;
+                    cmax = fmaxf(cmax, v);
+                }
+            cmax = fmaxf(cmax, __shfl_xor(cmax, 16, 64));
+            cmax = fmaxf(cmax, __shfl_xor(cmax, 32, 64));
+            const float m_new = fmaxf(m[qt], cmax);
+            const float alpha = exp2f(m[qt] - m_new);  // 0 on the first chunk
+            m[qt] = m_new;
+            lsum[qt] *= alpha;
+#pragma unroll
+            for (int dt = 0; dt < 4; ++dt) o[qt][dt] *= alpha;
+            bf16x8 ph, pl;
+#pragma unroll
+            for (int t = 0; t < 2; ++t)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const float p = exp2f(s[t][r] - m_new);
+                    lsum[qt] += p;
+                    ph[4 * t + r] = split_hi(p);
+                    pl[4 * t + r] = split_lo(p);
+                }
+#pragma unroll
+            for (int dt = 0; dt < 4; ++dt) o[qt][dt] = mma_x3(vh[dt], vl[dt], ph, pl, o[qt][dt]);
+        }
+    }
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt) {
+        float l = lsum[qt];
+        l += __shfl_xor(l, 16, 64);
+        l += __shfl_xor(l, 32, 64);
+        const float inv = 1.0f / l;
+        const int q = q_base + 16 * qt + c;
+        if (q < n) {
+            bf16 *out = ctx_split + (int64_t)(tok0 + q) * 2 * H + h * ATT_D + 4 * g;
+#pragma unroll
+            for (int dt = 0; dt < 4; ++dt) {
+                bf16x4 hv, lv;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const float y = o[qt][dt][r] * inv;
+                    hv[r] = split_hi(y);
+                    lv[r] = split_lo(y);
+                }
+                *reinterpret_cast<bf16x4 *>(out + dt * 16) = hv;
+                *reinterpret_cast<bf16x4 *>(out + H + dt * 16) = lv;
+            }
+        }
+    }
+}
+
+void launch_attention_x3(const float *qk, const float *vt, const int32_t *cu_seqlens, int n_docs,
+                         int max_len, int H, int ld_v, bf16 *ctx_split, hipStream_t s) {
+    DI_REQUIRE(H % ATT_D == 0, DI_EINVAL, "hidden %d is not a multiple of the head dim 64", H);
+    if (n_docs == 0 || max_len == 0) return;
+    const int n_heads = H / ATT_D, n_pairs = n_docs * n_heads;
+    const int n_qb = (max_len + 16 * QT - 1) / (16 * QT);
+    const int64_t blocks = (int64_t)((n_pairs + 7) / 8) * 8 * n_qb;
+    DI_REQUIRE(blocks < (1ll << 31), DI_ERANGE, "attention grid too large");
+    hipLaunchKernelGGL(attention_x3_kernel, dim3((unsigned)blocks), dim3(64), 0, s, qk, vt,
+                       cu_seqlens, H, ld_v, n_qb, n_heads, n_pairs, ctx_split);
+    check_launch("attention_x3");
+}
+
 // One 32-key step of the online softmax for 16 queries (lane holds 8 raw scores
 // of its query).  Lazy rescale: the reference max m only moves when a score
 // exceeds it by THR (2^8 in p) -- one compare per score and one ballot in the

@@ -31,6 +31,8 @@ void launch_attention(const T *qk, const T *vt, const int32_t *cu_seqlens, int n
                       int max_len, int H, int ld_v, T *ctx, hipStream_t s,
                       bf16 *ctx_split = nullptr);
 void launch_gemm256(int epi, const GemmArgs &g, hipStream_t s);
+void launch_attention_x3(const float *qk, const float *vt, const int32_t *cu_seqlens, int n_docs,
+                         int max_len, int H, int ld_v, bf16 *ctx_split, hipStream_t s);
 void launch_embed_ln_split(const int32_t *ids, const int32_t *cu, int n_docs, int M, int H,
                            const float *word, const float *pos, const float *type0,
                            const float *gamma, const float *beta, float eps, int pos_offset,
@@ -605,8 +607,9 @@ void forward_folded(di_encoder *e, const int32_t *d_ids, const int32_t *d_cu, in
 
 // fp32-faithful forward (DI_PREC_BF16X3): the unfolded post-LN structure of
 // forward<T> with every GEMM a split-bf16 256-tile GEMM (3 bf16 MFMA products per
-// fp32 product, f32 accumulate: ~2^-17 relative per product), attention in exact f32
-// MFMA, LayerNorms in f32 from f32 pre-LN rows.  Activations that feed a GEMM are
+// fp32 product, f32 accumulate: ~2^-17 relative per product), attention with split
+// bf16 products too (attention_x3_kernel; f32 softmax), LayerNorms in f32 from f32
+// pre-LN rows.  Activations that feed a GEMM are
 // split rows [hi | lo]; Q | K and V^T are f32; the pre-LN rows are f32.
 void forward_split(di_encoder *e, const int32_t *d_ids, const int32_t *d_cu, int n_docs,
                    int64_t M, int max_len, bool timing, hipStream_t s) {
@@ -652,8 +655,8 @@ void forward_split(di_encoder *e, const int32_t *d_ids, const int32_t *d_cu, int
         }
         {
             TimedLaunch tl(e->timer, timing, "attention", s);
-            launch_attention<float>(e->qk.as<float>(), e->vt.as<float>(), d_cu, n_docs, max_len,
-                                    H, e->ld_v, nullptr, s, ctx);
+            launch_attention_x3(e->qk.as<float>(), e->vt.as<float>(), d_cu, n_docs, max_len, H,
+                                e->ld_v, ctx, s);
         }
         g = base();
         g.A = ctx;
