@@ -218,14 +218,15 @@ attention_kernel(const T *__restrict__ qk, const T *__restrict__ vt,
         const float inv = 1.0f / l;
         const int q = q_base + 16 * qt + c;
         if (q < n && ctx_split) {
-            bf16 *out = ctx_split + (int64_t)(tok0 + q) * 2 * H + h * ATT_D + 4 * g;
+            bf16 *out = ctx_split + (int64_t)(tok0 + q) * 2 * H;
 #pragma unroll
             for (int dt = 0; dt < 4; ++dt) {
                 bf16x4 hv, lv;
 #pragma unroll
                 for (int r = 0; r < 4; ++r) hv[r] = split_hi(o[qt][dt][r] * inv), lv[r] = split_lo(o[qt][dt][r] * inv);
-                *reinterpret_cast<bf16x4 *>(out + dt * 16) = hv;
-                *reinterpret_cast<bf16x4 *>(out + H + dt * 16) = lv;
+                const int64_t sc0 = split_col(h * ATT_D + dt * 16 + 4 * g);
+                *reinterpret_cast<bf16x4 *>(out + sc0) = hv;
+                *reinterpret_cast<bf16x4 *>(out + sc0 + 32) = lv;
             }
         } else if (q < n) {
             T *out = ctx + (int64_t)(tok0 + q) * H + h * ATT_D + 4 * g;
@@ -384,7 +385,7 @@ attention_x3_kernel(const float *__restrict__ qk, const float *__restrict__ vt,
         const float inv = 1.0f / l;
         const int q = q_base + 16 * qt + c;
         if (q < n) {
-            bf16 *out = ctx_split + (int64_t)(tok0 + q) * 2 * H + h * ATT_D + 4 * g;
+            bf16 *out = ctx_split + (int64_t)(tok0 + q) * 2 * H;
 #pragma unroll
             for (int dt = 0; dt < 4; ++dt) {
                 bf16x4 hv, lv;
@@ -394,8 +395,9 @@ attention_x3_kernel(const float *__restrict__ qk, const float *__restrict__ vt,
                     hv[r] = split_hi(y);
                     lv[r] = split_lo(y);
                 }
-                *reinterpret_cast<bf16x4 *>(out + dt * 16) = hv;
-                *reinterpret_cast<bf16x4 *>(out + H + dt * 16) = lv;
+                const int64_t sc0 = split_col(h * ATT_D + dt * 16 + 4 * g);
+                *reinterpret_cast<bf16x4 *>(out + sc0) = hv;
+                *reinterpret_cast<bf16x4 *>(out + sc0 + 32) = lv;
             }
         }
     }

@@ -151,16 +151,20 @@ struct GemmArgs {
     const float *col_s, *col_c;          // EPI_FOLD*
     const float *res_gamma, *res_beta;   // EPI_RESID_STATS: LN params of resid
     const float *head_wg;                // EPI_RESID_STATS: w * gamma for the dot partial
-    // split-bf16 (bf16x3, the fp32-faithful mode): A rows are [hi(K) | lo(K)] bf16
-    // (row stride 2K), B rows [hi(K) | lo(K) | hi(K)] (stride 3K); the K loop runs over
-    // 3K so that acc = A_hi B_hi + A_hi B_lo + A_lo B_hi in f32.  Outputs: EPI_BIAS /
-    // EPI_BIAS_GELU split rows (ld_out = 2N), EPI_BIAS_RESID f32 rows (resid split),
-    // EPI_QKV f32 Q | K rows and f32 V^T.
+    // split-bf16 (bf16x3, the fp32-faithful mode): A and B rows are split rows (see
+    // split_col: every 32 columns as 32 hi then 32 lo bf16, row stride 2K), so that one
+    // 64-wide K tile holds the hi and lo halves of 32 k and each (A, B) fragment pair
+    // gives three MFMAs, acc += A_hi B_hi + A_lo B_hi + A_hi B_lo, in f32.  Outputs:
+    // EPI_BIAS / EPI_BIAS_GELU split rows (ld_out = 2N), EPI_BIAS_RESID f32 rows (resid
+    // split), EPI_QKV f32 Q | K rows and f32 V^T.
     int split;
 };
 
 // v = hi + lo with hi = bf16(v), lo = bf16(v - hi): 16 significant bits, relative
 // error <= 2^-17 (the split-bf16 storage of the fp32-faithful mode)
+// Split rows: logical column c of a row of width W sits at split_col(c) (hi) and
+// split_col(c) + 32 (lo) of a 2W-wide bf16 row -- 32-column chunks of hi then lo.
+__host__ __device__ __forceinline__ int64_t split_col(int64_t c) { return (c >> 5) * 64 + (c & 31); }
 __device__ __forceinline__ bf16 split_hi(float v) { return (bf16)v; }
 __device__ __forceinline__ bf16 split_lo(float v) { return (bf16)(v - (float)(bf16)v); }
 

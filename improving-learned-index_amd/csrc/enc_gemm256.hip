@@ -102,12 +102,11 @@ __global__ void __launch_bounds__(G2_T) gemm256_kernel(GemmArgs g) {
     const int gsz = min(GM, n_tm - first_m);
     const int in = bid % (GM * n_tn);
     const int M = g.M, N = g.N, K = g.K;
-    // SPLIT: virtual K tiles t < nkl read (A_hi, B_hi), nkl..2nkl-1 (A_hi, B_lo),
-    // 2nkl.. (A_lo, B_hi): A's physical tile is t - nkl past the first nkl
-    const int nkl = K / 64;
-    const int nk = SPLIT ? 3 * nkl : nkl;
-    const int lda = SPLIT ? 2 * K : K, ldb = SPLIT ? 3 * K : K;
-#define G2_AT(t) ((SPLIT && (t) >= nkl) ? (t) - nkl : (t))
+    // SPLIT: K tile t covers split columns [64 t, 64 t + 64) = the hi (k-step 0) and lo
+    // (k-step 1) halves of logical k [32 t, 32 t + 32)
+    const int nk = SPLIT ? K / 32 : K / 64;
+    const int lda = SPLIT ? 2 * K : K, ldb = lda;
+#define G2_AT(t) (t)
     // EPI_BIAS_RESID_LN: one block owns 256 whole rows (grid 1 x n_tm) and walks
     // their N/256 column tiles, so that the LayerNorm of its rows needs no other block
     constexpr bool LN = EPI == EPI_BIAS_RESID_LN;
@@ -205,16 +204,19 @@ __global__ void __launch_bounds__(G2_T) gemm256_kernel(GemmArgs g) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+    // (k-step pairs (sa, sb): (0, 0), (1, 1) plain; SPLIT (0, 0) hi*hi, (1, 0) A_lo B_hi,
+    // (0, 1) A_hi B_lo)
 #define G2_MFMA(mlo, nlo)                                                                      \
     do {                                                                                       \
         __builtin_amdgcn_sched_barrier(0);                                                     \
         __builtin_amdgcn_s_setprio(1);                                                         \
-        _Pragma("unroll") for (int s = 0; s < 2; ++s)                                          \
+        _Pragma("unroll") for (int p = 0; p < (SPLIT ? 3 : 2); ++p)                            \
             _Pragma("unroll") for (int mm = 0; mm < 4; ++mm)                                   \
                 _Pragma("unroll") for (int nn = 0; nn < 2; ++nn) {                             \
+                    const int sa = SPLIT ? (p == 1) : p, sb = SPLIT ? (p == 2) : p;            \
                     bf16x8 av, bv;                                                             \
-                    __builtin_memcpy(&av, &af[(mlo) + mm][s], 16);                             \
-                    __builtin_memcpy(&bv, &bq[(nlo) + nn][s], 16);                             \
+                    __builtin_memcpy(&av, &af[(mlo) + mm][sa], 16);                            \
+                    __builtin_memcpy(&bv, &bq[(nlo) + nn][sb], 16);                            \
                     acc[(mlo) + mm][(nlo) + nn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(     \
                         bv, av, acc[(mlo) + mm][(nlo) + nn], 0, 0, 0);                         \
                 }                                                                              \
@@ -520,11 +522,11 @@ __global__ void __launch_bounds__(G2_T) gemm256_kernel(GemmArgs g) {
             if (EPI == EPI_BIAS_GELU && !(g.ablate & 2)) gelu_erf8(v);  // ablate 2: no GELU (profiling)
             const int64_t o = (int64_t)row * g.ld_out + col_l + h * 32;
             if constexpr (EPI == EPI_BIAS_RESID || EPI == EPI_BIAS_RESID_LN) {
-                if constexpr (SPLIT) {  // residual rows [hi | lo]
+                if constexpr (SPLIT) {  // split residual rows
                     const bf16 *rp = static_cast<const bf16 *>(g.resid) + (int64_t)row * 2 * N +
-                                     col_l + h * 32;
+                                     split_col(col_l + h * 32);
                     const bf16x8 rh = *reinterpret_cast<const bf16x8 *>(rp);
-                    const bf16x8 rl = *reinterpret_cast<const bf16x8 *>(rp + N);
+                    const bf16x8 rl = *reinterpret_cast<const bf16x8 *>(rp + 32);
 #pragma unroll
                     for (int e = 0; e < 8; ++e) v[e] += (float)rh[e] + (float)rl[e];
                 } else {
@@ -539,12 +541,14 @@ __global__ void __launch_bounds__(G2_T) gemm256_kernel(GemmArgs g) {
                     float *op = static_cast<float *>(g.out) + o;
                     *reinterpret_cast<float4 *>(op) = make_float4(v[0], v[1], v[2], v[3]);
                     *reinterpret_cast<float4 *>(op + 4) = make_float4(v[4], v[5], v[6], v[7]);
-                } else {  // split rows: hi at o, lo at o + N (ld_out = 2N)
+                } else {  // split rows (ld_out = 2N): 8 columns of one 32-column chunk
                     bf16x8 hv, lv;
 #pragma unroll
                     for (int e = 0; e < 8; ++e) hv[e] = split_hi(v[e]), lv[e] = split_lo(v[e]);
-                    g2_store(static_cast<bf16 *>(g.out) + o, hv);
-                    g2_store(static_cast<bf16 *>(g.out) + o + N, lv);
+                    bf16 *op = static_cast<bf16 *>(g.out) + (int64_t)row * g.ld_out +
+                               split_col(col_l + h * 32);
+                    g2_store(op, hv);
+                    g2_store(op + 32, lv);
                 }
                 continue;
             }
@@ -694,7 +698,9 @@ bool gemm256_ok(int epi, const GemmArgs &g) {
     if (g.split && !(epi == EPI_BIAS || epi == EPI_BIAS_GELU || epi == EPI_BIAS_RESID ||
                      epi == EPI_QKV))
         return false;
-    return g.N % G2_TILE == 0 && g.K % 128 == 0 && g.K >= 128 && g.a_rows >= m_pad &&
+    // (SPLIT: K tiles of 32 logical k, K % 64 == 0 keeps their count even)
+    return g.N % G2_TILE == 0 && g.K % (g.split ? 64 : 128) == 0 && g.K >= 128 &&
+           g.a_rows >= m_pad &&
            (epi != EPI_QKV || (2 * g.hidden) % G2_TILE == 0) &&
            (epi != EPI_BIAS_RESID_LN || (g.N <= 1024 && g.ld_out == g.N));
 }

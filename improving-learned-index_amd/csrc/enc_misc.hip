@@ -161,13 +161,14 @@ __device__ __forceinline__ void st4(bf16 *p, const float (&f)[4]) {
 __device__ __forceinline__ void st4(float *p, const float (&f)[4]) {
     *reinterpret_cast<float4 *>(p) = make_float4(f[0], f[1], f[2], f[3]);
 }
-// split-bf16 row store (fp32-faithful mode): hi at p, lo at p + H
-__device__ __forceinline__ void st4_split(bf16 *p, int H, const float (&f)[4]) {
+// split-bf16 row store (fp32-faithful mode): 4 columns col.. of one 32-column chunk
+// of the split row at p (enc_common.h split_col)
+__device__ __forceinline__ void st4_split(bf16 *p, int col, const float (&f)[4]) {
     bf16x4 hi, lo;
 #pragma unroll
     for (int j = 0; j < 4; ++j) hi[j] = split_hi(f[j]), lo[j] = split_lo(f[j]);
-    *reinterpret_cast<bf16x4 *>(p) = hi;
-    *reinterpret_cast<bf16x4 *>(p + H) = lo;
+    *reinterpret_cast<bf16x4 *>(p + split_col(col)) = hi;
+    *reinterpret_cast<bf16x4 *>(p + split_col(col) + 32) = lo;
 }
 // row store of the LayerNorm kernels: OUT = T (plain rows) or split rows of 2H bf16
 template <typename T, bool SPLIT>
@@ -177,7 +178,7 @@ struct LnOut {
 template <bool SPLIT, typename O>
 __device__ __forceinline__ void st4_row(O *out, int64_t row, int H, int col, const float (&f)[4]) {
     if constexpr (SPLIT)
-        st4_split(out + row * 2 * H + col, H, f);
+        st4_split(out + row * 2 * H, col, f);
     else
         st4(out + row * H + col, f);
 }

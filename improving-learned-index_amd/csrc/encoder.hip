@@ -221,25 +221,24 @@ void upload(DevBuf &dst, const std::vector<const HostTensor *> &parts, int64_t r
     }
 }
 
-// split-bf16 GEMM weight (fp32-faithful mode): each [K] row of W becomes
-// [hi(K) | lo(K) | hi(K)], hi = bf16(w), lo = bf16(w - hi), so that the 3K-long
-// K loop of the split GEMM (A rows [hi | lo]) sums A_hi W_hi + A_hi W_lo + A_lo W_hi.
+// split-bf16 GEMM weight (fp32-faithful mode): each [K] row of W becomes a split row
+// (enc_common.h split_col: 32 hi then 32 lo bf16 per 32 columns), hi = bf16(w),
+// lo = bf16(w - hi), the layout the split GEMM's K tiles read.
 void upload_split3(DevBuf &dst, const std::vector<const HostTensor *> &parts, int K) {
     int64_t rows = 0;
     for (auto *p : parts) rows += p->numel() / K;
-    std::vector<uint16_t> h((size_t)(rows * 3 * K));
+    std::vector<uint16_t> h((size_t)(rows * 2 * K));
     int64_t r = 0;
     for (auto *p : parts) {
         const int64_t pr = p->numel() / K;
         for (int64_t i = 0; i < pr; ++i, ++r) {
-            uint16_t *o = &h[(size_t)(r * 3 * K)];
+            uint16_t *o = &h[(size_t)(r * 2 * K)];
             for (int k = 0; k < K; ++k) {
                 const float w = p->at(i * K + k);
                 const uint16_t hi = f32_to_bf16_bits(w);
                 const uint16_t lo = f32_to_bf16_bits(w - bf16_bits_to_f32(hi));
-                o[k] = hi;
-                o[K + k] = lo;
-                o[2 * K + k] = hi;
+                o[split_col(k)] = hi;
+                o[split_col(k) + 32] = lo;
             }
         }
     }
