@@ -266,8 +266,9 @@ def flops_per_doc(n, H=768, L=12, t=None):
 
 
 def prune_last_layer():
-    """The library's DI_PRUNE_LAST default (on) for the term-output encode."""
-    return os.environ.get("DI_PRUNE_LAST", "1")[:1] != "0"
+    """The bf16 term-output encode computes the last layer on the kept terms' rows only
+    (bit-identical impacts)."""
+    return True
 
 
 def encode_leg(args, rank, world, dev, precision="bf16"):

@@ -416,49 +416,14 @@ void launch_attention_x3(const float *qk, const float *vt, const int32_t *cu_seq
     check_launch("attention_x3");
 }
 
-// One 32-key step of the online softmax for 16 queries (lane holds 8 raw scores
-// of its query).  Lazy rescale: the reference max m only moves when a score
-// exceeds it by THR (2^8 in p) -- one compare per score and one ballot in the
-// common case; the full max / rescale path runs on the first chunk and rarely
-// after.  p = exp2(s * sc - m * sc) by the raw v_exp_f32 (inputs <= 8; underflow
-// to 0 is what softmax wants).
-__device__ __forceinline__ void softmax_step(f32x4 (&s)[2], float &m, float &msc, f32x4 (&o)[4],
-                                             f32x4 &l, bf16x8 &pb) {
-    constexpr float sc = 0.125f * 1.4426950408889634f;  // 1/sqrt(64) * log2(e)
-    constexpr float THR = 8.0f / sc;
-    const float lim = m + THR;
-    bool need = false;
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) need |= s[t][r] > lim;
-    if (__any(need)) {
-        float cmax = fmaxf(fmaxf(fmaxf(s[0][0], s[0][1]), fmaxf(s[0][2], s[0][3])),
-                           fmaxf(fmaxf(s[1][0], s[1][1]), fmaxf(s[1][2], s[1][3])));
-        const auto p16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(cmax),
-                                                          __float_as_uint(cmax), false, false);
-        cmax = fmaxf(__uint_as_float(p16[0]), __uint_as_float(p16[1]));
-        const auto p32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(cmax),
-                                                          __float_as_uint(cmax), false, false);
-        cmax = fmaxf(__uint_as_float(p32[0]), __uint_as_float(p32[1]));
-        const float m_new = fmaxf(m, cmax);
-        const float alpha = exp2f((m - m_new) * sc);  // 0 on the first chunk
-        m = m_new;
-        msc = m_new * sc;
-        l *= alpha;
-#pragma unroll
-        for (int dt = 0; dt < 4; ++dt) o[dt] *= alpha;
-    }
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        pb[r] = (bf16)__builtin_amdgcn_exp2f(fmaf(s[0][r], sc, -msc));
-        pb[4 + r] = (bf16)__builtin_amdgcn_exp2f(fmaf(s[1][r], sc, -msc));
-    }
-}
-
-// softmax_step split in its three parts (same arithmetic), so that the merged key
-// loop of attention_v3_kernel<., true> can test every query tile of a step with one
-// branch and keep the common path of both tiles in one basic block.
+// One 32-key step of the online softmax for 16 queries (lane holds 8 raw scores of
+// its query), in three parts so that attention_v3_kernel's key loop can test every
+// query tile of a step with one branch and keep the common path of both tiles in one
+// basic block.  Lazy rescale: the reference max m only moves when a score exceeds it
+// by THR (2^8 in p) -- one compare per score and one ballot in the common case; the
+// full max / rescale path runs on the first chunk and rarely after.
+// p = exp2(s * sc - m * sc) by the raw v_exp_f32 (inputs <= 8; underflow to 0 is
+// what softmax wants).
 __device__ __forceinline__ bool softmax_need(const f32x4 (&s)[2], float m) {
     constexpr float sc = 0.125f * 1.4426950408889634f;
     const float lim = m + 8.0f / sc;
@@ -497,287 +462,6 @@ __device__ __forceinline__ void softmax_p(const f32x4 (&s)[2], float msc, bf16x8
     }
 }
 
-// bf16 fast path.  Same swapped-product structure as attention_kernel, with the
-// softmax VALU work cut down (the f32/bf16 kernel above is VALU-issue-bound):
-//  * exp argument is one FMA on the raw score: p = exp2(s * c - m * c);
-//  * lazy rescale: the running max m only moves when some lane's chunk max exceeds
-//    it by more than 2^8 in p (one ballot per chunk); p <= 256 is exact enough in
-//    bf16/f32 and the final O / l normalisation is unchanged;
-//  * the row sum l comes from the MFMA: one extra 16x16x32 with an all-ones A
-//    fragment sums the bf16 P^T actually used for O (no per-element adds);
-//  * max over the 4 key groups by v_permlane16/32_swap (VALU) instead of
-//    ds_bpermute; key masking only on the last chunk.
-template <int QTB>
-__global__ void __launch_bounds__(64, QTB == 2 ? 4 : 2)
-attention_bf16_kernel(const bf16 *__restrict__ qk, const bf16 *__restrict__ vt,
-                      const int32_t *__restrict__ cu_seqlens, int H, int ld_v, int n_qb,
-                      int n_heads, int n_pairs, bf16 *__restrict__ ctx) {
-    const int id = blockIdx.x, x = id & 7, j = id >> 3;
-    const int pair = (j / n_qb) * 8 + x;
-    const int qb = j % n_qb;
-    if (pair >= n_pairs) return;
-    const int doc = pair / n_heads, h = pair % n_heads;
-    const int lane = threadIdx.x;
-    const int g = lane >> 4, c = lane & 15;
-    const int tok0 = cu_seqlens[doc], n = cu_seqlens[doc + 1] - tok0;
-    const int q_base = qb * (16 * QTB);
-    if (q_base >= n) return;
-    const int ldqk = 2 * H;
-
-    uint4 qf[QTB][2];
-#pragma unroll
-    for (int qt = 0; qt < QTB; ++qt) {
-        const int qrow = tok0 + min(q_base + 16 * qt + c, n - 1);
-#pragma unroll
-        for (int ch = 0; ch < 2; ++ch)
-            qf[qt][ch] = *reinterpret_cast<const uint4 *>(qk + (int64_t)qrow * ldqk + h * ATT_D +
-                                                          ch * 32 + 8 * g);
-    }
-    float m[QTB], msc[QTB];
-    f32x4 o[QTB][4], l[QTB];
-#pragma unroll
-    for (int qt = 0; qt < QTB; ++qt) {
-        m[qt] = -INFINITY;
-        msc[qt] = -INFINITY;
-        l[qt] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int dt = 0; dt < 4; ++dt) o[qt][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-    bf16x8 ones;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) ones[e] = (bf16)1.0f;
-    const bf16 *kbase = qk + H + h * ATT_D;
-    const bf16 *vbase = vt + (int64_t)(h * ATT_D) * ld_v + vt_base(doc, tok0);
-
-    for (int key0 = 0; key0 < n; key0 += 32) {
-        uint4 kf[2][2];
-#pragma unroll
-        for (int t = 0; t < 2; ++t) {
-            const int krow = tok0 + min(key0 + 16 * t + c, n - 1);
-#pragma unroll
-            for (int ch = 0; ch < 2; ++ch)
-                kf[t][ch] = *reinterpret_cast<const uint4 *>(kbase + (int64_t)krow * ldqk +
-                                                             ch * 32 + 8 * g);
-        }
-        bf16x8 vf[4];
-#pragma unroll
-        for (int dt = 0; dt < 4; ++dt) {
-            const bf16 *vrow = vbase + (int64_t)(dt * 16 + c) * ld_v + key0 + 4 * g;
-            const uint2 lo = *reinterpret_cast<const uint2 *>(vrow);
-            const uint2 hi = *reinterpret_cast<const uint2 *>(vrow + 16);
-            const uint4 v4 = make_uint4(lo.x, lo.y, hi.x, hi.y);
-            __builtin_memcpy(&vf[dt], &v4, 16);
-        }
-        const bool tail = key0 + 32 > n;
-#pragma unroll
-        for (int qt = 0; qt < QTB; ++qt) {
-            f32x4 s[2];
-#pragma unroll
-            for (int t = 0; t < 2; ++t) {
-                s[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-                for (int ch = 0; ch < 2; ++ch) mma_chunk(kf[t][ch], qf[qt][ch], s[t], bf16{});
-            }
-            // lane holds S^T[key0 + 16t + 4g + r][q_base + 16 qt + c] (raw q.k)
-            if (tail) {
-#pragma unroll
-                for (int t = 0; t < 2; ++t)
-#pragma unroll
-                    for (int r = 0; r < 4; ++r)
-                        if (key0 + 16 * t + 4 * g + r >= n) s[t][r] = -INFINITY;
-            }
-            bf16x8 pb;
-            softmax_step(s, m[qt], msc[qt], o[qt], l[qt], pb);
-#pragma unroll
-            for (int dt = 0; dt < 4; ++dt)
-                o[qt][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf[dt], pb, o[qt][dt], 0, 0, 0);
-            l[qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pb, l[qt], 0, 0, 0);
-        }
-    }
-#pragma unroll
-    for (int qt = 0; qt < QTB; ++qt) {
-        const float inv = 1.0f / l[qt][0];  // every row of the ones product is l
-        const int q = q_base + 16 * qt + c;
-        if (q < n) {
-            bf16 *out = ctx + (int64_t)(tok0 + q) * H + h * ATT_D + 4 * g;
-#pragma unroll
-            for (int dt = 0; dt < 4; ++dt) {
-                bf16x4 v;
-#pragma unroll
-                for (int r = 0; r < 4; ++r) v[r] = (bf16)(o[qt][dt][r] * inv);
-                *reinterpret_cast<bf16x4 *>(out + dt * 16) = v;
-            }
-        }
-    }
-}
-
-// LDS-staged form (bf16): one 256-thread workgroup per (doc, head).  The
-// register-direct kernels above load K / V^T fragments straight from L2 with
-// 16 rows per instruction (16 partial cache lines per load), which bounds them on
-// the address/texture path.  Here the workgroup copies the head's K [n][64] and
-// V^T [64][n] into LDS once with whole-line 16-byte loads; the four waves then
-// take the 64-query blocks of the document round-robin and read every fragment
-// with one ds_read_b128.
-//   K image : row r (key) = 128 B, 16-B chunk q at slot q ^ (r & 7) (2-way reads).
-//   V^T image: row d = 2*n32 + 16 bytes (n32 = n rounded up to 32; the odd 16-B
-//             row skew makes the 16 rows of a fragment read conflict-free).
-// Key order inside a 32-key chunk: S^T tile t, fragment row i holds key
-// 8(i>>2) + 4t + (i&3), so accumulator lane (g, c) ends up with the 8 consecutive
-// keys 8g..8g+7 -- exactly the MFMA k-slots 8g..8g+7 of the P^T operand, whose V^T
-// partner is then one contiguous 16-byte read.
-constexpr int ATT_LDS_WAVES = 4;
-
-__host__ __device__ inline int attn_lds_bytes(int max_len) {
-    const int n32 = (max_len + 31) / 32 * 32;
-    return max_len * 128 + 64 * (2 * n32 + 16);
-}
-
-template <int QTB>
-__global__ void __launch_bounds__(64 * ATT_LDS_WAVES, 2)
-attention_lds_kernel(const bf16 *__restrict__ qk, const bf16 *__restrict__ vt,
-                     const int32_t *__restrict__ cu_seqlens, int H, int ld_v, int n_heads,
-                     bf16 *__restrict__ ctx) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-    constexpr int NT = 64 * ATT_LDS_WAVES;
-    const int doc = blockIdx.x / n_heads, h = blockIdx.x % n_heads;
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int g = lane >> 4, c = lane & 15;
-    const int tok0 = cu_seqlens[doc], n = cu_seqlens[doc + 1] - tok0;
-    if (n <= 0) return;
-    const int n32 = (n + 31) & ~31;
-    const int SV = 2 * n32 + 16;  // V^T image row stride (bytes)
-    unsigned char *kim = lds;
-    unsigned char *vim = lds + n * 128;
-    const int ldqk = 2 * H;
-
-    // ---- stage K (n x 128 B) and V^T (64 x n32 keys) ---------------------------
-    // All of a thread's loads are issued before any LDS write, so the whole copy
-    // costs one memory round trip (10 + 10 pieces of 16 B per thread cover n <= 320).
-    {
-        constexpr int B = 10;
-        const bf16 *kg = qk + (int64_t)tok0 * ldqk + H + h * ATT_D;
-        const bf16 *vg = vt + (int64_t)(h * ATT_D) * ld_v + vt_base(doc, tok0);
-        const int nkc = n * 8;
-        const int q8 = n32 / 8;  // 16-byte pieces per V^T row
-        const int nvc = 64 * q8;
-        for (int base = tid; base < nkc || base < nvc; base += NT * B) {
-            uint4 kv[B], vv[B];
-#pragma unroll
-            for (int b = 0; b < B; ++b) {  // unconditional (clamped) loads stay in registers
-                const int id = min(base + NT * b, nkc - 1);
-                kv[b] = *reinterpret_cast<const uint4 *>(kg + (int64_t)(id >> 3) * ldqk +
-                                                         (id & 7) * 8);
-            }
-#pragma unroll
-            for (int b = 0; b < B; ++b) {
-                const int id = min(base + NT * b, nvc - 1);
-                vv[b] = *reinterpret_cast<const uint4 *>(vg + (int64_t)(id / q8) * ld_v +
-                                                         (id % q8) * 8);
-            }
-#pragma unroll
-            for (int b = 0; b < B; ++b) {
-                const int id = base + NT * b;
-                const int r = id >> 3, q = id & 7;
-                if (id < nkc)
-                    *reinterpret_cast<uint4 *>(kim + r * 128 + ((q ^ (r & 7)) << 4)) = kv[b];
-            }
-#pragma unroll
-            for (int b = 0; b < B; ++b) {
-                const int id = base + NT * b;
-                if (id < nvc)
-                    *reinterpret_cast<uint4 *>(vim + (id / q8) * SV + (id % q8) * 16) = vv[b];
-            }
-        }
-    }
-    __syncthreads();
-
-    bf16x8 ones;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) ones[e] = (bf16)1.0f;
-    const int krel = 8 * (c >> 2) + (c & 3);  // fragment row c -> key offset (t adds 4)
-    const int n_qb = (n + 16 * QTB - 1) / (16 * QTB);
-    for (int qb = wave; qb < n_qb; qb += ATT_LDS_WAVES) {
-        const int q_base = qb * 16 * QTB;
-        uint4 qf[QTB][2];
-#pragma unroll
-        for (int qt = 0; qt < QTB; ++qt) {
-            const int qrow = tok0 + min(q_base + 16 * qt + c, n - 1);
-#pragma unroll
-            for (int ch = 0; ch < 2; ++ch)
-                qf[qt][ch] = *reinterpret_cast<const uint4 *>(qk + (int64_t)qrow * ldqk +
-                                                              h * ATT_D + ch * 32 + 8 * g);
-        }
-        float m[QTB], msc[QTB];
-        f32x4 o[QTB][4], l[QTB];
-#pragma unroll
-        for (int qt = 0; qt < QTB; ++qt) {
-            m[qt] = -INFINITY;
-            msc[qt] = -INFINITY;
-            l[qt] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int dt = 0; dt < 4; ++dt) o[qt][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
-        }
-        for (int key0 = 0; key0 < n; key0 += 32) {
-            uint4 kf[2][2];
-#pragma unroll
-            for (int t = 0; t < 2; ++t) {
-                const int r = min(key0 + krel + 4 * t, n - 1);
-#pragma unroll
-                for (int ch = 0; ch < 2; ++ch)
-                    kf[t][ch] = *reinterpret_cast<const uint4 *>(
-                        kim + r * 128 + (((ch * 4 + g) ^ (r & 7)) << 4));
-            }
-            bf16x8 vf[4];
-#pragma unroll
-            for (int dt = 0; dt < 4; ++dt)
-                vf[dt] = *reinterpret_cast<const bf16x8 *>(vim + (dt * 16 + c) * SV +
-                                                           (key0 + 8 * g) * 2);
-            const bool tail = key0 + 32 > n;
-#pragma unroll
-            for (int qt = 0; qt < QTB; ++qt) {
-                f32x4 s[2];
-#pragma unroll
-                for (int t = 0; t < 2; ++t) {
-                    s[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-                    for (int ch = 0; ch < 2; ++ch) mma_chunk(kf[t][ch], qf[qt][ch], s[t], bf16{});
-                }
-                // lane (g, c) holds S^T[key0 + 8g + 4t + r][q_base + 16 qt + c]
-                if (tail) {
-#pragma unroll
-                    for (int t = 0; t < 2; ++t)
-#pragma unroll
-                        for (int r = 0; r < 4; ++r)
-                            if (key0 + 8 * g + 4 * t + r >= n) s[t][r] = -INFINITY;
-                }
-                bf16x8 pb;
-                softmax_step(s, m[qt], msc[qt], o[qt], l[qt], pb);
-#pragma unroll
-                for (int dt = 0; dt < 4; ++dt)
-                    o[qt][dt] =
-                        __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf[dt], pb, o[qt][dt], 0, 0, 0);
-                l[qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pb, l[qt], 0, 0, 0);
-            }
-        }
-#pragma unroll
-        for (int qt = 0; qt < QTB; ++qt) {
-            const float inv = 1.0f / l[qt][0];
-            const int q = q_base + 16 * qt + c;
-            if (q < n) {
-                bf16 *out = ctx + (int64_t)(tok0 + q) * H + h * ATT_D + 4 * g;
-#pragma unroll
-                for (int dt = 0; dt < 4; ++dt) {
-                    bf16x4 v;
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) v[r] = (bf16)(o[qt][dt][r] * inv);
-                    *reinterpret_cast<bf16x4 *>(out + dt * 16) = v;
-                }
-            }
-        }
-    }
-}
-
 // ---------------------------------------------------------------------------
 // Persistent, double-buffered form (bf16, max_len <= 320): the QKV projection is
 // written row-major [M][3H] (Q | K | V, no V^T scatter), and one 512-thread
@@ -811,12 +495,12 @@ __device__ __forceinline__ uint2 ds_read_tr_b16(uint32_t addr) {
     return r;
 }
 
-// MERGED = true (default): the key loop is instantiated per tile count (1 or 2) and
-// runs both tiles' S^T products, one shared rescale test (a branch only into the
-// rare path) and both tiles' exp / O^T products as one basic block, so that one
-// tile's softmax VALU overlaps the other tile's MFMAs; same arithmetic as the
-// per-tile loop (MERGED = false, DI_ATTN_V3_MERGED=0), bit-identical outputs.
-template <bool DB, bool MERGED>
+// The key loop is instantiated per tile count (1 or 2) and runs both tiles' S^T
+// products, one shared rescale test (a branch only into the rare path) and both
+// tiles' exp / O^T products as one basic block, so that one tile's softmax VALU
+// overlaps the other tile's MFMAs (-2.5% attention time against a per-tile loop,
+// bit-identical).
+template <bool DB>
 __global__ void __launch_bounds__(64 * ATT3_WAVES, 1)
 attention_v3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu_seqlens, int H,
                     int n_heads, int n_pairs, bf16 *__restrict__ ctx,
@@ -1089,7 +773,7 @@ attention_v3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
                 }
             }
         };
-        if constexpr (MERGED) {
+        {
 #pragma unroll
             for (int i = 0; i < 2; ++i) {
                 if (2 * i >= t_cnt) continue;
@@ -1099,71 +783,7 @@ attention_v3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
                 else
                     key_loop(std::integral_constant<int, 1>{}, qc[i], q_base);
             }
-        } else {
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            if (2 * i >= t_cnt) continue;  // (not break: keeps the loop unrolled, qf[i] static)
-            const int nqt = min(QTB, t_cnt - 2 * i);  // tiles in this step (1 or 2)
-            const int q_base = (t_first + 2 * i) * 16;
-            float m[QTB], msc[QTB];
-            f32x4 o[QTB][4], l[QTB];
-#pragma unroll
-            for (int qt = 0; qt < QTB; ++qt) {
-                m[qt] = -INFINITY;
-                msc[qt] = -INFINITY;
-                l[qt] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-                for (int dt = 0; dt < 4; ++dt) o[qt][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
-            }
-            for (int key0 = 0; key0 < n; key0 += 32) {
-                uint4 kf[2][2];
-                bf16x8 vf[4];
-                read_kv(key0, kf, vf);
-                const bool tail = key0 + 32 > n;
-#pragma unroll
-                for (int qt = 0; qt < QTB; ++qt) {
-                    if (qt >= nqt) continue;  // (wave-uniform)
-                    f32x4 s[2];
-#pragma unroll
-                    for (int t = 0; t < 2; ++t) {
-                        s[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-                        for (int ch = 0; ch < 2; ++ch)
-                            mma_chunk(kf[t][ch], qc[i][qt][ch], s[t], bf16{});
-                    }
-                    if (tail) {
-#pragma unroll
-                        for (int t = 0; t < 2; ++t)
-#pragma unroll
-                            for (int r = 0; r < 4; ++r)
-                                if (key0 + 8 * g + 4 * t + r >= n) s[t][r] = -INFINITY;
-                    }
-                    bf16x8 pb;
-                    softmax_step(s, m[qt], msc[qt], o[qt], l[qt], pb);
-#pragma unroll
-                    for (int dt = 0; dt < 4; ++dt)
-                        o[qt][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf[dt], pb, o[qt][dt],
-                                                                            0, 0, 0);
-                    l[qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pb, l[qt], 0, 0, 0);
-                }
-            }
-#pragma unroll
-            for (int qt = 0; qt < QTB; ++qt) {
-                const float inv = 1.0f / l[qt][0];
-                const int q = q_base + 16 * qt + c;
-                if (qt < nqt && q < nq) {
-                    bf16 *out = ctx + (int64_t)(out0 + q) * H + h * ATT_D + 4 * g;
-#pragma unroll
-                    for (int dt = 0; dt < 4; ++dt) {
-                        bf16x4 v;
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) v[r] = (bf16)(o[qt][dt][r] * inv);
-                        *reinterpret_cast<bf16x4 *>(out + dt * 16) = v;
-                    }
-                }
-            }
         }
-        }  // !MERGED
         __syncthreads();  // every wave is done with buffer b before it is restaged
     };
     uint4 qa[2][QTB][2], qb2[2][QTB][2];
@@ -1198,28 +818,16 @@ void launch_attention_v3(const bf16 *qkv, const int32_t *cu_seqlens, int n_docs,
     }();
     const int n_heads = H / ATT_D, n_pairs = n_docs * n_heads;
     const int grid = std::min(n_pairs, n_cu);
-    // A/B knob: DI_ATTN_V3_MERGED=0 runs the per-tile key loop (bit-identical)
-    static const bool merged = [] {
-        const char *e = std::getenv("DI_ATTN_V3_MERGED");
-        return !(e && std::atoi(e) == 0);
-    }();
     auto launch = [&](auto kern, int lds_bytes) {
         DI_HIP(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                                    lds_bytes));
         hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * ATT3_WAVES), lds_bytes, s, qkv, cu_seqlens,
                            H, n_heads, n_pairs, ctx, qsel, cu_qsel);
     };
-    if (max_len <= Att3<true>::ROWS) {
-        if (merged)
-            launch(attention_v3_kernel<true, true>, Att3<true>::LDS);
-        else
-            launch(attention_v3_kernel<true, false>, Att3<true>::LDS);
-    } else {
-        if (merged)
-            launch(attention_v3_kernel<false, true>, Att3<false>::LDS);
-        else
-            launch(attention_v3_kernel<false, false>, Att3<false>::LDS);
-    }
+    if (max_len <= Att3<true>::ROWS)
+        launch(attention_v3_kernel<true>, Att3<true>::LDS);
+    else
+        launch(attention_v3_kernel<false>, Att3<false>::LDS);
     check_launch("attention_v3");
 }
 
@@ -1257,41 +865,7 @@ void launch_attention(const T *qk, const T *vt, const int32_t *cu_seqlens, int n
     DI_REQUIRE(!ctx_split || sizeof(T) == 4, DI_EINVAL, "split output: f32 attention only");
     if (n_docs == 0 || max_len == 0) return;
     const int n_heads = H / ATT_D, n_pairs = n_docs * n_heads;
-    if constexpr (std::is_same<T, bf16>::value) {
-        // A/B knob (DI_ATTN): 1/3 LDS-staged (default; 3 = the encoder's v3 choice,
-        // which lands here when v3 does not apply), 0 the generic kernel, 2/4 the
-        // register-direct bf16 kernel with 2/4 query tiles per wave
-        static const int mode = [] {
-            const char *e = std::getenv("DI_ATTN");
-            return e ? std::atoi(e) : 1;
-        }();
-        if (mode == 1 || mode == 3) {  // LDS-staged (default when v3 does not apply)
-            const int lds_bytes = attn_lds_bytes(max_len);
-            DI_REQUIRE(lds_bytes <= 160 * 1024, DI_ERANGE, "attention: max_len %d too long",
-                       max_len);
-            DI_HIP(hipFuncSetAttribute((const void *)attention_lds_kernel<4>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes));
-            hipLaunchKernelGGL(attention_lds_kernel<4>, dim3((unsigned)n_pairs),
-                               dim3(64 * ATT_LDS_WAVES), lds_bytes, s, qk, vt, cu_seqlens, H, ld_v,
-                               n_heads, ctx);
-            check_launch("attention");
-            return;
-        }
-        if (mode == 2 || mode == 4) {
-            const int qtb = mode;
-            const int n_qb = (max_len + 16 * qtb - 1) / (16 * qtb);
-            const int64_t blocks = (int64_t)((n_pairs + 7) / 8) * 8 * n_qb;
-            DI_REQUIRE(blocks < (1ll << 31), DI_ERANGE, "attention grid too large");
-            if (qtb == 2)
-                hipLaunchKernelGGL(attention_bf16_kernel<2>, dim3((unsigned)blocks), dim3(64), 0, s,
-                                   qk, vt, cu_seqlens, H, ld_v, n_qb, n_heads, n_pairs, ctx);
-            else
-                hipLaunchKernelGGL(attention_bf16_kernel<4>, dim3((unsigned)blocks), dim3(64), 0, s,
-                                   qk, vt, cu_seqlens, H, ld_v, n_qb, n_heads, n_pairs, ctx);
-            check_launch("attention");
-            return;
-        }
-    }
+    // (bf16: the generic path of documents the persistent v3 kernel does not take)
     const int n_qb = (max_len + 16 * QT - 1) / (16 * QT);
     const int64_t blocks = (int64_t)((n_pairs + 7) / 8) * 8 * n_qb;
     DI_REQUIRE(blocks < (1ll << 31), DI_ERANGE, "attention grid too large");

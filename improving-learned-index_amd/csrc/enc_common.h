@@ -103,8 +103,7 @@ enum GemmEpi : int {
     EPI_BIAS_GELU = 1,   // out(T) = gelu(acc + bias)
     EPI_BIAS_RESID = 2,  // out(T) = acc + bias + resid(T), one rounding (pre-LayerNorm)
     EPI_QKV = 3,         // Q,K -> qk[M][2H] (T);  V -> vt[H][ldv] transposed (T)
-    EPI_BIAS_RESID_LN = 4,  // as EPI_BIAS_RESID into out, then LayerNorm of the whole
-                            // rows -> ln_out (and / or the impact head); 256-col tiles only
+    // (4: a fused-LayerNorm epilogue, removed -- measured slower than GEMM + LayerNorm)
     // LayerNorm folding (bf16, 256-col tiles): the GEMM that consumes LN(x) takes the
     // un-normalised x and weights W' = W diag(gamma) and corrects per row / column:
     //   LN(x) W^T + b = r (x W'^T) - r mu s + c,  s = W' 1,  c = b + W beta
@@ -131,17 +130,7 @@ struct GemmArgs {
                           // read past M without clamping)
     int tune_gm;          // 256-tile kernel: M tiles per group in the tile order (0 = default)
     int ablate;           // profiling only (tools/gemm_check): 1 = skip the epilogue
-    int stagger;          // 256-tile kernel: first-wave delay (shader cycles) of every other
-                          // CU's first tile, so the CUs' store bursts alternate (0 = off)
-    // EPI_BIAS_RESID_LN: LayerNorm(gamma, beta, eps) of the out rows -> ln_out (may be
-    // null); with head_w, impact[row] = act(LN(row) . head_w + head_b)
-    const float *ln_gamma, *ln_beta;
     float ln_eps;
-    void *ln_out;
-    const float *head_w;
-    float head_b;
-    int act;
-    float *impact;
     // LayerNorm folding: row statistics as float4 partials (sum, sumsq, dot, 0) per
     // 256-column tile: stats[t * stats_ld + row], t < n_part
     const float2 *row_ln;     // EPI_FOLD*: (rstd, -rstd mean) of A's rows; EPI_RESID_STATS:

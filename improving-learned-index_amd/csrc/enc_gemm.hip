@@ -251,32 +251,17 @@ __global__ void __launch_bounds__(G_THREADS) gemm_nt_kernel(GemmArgs g) {
     }
 }
 
-static bool force_gemm128() {
-    static const bool f = std::getenv("DI_GEMM128") != nullptr;  // A/B knob
-    return f;
-}
-
-// EPI_BIAS_RESID_LN exists only in the 256-tile bf16 kernel.
-// Opt-in (DI_FUSED_LN=1): measured slower than GEMM + ln_vec_kernel at the bench
-// shape -- one block per 256 whole rows leaves 807 blocks on 256 CUs (4 rounds at
-// 79 %), which costs more than the separate LayerNorm pass saves.
-bool gemm_fused_ln_ok(const GemmArgs &g) {
-    static const bool on = std::getenv("DI_FUSED_LN") != nullptr;
-    return on && !force_gemm128() && gemm256_ok(EPI_BIAS_RESID_LN, g);
-}
-
 template <typename T>
 void launch_gemm(int epi, const GemmArgs &g, hipStream_t s) {
     DI_REQUIRE(g.K % (ROW_BYTES / (int)sizeof(T)) == 0, DI_EINVAL,
                "GEMM K=%d must be a multiple of %d", g.K, ROW_BYTES / (int)sizeof(T));
     if (g.M == 0) return;
     if constexpr (std::is_same<T, bf16>::value) {
-        if (!force_gemm128() && gemm256_ok(epi, g)) {
+        if (gemm256_ok(epi, g)) {
             launch_gemm256(epi, g, s);
             return;
         }
     }
-    DI_REQUIRE(epi != EPI_BIAS_RESID_LN, DI_EINVAL, "fused LayerNorm GEMM needs the bf16 256-tile kernel");
     dim3 grid((g.N + GB_N - 1) / GB_N, (g.M + GB_M - 1) / GB_M);
     switch (epi) {
         case EPI_BIAS:

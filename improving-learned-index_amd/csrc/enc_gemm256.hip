@@ -78,18 +78,6 @@ __global__ void __launch_bounds__(G2_T) gemm256_kernel(GemmArgs g) {
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wr = wave >> 2, wc = wave & 3;
 
-    // Epilogue stagger (speed only): every block ends in a burst of stores that
-    // is HBM-write-bound when all CUs reach it together, and with equal work per
-    // tile they stay in lockstep.  Delaying every other CU's first tile by about
-    // half a tile keeps the two halves out of phase for the whole launch.
-    if (g.stagger > 0) {
-        const int b0 = blockIdx.y * gridDim.x + blockIdx.x;
-        if (b0 < 256 && ((b0 >> 3) & 1)) {
-            const uint64_t t0 = __builtin_amdgcn_s_memtime();
-            while (__builtin_amdgcn_s_memtime() - t0 < (uint64_t)g.stagger)
-                __builtin_amdgcn_s_sleep(8);
-        }
-    }
     // tile order: XCD remap (bijective) + grouped GM x all-N order (speed only)
     const int n_tn = gridDim.x, n_tm = gridDim.y, n_tiles = n_tn * n_tm;
     int bid = blockIdx.y * gridDim.x + blockIdx.x;
@@ -107,13 +95,8 @@ __global__ void __launch_bounds__(G2_T) gemm256_kernel(GemmArgs g) {
     const int nk = SPLIT ? K / 32 : K / 64;
     const int lda = SPLIT ? 2 * K : K, ldb = lda;
 #define G2_AT(t) (t)
-    // EPI_BIAS_RESID_LN: one block owns 256 whole rows (grid 1 x n_tm) and walks
-    // their N/256 column tiles, so that the LayerNorm of its rows needs no other block
-    constexpr bool LN = EPI == EPI_BIAS_RESID_LN;
-    const int m0 = LN ? blockIdx.y * G2_TILE : (first_m + in % gsz) * G2_TILE;
-    const int n_iter = LN ? N / G2_TILE : 1;
-    for (int it = 0; it < n_iter; ++it) {
-    const int n0 = LN ? it * G2_TILE : (in / gsz) * G2_TILE;
+    const int m0 = (first_m + in % gsz) * G2_TILE;
+    const int n0 = (in / gsz) * G2_TILE;
 
     // ---- staging sources (per lane) and LDS destinations (per wave) ----------
     // LDS row i (0..127) of a half tile = instruction j (0..1), wave, lane>>3:
@@ -521,7 +504,7 @@ __global__ void __launch_bounds__(G2_T) gemm256_kernel(GemmArgs g) {
             for (int e = 0; e < 8; ++e) v[e] = acc[mt][2 * h + (e >> 2)][e & 3] + bias_v[h][e];
             if (EPI == EPI_BIAS_GELU && !(g.ablate & 2)) gelu_erf8(v);  // ablate 2: no GELU (profiling)
             const int64_t o = (int64_t)row * g.ld_out + col_l + h * 32;
-            if constexpr (EPI == EPI_BIAS_RESID || EPI == EPI_BIAS_RESID_LN) {
+            if constexpr (EPI == EPI_BIAS_RESID) {
                 if constexpr (SPLIT) {  // split residual rows
                     const bf16 *rp = static_cast<const bf16 *>(g.resid) + (int64_t)row * 2 * N +
                                      split_col(col_l + h * 32);
@@ -565,130 +548,6 @@ __global__ void __launch_bounds__(G2_T) gemm256_kernel(GemmArgs g) {
         }
     }
     }  // generic epilogues
-    if constexpr (LN) __syncthreads();  // every wave is past its LDS reads of this tile
-    }  // column tiles
-
-    if constexpr (LN) {
-        // LayerNorm of the block's rows (the ln_vec_kernel arithmetic): the pre-LN
-        // rows were just written by this block's own waves; they are visible to
-        // plain loads once every wave's stores have completed (vmcnt(0) + barrier;
-        // this CU never read those lines, so its L1 holds no stale copy).
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        // opaque: nothing of this phase may be hoisted above the GEMM (VGPR pressure)
-        const void *pre_p = g.out, *gam_p = g.ln_gamma, *bet_p = g.ln_beta, *lno_p = g.ln_out,
-                   *hw_p = g.head_w;
-        void *imp_p = g.impact;
-        asm volatile("" : "+s"(pre_p), "+s"(gam_p), "+s"(bet_p), "+s"(lno_p), "+s"(hw_p),
-                     "+s"(imp_p));
-        const float *ln_gamma = static_cast<const float *>(gam_p);
-        const float *ln_beta = static_cast<const float *>(bet_p);
-        bf16 *ln_out = static_cast<bf16 *>(const_cast<void *>(lno_p));
-        const float *head_w = static_cast<const float *>(hw_p);
-        float *impact = static_cast<float *>(imp_p);
-        const int nc = N / 256;  // 256-column chunks per row (<= 4: H <= 1024)
-        // gamma / beta / head weights of this lane's columns 256c + 4 lane + j, once
-        float gmv[4][4], btv[4][4], hwv[4][4];
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            const int cc = c < nc ? c : 0;
-            const float4 a = *reinterpret_cast<const float4 *>(ln_gamma + 256 * cc + 4 * lane);
-            const float4 b = *reinterpret_cast<const float4 *>(ln_beta + 256 * cc + 4 * lane);
-            gmv[c][0] = a.x; gmv[c][1] = a.y; gmv[c][2] = a.z; gmv[c][3] = a.w;
-            btv[c][0] = b.x; btv[c][1] = b.y; btv[c][2] = b.z; btv[c][3] = b.w;
-            if (head_w) {
-                const float4 w = *reinterpret_cast<const float4 *>(head_w + 256 * cc + 4 * lane);
-                hwv[c][0] = w.x; hwv[c][1] = w.y; hwv[c][2] = w.z; hwv[c][3] = w.w;
-            }
-        }
-        // each wave normalises a slab of 32 rows, 8 rows at a time (loads of all 8 in
-        // flight, 8 independent reductions): the phase is latency-bound otherwise
-        constexpr int RB = 8;
-        for (int rb = 0; rb < G2_TILE / (G2_T / 64); rb += RB) {
-            const int r0 = m0 + wave * (G2_TILE / (G2_T / 64)) + rb;
-            float v[RB][4][4];
-#pragma unroll
-            for (int i = 0; i < RB; ++i) {
-                const int row = min(r0 + i, M - 1);  // clamped: always a valid row
-                const bf16 *pr = static_cast<const bf16 *>(pre_p) + (int64_t)row * N;
-#pragma unroll
-                for (int c = 0; c < 4; ++c) {
-                    const bf16x4 x = *reinterpret_cast<const bf16x4 *>(pr + 256 * (c < nc ? c : 0) + 4 * lane);
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) v[i][c][j] = (float)x[j];
-                }
-            }
-            float mean[RB], rstd[RB];
-#pragma unroll
-            for (int i = 0; i < RB; ++i) {
-                float s = 0.f;
-#pragma unroll
-                for (int c = 0; c < 4; ++c)
-                    if (c < nc) s += (v[i][c][0] + v[i][c][1]) + (v[i][c][2] + v[i][c][3]);
-                mean[i] = s;
-            }
-#pragma unroll
-            for (int d = 32; d >= 1; d >>= 1)
-#pragma unroll
-                for (int i = 0; i < RB; ++i) mean[i] += __shfl_xor(mean[i], d, 64);
-#pragma unroll
-            for (int i = 0; i < RB; ++i) {
-                mean[i] = mean[i] / (float)N;
-                float q = 0.f;
-#pragma unroll
-                for (int c = 0; c < 4; ++c)
-                    if (c < nc)
-#pragma unroll
-                        for (int j = 0; j < 4; ++j) {
-                            const float d = v[i][c][j] - mean[i];
-                            q += d * d;
-                        }
-                rstd[i] = q;
-            }
-#pragma unroll
-            for (int d = 32; d >= 1; d >>= 1)
-#pragma unroll
-                for (int i = 0; i < RB; ++i) rstd[i] += __shfl_xor(rstd[i], d, 64);
-            float hs[RB];
-#pragma unroll
-            for (int i = 0; i < RB; ++i) {
-                const int row = r0 + i;
-                const float rs = 1.0f / sqrtf(rstd[i] / (float)N + g.ln_eps);
-                hs[i] = 0.f;
-#pragma unroll
-                for (int c = 0; c < 4; ++c) {
-                    if (c < nc) {
-#pragma unroll
-                        for (int j = 0; j < 4; ++j)
-                            v[i][c][j] = (v[i][c][j] - mean[i]) * rs * gmv[c][j] + btv[c][j];
-                        if (ln_out && row < M)
-                            *reinterpret_cast<bf16x4 *>(ln_out + (int64_t)row * N + 256 * c + 4 * lane) =
-                                bf16x4{(bf16)v[i][c][0], (bf16)v[i][c][1], (bf16)v[i][c][2],
-                                       (bf16)v[i][c][3]};
-                        if (head_w)
-                            hs[i] += v[i][c][0] * hwv[c][0] + v[i][c][1] * hwv[c][1] +
-                                     v[i][c][2] * hwv[c][2] + v[i][c][3] * hwv[c][3];
-                    }
-                }
-            }
-            if (head_w) {
-#pragma unroll
-                for (int d = 32; d >= 1; d >>= 1)
-#pragma unroll
-                    for (int i = 0; i < RB; ++i) hs[i] += __shfl_xor(hs[i], d, 64);
-                if (lane == 0) {
-#pragma unroll
-                    for (int i = 0; i < RB; ++i) {
-                        if (r0 + i >= M) break;
-                        const float x = hs[i] + g.head_b;
-                        // nn.Softplus(beta=1, threshold=20) / ReLU
-                        impact[r0 + i] = g.act == 0 ? ((x > 20.0f) ? x : log1pf(expf(x)))
-                                                    : (x > 0.f ? x : 0.f);
-                    }
-                }
-            }
-        }
-    }
 }
 #undef G2_BAR
 
@@ -701,8 +560,7 @@ bool gemm256_ok(int epi, const GemmArgs &g) {
     // (SPLIT: K tiles of 32 logical k, K % 64 == 0 keeps their count even)
     return g.N % G2_TILE == 0 && g.K % (g.split ? 64 : 128) == 0 && g.K >= 128 &&
            g.a_rows >= m_pad &&
-           (epi != EPI_QKV || (2 * g.hidden) % G2_TILE == 0) &&
-           (epi != EPI_BIAS_RESID_LN || (g.N <= 1024 && g.ld_out == g.N));
+           (epi != EPI_QKV || (2 * g.hidden) % G2_TILE == 0);
 }
 
 // column width of one partial-statistics slot of the residual epilogues (the
@@ -711,7 +569,7 @@ int gemm_stats_cols() { return G2_TILE; }
 
 void launch_gemm256(int epi, const GemmArgs &g, hipStream_t s) {
     static_assert(G2_LDS <= 160 * 1024, "LDS");
-    dim3 grid(epi == EPI_BIAS_RESID_LN ? 1 : g.N / G2_TILE, (g.M + G2_TILE - 1) / G2_TILE);
+    dim3 grid(g.N / G2_TILE, (g.M + G2_TILE - 1) / G2_TILE);
     DI_REQUIRE(gemm256_ok(epi, g), DI_EINVAL, "gemm256: unsupported shape / epilogue");
     if (g.split) {
         switch (epi) {
@@ -743,7 +601,6 @@ void launch_gemm256(int epi, const GemmArgs &g, hipStream_t s) {
         G2_CASE(EPI_BIAS_GELU)
         G2_CASE(EPI_BIAS_RESID)
         G2_CASE(EPI_QKV)
-        G2_CASE(EPI_BIAS_RESID_LN)
         G2_CASE(EPI_FOLD)
         G2_CASE(EPI_FOLD_GELU)
         G2_CASE(EPI_RESID_STATS)

@@ -50,7 +50,6 @@ void launch_ln(const T *pre, int M, int H, const float *gamma, const float *beta
                T *out, const float *head_w, float head_b, int act, float *impact, hipStream_t s);
 void launch_vt_cols(const int32_t *cu, int n_docs, int M, int32_t *vcol, hipStream_t s);
 bool attention_v3_ok(int max_len, int H);
-bool gemm_fused_ln_ok(const GemmArgs &g);
 void launch_head_from_stats(const float4 *st, int ld, int n_part, int M, int H, float eps,
                             float sw, float cw, int act, float *impact, hipStream_t s);
 void launch_row_ln(const float4 *st, int ld, int n_part, int M, int H, float eps, float2 *out,
@@ -302,13 +301,8 @@ void forward(di_encoder *e, const int32_t *d_ids, const int32_t *d_cu, int n_doc
                            c.layer_norm_eps, pos_offset, c.vocab_size, c.max_positions, X,
                            e->err.as<int32_t>(), s);
     }
-    // attention path: DI_ATTN unset or 3 = v3 when it applies (bf16, max_len <= 320)
-    static const int attn_mode = [] {
-        const char *v = std::getenv("DI_ATTN");
-        return v ? std::atoi(v) : 3;
-    }();
-    const bool use_v3 = std::is_same<T, bf16>::value && attn_mode == 3 &&
-                        attention_v3_ok(max_len, H);
+    // attention path: the persistent v3 kernel when it applies (bf16, max_len <= 512)
+    const bool use_v3 = std::is_same<T, bf16>::value && attention_v3_ok(max_len, H);
     if (!use_v3) launch_vt_cols(d_cu, n_docs, (int)M, e->vcol.as<int32_t>(), s);
     for (size_t l = 0; l < e->layers.size(); ++l) {
         Layer &L = *e->layers[l];
@@ -370,16 +364,12 @@ void forward(di_encoder *e, const int32_t *d_ids, const int32_t *d_cu, int n_doc
         g.N = H;
         g.K = H;
         g.ld_out = H;
-        g.ln_gamma = L.ln1_g.as<float>();
-        g.ln_beta = L.ln1_b.as<float>();
         g.ln_eps = c.layer_norm_eps;
-        g.ln_out = X1;
-        const bool fuse_o = std::is_same<T, bf16>::value && gemm_fused_ln_ok(g);
         {
             TimedLaunch tl(e->timer, timing, "gemm_o", s);
-            launch_gemm<T>(fuse_o ? EPI_BIAS_RESID_LN : EPI_BIAS_RESID, g, s);
+            launch_gemm<T>(EPI_BIAS_RESID, g, s);
         }
-        if (!fuse_o) {
+        {
             TimedLaunch tl(e->timer, timing, "ln", s);
             launch_ln<T>(e->pre.as<T>(), (int)M, H, L.ln1_g.as<float>(), L.ln1_b.as<float>(),
                          c.layer_norm_eps, X1, nullptr, 0.f, c.activation, nullptr, s);
@@ -411,20 +401,12 @@ void forward(di_encoder *e, const int32_t *d_ids, const int32_t *d_cu, int n_doc
         g.N = H;
         g.K = F;
         g.ld_out = H;
-        g.ln_gamma = L.ln2_g.as<float>();
-        g.ln_beta = L.ln2_b.as<float>();
         g.ln_eps = c.layer_norm_eps;
-        g.ln_out = last ? nullptr : X;
-        g.head_w = last ? e->head_w.as<float>() : nullptr;
-        g.head_b = e->head_b;
-        g.act = c.activation;
-        g.impact = last ? e->impact.as<float>() : nullptr;
-        const bool fuse_f = std::is_same<T, bf16>::value && gemm_fused_ln_ok(g);
         {
             TimedLaunch tl(e->timer, timing, "gemm_ffn2", s);
-            launch_gemm<T>(fuse_f ? EPI_BIAS_RESID_LN : EPI_BIAS_RESID, g, s);
+            launch_gemm<T>(EPI_BIAS_RESID, g, s);
         }
-        if (!fuse_f) {
+        {
             TimedLaunch tl(e->timer, timing, "ln", s);
             launch_ln<T>(e->pre.as<T>(), (int)M, H, L.ln2_g.as<float>(), L.ln2_b.as<float>(),
                          c.layer_norm_eps, last ? nullptr : X,
@@ -464,22 +446,11 @@ void forward_folded(di_encoder *e, const int32_t *d_ids, const int32_t *d_cu, in
                               e->emb_b.as<float>(), c.layer_norm_eps, pos_offset, c.vocab_size,
                               c.max_positions, X, e->err.as<int32_t>(), s);
     }
-    // A/B knobs of the 256-tile GEMMs (tools / bench experiments): first-tile delay
-    // of every other CU (shader cycles) and the tile-order group size
-    static const int stagger = [] {
-        const char *v = std::getenv("DI_GEMM_STAGGER");
-        return v ? std::atoi(v) : 0;
-    }();
-    static const int tune_gm = [] {
-        const char *v = std::getenv("DI_GEMM_GM");
-        return v ? std::atoi(v) : 0;
-    }();
     auto base = [&]() {
         GemmArgs g{};
-        g.stagger = stagger;
         // tile-order group: 8 M-tiles (measured +4% QKV, +1% O / FFN1 over 4); FFN2
         // (K = 3072, N = 768) keeps 4
-        g.tune_gm = tune_gm ? tune_gm : 8;
+        g.tune_gm = 8;
         g.M = (int)M;
         g.a_rows = e->cap_rows;
         g.hidden = H;
@@ -581,7 +552,7 @@ void forward_folded(di_encoder *e, const int32_t *d_ids, const int32_t *d_cu, in
         g.N = H;
         g.K = F;
         g.ld_out = H;
-        if (tune_gm == 0) g.tune_gm = 4;
+        g.tune_gm = 4;
         g.row_ln = rl1;
         g.res_gamma = L.ln1_g.as<float>();
         g.res_beta = L.ln1_b.as<float>();
@@ -917,12 +888,8 @@ int di_encode(di_encoder *e, const int32_t *tok_ids, const int32_t *cu_seqlens, 
             d_tt = (const int32_t *)stage_in(term_tok, (size_t)n_terms * 4, dev, e->tt, s);
             d_cut = (const int32_t *)stage_in(cu_terms, (size_t)(n_docs + 1) * 4, dev, e->cut, s);
         }
-        // pruned last layer (bf16 folded path, term output; DI_PRUNE_LAST=0: off)
-        static const bool prune_env = [] {
-            const char *v = std::getenv("DI_PRUNE_LAST");
-            return !(v && v[0] == '0');
-        }();
-        const bool prune = prune_env && !token_out && e->esz == 2 && e->folded &&
+        // pruned last layer (bf16 folded path, term output)
+        const bool prune = !token_out && e->esz == 2 && e->folded &&
                            n_terms <= n_tokens;  // (packed term rows fit the row buffers)
         if (n_tokens > 0) {
             if (e->split)

@@ -60,6 +60,9 @@ constexpr int FAST_TERMS = 16;
 constexpr int HIST_BINS = 4096;
 constexpr int TIE_CAP = HIST_BINS;
 constexpr int QH_BINS = 4096;  // per-query candidate-score histogram (shared threshold)
+// Safe early termination (score-at-a-time over the impact classes, see score_item):
+// queries of at most ET_TERMS terms with the per-wave layout.
+constexpr int ET_TERMS = FAST_TERMS;
 
 struct ScoreShared {
     uint32_t acc[MAX_BLOCK_DOCS + 64];  // 128 KiB (+ the scatter's dummy words)
@@ -78,7 +81,11 @@ struct ScoreShared {
     uint32_t thr, above, ties, bin, bin_above;
     uint32_t tq;  // the query's shared threshold as this item read it
     uint32_t lmask[WTERMS / 32];      // terms (j < WTERMS) with a per-wave layout in this block
-    uint32_t wtab[WTERMS][WSEG];      // their per-wave runs: start << 16 | end (in the sublist)
+    union {
+        uint32_t wtab[WTERMS][WSEG];       // their per-wave runs: start << 16 | end (in the sublist)
+        uint16_t wcls[ET_TERMS][WSEG][8];  // early termination: per-wave class ends (wmeta)
+    } wt;
+    uint16_t segj[ET_TERMS][8];            // early termination: short terms' class ends (seg)
 };
 static_assert(sizeof(RadixScratch<SC_WAVES>) >= (HIST_BINS + 64) * 4,
               "histogram (+ 64 spare bins) overlays the radix scratch");
@@ -213,7 +220,23 @@ __device__ __forceinline__ void scatter_load(const uint32_t *p, int64_t avail, i
     for (int u = 0; u < UU; ++u)
         cur[u] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, (tid + u * NT) * 4, 0, 0);
 }
-template <int UU>
+// The word update.  Term order (MAXF false): touched w + (v << 16), first touch
+// (v << 16) | first_bits | v -- both one 24-bit multiply-add (v < 256, first_bits =
+// (255 - j) << 8: no carries).  Out of term order (MAXF, early termination): the
+// score adds up and the low half keeps the smallest term index, max of the old low
+// half and first_bits | v (distinct j: the larger is the earlier term and its value).
+template <bool MAXF>
+__device__ __forceinline__ uint32_t word_update(uint32_t w, uint32_t v, uint32_t first_bits) {
+    if constexpr (MAXF) {
+        return ((w & 0xFFFF0000u) + (v << 16)) | max(w & 0xFFFFu, first_bits | v);
+    } else {
+        const uint32_t t = __umul24(v, 0x10000u) + w;
+        const uint32_t f = __umul24(v, 0x10001u) + first_bits;
+        return w ? t : f;
+    }
+}
+
+template <int UU, bool MAXF = false>
 __device__ __forceinline__ void scatter_apply(uint32_t *acc, const uint32_t (&cur)[UU],
                                               uint32_t first_bits) {
     // LDS byte addresses formed here and the accesses in inline asm (the compiler's own
@@ -236,19 +259,16 @@ __device__ __forceinline__ void scatter_apply(uint32_t *acc, const uint32_t (&cu
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int u = 0; u < UU; ++u) {
-        // touched: w + (v << 16); first touch: (v << 16) | first_bits | v -- both one
-        // 24-bit multiply-add (v < 256, first_bits = (255 - j) << 8: no carries)
         const uint32_t v = cur[u] & 255u;
-        const uint32_t t = __umul24(v, 0x10000u) + w[u];
-        const uint32_t f = __umul24(v, 0x10001u) + first_bits;
-        asm volatile("ds_write_b32 %0, %1" ::"v"(a[u]), "v"(w[u] ? t : f) : "memory");
+        asm volatile("ds_write_b32 %0, %1" ::"v"(a[u]), "v"(word_update<MAXF>(w[u], v, first_bits))
+                     : "memory");
     }
 }
 
 // scatter_apply restricted to the docs [dlo, dhi) of one wave (a short term, whose
 // sublist every wave reads in full): the other postings (and the padding) update a
 // per-lane dummy word past the block instead.
-template <int UU>
+template <int UU, bool MAXF = false>
 __device__ __forceinline__ void scatter_apply_own(const uint32_t (&cur)[UU], uint32_t first_bits,
                                                   uint32_t dlo, uint32_t dn, uint32_t dummy) {
     uint32_t w[UU], a[UU];
@@ -265,9 +285,8 @@ __device__ __forceinline__ void scatter_apply_own(const uint32_t (&cur)[UU], uin
 #pragma unroll
     for (int u = 0; u < UU; ++u) {
         const uint32_t v = cur[u] & 255u;
-        const uint32_t t = __umul24(v, 0x10000u) + w[u];
-        const uint32_t f = __umul24(v, 0x10001u) + first_bits;
-        asm volatile("ds_write_b32 %0, %1" ::"v"(a[u]), "v"(w[u] ? t : f) : "memory");
+        asm volatile("ds_write_b32 %0, %1" ::"v"(a[u]), "v"(word_update<MAXF>(w[u], v, first_bits))
+                     : "memory");
     }
 }
 
@@ -328,6 +347,11 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
     // (one pass: the loads of both depend only on the term id, so they overlap);
     // ablate bit 128: all-wave form only
     const bool wl = nt <= WTERMS && !(ablate & 128);
+    // with the per-wave layout, short terms too are scattered by each wave over its own
+    // docs (ablate bit 256: the barrier form for them): then no term needs a barrier
+    const bool own_short = wl && !(ablate & 256);
+    // safe early termination (ablate bit 512: off, profiling / A-B)
+    const bool et = own_short && nt <= ET_TERMS && qhist != nullptr && !(ablate & 512);
     auto bounds = [&](int j, uint32_t t) {
         const uint32_t *bo = blk_off + (int64_t)t * (nb + 1) + b;
         lo[j] = term_start[t] + bo[0];
@@ -347,11 +371,19 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
             }
             const uint32_t id = lid[(int64_t)t * nb + b];
             if (w == 0) bounds(j, t);
-            if (id == 0xFFFFFFFFu) continue;
+            if (id == 0xFFFFFFFFu) {
+                if (et && w < 8) sh.segj[j][w] = seg[((int64_t)t * nb + b) * 8 + w];
+                continue;
+            }
             const uint16_t *m = wmeta + (int64_t)id * (WSEG * 8);
             const uint32_t s0 = w ? m[(w - 1) * 8 + 7] : 0u;
             const uint32_t e0 = m[w * 8 + min(min_cls, 7)];
-            sh.wtab[j][w] = (s0 << 16) | e0;
+            if (et) {
+#pragma unroll
+                for (int c = 0; c < 8; ++c) sh.wt.wcls[j][w][c] = m[w * 8 + c];
+            } else {
+                sh.wt.wtab[j][w] = (s0 << 16) | e0;
+            }
             if (w == 0) atomicOr(&sh.lmask[j >> 5], 1u << (j & 31));
         }
     } else {
@@ -379,6 +411,39 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
     }
 
     stamp(0);  // setup + zeroing
+    // The query's shared threshold (qhist, when given) counts the scores of every
+    // candidate its finished blocks emitted (distinct docs, full scores; bin 4095 =
+    // 4095 and above).  read_tq -> the largest s with >= k counted candidates scoring
+    // >= s: at least k docs score >= s, so the final k-th score is >= s.  A stale
+    // (smaller) count still gives a valid lower bound.  Block-wide (barriers).
+    uint32_t *qh = qhist ? qhist + (int64_t)q * QH_BINS : nullptr;
+    auto read_tq = [&]() -> uint32_t {
+        // thread t: bins 4t..4t+3 (relaxed atomic loads: other CUs add to them)
+        uint32_t hv[4], c = 0;
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+            c += (hv[e] = __hip_atomic_load(&qh[4 * tid + e], __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_AGENT));
+        uint32_t sfx = wave_suffix_sum(c);
+        if (lane == 0) sh.wsum[wave] = sfx;
+        if (tid == 0) sh.tq = 0;
+        __syncthreads();
+        for (int w2 = wave + 1; w2 < SC_WAVES; ++w2) sfx += sh.wsum[w2];
+        // one thread holds the crossing: count(>= 4t + e) >= k > count(>= 4t + e + 1)
+        if (sfx >= (uint32_t)k && sfx - c < (uint32_t)k) {
+            uint32_t above = sfx - c;
+            int e = 3;
+            for (; e > 0; --e) {
+                if (above + hv[e] >= (uint32_t)k) break;
+                above += hv[e];
+            }
+            sh.tq = (uint32_t)(4 * tid + e);
+        }
+        __syncthreads();
+        const uint32_t r = sh.tq;
+        __syncthreads();  // (wsum / tq are reused)
+        return r;
+    };
     // ---- scatter: terms in query order, barrier between terms -------------
     // A term's sublist goes in rounds of 16 postings per lane while 16 k remain, then
     // 4 per lane while more than 1 k remain, then 1: a short tail does not pay for a
@@ -394,18 +459,96 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
     uint32_t pre[4];
     bool have_pre = false;
     auto is_long = [&](int j) { return wl && ((sh.lmask[j >> 5] >> (j & 31)) & 1u); };
-    // with the per-wave layout, short terms too are scattered by each wave over its own
-    // docs (ablate bit 256: the barrier form for them): then no term needs a barrier
-    const bool own_short = wl && !(ablate & 256);
     const uint32_t wseg = ((uint32_t)block_docs + WSEG - 1) / WSEG;
     const uint32_t wdlo = (uint32_t)wave * wseg;
     const uint32_t wdn = wave == WSEG - 1 ? 0x7FFFFFFFu - wdlo : wseg;  // last: the rest
     const uint32_t wdummy = (uint32_t)(MAX_BLOCK_DOCS + lane) << 2;
-    for (int j = (ablate & 1) ? nt : 0; j < nt; ++j) {  // ablate bit 0: skip (profiling)
+    // Safe early termination (configs[4]; exact): the query's shared threshold Tq (see
+    // read_tq) is a lower bound of its final k-th score, and the postings of every (term,
+    // block[, wave segment]) sublist are grouped by impact class c (values in
+    // [2^(7-c), 2^(8-c))).  Each wave applies class 0 of every term, then class 1, ...
+    // to its own doc segment (no barriers: no other wave touches those docs); after
+    // class c, every doc of the segment can still gain at most
+    //   R = sum over the terms with postings left (classes > c) of 2^(7-c) - 1,
+    // so when the segment's best partial score + R < Tq no doc of it can reach Tq -- nor
+    // the query's top-k -- and the wave skips the rest of its postings.  Terms touch a
+    // doc out of term order, so the first-touch field keeps the smallest term index
+    // (MAXF updates: max of (255 - j) << 8 | v_j); sums are order-free integers.  Docs
+    // left with partial scores stay below Tq and are never emitted: the Tq path emits
+    // only docs >= Tq, and with more than k of those the block's top-k are all >= Tq.
+    uint32_t tq_et = 0;
+    if (et) tq_et = read_tq();
+    if (et && !(ablate & 1)) {
+        const uint32_t wend = min((uint32_t)n_local, wdlo + wseg);
+        const uint32_t wstart = min(wdlo, wend);
+        auto range = [&](int64_t pos, const int64_t end, const bool lj, const uint32_t fb) {
+            while (pos < end) {
+                const int64_t rem = end - pos;
+                if (rem > 8 * 64) {
+                    uint32_t r[16];
+                    scatter_load<16, 64>(post + pos, rem, lane, r);
+                    if (lj) scatter_apply<16, true>(sh.acc, r, fb);
+                    else scatter_apply_own<16, true>(r, fb, wdlo, wdn, wdummy);
+                    pos += 16 * 64;
+                } else if (rem > 4 * 64) {
+                    uint32_t r[8];
+                    scatter_load<8, 64>(post + pos, rem, lane, r);
+                    if (lj) scatter_apply<8, true>(sh.acc, r, fb);
+                    else scatter_apply_own<8, true>(r, fb, wdlo, wdn, wdummy);
+                    pos = end;
+                } else if (rem > 64) {
+                    uint32_t r[4];
+                    scatter_load<4, 64>(post + pos, rem, lane, r);
+                    if (lj) scatter_apply<4, true>(sh.acc, r, fb);
+                    else scatter_apply_own<4, true>(r, fb, wdlo, wdn, wdummy);
+                    pos = end;
+                } else {
+                    uint32_t r[1];
+                    scatter_load<1, 64>(post + pos, rem, lane, r);
+                    if (lj) scatter_apply<1, true>(sh.acc, r, fb);
+                    else scatter_apply_own<1, true>(r, fb, wdlo, wdn, wdummy);
+                    pos = end;
+                }
+            }
+        };
+        for (int c = 0; c <= min_cls; ++c) {
+            for (int j = 0; j < nt; ++j) {
+                const bool lj = is_long(j);
+                uint32_t cs, ce;
+                if (lj) {
+                    const uint16_t *e = sh.wt.wcls[j][wave];
+                    cs = c ? e[c - 1] : (wave ? sh.wt.wcls[j][wave - 1][7] : 0u);
+                    ce = e[c];
+                } else {
+                    cs = c ? sh.segj[j][c - 1] : 0u;
+                    ce = sh.segj[j][c];
+                }
+                range(lo[j] + cs, lo[j] + ce, lj, (uint32_t)(255 - j) << 8);
+            }
+            if (c < min_cls && tq_et > 0) {
+                const uint32_t cb = (1u << (7 - c)) - 1u;
+                uint32_t rb = 0;
+                for (int j = 0; j < nt; ++j) {
+                    const bool more = is_long(j)
+                                          ? sh.wt.wcls[j][wave][min_cls] > sh.wt.wcls[j][wave][c]
+                                          : sh.segj[j][min_cls] > sh.segj[j][c];
+                    rb += more ? cb : 0u;
+                }
+                if (rb == 0) break;  // nothing left in this segment
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's writes
+                uint32_t mx = 0;
+                for (uint32_t i = wstart + lane; i < wend; i += 64) mx = max(mx, sh.acc[i] >> 16);
+#pragma unroll
+                for (int d = 32; d >= 1; d >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, d, 64));
+                if (mx + rb < tq_et) break;  // the segment is out of the race: skip the rest
+            }
+        }
+    }
+    for (int j = (ablate & 1) || et ? nt : 0; j < nt; ++j) {  // ablate bit 0: skip (profiling)
         const uint32_t first_bits = (uint32_t)(255 - j) << 8;
         const bool lj = is_long(j);
         if (lj) {
-            const uint32_t se = sh.wtab[j][wave];
+            const uint32_t se = sh.wt.wtab[j][wave];
             int64_t pos = lo[j] + (se >> 16);
             const int64_t end = lo[j] + (se & 0xFFFFu);
             while (pos < end) {
@@ -528,8 +671,7 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
         }
     };
     // final candidates: copied out (staged) and counted into the query's score
-    // histogram (qhist, see below); called once per item, after a barrier
-    uint32_t *qh = qhist ? qhist + (int64_t)q * QH_BINS : nullptr;
+    // histogram (qhist, see read_tq); called once per item, after a barrier
     auto flush = [&](uint32_t n_c) {
         for (uint32_t i = tid; i < n_c; i += SC_THREADS) {
             const uint64_t key = staged ? stage[i] : ck[i];
@@ -558,29 +700,7 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
     // still gives a valid lower bound.
     uint32_t Tq = 0;
     if (qh) {
-        // thread t: bins 4t..4t+3 (relaxed atomic loads: other CUs add to them)
-        uint32_t hv[4], c = 0;
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-            c += (hv[e] = __hip_atomic_load(&qh[4 * tid + e], __ATOMIC_RELAXED,
-                                            __HIP_MEMORY_SCOPE_AGENT));
-        uint32_t sfx = wave_suffix_sum(c);
-        if (lane == 0) sh.wsum[wave] = sfx;
-        if (tid == 0) sh.tq = 0;
-        __syncthreads();
-        for (int w2 = wave + 1; w2 < SC_WAVES; ++w2) sfx += sh.wsum[w2];
-        // one thread holds the crossing: count(>= 4t + e) >= k > count(>= 4t + e + 1)
-        if (sfx >= (uint32_t)k && sfx - c < (uint32_t)k) {
-            uint32_t above = sfx - c;
-            int e = 3;
-            for (; e > 0; --e) {
-                if (above + hv[e] >= (uint32_t)k) break;
-                above += hv[e];
-            }
-            sh.tq = (uint32_t)(4 * tid + e);
-        }
-        __syncthreads();
-        Tq = sh.tq;
+        Tq = read_tq();
         if (Tq > 0) {
             const uint32_t thr_w = Tq << 16;
             const uint32_t n = compact_words(
@@ -1255,10 +1375,7 @@ void build_index(di_index *ix, const int64_t *term_off, int64_t n_terms, const u
     // (term, block) order.
     ix->lid.assign((size_t)std::max<int64_t>(n_terms * nb, 1), 0xFFFFFFFFu);
     {
-        static const int64_t wlong_min = [] {  // A/B: DI_WLONG_MIN (postings)
-            const char *e = std::getenv("DI_WLONG_MIN");
-            return e ? (int64_t)std::atoll(e) : (int64_t)WLONG_MIN;
-        }();
+        const int64_t wlong_min = WLONG_MIN;
         uint32_t n_long = 0;
         for (int64_t t = 0; t < n_terms; ++t)
             for (int b = 0; b < nb; ++b)
@@ -1395,17 +1512,10 @@ void launch_merge(const uint64_t *keys, const int32_t *counts, int n_q, int n_li
     if (n_lists > 1024 || want > MG_LDS_KEYS) want = std::max<int64_t>(k, MG_SEL_CAP);
     int cap = 64;
     while (cap < want) cap <<= 1;
-    // workgroup size of the merge (DI_MERGE_THREADS: A/B knob); 512 measured best for
-    // the 4-block x 1000-candidate bench merge (0.68 vs 0.73 ms at 1024, 0.86 at 256)
-    static const int mt = [] {
-        const char *e = std::getenv("DI_MERGE_THREADS");
-        return e ? std::atoi(e) : 512;
-    }();
-    // score-histogram selection before the sort (DI_MERGE_SELECT=0: sort everything)
-    static const int select = [] {
-        const char *e = std::getenv("DI_MERGE_SELECT");
-        return e && e[0] == '0' ? 0 : 1;
-    }();
+    // workgroup size of the merge: 512 measured best for the 4-block x 1000-candidate
+    // bench merge (0.68 vs 0.73 ms at 1024, 0.86 at 256); score-histogram selection
+    // before the sort (a full sort of 4000 candidates took 0.80 ms, selection 0.17)
+    constexpr int mt = 512, select = 1;
     // (the histogram follows the keys; only for cap <= MG_SEL_CAP, inside the attribute's max)
     const size_t sel_lds = cap > MG_SEL_MIN && cap <= MG_SEL_CAP ? (size_t)MG_SEL_BINS * 4 + MG_SEL_KEYS * 8 : 0;
     if (cap <= 256 || mt == 256) {
@@ -1448,12 +1558,16 @@ int di_index_create(const int64_t *term_off, int64_t n_terms, const uint32_t *pd
         ix->own_stream = true;
         enable_big_lds();
         if (const char *ab = std::getenv("DI_PROFILE_ABLATE")) ix->ablate = std::atoi(ab);
-        if (const char *sw = std::getenv("DI_SCATTER_WAVE"))  // A/B: 0 = all-wave scatter only
-            if (sw[0] == '0') ix->ablate |= 128;
-        if (const char *ss = std::getenv("DI_SCATTER_SHORT"))  // A/B: 0 = barrier form for
-            if (ss[0] == '0') ix->ablate |= 256;                  // the short terms
         if (const char *st = std::getenv("DI_SCORE_THRESHOLD"))  // (tested both ways)
             ix->shared_thr = st[0] != '0' ? 1 : 0;
+        // safe early termination: opt-in (DI_EARLY_TERMINATION=1; tested both ways).  On
+        // the SURVEY §8d synthetic collection no doc range can be skipped (97.6% of even
+        // 64-doc ranges can still reach the k-th score: tools/et_potential.py), and the
+        // class-major order costs 3x in score_blocks (1.1M docs: 51 vs 17 ms per step)
+        {
+            const char *et = std::getenv("DI_EARLY_TERMINATION");
+            if (!(et && et[0] == '1')) ix->ablate |= 512;
+        }
         build_index(ix.get(), term_off, n_terms, pdoc, pval, doc_lo, doc_hi);
         *out = ix.release();
     });

@@ -198,9 +198,12 @@ def test_shared_threshold_off_equals_oracle(L, synth, monkeypatch):
     off = L.DeviceIndex.from_postings(term_off, pdoc, pval)
     assert off.search(qs, 1000) == want
     monkeypatch.setenv("DI_SCORE_THRESHOLD", "1")
-    on = L.DeviceIndex.from_postings(term_off, pdoc, pval)
-    assert on.search(qs, 1000) == want
-    assert on.search(qs, 7) == ora.score_ids(qs, 7, n_threads=8)
+    for et in ("1", "0"):  # safe early termination on / off
+        monkeypatch.setenv("DI_EARLY_TERMINATION", et)
+        on = L.DeviceIndex.from_postings(term_off, pdoc, pval)
+        assert on.search(qs, 1000) == want
+        assert on.search(qs, 7) == ora.score_ids(qs, 7, n_threads=8)
+        assert on.search(qs, 1) == ora.score_ids(qs, 1, n_threads=8)
 
 
 @pytest.fixture(scope="module")
@@ -217,11 +220,14 @@ def million():
     return term_off, pdoc, pval, ora
 
 
-@pytest.mark.parametrize("k", [10, 1000])
-def test_million_doc_shard_matches_oracle(L, million, k):
+@pytest.mark.parametrize("k,et", [(10, "1"), (1000, "1"), (1000, "0")])
+def test_million_doc_shard_matches_oracle(L, million, k, et, monkeypatch):
+    """34 blocks, shared threshold on; safe early termination (configs[4]) on and off:
+    the exact top-k either way."""
     from improving_learned_index_amd import synthetic as S
 
     term_off, pdoc, pval, ora = million
+    monkeypatch.setenv("DI_EARLY_TERMINATION", et)
     dev = L.DeviceIndex.from_postings(term_off, pdoc, pval, 0, ora.n_docs)
     assert dev.info()["n_blocks"] == 34
     qs = S.msmarco_like_queries(24, 200_000, seed=k) + _queries(200_000, 8, seed=k)
