@@ -70,6 +70,7 @@ SIGNATURES = {
     "di_format_impact_lines": (ctypes.c_int, [P, P, P, P, I32, P, I64, P]),
     "di_sparse_create": (ctypes.c_int, [P, I64, P, P, U32, ctypes.c_int, P]),
     "di_sparse_search": (ctypes.c_int, [P, P, P, I32, I32, P, P, P, P, U32]),
+    "di_sparse_search_f64": (ctypes.c_int, [P, P, P, I32, I32, P, P, P, U32]),
     "di_sparse_info": (ctypes.c_int, [P, P, P, P, P]),
     "di_sparse_timing": (ctypes.c_int, [P, ctypes.c_char_p, P, ctypes.c_int]),
     "di_sparse_destroy": (ctypes.c_int, [P]),
@@ -295,13 +296,25 @@ class DeviceSparseIndex:
                                      n_docs, device, ctypes.byref(h)))
         self._h = h
 
-    def search_csr(self, q_terms, cu_q, k, with_keys=False):
+    def search_csr(self, q_terms, cu_q, k, with_keys=False, accumulation="f32"):
+        """accumulation "f32" (numpy >= 2) or "f64" (the reference's pinned numpy 1.25:
+        f64 scores; no keys)."""
         q_terms = np.ascontiguousarray(q_terms, np.uint32)
         if q_terms.size == 0:
             q_terms = np.zeros(1, np.uint32)
         cu_q = np.ascontiguousarray(cu_q, np.int32)
         n_q = len(cu_q) - 1
         docs = np.zeros((max(n_q, 1), k), np.uint32)
+        if accumulation == "f64":
+            if with_keys:
+                raise ValueError("f64 search has no 64-bit merge keys")
+            scores = np.zeros((max(n_q, 1), k), np.float64)
+            n = np.zeros(max(n_q, 1), np.int32)
+            check(lib().di_sparse_search_f64(self._h, ptr(q_terms), ptr(cu_q), n_q, k, ptr(docs),
+                                             ptr(scores), ptr(n), 0))
+            return docs[:n_q], scores[:n_q], n[:n_q], None
+        if accumulation != "f32":
+            raise ValueError(f"accumulation must be 'f32' or 'f64', not {accumulation!r}")
         scores = np.zeros((max(n_q, 1), k), np.float32)
         n = np.zeros(max(n_q, 1), np.int32)
         keys = np.zeros((max(n_q, 1), k), np.uint64) if with_keys else None
@@ -309,9 +322,9 @@ class DeviceSparseIndex:
                                      ptr(scores), ptr(n), ptr(keys), 0))
         return docs[:n_q], scores[:n_q], n[:n_q], (keys[:n_q] if with_keys else None)
 
-    def search(self, queries, k):
+    def search(self, queries, k, accumulation="f32"):
         flat, cu = csr(queries)
-        docs, scores, n, _ = self.search_csr(flat, cu, k)
+        docs, scores, n, _ = self.search_csr(flat, cu, k, accumulation=accumulation)
         return [list(zip(docs[i, :n[i]].tolist(), scores[i, :n[i]].tolist()))
                 for i in range(len(queries))]
 

@@ -28,7 +28,12 @@ from .metrics import evaluate_retrieval, ndcg_at_k  # noqa: F401
 
 class SparseSearch:
     def __init__(self, model, batch_size: int, verbose: bool = False, device: int = 0,
-                 encode_batch_size: Optional[int] = None):
+                 encode_batch_size: Optional[int] = None, accumulation: str = "f32"):
+        """accumulation: "f32" -- `0.0 + np.float32` under numpy >= 2; "f64" -- under the
+        reference's pinned numpy 1.25.1 (f64 doc scores)."""
+        if accumulation not in ("f32", "f64"):
+            raise ValueError(f"accumulation must be 'f32' or 'f64', not {accumulation!r}")
+        self.accumulation = accumulation
         self.model = model
         self.batch_size = batch_size
         self.encode_batch_size = encode_batch_size or max(batch_size, 256)
@@ -68,7 +73,8 @@ class SparseSearch:
         qterms = [[self.vocab[t] for t in self.model.process_query(queries[q]) if t in self.vocab]
                   for q in qids]
         flat, cu = csr(qterms)
-        docs, scores, n, _ = self.inverted_index.search_csr(flat, cu, k)
+        docs, scores, n, _ = self.inverted_index.search_csr(flat, cu, k,
+                                                            accumulation=self.accumulation)
         out = {}
         for i, qid in enumerate(qids):
             out[qid] = {self.corpus_ids[d]: float(s)
@@ -116,8 +122,10 @@ class NanoBEIREvaluator:
     (the hub's NanoBEIR files); ``evaluate_all`` walks ``data_dir``/Nano<Name> for the
     13 datasets (those present) and adds their average as metrics["avg"]."""
 
-    def __init__(self, batch_size=16, verbose=False, device=0, data_dir=None):
+    def __init__(self, batch_size=16, verbose=False, device=0, data_dir=None,
+                 accumulation="f32"):
         self.batch_size, self.verbose, self.device = batch_size, verbose, device
+        self.accumulation = accumulation
         self.data_dir = Path(data_dir) if data_dir is not None else None
 
     def _load_dataset(self, dataset):
@@ -132,7 +140,7 @@ class NanoBEIREvaluator:
     def search(self, model, dataset, k=1000):
         corpus, queries, qrels = self._load_dataset(dataset)
         searcher = SparseSearch(model, batch_size=self.batch_size, verbose=self.verbose,
-                                device=self.device)
+                                device=self.device, accumulation=self.accumulation)
         return searcher.search(queries, corpus, k=k), qrels
 
     def evaluate_dataset(self, model, dataset):
@@ -180,12 +188,14 @@ def main(argv=None):
     p.add_argument("--batch_size", type=int, default=16)
     p.add_argument("--device", type=int, default=0)
     p.add_argument("--dataset", type=str, default=None, help="one dataset name only")
+    p.add_argument("--accumulation", choices=["f32", "f64"], default="f32",
+                   help="doc-score sums: f32 (numpy >= 2) or f64 (the reference's numpy 1.25.1)")
     a = p.parse_args(argv)
     model = DeepImpact.load(a.model_checkpoint_path, tokenizer_path=a.tokenizer_path,
                             precision=a.precision, device=a.device, variant=a.variant,
                             max_length=a.max_length)
     ev = NanoBEIREvaluator(batch_size=a.batch_size, verbose=True, device=a.device,
-                           data_dir=a.data_dir)
+                           data_dir=a.data_dir, accumulation=a.accumulation)
     out = ev.evaluate_dataset(model, a.dataset) if a.dataset else ev.evaluate_all(model)
     print(out)
     return out

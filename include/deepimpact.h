@@ -150,6 +150,13 @@ int di_sparse_create(const int64_t *term_off, int64_t n_terms, const uint32_t *p
 int di_sparse_search(di_sparse *sp, const uint32_t *q_terms, const int32_t *cu_q, int32_t n_q,
                      int32_t k, uint32_t *out_doc, float *out_score, int32_t *out_n,
                      uint64_t *out_key, uint32_t flags);
+/* The same search with float64 accumulation: the reference's pinned numpy 1.25.1,
+ * where `0.0 + np.float32` is an np.float64 (nano_beir_evaluator.py:113-121, SURVEY
+ * App. B.4).  f64 sums formed in the reference's order, top-k by f64 score with
+ * ties in first-touch order; out_score: the f64 scores (the reference's float()). */
+int di_sparse_search_f64(di_sparse *sp, const uint32_t *q_terms, const int32_t *cu_q,
+                         int32_t n_q, int32_t k, uint32_t *out_doc, double *out_score,
+                         int32_t *out_n, uint32_t flags);
 int di_sparse_info(const di_sparse *sp, int64_t *n_terms, int64_t *n_postings, uint32_t *n_docs,
                    int32_t *n_blocks);
 int di_sparse_timing(di_sparse *sp, const char *name, di_timing *out, int reset);
