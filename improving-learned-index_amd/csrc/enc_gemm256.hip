@@ -1,4 +1,5 @@
-// enc_gemm256.hip -- 256x256-tile bf16 MFMA GEMM, 8-phase pipelined K loop (gfx950).
+// enc_gemm256.hip -- 256x256-tile bf16 MFMA GEMM, 8-phase pipelined K loop, persistent
+// over tiles with the next tile's prologue in flight during the epilogue (gfx950).
 //
 // Same contract as enc_gemm.hip (C[M,N] = A[M,K] * B[N,K]^T + fused epilogue; the
 // encoder's QKV / O / FFN1 / FFN2 projections, reference xlmr_original.py:70-75),
@@ -37,6 +38,7 @@
 // prefetch in flight across barriers; all LDS is one dynamic array.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <type_traits>
 
 #include "di_common.h"
@@ -47,29 +49,40 @@ namespace di {
 constexpr int G2_T = 512;
 constexpr int G2_TILE = 256;
 constexpr int G2_BUF = 65536;                  // one K tile: A image 32 KiB + B image 32 KiB
-// Epilogue parameters of the tile, staged by LDS-DMA with the prologue (their load
+// Epilogue parameters of a tile, staged by LDS-DMA with the tile's prologue (their load
 // latency then hides behind the K loop): 256 row params (float2) + up to four
-// 256-column float vectors (bias or c, s or gamma, beta, head w*gamma).
-constexpr int G2_PAR = 2 * G2_BUF;            // byte offset of the parameter area
+// 256-column float vectors (bias or c, s or gamma, beta, head w*gamma).  Two slots:
+// the next tile's parameters arrive while the current tile's epilogue reads its own.
+constexpr int G2_PAR = 2 * G2_BUF;            // byte offset of the parameter slots
+constexpr int G2_PARSZ = 6144;
 constexpr int G2_PAR_ROW = 0, G2_PAR_C0 = 2048, G2_PAR_C1 = 3072, G2_PAR_C2 = 4096,
               G2_PAR_C3 = 5120;
-constexpr int G2_LDS = 2 * G2_BUF + 6144;
+constexpr int G2_LDS = 2 * G2_BUF + 2 * G2_PARSZ;
 
-// Epilogue row store (16 B per lane).  DI_NT_STORE (experiment builds only): the
-// non-temporal form, so the streamed output does not evict the operand panels.
+// Epilogue row store (16 B per lane).
 __device__ __forceinline__ void g2_store(bf16 *p, const bf16x8 &v) {
-#ifdef DI_NT_STORE
-    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-    u32x4 u;
-    __builtin_memcpy(&u, &v, 16);
-    __builtin_nontemporal_store(u, reinterpret_cast<u32x4 *>(p));
-#else
     *reinterpret_cast<bf16x8 *>(p) = v;
-#endif
+}
+
+// Global stores one wave issues in the store phase of a full tile (every row < M):
+// the next tile's first counted wait lets exactly these stay in flight.  (V^T tiles,
+// partial tiles and the profiling ablations wait as if there were none.)
+// EPI_RESID_STATS stores with its row statistics, before the prefetch: none in flight.
+template <int EPI, bool SPLIT>
+constexpr int g2_stores() {
+    return EPI == EPI_RESID_STATS ? 0
+           : (SPLIT && EPI != EPI_FOLD && EPI != EPI_FOLD_GELU) ? 32 : 16;
 }
 
 #define G2_BAR() asm volatile("s_barrier" ::: "memory")
+#define G2_WAITV(n) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(n) : "memory")
 
+// Persistent: one workgroup per CU walks a chunk of tiles; after a tile's K loop it
+// (1) does every epilogue step that reads LDS or global memory (parameters, residual
+// rows, the row statistics exchange), (2) issues the next tile's parameter and
+// prologue loads into the now idle LDS buffers, (3) computes and stores the outputs
+// while those loads are in flight, and (4) starts the next K loop with a counted wait
+// that leaves the stores of (3) outstanding.
 template <int EPI, bool SPLIT>
 __global__ void __launch_bounds__(G2_T) gemm256_kernel(GemmArgs g) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
@@ -77,26 +90,25 @@ __global__ void __launch_bounds__(G2_T) gemm256_kernel(GemmArgs g) {
     // wave-uniform in SGPRs: the LDS-DMA destination (M0) is then scalar arithmetic
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wr = wave >> 2, wc = wave & 3;
-
-    // tile order: XCD remap (bijective) + grouped GM x all-N order (speed only)
-    const int n_tn = gridDim.x, n_tm = gridDim.y, n_tiles = n_tn * n_tm;
-    int bid = blockIdx.y * gridDim.x + blockIdx.x;
-    {
-        const int q = n_tiles / 8, r = n_tiles % 8, x = bid % 8;
-        bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
-    }
-    const int GM = g.tune_gm > 0 ? g.tune_gm : 4;
-    const int grp = bid / (GM * n_tn), first_m = grp * GM;
-    const int gsz = min(GM, n_tm - first_m);
-    const int in = bid % (GM * n_tn);
     const int M = g.M, N = g.N, K = g.K;
+    const int n_tn = N / G2_TILE, n_tm = (M + G2_TILE - 1) / G2_TILE, n_tiles = n_tn * n_tm;
+
+    // tile schedule: workgroup b runs on XCD b % 8 (round-robin dispatch); XCD x owns
+    // the contiguous chunk x of the tile order, walked by its workgroups in lockstep,
+    // so the tiles in flight on one XCD are neighbours in the grouped order (GM
+    // M-tiles x all N-tiles: A panels and weight tiles shared in that XCD's L2)
+    const int xcd = blockIdx.x % 8, slot = blockIdx.x / 8;
+    const int wx = ((int)gridDim.x - xcd + 7) / 8;  // workgroups on this XCD
+    const int cq = n_tiles / 8, cr = n_tiles % 8;
+    const int c_lo = xcd * cq + min(xcd, cr), c_hi = c_lo + cq + (xcd < cr ? 1 : 0);
+    int tix = c_lo + slot;
+    if (tix >= c_hi) return;
+    const int GM = g.tune_gm > 0 ? g.tune_gm : 4;
+
     // SPLIT: K tile t covers split columns [64 t, 64 t + 64) = the hi (k-step 0) and lo
     // (k-step 1) halves of logical k [32 t, 32 t + 32)
     const int nk = SPLIT ? K / 32 : K / 64;
     const int lda = SPLIT ? 2 * K : K, ldb = lda;
-#define G2_AT(t) (t)
-    const int m0 = (first_m + in % gsz) * G2_TILE;
-    const int n0 = (in / gsz) * G2_TILE;
 
     // ---- staging sources (per lane) and LDS destinations (per wave) ----------
     // LDS row i (0..127) of a half tile = instruction j (0..1), wave, lane>>3:
@@ -105,45 +117,53 @@ __global__ void __launch_bounds__(G2_T) gemm256_kernel(GemmArgs g) {
     // A half h, row i -> tile row j*128 + h*64 + (i&63)
     // B half h, row i -> tile col j*128 + (wave>>2)*64 + h*32 + (wave&3)*8 + (lane>>3)
     const int chunk = ((lane & 7) ^ ((lane >> 3) & 7)) * 8;
-    // opaque per tile: stops the compiler hoisting the per-(half, instruction)
-    // source addresses of every tile out of the column-tile loop (register spills)
-    const void *A_p = g.A, *B_p = g.B;
-    int m0s = m0;
-    asm volatile("" : "+s"(A_p), "+s"(B_p), "+s"(m0s));
-    const bf16 *a_src = static_cast<const bf16 *>(A_p) +
-                        (int64_t)(m0s + wave * 8 + (lane >> 3)) * lda + chunk;
     // B rows are stored permuted inside each 32-column group: LDS row q = sub*16 +
     // g*4 + r holds column g*8 + sub*4 + r, so that MFMA fragment nt (rows sub*16..+15
     // of half nt>>1) gives, in the C^T layout below, every lane 8 consecutive output
     // columns across the fragment pair (2h, 2h+1).
     const int qb = (wave & 3) * 8 + (lane >> 3);  // LDS row within the 32-column group
     const int b_col = ((qb >> 2) & 3) * 8 + (qb >> 4) * 4 + (qb & 3);
-    const bf16 *b_src = static_cast<const bf16 *>(B_p) +
-                        (int64_t)(n0 + (wave >> 2) * 64 + b_col) * ldb + chunk;
-    const int64_t a_h = (int64_t)64 * lda, a_j = (int64_t)128 * lda;
-    const int64_t b_h = (int64_t)32 * ldb, b_j = (int64_t)128 * ldb;
+    // Stage addresses: a wave-uniform 64-bit base (SGPRs: tile origin, half, K tile)
+    // plus a per-lane 32-bit byte offset, the global_load_lds saddr form (one offset
+    // VGPR per operand instead of a 64-bit pointer per (half, instruction)).
+    uint32_t a_voff = (uint32_t)(((wave * 8 + (lane >> 3)) * lda + chunk) * 2);
+    uint32_t b_voff = (uint32_t)((((wave >> 2) * 64 + b_col) * ldb + chunk) * 2);
+    int m0 = 0, n0 = 0;
+    const char *a_base = nullptr, *b_base = nullptr;
+    auto setup = [&](int t) {
+        const int grp = t / (GM * n_tn), first_m = grp * GM;
+        const int gsz = min(GM, n_tm - first_m);
+        const int in = t % (GM * n_tn);
+        m0 = (first_m + in % gsz) * G2_TILE;
+        n0 = (in / gsz) * G2_TILE;
+        a_base = reinterpret_cast<const char *>(static_cast<const bf16 *>(g.A) + (int64_t)m0 * lda);
+        b_base = reinterpret_cast<const char *>(static_cast<const bf16 *>(g.B) + (int64_t)n0 * ldb);
+    };
+    const int64_t a_h = (int64_t)64 * lda * 2, a_j = (int64_t)128 * lda * 2;  // bytes
+    const int64_t b_h = (int64_t)32 * ldb * 2, b_j = (int64_t)128 * ldb * 2;
     typedef __attribute__((address_space(3))) void lds_void;
 #define G2_STAGE_A(buf, h, t)                                                                  \
     do {                                                                                       \
-        __builtin_amdgcn_global_load_lds((const void *)(a_src + (h) * a_h + G2_AT(t) * 64),    \
+        asm volatile("" : "+v"(a_voff)); /* opaque: no hoisted 64-bit lane pointers */         \
+        __builtin_amdgcn_global_load_lds((const void *)(a_base + ((h) * a_h + (t) * 128) + a_voff), \
                                          (lds_void *)(lds + (buf) * G2_BUF + (h) * 16384 +     \
                                                       wave * 1024),                            \
                                          16, 0, 0);                                            \
-        __builtin_amdgcn_global_load_lds((const void *)(a_src + (h) * a_h + a_j + G2_AT(t) * 64), \
-                                         (lds_void *)(lds + (buf) * G2_BUF + (h) * 16384 +     \
-                                                      8192 + wave * 1024),                     \
-                                         16, 0, 0);                                            \
+        __builtin_amdgcn_global_load_lds(                                                      \
+            (const void *)(a_base + ((h) * a_h + a_j + (t) * 128) + a_voff),                   \
+            (lds_void *)(lds + (buf) * G2_BUF + (h) * 16384 + 8192 + wave * 1024), 16, 0, 0);  \
     } while (0)
 #define G2_STAGE_B(buf, h, t)                                                                  \
     do {                                                                                       \
-        __builtin_amdgcn_global_load_lds((const void *)(b_src + (h) * b_h + (t) * 64),         \
+        asm volatile("" : "+v"(b_voff));                                                       \
+        __builtin_amdgcn_global_load_lds((const void *)(b_base + ((h) * b_h + (t) * 128) + b_voff), \
                                          (lds_void *)(lds + (buf) * G2_BUF + 32768 +           \
                                                       (h) * 16384 + wave * 1024),              \
                                          16, 0, 0);                                            \
-        __builtin_amdgcn_global_load_lds((const void *)(b_src + (h) * b_h + b_j + (t) * 64),   \
-                                         (lds_void *)(lds + (buf) * G2_BUF + 32768 +           \
-                                                      (h) * 16384 + 8192 + wave * 1024),       \
-                                         16, 0, 0);                                            \
+        __builtin_amdgcn_global_load_lds(                                                      \
+            (const void *)(b_base + ((h) * b_h + b_j + (t) * 128) + b_voff),                   \
+            (lds_void *)(lds + (buf) * G2_BUF + 32768 + (h) * 16384 + 8192 + wave * 1024), 16, \
+            0, 0);                                                                             \
     } while (0)
 
     // ---- fragment reads ------------------------------------------------------
@@ -182,10 +202,6 @@ __global__ void __launch_bounds__(G2_T) gemm256_kernel(GemmArgs g) {
     } while (0)
 
     f32x4 acc[8][4];
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
     // (k-step pairs (sa, sb): (0, 0), (1, 1) plain; SPLIT (0, 0) hi*hi, (1, 0) A_lo B_hi,
     // (0, 1) A_hi B_lo)
@@ -208,348 +224,453 @@ __global__ void __launch_bounds__(G2_T) gemm256_kernel(GemmArgs g) {
     } while (0)
 #define G2_SYNC_READS() asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory")
 
-    // ---- epilogue parameters (wave 0; older than every stage load, so the
-    // prologue's counted wait retires them) -----------------------------------------
-    {
-        constexpr bool FOLD = EPI == EPI_FOLD || EPI == EPI_FOLD_GELU;
-        constexpr bool RS = EPI == EPI_RESID_STATS;
-        if (wave == 0) {
-            auto par1k = [&](const void *src, int off) {  // 1 KiB: 16 B per lane
-                __builtin_amdgcn_global_load_lds(
-                    (const void *)(static_cast<const char *>(src) + lane * 16),
-                    (lds_void *)(lds + G2_PAR + off), 16, 0, 0);
-            };
-            par1k((FOLD ? g.col_c : g.bias) + n0, G2_PAR_C0);
-            if (FOLD) par1k(g.col_s + n0, G2_PAR_C1);
-            if (RS && g.row_ln) {
-                par1k(g.res_gamma + n0, G2_PAR_C1);
-                par1k(g.res_beta + n0, G2_PAR_C2);
-            }
-            if (RS && g.head_wg) par1k(g.head_wg + n0, G2_PAR_C3);
-            if (FOLD || (RS && g.row_ln)) {
-                int m0r = m0;
-                asm volatile("" : "+s"(m0r));
-                par1k(g.row_ln + m0r, G2_PAR_ROW);
-                par1k(g.row_ln + m0r + 128, G2_PAR_ROW + 1024);
-            }
+    // ---- epilogue parameters of a tile (wave 0, older than the tile's stage loads,
+    // so its first counted wait retires them) ---------------------------------------
+    constexpr bool FOLD = EPI == EPI_FOLD || EPI == EPI_FOLD_GELU;
+    constexpr bool RS = EPI == EPI_RESID_STATS;
+    auto stage_params = [&](int pb) {
+        if (wave != 0) return;
+        uint32_t l16 = lane * 16;
+        asm volatile("" : "+v"(l16));  // opaque: uniform base + 32-bit offset (saddr form)
+        auto par1k = [&](const void *src, int off) {  // 1 KiB: 16 B per lane
+            __builtin_amdgcn_global_load_lds(
+                (const void *)(static_cast<const char *>(src) + l16),
+                (lds_void *)(lds + G2_PAR + pb * G2_PARSZ + off), 16, 0, 0);
+        };
+        par1k((FOLD ? g.col_c : g.bias) + n0, G2_PAR_C0);
+        if (FOLD) par1k(g.col_s + n0, G2_PAR_C1);
+        if (RS && g.row_ln) {
+            par1k(g.res_gamma + n0, G2_PAR_C1);
+            par1k(g.res_beta + n0, G2_PAR_C2);
         }
-    }
-    // ---- prologue: K tile 0 whole, K tile 1 minus its B1 half --------------------
-    G2_STAGE_A(0, 0, 0);
-    G2_STAGE_B(0, 0, 0);
-    G2_STAGE_A(0, 1, 0);
-    G2_STAGE_B(0, 1, 0);
-    G2_STAGE_A(1, 0, 1);
-    G2_STAGE_B(1, 0, 1);
-    G2_STAGE_A(1, 1, 1);
-    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-    G2_BAR();
-    if (wr == 1) G2_BAR();  // group 1 runs one barrier behind group 0
+        if (RS && g.head_wg) par1k(g.head_wg + n0, G2_PAR_C3);
+        if (FOLD || (RS && g.row_ln)) {
+            int m0r = m0;
+            asm volatile("" : "+s"(m0r));
+            par1k(g.row_ln + m0r, G2_PAR_ROW);
+            par1k(g.row_ln + m0r + 128, G2_PAR_ROW + 1024);
+        }
+    };
+    // prologue of a tile: K tile 0 whole, K tile 1 minus its B1 half
+    auto prologue = [&]() {
+        G2_STAGE_A(0, 0, 0);
+        G2_STAGE_B(0, 0, 0);
+        G2_STAGE_A(0, 1, 0);
+        G2_STAGE_B(0, 1, 0);
+        G2_STAGE_A(1, 0, 1);
+        G2_STAGE_B(1, 0, 1);
+        G2_STAGE_A(1, 1, 1);
+    };
 
-    for (int t = 0; t < nk; t += 2) {
-        const bool more = t + 2 < nk;  // K tiles t+2, t+3 exist (nk is even)
-        // phase 1: buffer 0, A0 + B0
-        G2_READ_B(0, 0);
-        G2_READ_A(0, 0);
-        G2_STAGE_B(1, 1, t + 1);
-        G2_SYNC_READS();
+    int pb = 0;  // parameter slot of the current tile
+    setup(tix);
+    stage_params(pb);
+    prologue();
+    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    for (;;) {
         G2_BAR();
-        G2_MFMA(0, 0);
-        G2_BAR();
-        // phase 2: A1
-        G2_READ_A(0, 4);
-        if (more) G2_STAGE_A(0, 0, t + 2);
-        G2_SYNC_READS();
-        G2_BAR();
-        G2_MFMA(4, 0);
-        G2_BAR();
-        // phase 3: B1
-        G2_READ_B(0, 2);
-        if (more) G2_STAGE_B(0, 0, t + 2);
-        G2_SYNC_READS();
-        G2_BAR();
-        G2_MFMA(4, 2);
-        G2_BAR();
-        // phase 4: registers only; retire K tile t+1 for phase 5
-        if (more) {
-            G2_STAGE_A(0, 1, t + 2);
-            asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-        } else {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (wr == 1) G2_BAR();  // group 1 runs one barrier behind group 0
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+        for (int t = 0; t < nk; t += 2) {
+            const bool more = t + 2 < nk;  // K tiles t+2, t+3 exist (nk is even)
+            // phase 1: buffer 0, A0 + B0
+            G2_READ_B(0, 0);
+            G2_READ_A(0, 0);
+            G2_STAGE_B(1, 1, t + 1);
+            G2_SYNC_READS();
+            G2_BAR();
+            G2_MFMA(0, 0);
+            G2_BAR();
+            // phase 2: A1
+            G2_READ_A(0, 4);
+            if (more) G2_STAGE_A(0, 0, t + 2);
+            G2_SYNC_READS();
+            G2_BAR();
+            G2_MFMA(4, 0);
+            G2_BAR();
+            // phase 3: B1
+            G2_READ_B(0, 2);
+            if (more) G2_STAGE_B(0, 0, t + 2);
+            G2_SYNC_READS();
+            G2_BAR();
+            G2_MFMA(4, 2);
+            G2_BAR();
+            // phase 4: registers only; retire K tile t+1 for phase 5
+            if (more) {
+                G2_STAGE_A(0, 1, t + 2);
+                asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+            } else {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            G2_BAR();
+            G2_MFMA(0, 2);
+            G2_BAR();
+            // phase 5: buffer 1, A0 + B0
+            G2_READ_B(1, 0);
+            G2_READ_A(1, 0);
+            if (more) G2_STAGE_B(0, 1, t + 2);
+            G2_SYNC_READS();
+            G2_BAR();
+            G2_MFMA(0, 0);
+            G2_BAR();
+            // phase 6
+            G2_READ_A(1, 4);
+            if (more) G2_STAGE_A(1, 0, t + 3);
+            G2_SYNC_READS();
+            G2_BAR();
+            G2_MFMA(4, 0);
+            G2_BAR();
+            // phase 7
+            G2_READ_B(1, 2);
+            if (more) G2_STAGE_B(1, 0, t + 3);
+            G2_SYNC_READS();
+            G2_BAR();
+            G2_MFMA(4, 2);
+            G2_BAR();
+            // phase 8: retire K tile t+2 for the next phase 1
+            if (more) {
+                G2_STAGE_A(1, 1, t + 3);
+                asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+            }
+            G2_BAR();
+            G2_MFMA(0, 2);
+            G2_BAR();
         }
-        G2_BAR();
-        G2_MFMA(0, 2);
-        G2_BAR();
-        // phase 5: buffer 1, A0 + B0
-        G2_READ_B(1, 0);
-        G2_READ_A(1, 0);
-        if (more) G2_STAGE_B(0, 1, t + 2);
-        G2_SYNC_READS();
-        G2_BAR();
-        G2_MFMA(0, 0);
-        G2_BAR();
-        // phase 6
-        G2_READ_A(1, 4);
-        if (more) G2_STAGE_A(1, 0, t + 3);
-        G2_SYNC_READS();
-        G2_BAR();
-        G2_MFMA(4, 0);
-        G2_BAR();
-        // phase 7
-        G2_READ_B(1, 2);
-        if (more) G2_STAGE_B(1, 0, t + 3);
-        G2_SYNC_READS();
-        G2_BAR();
-        G2_MFMA(4, 2);
-        G2_BAR();
-        // phase 8: retire K tile t+2 for the next phase 1
-        if (more) {
-            G2_STAGE_A(1, 1, t + 3);
-            asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        if (wr == 0) G2_BAR();  // re-align the two groups: every LDS read has retired
+
+        // ---- epilogue ----------------------------------------------------------
+        // C^T layout (the MFMA took the weight fragment as its first operand): lane l
+        // holds, for A fragment mt and weight-column half h, output row
+        //   m = m0 + wr*128 + mt*16 + (l & 15)
+        // and the 8 consecutive columns n = n0 + wc*64 + h*32 + (l >> 4)*8 + e, e = 0..7,
+        // in acc[mt][2h][0..3], acc[mt][2h+1][0..3].  Stores go straight from registers,
+        // 16 B (bf16) / 32 B (f32) per lane, no LDS round trip.
+        const int nxt = tix + wx;
+        // (the residual epilogues run one tile per workgroup, see launch_gemm256)
+        constexpr bool PERSIST = EPI != EPI_BIAS_RESID && EPI != EPI_RESID_STATS;
+        const bool has_next = PERSIST && nxt < c_hi;
+        const bool full = m0 + G2_TILE <= M;
+        int m0e = m0;  // opaque: keeps the per-row epilogue offsets out of the K loop
+        asm volatile("" : "+s"(m0e));
+        const int row_l = m0e + wr * 128 + (lane & 15);
+        const int col_l = n0 + wc * 64 + (lane >> 4) * 8;
+        // global addresses: a wave-uniform base (row m0 + wr*128, column n0 + wc*64) +
+        // mt * (16 rows) in SGPRs, and one 32-bit lane offset (row lane&15, column
+        // (lane>>4)*8) -- no 64-bit pointer per row held across the prefetch
+        const int64_t row_w = m0e + wr * 128, col_w = n0 + wc * 64;
+        auto lane_off = [&](int ld, int esz) {
+            return (uint32_t)(((lane & 15) * ld + (lane >> 4) * 8) * esz);
+        };
+        const bool vtile = EPI == EPI_QKV && n0 >= 2 * g.hidden;
+        const unsigned char *par = lds + G2_PAR + pb * G2_PARSZ;
+        // tile-local indices into the staged parameters
+        const int prow = wr * 128 + (lane & 15);          // + mt * 16
+        const int pcol = wc * 64 + (lane >> 4) * 8;        // + h * 32 + e
+        auto par8 = [&](int off, int h, float (&v)[8]) {   // 8 column params from LDS
+            const float4 a = *reinterpret_cast<const float4 *>(par + off + (pcol + h * 32) * 4);
+            const float4 b = *reinterpret_cast<const float4 *>(par + off + (pcol + h * 32 + 4) * 4);
+            v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+            v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+        };
+        auto prow2 = [&](int mt) {  // (rstd, -rstd mean) of row prow + 16 mt
+            return *reinterpret_cast<const float2 *>(par + G2_PAR_ROW + (prow + mt * 16) * 8);
+        };
+
+        // (1) reads: parameters, residual rows, V^T columns, row statistics
+        float bias_v[2][8];  // (the folded epilogues carry their bias inside col_c)
+        float cs2[2][8], ra[8], rb[8];
+        int vc[8];
+        // (full tiles: straight-line code, no per-row guards)
+        auto reads = [&](auto full_c) {
+            constexpr bool FULL = decltype(full_c)::value;
+            par8(G2_PAR_C0, 0, bias_v[0]);
+            par8(G2_PAR_C0, 1, bias_v[1]);
+            if constexpr (FOLD) {
+#pragma unroll
+                for (int mt = 0; mt < 8; ++mt) {
+                    const float2 p = prow2(mt);
+                    ra[mt] = p.x;
+                    rb[mt] = p.y;
+                }
+                par8(G2_PAR_C1, 0, cs2[0]);
+                par8(G2_PAR_C1, 1, cs2[1]);
+            }
+            if (vtile) {
+#pragma unroll
+                for (int mt = 0; mt < 8; ++mt) {
+                    const int row = row_l + mt * 16;
+                    vc[mt] = (FULL || row < M) ? g.vcol[row] : -1;
+                }
+#pragma unroll
+                for (int mt = 0; mt < 8; ++mt)  // consumed here: the load's wait stays
+                    asm volatile("" : "+v"(vc[mt]));  // ahead of the prefetch
+            }
+            if constexpr (EPI == EPI_BIAS_RESID) {  // acc <- (acc + bias) + resid
+                // (SPLIT: split residual rows, stride 2N, 32-column chunks of hi then lo).
+                const int rld = SPLIT ? 2 * N : N;
+                const char *rbase = static_cast<const char *>(g.resid) +
+                                    (row_w * rld + (SPLIT ? 2 * col_w : col_w)) * 2;
+                const uint32_t rlo = lane_off(rld, 2);
+#pragma unroll
+                for (int mt = 0; mt < 8; ++mt) {
+                    if (!FULL && row_l + mt * 16 >= M) continue;
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        const char *rp = rbase + (int64_t)mt * 16 * rld * 2 + h * (SPLIT ? 128 : 64) + rlo;
+                        float r[8];
+                        if constexpr (SPLIT) {
+                            const bf16x8 rh = *reinterpret_cast<const bf16x8 *>(rp);
+                            const bf16x8 rl = *reinterpret_cast<const bf16x8 *>(rp + 64);
+#pragma unroll
+                            for (int e = 0; e < 8; ++e) r[e] = (float)rh[e] + (float)rl[e];
+                        } else {
+                            const bf16x8 rv = *reinterpret_cast<const bf16x8 *>(rp);
+#pragma unroll
+                            for (int e = 0; e < 8; ++e) r[e] = (float)rv[e];
+                        }
+#pragma unroll
+                        for (int e = 0; e < 8; ++e)
+                            acc[mt][2 * h + (e >> 2)][e & 3] =
+                                (acc[mt][2 * h + (e >> 2)][e & 3] + bias_v[h][e]) + r[e];
+                    }
+                }
+            }
+            if constexpr (EPI == EPI_RESID_STATS) {
+                // out = acc + bias + LN(resid) (resid normalised on the fly from its row
+                // statistics, or plain), and this tile's partial statistics of the
+                // rounded out
+                const bool res_ln = g.row_ln != nullptr;
+                float ss[8], sq[8], sd[8], rr[8], rs[8];
+                float gm[2][8], bt[2][8], wg[2][8];
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    if (res_ln) {
+                        par8(G2_PAR_C1, h, gm[h]);
+                        par8(G2_PAR_C2, h, bt[h]);
+                    } else {
+#pragma unroll
+                        for (int e = 0; e < 8; ++e) {
+                            gm[h][e] = 1.f;
+                            bt[h][e] = 0.f;
+                        }
+                    }
+                    if (g.head_wg) {
+                        par8(G2_PAR_C3, h, wg[h]);
+                    } else {
+#pragma unroll
+                        for (int e = 0; e < 8; ++e) wg[h][e] = 0.f;
+                    }
+                }
+#pragma unroll
+                for (int mt = 0; mt < 8; ++mt) {
+                    ss[mt] = sq[mt] = sd[mt] = 0.f;
+                    rr[mt] = 1.f;
+                    rs[mt] = 0.f;
+                    if (res_ln) {
+                        const float2 p = prow2(mt);
+                        rr[mt] = p.x;
+                        rs[mt] = p.y;
+                    }
+                }
+                const char *rbase = static_cast<const char *>(g.resid) + (row_w * N + col_w) * 2;
+                const uint32_t rlo = lane_off(N, 2);
+                char *ob = static_cast<char *>(g.out) + (row_w * g.ld_out + col_w) * 2;
+                const uint32_t olo = lane_off(g.ld_out, 2);
+#pragma unroll
+                for (int mt = 0; mt < 8; ++mt) {
+                    if (!FULL && row_l + mt * 16 >= M) continue;
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        const bf16x8 rv = *reinterpret_cast<const bf16x8 *>(
+                            rbase + (int64_t)mt * 16 * N * 2 + h * 64 + rlo);
+                        bf16x8 o;
+#pragma unroll
+                        for (int e = 0; e < 8; ++e) {
+                            const float res = fmaf(gm[h][e], fmaf(rr[mt], (float)rv[e], rs[mt]), bt[h][e]);
+                            o[e] = (bf16)(acc[mt][2 * h + (e >> 2)][e & 3] + bias_v[h][e] + res);
+                            const float yb = (float)o[e];
+                            ss[mt] += yb;
+                            sq[mt] = fmaf(yb, yb, sq[mt]);
+                            sd[mt] = fmaf(yb, wg[h][e], sd[mt]);
+                        }
+                        if (!(g.ablate & 4))
+                            g2_store(reinterpret_cast<bf16 *>(ob + (int64_t)mt * 16 * g.ld_out * 2 +
+                                                              h * 64 + olo),
+                                     o);
+                    }
+                }
+                // partials: the 4 lane groups (lanes l, l^16, l^32, l^48 share a row),
+                // then the 4 wc waves through LDS (the staging buffers are idle until
+                // the prefetch below), fixed order
+#pragma unroll
+                for (int mt = 0; mt < 8; ++mt) {
+#pragma unroll
+                    for (int d = 16; d <= 32; d <<= 1) {
+                        ss[mt] += __shfl_xor(ss[mt], d, 64);
+                        sq[mt] += __shfl_xor(sq[mt], d, 64);
+                        sd[mt] += __shfl_xor(sd[mt], d, 64);
+                    }
+                }
+                float4 *part = reinterpret_cast<float4 *>(lds);  // [4 wc][256 rows]
+                if (lane < 16) {
+#pragma unroll
+                    for (int mt = 0; mt < 8; ++mt)
+                        part[wc * G2_TILE + wr * 128 + mt * 16 + lane] =
+                            make_float4(ss[mt], sq[mt], sd[mt], 0.f);
+                }
+                __syncthreads();
+                if (tid < G2_TILE && m0e + tid < M) {
+                    float4 t = part[tid];
+#pragma unroll
+                    for (int w = 1; w < 4; ++w) {
+                        const float4 u = part[w * G2_TILE + tid];
+                        t.x += u.x;
+                        t.y += u.y;
+                        t.z += u.z;
+                    }
+                    g.stats_out[(int64_t)(n0 / G2_TILE) * g.stats_ld + m0e + tid] = t;
+                }
+                __syncthreads();  // part[] read before the prefetch overwrites it
+            }
+        };
+        if (full && PERSIST && EPI != EPI_QKV)  // (measured: no spills)
+            reads(std::true_type{});
+        else
+            reads(std::false_type{});
+
+        // (2) the next tile's parameters and prologue (a compiler memory barrier: no
+        // load of (1) may sink below the prefetch, whose wait would then drain it)
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        if (has_next) {
+            setup(nxt);
+            stage_params(pb ^ 1);
+            prologue();
         }
-        G2_BAR();
-        G2_MFMA(0, 2);
-        G2_BAR();
+        __builtin_amdgcn_sched_barrier(0);
+
+        // (3) compute and store (registers and global stores only)
+        auto stores = [&](auto full_c) {
+            constexpr bool FULL = decltype(full_c)::value;
+            if (vtile) {  // V columns: transposed element stores into V^T
+                typedef typename std::conditional<SPLIT, float, bf16>::type VT;  // SPLIT: f32 V^T
+                char *vb = static_cast<char *>(g.out2) + (col_w - 2 * g.hidden) * g.ld_v * (int64_t)sizeof(VT);
+#pragma unroll
+                for (int mt = 0; mt < 8; ++mt) {
+                    if (vc[mt] < 0) continue;
+#pragma unroll
+                    for (int h = 0; h < 2; ++h)
+#pragma unroll
+                        for (int e = 0; e < 8; ++e)
+                            *reinterpret_cast<VT *>(
+                                vb + (uint32_t)((((lane >> 4) * 8 + h * 32 + e) * g.ld_v + vc[mt]) *
+                                                (int)sizeof(VT))) =
+                                (VT)(acc[mt][2 * h + (e >> 2)][e & 3] + bias_v[h][e]);
+                }
+            } else if constexpr (FOLD) {
+                // LN folded into this GEMM: y = r acc - r mu s + c  (per row r, mu; per
+                // column s, c); row-major order: both 64-byte halves of a row's 128-byte
+                // segment are stored by consecutive instructions
+                char *ob = static_cast<char *>(g.out) + (row_w * g.ld_out + col_w) * 2;
+                const uint32_t olo = lane_off(g.ld_out, 2);
+#pragma unroll
+                for (int mt = 0; mt < 8; ++mt) {
+                    const int row = row_l + mt * 16;
+                    if (!FULL && row >= M) continue;
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        float v[8];
+#pragma unroll
+                        for (int e = 0; e < 8; ++e)
+                            v[e] = fmaf(ra[mt], acc[mt][2 * h + (e >> 2)][e & 3],
+                                        fmaf(rb[mt], cs2[h][e], bias_v[h][e]));
+                        if constexpr (EPI == EPI_FOLD_GELU) {
+                            if (!(g.ablate & 2)) gelu_erf8(v);
+                        }
+                        bf16x8 o;
+#pragma unroll
+                        for (int e = 0; e < 8; ++e) o[e] = (bf16)v[e];
+                        if (!(g.ablate & 4))
+                            g2_store(reinterpret_cast<bf16 *>(ob + (int64_t)mt * 16 * g.ld_out * 2 +
+                                                              h * 64 + olo),
+                                     o);
+                    }
+                }
+            } else if constexpr (RS) {
+                // (stored with the statistics, before the prefetch)
+            } else {
+                // element size and column of the output rows: bf16 rows; SPLIT: f32 rows
+                // (Q | K, pre-LN) or split rows (ld_out = 2N, hi chunk then lo chunk)
+                constexpr bool F32 = SPLIT && (EPI == EPI_QKV || EPI == EPI_BIAS_RESID);
+                constexpr int ESZ = F32 ? 4 : 2;
+                constexpr int HSTEP = F32 ? 128 : (SPLIT ? 128 : 64);  // bytes per 32 columns
+                char *ob = static_cast<char *>(g.out) +
+                           (row_w * g.ld_out + ((SPLIT && !F32) ? 2 * col_w : col_w)) * ESZ;
+                const uint32_t olo = lane_off(g.ld_out, ESZ);
+#pragma unroll
+                for (int mt = 0; mt < 8; ++mt) {
+                    const int row = row_l + mt * 16;
+                    if (!FULL && row >= M) continue;
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        float v[8];
+#pragma unroll
+                        for (int e = 0; e < 8; ++e)
+                            v[e] = EPI == EPI_BIAS_RESID ? acc[mt][2 * h + (e >> 2)][e & 3]
+                                                         : acc[mt][2 * h + (e >> 2)][e & 3] +
+                                                               bias_v[h][e];
+                        if constexpr (EPI == EPI_BIAS_GELU) {
+                            if (!(g.ablate & 2)) gelu_erf8(v);
+                        }
+                        if (g.ablate & 4) continue;
+                        char *op = ob + (int64_t)mt * 16 * g.ld_out * ESZ + h * HSTEP + olo;
+                        if constexpr (F32) {
+                            *reinterpret_cast<float4 *>(op) = make_float4(v[0], v[1], v[2], v[3]);
+                            *reinterpret_cast<float4 *>(op + 16) = make_float4(v[4], v[5], v[6], v[7]);
+                        } else if constexpr (SPLIT) {  // 8 columns of one 32-column chunk
+                            bf16x8 hv, lv;
+#pragma unroll
+                            for (int e = 0; e < 8; ++e) hv[e] = split_hi(v[e]), lv[e] = split_lo(v[e]);
+                            g2_store(reinterpret_cast<bf16 *>(op), hv);
+                            g2_store(reinterpret_cast<bf16 *>(op + 64), lv);
+                        } else {
+                            bf16x8 o8;
+#pragma unroll
+                            for (int e = 0; e < 8; ++e) o8[e] = (bf16)v[e];
+                            g2_store(reinterpret_cast<bf16 *>(op), o8);
+                        }
+                    }
+                }
+            }
+        };
+        if (full)
+            stores(std::true_type{});
+        else
+            stores(std::false_type{});
+        if (!has_next) break;
+        // (4) retire the next tile's K tile 0 (the parameters are older still), leaving
+        // this tile's stores in flight when their count is known
+        if (full && !vtile && !(g.ablate & 4))
+            G2_WAITV((6 + g2_stores<EPI, SPLIT>()));
+        else
+            G2_WAITV(6);
+        tix = nxt;
+        pb ^= 1;
     }
-    if (wr == 0) G2_BAR();  // re-align the two groups (every barrier is matched)
 #undef G2_STAGE_A
 #undef G2_STAGE_B
-#undef G2_AT
 #undef G2_LD
 #undef G2_READ_A
 #undef G2_READ_B
 #undef G2_MFMA
 #undef G2_SYNC_READS
-
-    // ---- epilogue ------------------------------------------------------------
-    if (g.ablate & 1) {  // profiling: main loop only (accumulators kept live)
-#pragma unroll
-        for (int i = 0; i < 8; ++i)
-#pragma unroll
-            for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(acc[i][j]));
-        return;
-    }
-    // C^T layout (the MFMA took the weight fragment as its first operand): lane l
-    // holds, for A fragment mt and weight-column half h, output row
-    //   m = m0 + wr*128 + mt*16 + (l & 15)
-    // and the 8 consecutive columns n = n0 + wc*64 + h*32 + (l >> 4)*8 + e, e = 0..7,
-    // in acc[mt][2h][0..3], acc[mt][2h+1][0..3].  Stores go straight from registers,
-    // 16 B (bf16) / 32 B (f32) per lane, no LDS round trip and no barrier.
-    int m0e = m0;  // opaque: keeps the per-row epilogue offsets out of the K loop
-    asm volatile("" : "+s"(m0e));
-    const int row_l = m0e + wr * 128 + (lane & 15);
-    const int col_l = n0 + wc * 64 + (lane >> 4) * 8;
-    // tile-local indices into the staged parameters
-    const int prow = wr * 128 + (lane & 15);          // + mt * 16
-    const int pcol = wc * 64 + (lane >> 4) * 8;        // + h * 32 + e
-    auto par8 = [&](int off, int h, float (&v)[8]) {   // 8 column params from LDS
-        const float4 a = *reinterpret_cast<const float4 *>(lds + G2_PAR + off + (pcol + h * 32) * 4);
-        const float4 b = *reinterpret_cast<const float4 *>(lds + G2_PAR + off + (pcol + h * 32 + 4) * 4);
-        v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
-        v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
-    };
-    auto prow2 = [&](int mt) {  // (rstd, -rstd mean) of row prow + 16 mt
-        return *reinterpret_cast<const float2 *>(lds + G2_PAR + G2_PAR_ROW + (prow + mt * 16) * 8);
-    };
-    float bias_v[2][8];  // (the folded epilogues carry their bias inside col_c)
-    par8(G2_PAR_C0, 0, bias_v[0]);
-    par8(G2_PAR_C0, 1, bias_v[1]);
-    if constexpr (EPI == EPI_QKV) {
-        if (n0 >= 2 * g.hidden) {  // V columns: transposed element stores into V^T
-            typedef typename std::conditional<SPLIT, float, bf16>::type VT;  // SPLIT: f32 V^T
-            VT *vt = static_cast<VT *>(g.out2) + (int64_t)(col_l - 2 * g.hidden) * g.ld_v;
-#pragma unroll
-            for (int mt = 0; mt < 8; ++mt) {
-                const int row = row_l + mt * 16;
-                if (row < M) {
-                    const int vc = g.vcol[row];
-#pragma unroll
-                    for (int h = 0; h < 2; ++h)
-#pragma unroll
-                        for (int e = 0; e < 8; ++e)
-                            vt[(int64_t)(h * 32 + e) * g.ld_v + vc] =
-                                (VT)(acc[mt][2 * h + (e >> 2)][e & 3] + bias_v[h][e]);
-                }
-            }
-            return;
-        }
-    }
-    if constexpr (EPI == EPI_FOLD || EPI == EPI_FOLD_GELU) {
-        // LN folded into this GEMM: y = r acc - r mu s + c  (per row r, mu; per column s, c)
-        float ra[8], rb[8];
-#pragma unroll
-        for (int mt = 0; mt < 8; ++mt) {
-            const float2 p = prow2(mt);
-            ra[mt] = p.x;
-            rb[mt] = p.y;
-        }
-        float cs2[2][8];
-        par8(G2_PAR_C1, 0, cs2[0]);
-        par8(G2_PAR_C1, 1, cs2[1]);
-        // row-major order: both 64-byte halves of a row's 128-byte segment are
-        // stored by consecutive instructions (FFN1 -3.5%, QKV -2% against the
-        // column-half-major order; same values)
-#pragma unroll
-        for (int mt = 0; mt < 8; ++mt) {
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                const float(&cs)[8] = cs2[h];
-                const float(&cc)[8] = bias_v[h];
-                const int row = row_l + mt * 16;
-                if (row >= M) continue;
-                float v[8];
-#pragma unroll
-                for (int e = 0; e < 8; ++e)
-                    v[e] = fmaf(ra[mt], acc[mt][2 * h + (e >> 2)][e & 3], fmaf(rb[mt], cs[e], cc[e]));
-                if constexpr (EPI == EPI_FOLD_GELU) gelu_erf8(v);
-                bf16x8 ov;
-#pragma unroll
-                for (int e = 0; e < 8; ++e) ov[e] = (bf16)v[e];
-                g2_store(static_cast<bf16 *>(g.out) + (int64_t)row * g.ld_out + col_l + h * 32, ov);
-            }
-        }
-    } else if constexpr (EPI == EPI_RESID_STATS) {
-        // out = acc + bias + LN(resid) (resid normalised on the fly from its row
-        // statistics, or plain), and this tile's partial statistics of the rounded out
-        const bool res_ln = g.row_ln != nullptr;
-        float ra[8], rb[8], ss[8], sq[8], sd[8];
-#pragma unroll
-        for (int mt = 0; mt < 8; ++mt) {
-            ss[mt] = sq[mt] = sd[mt] = 0.f;
-            ra[mt] = 1.f;
-            rb[mt] = 0.f;
-            if (res_ln) {
-                const float2 p = prow2(mt);
-                ra[mt] = p.x;
-                rb[mt] = p.y;
-            }
-        }
-        // row-major order, as in the folded epilogues (O -4%)
-#pragma unroll
-        for (int mt = 0; mt < 8; ++mt) {
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-            float gm[8], bt[8], wg[8];
-            if (res_ln) {
-                par8(G2_PAR_C1, h, gm);
-                par8(G2_PAR_C2, h, bt);
-            } else {
-#pragma unroll
-                for (int e = 0; e < 8; ++e) {
-                    gm[e] = 1.f;
-                    bt[e] = 0.f;
-                }
-            }
-            if (g.head_wg) {
-                par8(G2_PAR_C3, h, wg);
-            } else {
-#pragma unroll
-                for (int e = 0; e < 8; ++e) wg[e] = 0.f;
-            }
-                const int row = row_l + mt * 16;
-                if (row >= M) continue;
-                const bf16x8 rv = *reinterpret_cast<const bf16x8 *>(
-                    static_cast<const bf16 *>(g.resid) + (int64_t)row * N + col_l + h * 32);
-                bf16x8 ov;
-#pragma unroll
-                for (int e = 0; e < 8; ++e) {
-                    const float res = fmaf(gm[e], fmaf(ra[mt], (float)rv[e], rb[mt]), bt[e]);
-                    ov[e] = (bf16)(acc[mt][2 * h + (e >> 2)][e & 3] + bias_v[h][e] + res);
-                    const float yb = (float)ov[e];
-                    ss[mt] += yb;
-                    sq[mt] = fmaf(yb, yb, sq[mt]);
-                    sd[mt] = fmaf(yb, wg[e], sd[mt]);
-                }
-                g2_store(static_cast<bf16 *>(g.out) + (int64_t)row * g.ld_out + col_l + h * 32, ov);
-            }
-        }
-        // partials: the 4 lane groups (lanes l, l^16, l^32, l^48 share a row), then
-        // the 4 wc waves through LDS (the staging buffers are free), fixed order
-#pragma unroll
-        for (int mt = 0; mt < 8; ++mt) {
-#pragma unroll
-            for (int d = 16; d <= 32; d <<= 1) {
-                ss[mt] += __shfl_xor(ss[mt], d, 64);
-                sq[mt] += __shfl_xor(sq[mt], d, 64);
-                sd[mt] += __shfl_xor(sd[mt], d, 64);
-            }
-        }
-        float4 *part = reinterpret_cast<float4 *>(lds);  // [4 wc][256 rows]
-        if (lane < 16) {
-#pragma unroll
-            for (int mt = 0; mt < 8; ++mt)
-                part[wc * G2_TILE + wr * 128 + mt * 16 + lane] = make_float4(ss[mt], sq[mt], sd[mt], 0.f);
-        }
-        __syncthreads();
-        if (tid < G2_TILE && m0e + tid < M) {
-            float4 t = part[tid];
-#pragma unroll
-            for (int w = 1; w < 4; ++w) {
-                const float4 u = part[w * G2_TILE + tid];
-                t.x += u.x;
-                t.y += u.y;
-                t.z += u.z;
-            }
-            g.stats_out[(int64_t)(n0 / G2_TILE) * g.stats_ld + m0e + tid] = t;
-        }
-    } else {
-#pragma unroll
-    for (int mt = 0; mt < 8; ++mt) {
-        const int row = row_l + mt * 16;
-        if (row >= M) continue;
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            float v[8];
-#pragma unroll
-            for (int e = 0; e < 8; ++e) v[e] = acc[mt][2 * h + (e >> 2)][e & 3] + bias_v[h][e];
-            if (EPI == EPI_BIAS_GELU && !(g.ablate & 2)) gelu_erf8(v);  // ablate 2: no GELU (profiling)
-            const int64_t o = (int64_t)row * g.ld_out + col_l + h * 32;
-            if constexpr (EPI == EPI_BIAS_RESID) {
-                if constexpr (SPLIT) {  // split residual rows
-                    const bf16 *rp = static_cast<const bf16 *>(g.resid) + (int64_t)row * 2 * N +
-                                     split_col(col_l + h * 32);
-                    const bf16x8 rh = *reinterpret_cast<const bf16x8 *>(rp);
-                    const bf16x8 rl = *reinterpret_cast<const bf16x8 *>(rp + 32);
-#pragma unroll
-                    for (int e = 0; e < 8; ++e) v[e] += (float)rh[e] + (float)rl[e];
-                } else {
-                    const bf16x8 rv = *reinterpret_cast<const bf16x8 *>(
-                        static_cast<const bf16 *>(g.resid) + (int64_t)row * N + col_l + h * 32);
-#pragma unroll
-                    for (int e = 0; e < 8; ++e) v[e] += (float)rv[e];
-                }
-            }
-            if constexpr (SPLIT) {
-                if constexpr (EPI == EPI_QKV || EPI == EPI_BIAS_RESID) {  // f32 rows
-                    float *op = static_cast<float *>(g.out) + o;
-                    *reinterpret_cast<float4 *>(op) = make_float4(v[0], v[1], v[2], v[3]);
-                    *reinterpret_cast<float4 *>(op + 4) = make_float4(v[4], v[5], v[6], v[7]);
-                } else {  // split rows (ld_out = 2N): 8 columns of one 32-column chunk
-                    bf16x8 hv, lv;
-#pragma unroll
-                    for (int e = 0; e < 8; ++e) hv[e] = split_hi(v[e]), lv[e] = split_lo(v[e]);
-                    bf16 *op = static_cast<bf16 *>(g.out) + (int64_t)row * g.ld_out +
-                               split_col(col_l + h * 32);
-                    g2_store(op, hv);
-                    g2_store(op + 32, lv);
-                }
-                continue;
-            }
-            bf16x8 ov;
-#pragma unroll
-            for (int e = 0; e < 8; ++e) ov[e] = (bf16)v[e];
-            if (g.ablate & 4) {  // profiling: no stores (values kept live)
-                uint4 u;
-                __builtin_memcpy(&u, &ov, 16);
-                asm volatile("" ::"v"(u.x), "v"(u.y), "v"(u.z), "v"(u.w));
-            } else {
-                g2_store(static_cast<bf16 *>(g.out) + o, ov);
-            }
-        }
-    }
-    }  // generic epilogues
 }
 #undef G2_BAR
+#undef G2_WAITV
 
 // Shapes the 8-phase kernel takes; everything else goes to the 128x128 kernel.
 bool gemm256_ok(int epi, const GemmArgs &g) {
@@ -569,8 +690,14 @@ int gemm_stats_cols() { return G2_TILE; }
 
 void launch_gemm256(int epi, const GemmArgs &g, hipStream_t s) {
     static_assert(G2_LDS <= 160 * 1024, "LDS");
-    dim3 grid(g.N / G2_TILE, (g.M + G2_TILE - 1) / G2_TILE);
     DI_REQUIRE(gemm256_ok(epi, g), DI_EINVAL, "gemm256: unsupported shape / epilogue");
+    const int n_tiles = g.N / G2_TILE * ((g.M + G2_TILE - 1) / G2_TILE);
+    if (n_tiles == 0) return;
+    // persistent (one workgroup per CU) where the epilogue reads no global memory;
+    // the residual epilogues run one tile per workgroup (their residual loads would
+    // otherwise queue behind the next tile's prefetch: measured O 0.31 -> 0.36 ms)
+    const bool resid = epi == EPI_BIAS_RESID || epi == EPI_RESID_STATS;
+    const dim3 grid(resid ? n_tiles : std::min(n_tiles, n_cu()));
     if (g.split) {
         switch (epi) {
 #define G2_SCASE(E)                                                                            \
