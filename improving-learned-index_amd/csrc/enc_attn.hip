@@ -12,7 +12,7 @@
 //   O^T[d][q]   = V^T P^T        (B = P^T is the S^T accumulator itself; the
 //                                 MFMA k index is permuted consistently on A)
 // V^T comes pre-transposed from the QKV GEMM epilogue, laid out [H][ld_v] with
-// every document starting at a 4-aligned column vbase(d) = 4*(d + cu[d]/4), so
+// every document starting at a 32-aligned column vt_base(d) = 32*(d + cu[d]/32), so
 // 4 consecutive keys are one 8-byte (bf16) / 16-byte (f32) load.
 // Online softmax in f32 (exp2 with log2(e)/8 folded into the scores).
 #include <hip/hip_runtime.h>
@@ -29,8 +29,9 @@ namespace di {
 constexpr int ATT_D = 64;
 constexpr int QT = 4;  // query tiles of 16 per wave
 
-// doc d's first V^T column: 8-aligned (16 B), at most 7 gap columns per document
-__host__ __device__ __forceinline__ int vt_base(int doc, int tok0) { return 8 * (doc + (tok0 >> 3)); }
+// doc d's first V^T column: 32-aligned (one split chunk; 16 B loads for bf16 / f32),
+// at most 31 gap columns per document
+__host__ __device__ __forceinline__ int vt_base(int doc, int tok0) { return 32 * (doc + (tok0 >> 5)); }
 
 template <typename T>
 struct AttnOps;
@@ -247,172 +248,277 @@ attention_kernel(const T *__restrict__ qk, const T *__restrict__ vt,
     }
 }
 
-// fp32-faithful attention (precision bf16x3): attention_kernel's register-direct
-// structure on the f32 Q | K rows and f32 V^T of the split QKV GEMM, with every
-// product as split bf16 (x = x_hi + x_lo, three 16x16x32 bf16 MFMAs per f32 product:
-// hi*hi + lo*hi + hi*lo, f32 accumulate, ~2^-17 relative per product) instead of
-// f32 MFMA (1/16 of the bf16 rate): S^T = K Q^T from split K and Q, O^T = V^T P^T
-// from split V^T and the split probabilities; softmax and the row sums in f32.
-// Output: split-bf16 ctx rows [hi(H) | lo(H)] for the O GEMM.
-__device__ __forceinline__ void split8(const float4 &a, const float4 &b, bf16x8 &hi,
-                                       bf16x8 &lo) {
-    const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-        hi[e] = split_hi(v[e]);
-        lo[e] = split_lo(v[e]);
-    }
-}
+// fp32-faithful attention (precision bf16x3): every product as split bf16 (x = x_hi +
+// x_lo, three 16x16x32 bf16 MFMAs per f32 product: hi*hi + lo*hi + hi*lo, f32
+// accumulate, ~2^-17 relative per product) instead of f32 MFMA (1/16 of the bf16
+// rate): S^T = K Q^T from split K and Q, O^T = V^T P^T from split V and the split
+// probabilities; softmax and the row sums in f32.  Q | K | V arrive as split rows
+// [M][6H] from the QKV GEMM (split_col over the 3H logical columns): no V^T scatter.
+//
+// One 512-thread workgroup per (doc, head): the 8 waves own 32 queries each (two
+// 16-query tiles; documents past 256 tokens take a second pass), and the keys stream
+// through LDS in 32-key chunks, double-buffered: chunk i+1 is copied by LDS-DMA
+// (global_load_lds, every wave one 1 KiB piece of K and one of V) while chunk i is
+// computed, so every K / V byte is read from memory once per pass for the workgroup.
+//   K and V images (8 KiB each): key row r = the head's 256 B [ch0 hi | ch0 lo | ch1 hi
+//   | ch1 lo] (16-byte slots), slot j stored at j ^ (r & 15).
+//   S^T fragment row c of tile t = key 8 (c >> 2) + 4 t + (c & 3), so lane group g holds
+//   the consecutive keys 8 g..8 g + 7 of P^T (as attention_v3_kernel); the O^T A
+//   operand (V^T) is read from the V rows with ds_read_b64_tr_b16.
+// Fragment reads are inline-asm ds_reads with their lgkmcnt wait in the same statement
+// (the compiler would otherwise drain the in-flight prefetch with vmcnt(0) before an
+// LDS read it cannot tell apart from the DMA's destination).
+constexpr int AX_WAVES = 8, AX_QT = 2, AX_KC = 32;
+constexpr int AX_IMG = AX_KC * 256, AX_STAGE = 2 * AX_IMG;
+constexpr int AX_LDS = 2 * AX_STAGE;
 
-__device__ __forceinline__ f32x4 mma_x3(const bf16x8 &ah, const bf16x8 &al, const bf16x8 &bh,
-                                        const bf16x8 &bl, f32x4 acc) {
-    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh, acc, 0, 0, 0);
-    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl, acc, 0, 0, 0);
-}
-
-__global__ void __launch_bounds__(64)
-attention_x3_kernel(const float *__restrict__ qk, const float *__restrict__ vt,
-                    const int32_t *__restrict__ cu_seqlens, int H, int ld_v, int n_qb,
-                    int n_heads, int n_pairs, bf16 *__restrict__ ctx_split) {
-    const int id = blockIdx.x, x = id & 7, j = id >> 3;  // XCD-grouped, as attention_kernel
-    const int pair = (j / n_qb) * 8 + x;
-    const int qb = j % n_qb;
-    if (pair >= n_pairs) return;
-    const int doc = pair / n_heads, h = pair % n_heads;
-    const int lane = threadIdx.x;
+__global__ void __launch_bounds__(64 * AX_WAVES)
+attention_x3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu_seqlens, int H,
+                    int n_heads, bf16 *__restrict__ ctx_split) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    typedef __attribute__((address_space(3))) void lds_void;
+    const int pair = blockIdx.x, doc = pair / n_heads, h = pair % n_heads;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int g = lane >> 4, c = lane & 15;
     const int tok0 = cu_seqlens[doc], n = cu_seqlens[doc + 1] - tok0;
-    const int q_base = qb * (16 * QT);
-    if (q_base >= n) return;
-    const int ldqk = 2 * H;
-
-    // B operands Q^T, lane (g, c): Q[q_base + 16 qt + c][32 ch + 8 g + e]
-    bf16x8 qh[QT][2], ql[QT][2];
-#pragma unroll
-    for (int qt = 0; qt < QT; ++qt) {
-        const int qrow = tok0 + min(q_base + 16 * qt + c, n - 1);
-#pragma unroll
-        for (int ch = 0; ch < 2; ++ch) {
-            const float *src = qk + (int64_t)qrow * ldqk + h * ATT_D + ch * 32 + 8 * g;
-            split8(*reinterpret_cast<const float4 *>(src),
-                   *reinterpret_cast<const float4 *>(src + 4), qh[qt][ch], ql[qt][ch]);
-        }
-    }
+    if (n <= 0) return;
+    const int64_t ld = 6 * (int64_t)H;  // split row: 3H logical columns
+    const bf16 *kg = qkv + split_col(H + h * ATT_D);      // + key row * ld: 256 B
+    const bf16 *vg = qkv + split_col(2 * H + h * ATT_D);
+    const int n_chunks = (n + AX_KC - 1) / AX_KC;
+    const uint32_t lds_base =
+        (uint32_t)(uintptr_t)((__attribute__((address_space(3))) unsigned char *)lds);
     const float sc = 0.125f * 1.4426950408889634f;  // 1/sqrt(64) * log2(e)
-    float m[QT], lsum[QT];
-    f32x4 o[QT][4];
-#pragma unroll
-    for (int qt = 0; qt < QT; ++qt) {
-        m[qt] = -INFINITY;
-        lsum[qt] = 0.f;
-#pragma unroll
-        for (int dt = 0; dt < 4; ++dt) o[qt][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-    const float *kbase = qk + H + h * ATT_D;
-    const float *vbase = vt + (int64_t)(h * ATT_D) * ld_v + vt_base(doc, tok0);
 
-    for (int key0 = 0; key0 < n; key0 += 32) {
-        // A operands K (two 16-key tiles), lane (g, c): K[key0 + 16 t + c][32 ch + 8 g + e]
-        bf16x8 kh[2][2], kl[2][2];
+    // chunk ci -> stage buffer b: key rows 4 wave..+3 of K and of V, 16 B per lane,
+    // source slots permuted by the swizzle
+    const int sr = 4 * wave + (lane >> 4), sj = (lane & 15) ^ (sr & 15);
+    auto stage = [&](int ci, int b) {
+        const int row = tok0 + min(ci * AX_KC + sr, n - 1);
+        __builtin_amdgcn_global_load_lds((const void *)(kg + row * ld + sj * 8),
+                                         (lds_void *)(lds + b * AX_STAGE + wave * 1024), 16, 0,
+                                         0);
+        __builtin_amdgcn_global_load_lds((const void *)(vg + row * ld + sj * 8),
+                                         (lds_void *)(lds + b * AX_STAGE + AX_IMG + wave * 1024),
+                                         16, 0, 0);
+    };
+    // fragment addresses (buffer 0; buffer 1 is the immediate offset AX_STAGE)
+    uint32_t ka[2][2][2];  // [t][ch][hi, lo]: key row 8 (c >> 2) + 4 t + (c & 3)
 #pragma unroll
-        for (int t = 0; t < 2; ++t) {
-            const int krow = tok0 + min(key0 + 16 * t + c, n - 1);
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int ch = 0; ch < 2; ++ch)
+#pragma unroll
+            for (int pt = 0; pt < 2; ++pt) {
+                const int r = 8 * (c >> 2) + 4 * t + (c & 3), j = ch * 8 + pt * 4 + g;
+                ka[t][ch][pt] = lds_base + r * 256 + ((j ^ (r & 15)) << 4);
+            }
+    // [dt][hi, lo][h2]: ds_read_b64_tr_b16 roles -- lane 4 q + p of a 16-lane group
+    // addresses key row 8 g + 4 h2 + q, columns 16 dt + 4 p..+3 (one 8-byte half slot);
+    // lane i then holds column d = 16 dt + i for keys 8 g + 4 h2 + 0..3
+    uint32_t va[4][2][2];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+        for (int pt = 0; pt < 2; ++pt)
+#pragma unroll
+            for (int h2 = 0; h2 < 2; ++h2) {
+                const int q = c >> 2, pp = c & 3;
+                const int r = 8 * g + 4 * h2 + q;
+                const int j = (dt >> 1) * 8 + pt * 4 + 2 * (dt & 1) + (pp >> 1);
+                va[dt][pt][h2] = lds_base + AX_IMG + r * 256 + ((j ^ (r & 15)) << 4) + 8 * (pp & 1);
+            }
+
+    for (int q0 = 0; q0 < n; q0 += AX_WAVES * AX_QT * 16) {  // passes of 256 queries
+        const int q_base = q0 + wave * (AX_QT * 16);
+        const bool has_q = q_base < n;
+        // B operands Q^T, lane (g, c): Q[q_base + 16 qt + c][32 ch + 8 g + e] (hi; lo +32)
+        bf16x8 qh[AX_QT][2], ql[AX_QT][2];
+        const bf16 *qbase = qkv + split_col(h * ATT_D) + 8 * g;
+#pragma unroll
+        for (int qt = 0; qt < AX_QT; ++qt) {
+            const int qrow = tok0 + min(q_base + 16 * qt + c, n - 1);
 #pragma unroll
             for (int ch = 0; ch < 2; ++ch) {
-                const float *src = kbase + (int64_t)krow * ldqk + ch * 32 + 8 * g;
-                split8(*reinterpret_cast<const float4 *>(src),
-                       *reinterpret_cast<const float4 *>(src + 4), kh[t][ch], kl[t][ch]);
+                const bf16 *src = qbase + qrow * ld + ch * 64;
+                qh[qt][ch] = *reinterpret_cast<const bf16x8 *>(src);
+                ql[qt][ch] = *reinterpret_cast<const bf16x8 *>(src + 32);
             }
         }
-        // A operands V^T, lane (g, c) of d-tile dt: d = 16 dt + c, keys key0 + 4 g..+3
-        // then key0 + 16 + 4 g..+3 (the P^T k permutation, as the bf16 path)
-        bf16x8 vh[4], vl[4];
+        float m[AX_QT], lsum[AX_QT];
+        f32x4 o[AX_QT][4];
 #pragma unroll
-        for (int dt = 0; dt < 4; ++dt) {
-            const float *vrow = vbase + (int64_t)(dt * 16 + c) * ld_v + key0 + 4 * g;
-            split8(*reinterpret_cast<const float4 *>(vrow),
-                   *reinterpret_cast<const float4 *>(vrow + 16), vh[dt], vl[dt]);
+        for (int qt = 0; qt < AX_QT; ++qt) {
+            m[qt] = -INFINITY;
+            lsum[qt] = 0.f;
+#pragma unroll
+            for (int dt = 0; dt < 4; ++dt) o[qt][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
         }
+        stage(0, 0);
+        for (int ci = 0; ci < n_chunks; ++ci) {
+            const int b = ci & 1, key0 = ci * AX_KC;
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pieces of chunk ci
+            __syncthreads();  // every piece landed; buffer b ^ 1 no longer read
+            if (ci + 1 < n_chunks) stage(ci + 1, b ^ 1);
+            if (!has_q) continue;
+            uint4 kf[2][2][2];
+            uint2 vt2[4][2][2];
+            // one asm statement for the 24 reads and their wait (outputs exist only
+            // after it); the stage buffer is the immediate offset
+#define AX_READ(OFF)                                                                               \
+    asm volatile(                                                                                  \
+        "ds_read_b128 %0, %24 offset:" #OFF "\n\tds_read_b128 %1, %25 offset:" #OFF                \
+        "\n\tds_read_b128 %2, %26 offset:" #OFF "\n\tds_read_b128 %3, %27 offset:" #OFF            \
+        "\n\tds_read_b128 %4, %28 offset:" #OFF "\n\tds_read_b128 %5, %29 offset:" #OFF            \
+        "\n\tds_read_b128 %6, %30 offset:" #OFF "\n\tds_read_b128 %7, %31 offset:" #OFF            \
+        "\n\tds_read_b64_tr_b16 %8, %32 offset:" #OFF "\n\tds_read_b64_tr_b16 %9, %33 offset:" #OFF  \
+        "\n\tds_read_b64_tr_b16 %10, %34 offset:" #OFF "\n\tds_read_b64_tr_b16 %11, %35 offset:" #OFF \
+        "\n\tds_read_b64_tr_b16 %12, %36 offset:" #OFF "\n\tds_read_b64_tr_b16 %13, %37 offset:" #OFF \
+        "\n\tds_read_b64_tr_b16 %14, %38 offset:" #OFF "\n\tds_read_b64_tr_b16 %15, %39 offset:" #OFF \
+        "\n\tds_read_b64_tr_b16 %16, %40 offset:" #OFF "\n\tds_read_b64_tr_b16 %17, %41 offset:" #OFF \
+        "\n\tds_read_b64_tr_b16 %18, %42 offset:" #OFF "\n\tds_read_b64_tr_b16 %19, %43 offset:" #OFF \
+        "\n\tds_read_b64_tr_b16 %20, %44 offset:" #OFF "\n\tds_read_b64_tr_b16 %21, %45 offset:" #OFF \
+        "\n\tds_read_b64_tr_b16 %22, %46 offset:" #OFF "\n\tds_read_b64_tr_b16 %23, %47 offset:" #OFF \
+        "\n\ts_waitcnt lgkmcnt(0)"                                                                 \
+        : "=&v"(kf[0][0][0]), "=&v"(kf[0][0][1]), "=&v"(kf[0][1][0]), "=&v"(kf[0][1][1]),         \
+          "=&v"(kf[1][0][0]), "=&v"(kf[1][0][1]), "=&v"(kf[1][1][0]), "=&v"(kf[1][1][1]),         \
+          "=&v"(vt2[0][0][0]), "=&v"(vt2[0][0][1]), "=&v"(vt2[0][1][0]), "=&v"(vt2[0][1][1]),     \
+          "=&v"(vt2[1][0][0]), "=&v"(vt2[1][0][1]), "=&v"(vt2[1][1][0]), "=&v"(vt2[1][1][1]),     \
+          "=&v"(vt2[2][0][0]), "=&v"(vt2[2][0][1]), "=&v"(vt2[2][1][0]), "=&v"(vt2[2][1][1]),     \
+          "=&v"(vt2[3][0][0]), "=&v"(vt2[3][0][1]), "=&v"(vt2[3][1][0]), "=&v"(vt2[3][1][1])      \
+        : "v"(ka[0][0][0]), "v"(ka[0][0][1]), "v"(ka[0][1][0]), "v"(ka[0][1][1]),                 \
+          "v"(ka[1][0][0]), "v"(ka[1][0][1]), "v"(ka[1][1][0]), "v"(ka[1][1][1]),                 \
+          "v"(va[0][0][0]), "v"(va[0][0][1]), "v"(va[0][1][0]), "v"(va[0][1][1]),                 \
+          "v"(va[1][0][0]), "v"(va[1][0][1]), "v"(va[1][1][0]), "v"(va[1][1][1]),                 \
+          "v"(va[2][0][0]), "v"(va[2][0][1]), "v"(va[2][1][0]), "v"(va[2][1][1]),                 \
+          "v"(va[3][0][0]), "v"(va[3][0][1]), "v"(va[3][1][0]), "v"(va[3][1][1])                  \
+        : "memory")
+            static_assert(AX_STAGE == 16384, "AX_READ offsets");
+            if (b == 0)
+                AX_READ(0);
+            else
+                AX_READ(16384);
+#undef AX_READ
+            __builtin_amdgcn_sched_barrier(0);
+            bf16x8 kfr[2][2][2], vfr[4][2];  // [t][ch][hi, lo], [dt][hi, lo]
 #pragma unroll
-        for (int qt = 0; qt < QT; ++qt) {
-            f32x4 s[2];
-#pragma unroll
-            for (int t = 0; t < 2; ++t) {
-                s[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+            for (int t = 0; t < 2; ++t)
 #pragma unroll
                 for (int ch = 0; ch < 2; ++ch)
-                    s[t] = mma_x3(kh[t][ch], kl[t][ch], qh[qt][ch], ql[qt][ch], s[t]);
+#pragma unroll
+                    for (int pt = 0; pt < 2; ++pt) __builtin_memcpy(&kfr[t][ch][pt], &kf[t][ch][pt], 16);
+#pragma unroll
+            for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+                for (int pt = 0; pt < 2; ++pt) {
+                    const uint4 v4 = make_uint4(vt2[dt][pt][0].x, vt2[dt][pt][0].y,
+                                                vt2[dt][pt][1].x, vt2[dt][pt][1].y);
+                    __builtin_memcpy(&vfr[dt][pt], &v4, 16);
+                }
+            // S^T for both query tiles, each product stage over the 4 independent
+            // accumulators before the next (one accumulator's 3 products are a chain)
+            f32x4 s[AX_QT][2];
+#pragma unroll
+            for (int qt = 0; qt < AX_QT; ++qt)
+#pragma unroll
+                for (int t = 0; t < 2; ++t) s[qt][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int ch = 0; ch < 2; ++ch)
+#pragma unroll
+                for (int p = 0; p < 3; ++p)
+#pragma unroll
+                    for (int qt = 0; qt < AX_QT; ++qt)
+#pragma unroll
+                        for (int t = 0; t < 2; ++t)
+                            s[qt][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                                kfr[t][ch][p == 1], p == 2 ? ql[qt][ch] : qh[qt][ch], s[qt][t], 0,
+                                0, 0);
+            const bool full = key0 + AX_KC <= n;  // (uniform) no masked key in this chunk
+            bf16x8 ph[AX_QT], pl[AX_QT];
+#pragma unroll
+            for (int qt = 0; qt < AX_QT; ++qt) {
+                // lane holds S^T[key0 + 8 g + 4 t + r][q_base + 16 qt + c]
+                float cmax = -INFINITY;
+#pragma unroll
+                for (int t = 0; t < 2; ++t)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int key = key0 + 8 * g + 4 * t + r;
+                        const float v = (full || key < n) ? s[qt][t][r] * sc : -INFINITY;
+                        s[qt][t][r] = v;
+                        cmax = fmaxf(cmax, v);
+                    }
+                cmax = fmaxf(cmax, __shfl_xor(cmax, 16, 64));
+                cmax = fmaxf(cmax, __shfl_xor(cmax, 32, 64));
+                const float m_new = fmaxf(m[qt], cmax);
+                // rescale only when some running max moved (alpha == 1 exactly otherwise)
+                if (__any(m_new != m[qt])) {
+                    const float alpha = __builtin_amdgcn_exp2f(m[qt] - m_new);  // 0 at first
+                    lsum[qt] *= alpha;
+#pragma unroll
+                    for (int dt = 0; dt < 4; ++dt) o[qt][dt] *= alpha;
+                }
+                m[qt] = m_new;
+#pragma unroll
+                for (int t = 0; t < 2; ++t)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        // (raw v_exp_f32: no denormal-range rescale; p < 2^-126 is 0 here)
+                        const float pr = __builtin_amdgcn_exp2f(s[qt][t][r] - m_new);
+                        lsum[qt] += pr;
+                        ph[qt][4 * t + r] = split_hi(pr);
+                        pl[qt][4 * t + r] = split_lo(pr);
+                    }
             }
-            // lane holds S^T[key0 + 16 t + 4 g + r][q_base + 16 qt + c]
-            float cmax = -INFINITY;
 #pragma unroll
-            for (int t = 0; t < 2; ++t)
+            for (int p = 0; p < 3; ++p)
 #pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int key = key0 + 16 * t + 4 * g + r;
-                    const float v = (key < n) ? s[t][r] * sc : -INFINITY;
-                    s[t][r] = v;
-                    cmax = fmaxf(cmax, v);
-                }
-            cmax = fmaxf(cmax, __shfl_xor(cmax, 16, 64));
-            cmax = fmaxf(cmax, __shfl_xor(cmax, 32, 64));
-            const float m_new = fmaxf(m[qt], cmax);
-            const float alpha = exp2f(m[qt] - m_new);  // 0 on the first chunk
-            m[qt] = m_new;
-            lsum[qt] *= alpha;
+                for (int qt = 0; qt < AX_QT; ++qt)
 #pragma unroll
-            for (int dt = 0; dt < 4; ++dt) o[qt][dt] *= alpha;
-            bf16x8 ph, pl;
-#pragma unroll
-            for (int t = 0; t < 2; ++t)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const float p = exp2f(s[t][r] - m_new);
-                    lsum[qt] += p;
-                    ph[4 * t + r] = split_hi(p);
-                    pl[4 * t + r] = split_lo(p);
-                }
-#pragma unroll
-            for (int dt = 0; dt < 4; ++dt) o[qt][dt] = mma_x3(vh[dt], vl[dt], ph, pl, o[qt][dt]);
+                    for (int dt = 0; dt < 4; ++dt)
+                        o[qt][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                            vfr[dt][p == 1], p == 2 ? pl[qt] : ph[qt], o[qt][dt], 0, 0, 0);
         }
-    }
+        if (has_q) {
 #pragma unroll
-    for (int qt = 0; qt < QT; ++qt) {
-        float l = lsum[qt];
-        l += __shfl_xor(l, 16, 64);
-        l += __shfl_xor(l, 32, 64);
-        const float inv = 1.0f / l;
-        const int q = q_base + 16 * qt + c;
-        if (q < n) {
-            bf16 *out = ctx_split + (int64_t)(tok0 + q) * 2 * H;
+            for (int qt = 0; qt < AX_QT; ++qt) {
+                float l = lsum[qt];
+                l += __shfl_xor(l, 16, 64);
+                l += __shfl_xor(l, 32, 64);
+                const float inv = 1.0f / l;
+                const int q = q_base + 16 * qt + c;
+                if (q < n) {
+                    bf16 *out = ctx_split + (int64_t)(tok0 + q) * 2 * H;
 #pragma unroll
-            for (int dt = 0; dt < 4; ++dt) {
-                bf16x4 hv, lv;
+                    for (int dt = 0; dt < 4; ++dt) {
+                        bf16x4 hv, lv;
 #pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const float y = o[qt][dt][r] * inv;
-                    hv[r] = split_hi(y);
-                    lv[r] = split_lo(y);
+                        for (int r = 0; r < 4; ++r) {
+                            const float y = o[qt][dt][r] * inv;
+                            hv[r] = split_hi(y);
+                            lv[r] = split_lo(y);
+                        }
+                        const int64_t sc0 = split_col(h * ATT_D + dt * 16 + 4 * g);
+                        *reinterpret_cast<bf16x4 *>(out + sc0) = hv;
+                        *reinterpret_cast<bf16x4 *>(out + sc0 + 32) = lv;
+                    }
                 }
-                const int64_t sc0 = split_col(h * ATT_D + dt * 16 + 4 * g);
-                *reinterpret_cast<bf16x4 *>(out + sc0) = hv;
-                *reinterpret_cast<bf16x4 *>(out + sc0 + 32) = lv;
             }
         }
+        __syncthreads();  // the next pass restages buffer 0
     }
 }
 
-void launch_attention_x3(const float *qk, const float *vt, const int32_t *cu_seqlens, int n_docs,
-                         int max_len, int H, int ld_v, bf16 *ctx_split, hipStream_t s) {
+void launch_attention_x3(const bf16 *qkv, const int32_t *cu_seqlens, int n_docs, int H,
+                         bf16 *ctx_split, hipStream_t s) {
     DI_REQUIRE(H % ATT_D == 0, DI_EINVAL, "hidden %d is not a multiple of the head dim 64", H);
-    if (n_docs == 0 || max_len == 0) return;
-    const int n_heads = H / ATT_D, n_pairs = n_docs * n_heads;
-    const int n_qb = (max_len + 16 * QT - 1) / (16 * QT);
-    const int64_t blocks = (int64_t)((n_pairs + 7) / 8) * 8 * n_qb;
-    DI_REQUIRE(blocks < (1ll << 31), DI_ERANGE, "attention grid too large");
-    hipLaunchKernelGGL(attention_x3_kernel, dim3((unsigned)blocks), dim3(64), 0, s, qk, vt,
-                       cu_seqlens, H, ld_v, n_qb, n_heads, n_pairs, ctx_split);
+    if (n_docs == 0) return;
+    const int n_heads = H / ATT_D;
+    const int64_t n_pairs = (int64_t)n_docs * n_heads;
+    DI_REQUIRE(n_pairs < (1ll << 31), DI_ERANGE, "attention grid too large");
+    hipLaunchKernelGGL(attention_x3_kernel, dim3((unsigned)n_pairs), dim3(64 * AX_WAVES), AX_LDS,
+                       s, qkv, cu_seqlens, H, n_heads, ctx_split);
     check_launch("attention_x3");
 }
 
@@ -853,8 +959,8 @@ void launch_vt_cols(const int32_t *cu, int n_docs, int M, int32_t *vcol, hipStre
 }
 
 int vt_ld(int64_t M, int n_docs) {
-    // 8*(n_docs + M/8) + 32 keys of read-ahead (+ slack), rounded to 64 columns
-    int64_t need = 8 * ((int64_t)n_docs + M / 8) + 64 + 32;
+    // 32*(n_docs + M/32) + 32 keys of read-ahead (+ slack), rounded to 64 columns
+    int64_t need = 32 * ((int64_t)n_docs + M / 32) + 64 + 32;
     return (int)((need + 63) / 64 * 64);
 }
 

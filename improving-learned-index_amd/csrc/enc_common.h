@@ -145,7 +145,7 @@ struct GemmArgs {
     // 64-wide K tile holds the hi and lo halves of 32 k and each (A, B) fragment pair
     // gives three MFMAs, acc += A_hi B_hi + A_lo B_hi + A_hi B_lo, in f32.  Outputs:
     // EPI_BIAS / EPI_BIAS_GELU split rows (ld_out = 2N), EPI_BIAS_RESID f32 rows (resid
-    // split), EPI_QKV f32 Q | K rows and f32 V^T.
+    // split).  (The fp32-faithful QKV projection is EPI_BIAS into split rows [M][6H].)
     int split;
 };
 

@@ -357,7 +357,6 @@ __global__ void __launch_bounds__(G2_T) gemm256_kernel(GemmArgs g) {
         int m0e = m0;  // opaque: keeps the per-row epilogue offsets out of the K loop
         asm volatile("" : "+s"(m0e));
         const int row_l = m0e + wr * 128 + (lane & 15);
-        const int col_l = n0 + wc * 64 + (lane >> 4) * 8;
         // global addresses: a wave-uniform base (row m0 + wr*128, column n0 + wc*64) +
         // mt * (16 rows) in SGPRs, and one 32-bit lane offset (row lane&15, column
         // (lane>>4)*8) -- no 64-bit pointer per row held across the prefetch
@@ -557,8 +556,7 @@ __global__ void __launch_bounds__(G2_T) gemm256_kernel(GemmArgs g) {
         auto stores = [&](auto full_c) {
             constexpr bool FULL = decltype(full_c)::value;
             if (vtile) {  // V columns: transposed element stores into V^T
-                typedef typename std::conditional<SPLIT, float, bf16>::type VT;  // SPLIT: f32 V^T
-                char *vb = static_cast<char *>(g.out2) + (col_w - 2 * g.hidden) * g.ld_v * (int64_t)sizeof(VT);
+                char *vb = static_cast<char *>(g.out2) + (col_w - 2 * g.hidden) * g.ld_v * (int64_t)2;
 #pragma unroll
                 for (int mt = 0; mt < 8; ++mt) {
                     if (vc[mt] < 0) continue;
@@ -566,10 +564,9 @@ __global__ void __launch_bounds__(G2_T) gemm256_kernel(GemmArgs g) {
                     for (int h = 0; h < 2; ++h)
 #pragma unroll
                         for (int e = 0; e < 8; ++e)
-                            *reinterpret_cast<VT *>(
-                                vb + (uint32_t)((((lane >> 4) * 8 + h * 32 + e) * g.ld_v + vc[mt]) *
-                                                (int)sizeof(VT))) =
-                                (VT)(acc[mt][2 * h + (e >> 2)][e & 3] + bias_v[h][e]);
+                            *reinterpret_cast<bf16 *>(
+                                vb + (uint32_t)((((lane >> 4) * 8 + h * 32 + e) * g.ld_v + vc[mt]) * 2)) =
+                                (bf16)(acc[mt][2 * h + (e >> 2)][e & 3] + bias_v[h][e]);
                 }
             } else if constexpr (FOLD) {
                 // LN folded into this GEMM: y = r acc - r mu s + c  (per row r, mu; per
@@ -604,8 +601,8 @@ __global__ void __launch_bounds__(G2_T) gemm256_kernel(GemmArgs g) {
                 // (stored with the statistics, before the prefetch)
             } else {
                 // element size and column of the output rows: bf16 rows; SPLIT: f32 rows
-                // (Q | K, pre-LN) or split rows (ld_out = 2N, hi chunk then lo chunk)
-                constexpr bool F32 = SPLIT && (EPI == EPI_QKV || EPI == EPI_BIAS_RESID);
+                // (pre-LN) or split rows (ld_out = 2N: hi chunk then lo)
+                constexpr bool F32 = SPLIT && EPI == EPI_BIAS_RESID;
                 constexpr int ESZ = F32 ? 4 : 2;
                 constexpr int HSTEP = F32 ? 128 : (SPLIT ? 128 : 64);  // bytes per 32 columns
                 char *ob = static_cast<char *>(g.out) +
@@ -675,8 +672,7 @@ __global__ void __launch_bounds__(G2_T) gemm256_kernel(GemmArgs g) {
 // Shapes the 8-phase kernel takes; everything else goes to the 128x128 kernel.
 bool gemm256_ok(int epi, const GemmArgs &g) {
     const int64_t m_pad = ((int64_t)g.M + G2_TILE - 1) / G2_TILE * G2_TILE;
-    if (g.split && !(epi == EPI_BIAS || epi == EPI_BIAS_GELU || epi == EPI_BIAS_RESID ||
-                     epi == EPI_QKV))
+    if (g.split && !(epi == EPI_BIAS || epi == EPI_BIAS_GELU || epi == EPI_BIAS_RESID))
         return false;
     // (SPLIT: K tiles of 32 logical k, K % 64 == 0 keeps their count even)
     return g.N % G2_TILE == 0 && g.K % (g.split ? 64 : 128) == 0 && g.K >= 128 &&
@@ -709,7 +705,6 @@ void launch_gemm256(int epi, const GemmArgs &g, hipStream_t s) {
             G2_SCASE(EPI_BIAS)
             G2_SCASE(EPI_BIAS_GELU)
             G2_SCASE(EPI_BIAS_RESID)
-            G2_SCASE(EPI_QKV)
 #undef G2_SCASE
             default:
                 fail(DI_EINVAL, "bad split GEMM epilogue");

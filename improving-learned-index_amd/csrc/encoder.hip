@@ -31,8 +31,8 @@ void launch_attention(const T *qk, const T *vt, const int32_t *cu_seqlens, int n
                       int max_len, int H, int ld_v, T *ctx, hipStream_t s,
                       bf16 *ctx_split = nullptr);
 void launch_gemm256(int epi, const GemmArgs &g, hipStream_t s);
-void launch_attention_x3(const float *qk, const float *vt, const int32_t *cu_seqlens, int n_docs,
-                         int max_len, int H, int ld_v, bf16 *ctx_split, hipStream_t s);
+void launch_attention_x3(const bf16 *qkv, const int32_t *cu_seqlens, int n_docs, int H,
+                         bf16 *ctx_split, hipStream_t s);
 void launch_embed_ln_split(const int32_t *ids, const int32_t *cu, int n_docs, int M, int H,
                            const float *word, const float *pos, const float *type0,
                            const float *gamma, const float *beta, float eps, int pos_offset,
@@ -579,8 +579,8 @@ void forward_folded(di_encoder *e, const int32_t *d_ids, const int32_t *d_cu, in
 // forward<T> with every GEMM a split-bf16 256-tile GEMM (3 bf16 MFMA products per
 // fp32 product, f32 accumulate: ~2^-17 relative per product), attention with split
 // bf16 products too (attention_x3_kernel; f32 softmax), LayerNorms in f32 from f32
-// pre-LN rows.  Activations that feed a GEMM are
-// split rows [hi | lo]; Q | K and V^T are f32; the pre-LN rows are f32.
+// pre-LN rows.  Activations that feed a GEMM or the attention products are split
+// rows (Q | K and V^T included); the pre-LN rows are f32.
 void forward_split(di_encoder *e, const int32_t *d_ids, const int32_t *d_cu, int n_docs,
                    int64_t M, int max_len, bool timing, hipStream_t s) {
     const auto &c = e->cfg;
@@ -595,7 +595,6 @@ void forward_split(di_encoder *e, const int32_t *d_ids, const int32_t *d_cu, int
                               e->emb_b.as<float>(), c.layer_norm_eps, pos_offset, c.vocab_size,
                               c.max_positions, X, e->err.as<int32_t>(), s);
     }
-    launch_vt_cols(d_cu, n_docs, (int)M, e->vcol.as<int32_t>(), s);
     auto base = [&]() {
         GemmArgs g{};
         g.M = (int)M;
@@ -612,21 +611,17 @@ void forward_split(di_encoder *e, const int32_t *d_ids, const int32_t *d_cu, int
         g.A = X;
         g.B = L.w_qkv.p;
         g.bias = L.b_qkv.as<float>();
-        g.out = e->qk.p;  // f32 Q | K rows
-        g.out2 = e->vt.p; // f32 V^T
+        g.out = e->qk.p;  // split Q | K | V rows [M][6H]
         g.N = 3 * H;
         g.K = H;
-        g.ld_out = 2 * H;
-        g.ld_v = e->ld_v;
-        g.vcol = e->vcol.as<int32_t>();
+        g.ld_out = 6 * H;
         {
             TimedLaunch tl(e->timer, timing, "gemm_qkv", s);
-            launch_gemm256(EPI_QKV, g, s);
+            launch_gemm256(EPI_BIAS, g, s);
         }
         {
             TimedLaunch tl(e->timer, timing, "attention", s);
-            launch_attention_x3(e->qk.as<float>(), e->vt.as<float>(), d_cu, n_docs, max_len, H,
-                                e->ld_v, ctx, s);
+            launch_attention_x3(e->qk.as<bf16>(), d_cu, n_docs, H, ctx, s);
         }
         g = base();
         g.A = ctx;
