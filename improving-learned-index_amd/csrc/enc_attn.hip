@@ -255,8 +255,9 @@ attention_kernel(const T *__restrict__ qk, const T *__restrict__ vt,
 // probabilities; softmax and the row sums in f32.  Q | K | V arrive as split rows
 // [M][6H] from the QKV GEMM (split_col over the 3H logical columns): no V^T scatter.
 //
-// One 512-thread workgroup per (doc, head): the 8 waves own 32 queries each (two
-// 16-query tiles; documents past 256 tokens take a second pass), and the keys stream
+// One persistent 512-thread workgroup per CU walks the (doc, head) pairs; the 8 waves
+// own 32 queries each (two 16-query tiles; documents past 256 tokens take a second
+// pass), and the keys stream
 // through LDS in 32-key chunks, double-buffered: chunk i+1 is copied by LDS-DMA
 // (global_load_lds, every wave one 1 KiB piece of K and one of V) while chunk i is
 // computed, so every K / V byte is read from memory once per pass for the workgroup.
@@ -268,40 +269,84 @@ attention_kernel(const T *__restrict__ qk, const T *__restrict__ vt,
 // Fragment reads are inline-asm ds_reads with their lgkmcnt wait in the same statement
 // (the compiler would otherwise drain the in-flight prefetch with vmcnt(0) before an
 // LDS read it cannot tell apart from the DMA's destination).
-constexpr int AX_WAVES = 8, AX_QT = 2, AX_KC = 32;
+constexpr int AX_WAVES = 8, AX_QT = 2, AX_KC = 64;  // keys per staged chunk (2 x 32)
 constexpr int AX_IMG = AX_KC * 256, AX_STAGE = 2 * AX_IMG;
 constexpr int AX_LDS = 2 * AX_STAGE;
 
 __global__ void __launch_bounds__(64 * AX_WAVES)
 attention_x3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu_seqlens, int H,
-                    int n_heads, bf16 *__restrict__ ctx_split) {
+                    int n_heads, int n_pairs, bf16 *__restrict__ ctx_split) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     typedef __attribute__((address_space(3))) void lds_void;
-    const int pair = blockIdx.x, doc = pair / n_heads, h = pair % n_heads;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int g = lane >> 4, c = lane & 15;
-    const int tok0 = cu_seqlens[doc], n = cu_seqlens[doc + 1] - tok0;
-    if (n <= 0) return;
     const int64_t ld = 6 * (int64_t)H;  // split row: 3H logical columns
-    const bf16 *kg = qkv + split_col(H + h * ATT_D);      // + key row * ld: 256 B
-    const bf16 *vg = qkv + split_col(2 * H + h * ATT_D);
-    const int n_chunks = (n + AX_KC - 1) / AX_KC;
     const uint32_t lds_base =
         (uint32_t)(uintptr_t)((__attribute__((address_space(3))) unsigned char *)lds);
     const float sc = 0.125f * 1.4426950408889634f;  // 1/sqrt(64) * log2(e)
+    constexpr int PASS_Q = AX_WAVES * AX_QT * 16;   // queries per pass (256)
 
-    // chunk ci -> stage buffer b: key rows 4 wave..+3 of K and of V, 16 B per lane,
-    // source slots permuted by the swizzle
-    const int sr = 4 * wave + (lane >> 4), sj = (lane & 15) ^ (sr & 15);
-    auto stage = [&](int ci, int b) {
-        const int row = tok0 + min(ci * AX_KC + sr, n - 1);
-        __builtin_amdgcn_global_load_lds((const void *)(kg + row * ld + sj * 8),
-                                         (lds_void *)(lds + b * AX_STAGE + wave * 1024), 16, 0,
-                                         0);
-        __builtin_amdgcn_global_load_lds((const void *)(vg + row * ld + sj * 8),
-                                         (lds_void *)(lds + b * AX_STAGE + AX_IMG + wave * 1024),
-                                         16, 0, 0);
+    // Work units: (pair, pass), pairs blockIdx.x, + gridDim.x, ... (persistent); the
+    // next unit's Q and first K / V chunk load while the current unit's last chunk
+    // computes.
+    struct Unit {
+        int pair, pass, tok0, n, h;
+    };
+    auto make_unit = [&](int pr, int pass, Unit &u) {
+        const int doc = pr / n_heads;
+        u.pair = pr;
+        u.pass = pass;
+        u.h = pr % n_heads;
+        u.tok0 = cu_seqlens[doc];
+        u.n = cu_seqlens[doc + 1] - u.tok0;
+    };
+    // the unit after `u` with at least one token, or false
+    auto next_unit = [&](const Unit &u, Unit &nu) {
+        if ((u.pass + 1) * PASS_Q < u.n) {
+            nu = u;
+            nu.pass = u.pass + 1;
+            return true;
+        }
+        for (int pr = u.pair + (int)gridDim.x; pr < n_pairs; pr += (int)gridDim.x) {
+            make_unit(pr, 0, nu);
+            if (nu.n > 0) return true;
+        }
+        return false;
+    };
+    // chunk ci of unit u -> stage buffer b: key rows 8 wave..+7 of K and of V (two
+    // 1 KiB pieces each), 16 B per lane, source slots permuted by the swizzle
+    const int sr = 8 * wave + (lane >> 4);
+    auto stage = [&](const Unit &u, int ci, int b) {
+        const bf16 *kg = qkv + split_col(H + u.h * ATT_D);      // + key row * ld: 256 B
+        const bf16 *vg = qkv + split_col(2 * H + u.h * ATT_D);
+#pragma unroll
+        for (int pc = 0; pc < 2; ++pc) {
+            const int row = u.tok0 + min(ci * AX_KC + sr + 4 * pc, u.n - 1);
+            const int j = (lane & 15) ^ ((sr + 4 * pc) & 15);
+            __builtin_amdgcn_global_load_lds(
+                (const void *)(kg + row * ld + j * 8),
+                (lds_void *)(lds + b * AX_STAGE + wave * 2048 + pc * 1024), 16, 0, 0);
+            __builtin_amdgcn_global_load_lds(
+                (const void *)(vg + row * ld + j * 8),
+                (lds_void *)(lds + b * AX_STAGE + AX_IMG + wave * 2048 + pc * 1024), 16, 0, 0);
+        }
+    };
+    // B operands Q^T of unit u, lane (g, c): Q[q_base + 16 qt + c][32 ch + 8 g + e]
+    // (hi; lo 32 later)
+    auto load_q = [&](const Unit &u, bf16x8 (&qh)[AX_QT][2], bf16x8 (&ql)[AX_QT][2]) {
+        const int q_base = u.pass * PASS_Q + wave * (AX_QT * 16);
+        const bf16 *qbase = qkv + split_col(u.h * ATT_D) + 8 * g;
+#pragma unroll
+        for (int qt = 0; qt < AX_QT; ++qt) {
+            const int qrow = u.tok0 + min(q_base + 16 * qt + c, u.n - 1);
+#pragma unroll
+            for (int ch = 0; ch < 2; ++ch) {
+                const bf16 *src = qbase + qrow * ld + ch * 64;
+                qh[qt][ch] = *reinterpret_cast<const bf16x8 *>(src);
+                ql[qt][ch] = *reinterpret_cast<const bf16x8 *>(src + 32);
+            }
+        }
     };
     // fragment addresses (buffer 0; buffer 1 is the immediate offset AX_STAGE)
     uint32_t ka[2][2][2];  // [t][ch][hi, lo]: key row 8 (c >> 2) + 4 t + (c & 3)
@@ -330,22 +375,26 @@ attention_x3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
                 va[dt][pt][h2] = lds_base + AX_IMG + r * 256 + ((j ^ (r & 15)) << 4) + 8 * (pp & 1);
             }
 
-    for (int q0 = 0; q0 < n; q0 += AX_WAVES * AX_QT * 16) {  // passes of 256 queries
-        const int q_base = q0 + wave * (AX_QT * 16);
-        const bool has_q = q_base < n;
-        // B operands Q^T, lane (g, c): Q[q_base + 16 qt + c][32 ch + 8 g + e] (hi; lo +32)
-        bf16x8 qh[AX_QT][2], ql[AX_QT][2];
-        const bf16 *qbase = qkv + split_col(h * ATT_D) + 8 * g;
-#pragma unroll
-        for (int qt = 0; qt < AX_QT; ++qt) {
-            const int qrow = tok0 + min(q_base + 16 * qt + c, n - 1);
-#pragma unroll
-            for (int ch = 0; ch < 2; ++ch) {
-                const bf16 *src = qbase + qrow * ld + ch * 64;
-                qh[qt][ch] = *reinterpret_cast<const bf16x8 *>(src);
-                ql[qt][ch] = *reinterpret_cast<const bf16x8 *>(src + 32);
-            }
+    Unit cu;
+    {
+        int pr = blockIdx.x;
+        for (; pr < n_pairs; pr += (int)gridDim.x) {
+            make_unit(pr, 0, cu);
+            if (cu.n > 0) break;
         }
+        if (pr >= n_pairs) return;
+    }
+    bf16x8 qh[AX_QT][2], ql[AX_QT][2], qnh[AX_QT][2], qnl[AX_QT][2];
+    load_q(cu, qh, ql);
+    stage(cu, 0, 0);
+    int b = 0;  // stage buffer of the next chunk to compute
+    for (;;) {
+        const int n = cu.n, tok0 = cu.tok0, h = cu.h;
+        const int q_base = cu.pass * PASS_Q + wave * (AX_QT * 16);
+        const bool has_q = q_base < n;
+        const int n_chunks = (n + AX_KC - 1) / AX_KC;
+        Unit nu;
+        const bool more = next_unit(cu, nu);
         float m[AX_QT], lsum[AX_QT];
         f32x4 o[AX_QT][4];
 #pragma unroll
@@ -355,67 +404,79 @@ attention_x3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
 #pragma unroll
             for (int dt = 0; dt < 4; ++dt) o[qt][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
         }
-        stage(0, 0);
-        for (int ci = 0; ci < n_chunks; ++ci) {
-            const int b = ci & 1, key0 = ci * AX_KC;
+        for (int ci = 0; ci < n_chunks; ++ci, b ^= 1) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pieces of chunk ci
             __syncthreads();  // every piece landed; buffer b ^ 1 no longer read
-            if (ci + 1 < n_chunks) stage(ci + 1, b ^ 1);
+            if (ci + 1 < n_chunks) {
+                stage(cu, ci + 1, b ^ 1);
+            } else if (more) {  // the next unit's first chunk and Q
+                stage(nu, 0, b ^ 1);
+                load_q(nu, qnh, qnl);
+            }
             if (!has_q) continue;
+#pragma unroll
+            for (int u = 0; u < AX_KC / 32; ++u) {  // 32-key sub-chunks
+            const int key0 = ci * AX_KC + 32 * u;
+            if (key0 >= n) break;
             uint4 kf[2][2][2];
             uint2 vt2[4][2][2];
-            // one asm statement for the 24 reads and their wait (outputs exist only
-            // after it); the stage buffer is the immediate offset
-#define AX_READ(OFF)                                                                               \
+            // K fragments: one asm statement for the 8 reads and their wait (outputs
+            // exist only after it); V^T fragments: issued here, waited for after the
+            // softmax (their latency hides behind it), the wait naming every one of
+            // them ("+v") so that nothing reads them earlier.  The stage buffer and the
+            // sub-chunk are the immediate offset.
+#define AX_READ_K(OFF)                                                                             \
+    asm volatile("ds_read_b128 %0, %8 offset:" #OFF "\n\tds_read_b128 %1, %9 offset:" #OFF         \
+                 "\n\tds_read_b128 %2, %10 offset:" #OFF "\n\tds_read_b128 %3, %11 offset:" #OFF   \
+                 "\n\tds_read_b128 %4, %12 offset:" #OFF "\n\tds_read_b128 %5, %13 offset:" #OFF   \
+                 "\n\tds_read_b128 %6, %14 offset:" #OFF "\n\tds_read_b128 %7, %15 offset:" #OFF   \
+                 "\n\ts_waitcnt lgkmcnt(0)"                                                        \
+                 : "=&v"(kf[0][0][0]), "=&v"(kf[0][0][1]), "=&v"(kf[0][1][0]), "=&v"(kf[0][1][1]), \
+                   "=&v"(kf[1][0][0]), "=&v"(kf[1][0][1]), "=&v"(kf[1][1][0]), "=&v"(kf[1][1][1])  \
+                 : "v"(ka[0][0][0]), "v"(ka[0][0][1]), "v"(ka[0][1][0]), "v"(ka[0][1][1]),         \
+                   "v"(ka[1][0][0]), "v"(ka[1][0][1]), "v"(ka[1][1][0]), "v"(ka[1][1][1])          \
+                 : "memory")
+#define AX_READ_V(OFF)                                                                             \
     asm volatile(                                                                                  \
-        "ds_read_b128 %0, %24 offset:" #OFF "\n\tds_read_b128 %1, %25 offset:" #OFF                \
-        "\n\tds_read_b128 %2, %26 offset:" #OFF "\n\tds_read_b128 %3, %27 offset:" #OFF            \
-        "\n\tds_read_b128 %4, %28 offset:" #OFF "\n\tds_read_b128 %5, %29 offset:" #OFF            \
-        "\n\tds_read_b128 %6, %30 offset:" #OFF "\n\tds_read_b128 %7, %31 offset:" #OFF            \
-        "\n\tds_read_b64_tr_b16 %8, %32 offset:" #OFF "\n\tds_read_b64_tr_b16 %9, %33 offset:" #OFF  \
-        "\n\tds_read_b64_tr_b16 %10, %34 offset:" #OFF "\n\tds_read_b64_tr_b16 %11, %35 offset:" #OFF \
-        "\n\tds_read_b64_tr_b16 %12, %36 offset:" #OFF "\n\tds_read_b64_tr_b16 %13, %37 offset:" #OFF \
-        "\n\tds_read_b64_tr_b16 %14, %38 offset:" #OFF "\n\tds_read_b64_tr_b16 %15, %39 offset:" #OFF \
-        "\n\tds_read_b64_tr_b16 %16, %40 offset:" #OFF "\n\tds_read_b64_tr_b16 %17, %41 offset:" #OFF \
-        "\n\tds_read_b64_tr_b16 %18, %42 offset:" #OFF "\n\tds_read_b64_tr_b16 %19, %43 offset:" #OFF \
-        "\n\tds_read_b64_tr_b16 %20, %44 offset:" #OFF "\n\tds_read_b64_tr_b16 %21, %45 offset:" #OFF \
-        "\n\tds_read_b64_tr_b16 %22, %46 offset:" #OFF "\n\tds_read_b64_tr_b16 %23, %47 offset:" #OFF \
-        "\n\ts_waitcnt lgkmcnt(0)"                                                                 \
-        : "=&v"(kf[0][0][0]), "=&v"(kf[0][0][1]), "=&v"(kf[0][1][0]), "=&v"(kf[0][1][1]),         \
-          "=&v"(kf[1][0][0]), "=&v"(kf[1][0][1]), "=&v"(kf[1][1][0]), "=&v"(kf[1][1][1]),         \
-          "=&v"(vt2[0][0][0]), "=&v"(vt2[0][0][1]), "=&v"(vt2[0][1][0]), "=&v"(vt2[0][1][1]),     \
+        "ds_read_b64_tr_b16 %0, %16 offset:" #OFF "\n\tds_read_b64_tr_b16 %1, %17 offset:" #OFF    \
+        "\n\tds_read_b64_tr_b16 %2, %18 offset:" #OFF "\n\tds_read_b64_tr_b16 %3, %19 offset:" #OFF \
+        "\n\tds_read_b64_tr_b16 %4, %20 offset:" #OFF "\n\tds_read_b64_tr_b16 %5, %21 offset:" #OFF \
+        "\n\tds_read_b64_tr_b16 %6, %22 offset:" #OFF "\n\tds_read_b64_tr_b16 %7, %23 offset:" #OFF \
+        "\n\tds_read_b64_tr_b16 %8, %24 offset:" #OFF "\n\tds_read_b64_tr_b16 %9, %25 offset:" #OFF \
+        "\n\tds_read_b64_tr_b16 %10, %26 offset:" #OFF "\n\tds_read_b64_tr_b16 %11, %27 offset:" #OFF \
+        "\n\tds_read_b64_tr_b16 %12, %28 offset:" #OFF "\n\tds_read_b64_tr_b16 %13, %29 offset:" #OFF \
+        "\n\tds_read_b64_tr_b16 %14, %30 offset:" #OFF "\n\tds_read_b64_tr_b16 %15, %31 offset:" #OFF \
+        : "=&v"(vt2[0][0][0]), "=&v"(vt2[0][0][1]), "=&v"(vt2[0][1][0]), "=&v"(vt2[0][1][1]),     \
           "=&v"(vt2[1][0][0]), "=&v"(vt2[1][0][1]), "=&v"(vt2[1][1][0]), "=&v"(vt2[1][1][1]),     \
           "=&v"(vt2[2][0][0]), "=&v"(vt2[2][0][1]), "=&v"(vt2[2][1][0]), "=&v"(vt2[2][1][1]),     \
           "=&v"(vt2[3][0][0]), "=&v"(vt2[3][0][1]), "=&v"(vt2[3][1][0]), "=&v"(vt2[3][1][1])      \
-        : "v"(ka[0][0][0]), "v"(ka[0][0][1]), "v"(ka[0][1][0]), "v"(ka[0][1][1]),                 \
-          "v"(ka[1][0][0]), "v"(ka[1][0][1]), "v"(ka[1][1][0]), "v"(ka[1][1][1]),                 \
-          "v"(va[0][0][0]), "v"(va[0][0][1]), "v"(va[0][1][0]), "v"(va[0][1][1]),                 \
+        : "v"(va[0][0][0]), "v"(va[0][0][1]), "v"(va[0][1][0]), "v"(va[0][1][1]),                 \
           "v"(va[1][0][0]), "v"(va[1][0][1]), "v"(va[1][1][0]), "v"(va[1][1][1]),                 \
           "v"(va[2][0][0]), "v"(va[2][0][1]), "v"(va[2][1][0]), "v"(va[2][1][1]),                 \
           "v"(va[3][0][0]), "v"(va[3][0][1]), "v"(va[3][1][0]), "v"(va[3][1][1])                  \
         : "memory")
-            static_assert(AX_STAGE == 16384, "AX_READ offsets");
-            if (b == 0)
-                AX_READ(0);
-            else
-                AX_READ(16384);
-#undef AX_READ
+#define AX_SEL(M)                                                                                  \
+    do {                                                                                           \
+        if (b == 0 && u == 0)                                                                      \
+            M(0);                                                                                  \
+        else if (b == 0)                                                                           \
+            M(8192);                                                                               \
+        else if (u == 0)                                                                           \
+            M(32768);                                                                              \
+        else                                                                                       \
+            M(40960);                                                                              \
+    } while (0)
+            // (immediate offset: buffer b at b * AX_STAGE, sub-chunk u at u * 32 rows)
+            static_assert(AX_STAGE == 32768 && AX_KC == 64, "AX_READ offsets");
+            AX_SEL(AX_READ_K);
             __builtin_amdgcn_sched_barrier(0);
-            bf16x8 kfr[2][2][2], vfr[4][2];  // [t][ch][hi, lo], [dt][hi, lo]
+            bf16x8 kfr[2][2][2];  // [t][ch][hi, lo]
 #pragma unroll
             for (int t = 0; t < 2; ++t)
 #pragma unroll
                 for (int ch = 0; ch < 2; ++ch)
 #pragma unroll
                     for (int pt = 0; pt < 2; ++pt) __builtin_memcpy(&kfr[t][ch][pt], &kf[t][ch][pt], 16);
-#pragma unroll
-            for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-                for (int pt = 0; pt < 2; ++pt) {
-                    const uint4 v4 = make_uint4(vt2[dt][pt][0].x, vt2[dt][pt][0].y,
-                                                vt2[dt][pt][1].x, vt2[dt][pt][1].y);
-                    __builtin_memcpy(&vfr[dt][pt], &v4, 16);
-                }
             // S^T for both query tiles, each product stage over the 4 independent
             // accumulators before the next (one accumulator's 3 products are a chain)
             f32x4 s[AX_QT][2];
@@ -434,7 +495,10 @@ attention_x3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
                             s[qt][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
                                 kfr[t][ch][p == 1], p == 2 ? ql[qt][ch] : qh[qt][ch], s[qt][t], 0,
                                 0, 0);
-            const bool full = key0 + AX_KC <= n;  // (uniform) no masked key in this chunk
+            __builtin_amdgcn_sched_barrier(0);
+            AX_SEL(AX_READ_V);
+            __builtin_amdgcn_sched_barrier(0);
+            const bool full = key0 + 32 <= n;  // (uniform) no masked key in this sub-chunk
             bf16x8 ph[AX_QT], pl[AX_QT];
 #pragma unroll
             for (int qt = 0; qt < AX_QT; ++qt) {
@@ -449,8 +513,14 @@ attention_x3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
                         s[qt][t][r] = v;
                         cmax = fmaxf(cmax, v);
                     }
-                cmax = fmaxf(cmax, __shfl_xor(cmax, 16, 64));
-                cmax = fmaxf(cmax, __shfl_xor(cmax, 32, 64));
+                {  // max over the 4 lane groups (lanes l, l^16, l^32, l^48): permlane swaps
+                    const auto p16 = __builtin_amdgcn_permlane16_swap(
+                        __float_as_uint(cmax), __float_as_uint(cmax), false, false);
+                    cmax = fmaxf(__uint_as_float(p16[0]), __uint_as_float(p16[1]));
+                    const auto p32 = __builtin_amdgcn_permlane32_swap(
+                        __float_as_uint(cmax), __float_as_uint(cmax), false, false);
+                    cmax = fmaxf(__uint_as_float(p32[0]), __uint_as_float(p32[1]));
+                }
                 const float m_new = fmaxf(m[qt], cmax);
                 // rescale only when some running max moved (alpha == 1 exactly otherwise)
                 if (__any(m_new != m[qt])) {
@@ -471,6 +541,25 @@ attention_x3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
                         pl[qt][4 * t + r] = split_lo(pr);
                     }
             }
+            asm volatile("s_waitcnt lgkmcnt(0)"
+                         : "+v"(vt2[0][0][0]), "+v"(vt2[0][0][1]), "+v"(vt2[0][1][0]),
+                           "+v"(vt2[0][1][1]), "+v"(vt2[1][0][0]), "+v"(vt2[1][0][1]),
+                           "+v"(vt2[1][1][0]), "+v"(vt2[1][1][1]), "+v"(vt2[2][0][0]),
+                           "+v"(vt2[2][0][1]), "+v"(vt2[2][1][0]), "+v"(vt2[2][1][1]),
+                           "+v"(vt2[3][0][0]), "+v"(vt2[3][0][1]), "+v"(vt2[3][1][0]),
+                           "+v"(vt2[3][1][1])
+                         :
+                         : "memory");
+            __builtin_amdgcn_sched_barrier(0);
+            bf16x8 vfr[4][2];  // [dt][hi, lo]
+#pragma unroll
+            for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+                for (int pt = 0; pt < 2; ++pt) {
+                    const uint4 v4 = make_uint4(vt2[dt][pt][0].x, vt2[dt][pt][0].y,
+                                                vt2[dt][pt][1].x, vt2[dt][pt][1].y);
+                    __builtin_memcpy(&vfr[dt][pt], &v4, 16);
+                }
 #pragma unroll
             for (int p = 0; p < 3; ++p)
 #pragma unroll
@@ -479,6 +568,7 @@ attention_x3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
                     for (int dt = 0; dt < 4; ++dt)
                         o[qt][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
                             vfr[dt][p == 1], p == 2 ? pl[qt] : ph[qt], o[qt][dt], 0, 0, 0);
+            }
         }
         if (has_q) {
 #pragma unroll
@@ -506,8 +596,19 @@ attention_x3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
                 }
             }
         }
-        __syncthreads();  // the next pass restages buffer 0
+        if (!more) break;
+        cu = nu;
+#pragma unroll
+        for (int qt = 0; qt < AX_QT; ++qt)
+#pragma unroll
+            for (int ch = 0; ch < 2; ++ch) {
+                qh[qt][ch] = qnh[qt][ch];
+                ql[qt][ch] = qnl[qt][ch];
+            }
     }
+#undef AX_READ_K
+#undef AX_READ_V
+#undef AX_SEL
 }
 
 void launch_attention_x3(const bf16 *qkv, const int32_t *cu_seqlens, int n_docs, int H,
@@ -517,8 +618,9 @@ void launch_attention_x3(const bf16 *qkv, const int32_t *cu_seqlens, int n_docs,
     const int n_heads = H / ATT_D;
     const int64_t n_pairs = (int64_t)n_docs * n_heads;
     DI_REQUIRE(n_pairs < (1ll << 31), DI_ERANGE, "attention grid too large");
-    hipLaunchKernelGGL(attention_x3_kernel, dim3((unsigned)n_pairs), dim3(64 * AX_WAVES), AX_LDS,
-                       s, qkv, cu_seqlens, H, n_heads, ctx_split);
+    const int grid = (int)std::min<int64_t>(n_pairs, n_cu());  // persistent, one per CU
+    hipLaunchKernelGGL(attention_x3_kernel, dim3(grid), dim3(64 * AX_WAVES), AX_LDS, s, qkv,
+                       cu_seqlens, H, n_heads, (int)n_pairs, ctx_split);
     check_launch("attention_x3");
 }
 
