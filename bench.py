@@ -431,6 +431,66 @@ def cpu_baseline_retrieve(args, term_off, pdoc, pval, queries, out_doc, out_scor
                       f"(OpenMP over queries), {el:.1f}s"}
 
 
+def index_e2e_leg(args, dev):
+    """A1-A9 end to end through the drop-in CLI's own code path (index.py: collection
+    file -> CollectionParser -> TokenizerPool workers -> HIP encoder -> native TSV
+    writer), bf16x3 (the CLI default, fp32-faithful).  The collection is synthetic
+    MS MARCO-shaped text over the repo's local XLM-R-style tokenizer vocabulary
+    (tests/golden/tokenizer.json: the hub tokenizer does not exist offline), word counts
+    clip(N(150, 45), 6, 230); the checkpoint is random-init xlm-roberta-base.  Setup
+    (checkpoint load, weight upload, worker start) is timed apart from the indexing."""
+    import tempfile
+
+    from improving_learned_index_amd import index as index_cli
+    from improving_learned_index_amd.encoder import EncoderConfig
+    from improving_learned_index_amd.indexer import Indexer, TokenizerPool, resolve_tokenizer
+    from improving_learned_index_amd.models import DeepImpact
+
+    tok_path = ROOT / "tests" / "golden" / "tokenizer.json"
+    vocab = json.loads(tok_path.read_text())["model"]["vocab"]
+    words = np.array([w[1:] for w, _ in vocab if w.startswith("\u2581") and len(w) > 2])
+    rng = np.random.default_rng(7)
+    n_docs = args.e2e_docs
+    lens = np.clip(rng.normal(150, 45, n_docs), 6, 230).astype(int)
+    procs = max(1, min(args.e2e_procs, os.cpu_count() or 1))
+    with tempfile.TemporaryDirectory(dir="/tmp") as td:
+        td = Path(td)
+        coll = td / "collection.tsv"
+        with open(coll, "w") as f:
+            for i, n in enumerate(lens):
+                f.write(f"{i}\t{' '.join(words[rng.integers(0, len(words), n)])}\n")
+        cfg = EncoderConfig.xlmr_base()
+        ckpt = td / "DeepImpact.pt"
+        torch.save({"model_state_dict": synthetic_state_dict(cfg, seed=0)}, ckpt)
+        t0 = time.perf_counter()
+        tok = resolve_tokenizer(str(ckpt), tok_path)
+        pool = TokenizerPool(procs, tok, 300, "word_ids")
+        try:
+            model = DeepImpact.load(str(ckpt), tokenizer_path=tok_path, precision="bf16x3",
+                                    device=dev, max_length=300)
+            indexer = Indexer(model, model_batch_size=index_cli.BATCH_SIZE, num_processes=procs,
+                              pool=pool)
+            with open(os.devnull, "w") as dn:  # warm the workers (imports, tokenizer)
+                with open(coll) as f:
+                    indexer.index([next(f).split("\t", 1)[1] for _ in range(4 * procs)], dn)
+            t_setup = time.perf_counter() - t0
+            t1 = time.perf_counter()
+            n = index_cli._index_file(indexer, coll, "msmarco", td / "collection.index",
+                                      50 * index_cli.BATCH_SIZE, None, t1)
+            el = time.perf_counter() - t1
+            out_bytes = (td / "collection.index").stat().st_size
+        finally:
+            pool.close()
+    log(f"index e2e: {n} docs in {el:.2f}s after {t_setup:.1f}s setup ({procs} tokenizer "
+        f"workers)")
+    return {"value": round(n / el, 1), "unit": "docs/s", "docs": int(n), "seconds": round(el, 3),
+            "setup_seconds": round(t_setup, 2), "tokenizer_workers": procs,
+            "precision": "bf16x3", "output_bytes": int(out_bytes),
+            "path": "index.py _index_file: CollectionParser -> TokenizerPool -> di_encode "
+                    "(bf16x3, ROUND3) -> di_format_impact_lines, reference defaults "
+                    "(process batch 1600, model batch 32 -> 256-doc device chunks)"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -442,10 +502,13 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--docs", type=int, default=8192, help="docs encoded per step per GPU (1024: -3%%, 4096: -1%%: the 256-row GEMM tiles quantize less on 256 CUs with more rows)")
     ap.add_argument("--max-len", type=int, default=300)
-    ap.add_argument("--legs", default="encode,encode_x3,retrieve,retrieve_shard",
+    ap.add_argument("--e2e-docs", type=int, default=16000, help="index_e2e leg: documents")
+    ap.add_argument("--e2e-procs", type=int, default=16, help="index_e2e leg: tokenizer workers")
+    ap.add_argument("--legs", default="encode,encode_x3,retrieve,retrieve_shard,index_e2e",
                     help="encode (bf16, configs[1]), encode_x3 (fp32-faithful bf16x3), retrieve "
                          "(100k-doc shard, configs[1]), retrieve_shard (1.1M docs: one 8-way shard "
-                         "of configs[2]), retrieve_full (8.8M docs on one GPU, configs[2])")
+                         "of configs[2]), retrieve_full (8.8M docs on one GPU, configs[2]), "
+                         "index_e2e (index.py's path end to end, tokenizer workers included)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -472,23 +535,24 @@ def main():
         x3_res, _ = encode_leg(args, rank, world, dev, precision="bf16x3")
     if "retrieve" in legs:
         ret_res, ret_ctx = retrieve_leg(args, rank, world, dev)
+    e2e_res = index_e2e_leg(args, dev) if "index_e2e" in legs and world == 1 else None
     big = {}
     for leg, nd in (("retrieve_shard", 1_100_000), ("retrieve_full", 8_800_000)):
         if leg in legs:
             big[leg], _ = retrieve_leg(args, rank, world, dev, n_docs=nd, check_queries=20)
             torch.cuda.empty_cache()
-    primary = next((r for r in (enc_res, x3_res, ret_res) + tuple(big.values())
+    primary = next((r for r in (enc_res, x3_res, ret_res) + tuple(big.values()) + (e2e_res,)
                     if r is not None), None)
     if primary is None:
         raise SystemExit("no bench leg selected")
     out = {
         "metric": "docs/sec encoded + queries/sec@top-1000, MS MARCO passage, 1/2/4/8 MI355X",
         "value": round(primary["value"], 2),
-        "unit": "docs/s" if primary is enc_res or primary is x3_res else "queries/s",
+        "unit": "docs/s" if primary in (enc_res, x3_res, e2e_res) else "queries/s",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": round(primary["ms_per_step"], 4),
+        "ms_per_step": round(primary.get("ms_per_step") or 1e3 * primary.get("seconds", 0), 4),
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
@@ -506,7 +570,7 @@ def main():
                                     "computes only the rows the gather reads -- bit-identical "
                                     "impacts, DESIGN.md §3" if prune_last_layer() else
                                     "term impacts (A8/A9 gather + round3), every row computed"},
-        "roofline": primary["roofline"],
+        "roofline": primary.get("roofline"),
         "cpu_baseline": None,
     }
     if enc_res is not None:
@@ -527,6 +591,8 @@ def main():
                            "postings_per_query": round(ret_res["postings_per_query"], 1),
                            "kernel_ms": ret_res["kernel_ms"], "roofline": ret_res["roofline"],
                            "cpu_baseline": None}
+    if e2e_res is not None:
+        out["index_e2e"] = e2e_res
     for leg, r in big.items():
         out[leg] = {"value": round(r["value"], 2), "unit": "queries/s",
                     "docs_per_shard": r["docs"], "postings": r["postings"], "blocks": r["blocks"],

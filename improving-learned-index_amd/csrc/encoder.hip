@@ -262,8 +262,10 @@ void ensure_workspace(di_encoder *e, int64_t M, int n_docs, int64_t n_terms) {
         e->pre.reserve(cap * H * es);
         e->impact.reserve(cap * 4);
         e->ids.reserve(cap * 4);
-        e->vcol.reserve(cap * 4);
-        const size_t vt_bytes = (size_t)H * vt_ld(cap, capd) * es;
+        // V^T (doc-aligned) for the generic attention kernels; the split (bf16x3)
+        // attention reads V rows, the bf16 v3 attention too
+        const size_t vt_bytes = e->split ? 0 : (size_t)H * vt_ld(cap, capd) * es;
+        if (!e->split) e->vcol.reserve(cap * 4);
         if (vt_bytes > e->vt.bytes) {
             e->vt.reserve(vt_bytes);
             // never-written gap columns between documents must read as finite zeros
