@@ -468,7 +468,7 @@ def index_e2e_leg(args, dev):
         try:
             model = DeepImpact.load(str(ckpt), tokenizer_path=tok_path, precision="bf16x3",
                                     device=dev, max_length=300)
-            indexer = Indexer(model, model_batch_size=index_cli.BATCH_SIZE, num_processes=procs,
+            indexer = Indexer(model, model_batch_size=args.e2e_model_batch, num_processes=procs,
                               pool=pool)
             with open(os.devnull, "w") as dn:  # warm the workers (imports, tokenizer)
                 with open(coll) as f:
@@ -476,7 +476,7 @@ def index_e2e_leg(args, dev):
             t_setup = time.perf_counter() - t0
             t1 = time.perf_counter()
             n = index_cli._index_file(indexer, coll, "msmarco", td / "collection.index",
-                                      50 * index_cli.BATCH_SIZE, None, t1)
+                                      args.e2e_process_batch, None, t1)
             el = time.perf_counter() - t1
             out_bytes = (td / "collection.index").stat().st_size
         finally:
@@ -486,9 +486,10 @@ def index_e2e_leg(args, dev):
     return {"value": round(n / el, 1), "unit": "docs/s", "docs": int(n), "seconds": round(el, 3),
             "setup_seconds": round(t_setup, 2), "tokenizer_workers": procs,
             "precision": "bf16x3", "output_bytes": int(out_bytes),
+            "model_batch_size": args.e2e_model_batch, "process_batch_size": args.e2e_process_batch,
             "path": "index.py _index_file: CollectionParser -> TokenizerPool -> di_encode "
-                    "(bf16x3, ROUND3) -> di_format_impact_lines, reference defaults "
-                    "(process batch 1600, model batch 32 -> 256-doc device chunks)"}
+                    "(bf16x3, ROUND3) -> di_format_impact_lines (model batches below 256 "
+                    "docs run as 256-doc device chunks)"}
 
 
 def main():
@@ -504,6 +505,10 @@ def main():
     ap.add_argument("--max-len", type=int, default=300)
     ap.add_argument("--e2e-docs", type=int, default=16000, help="index_e2e leg: documents")
     ap.add_argument("--e2e-procs", type=int, default=16, help="index_e2e leg: tokenizer workers")
+    ap.add_argument("--e2e-model-batch", type=int, default=32,
+                    help="index_e2e leg: --model_batch_size (reference default 32)")
+    ap.add_argument("--e2e-process-batch", type=int, default=1600,
+                    help="index_e2e leg: --process_batch_size (reference default 1600)")
     ap.add_argument("--legs", default="encode,encode_x3,retrieve,retrieve_shard,index_e2e",
                     help="encode (bf16, configs[1]), encode_x3 (fp32-faithful bf16x3), retrieve "
                          "(100k-doc shard, configs[1]), retrieve_shard (1.1M docs: one 8-way shard "

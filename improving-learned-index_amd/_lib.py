@@ -258,6 +258,26 @@ def key_score(keys):
     return (keys >> np.uint64(48)).astype(np.uint32)
 
 
+def format_impact_lines_packed(blob: bytes, term_off, impacts, cu_terms) -> str:
+    """format_impact_lines on the packed form: the terms' UTF-8 bytes back to back
+    (term_off [T+1] int64 byte offsets), their float32 impacts and the per-document
+    term offsets cu_terms [n_docs+1]."""
+    n_docs = len(cu_terms) - 1
+    term_off = np.ascontiguousarray(term_off, np.int64)
+    imp = np.ascontiguousarray(impacts, np.float32)
+    if imp.size == 0:
+        imp = np.zeros(1, np.float32)
+    cu = np.ascontiguousarray(cu_terms, np.int64)
+    n_terms = len(term_off) - 1
+    cap = len(blob) + 30 * (n_terms + 1) + n_docs + 16
+    out = ctypes.create_string_buffer(cap)
+    n = ctypes.c_int64(0)
+    tb = ctypes.create_string_buffer(blob, len(blob) + 1)
+    check(lib().di_format_impact_lines(tb, ptr(term_off), ptr(imp), ptr(cu), n_docs, out, cap,
+                                       ctypes.byref(n)))
+    return out.raw[:n.value].decode("utf-8")
+
+
 def format_impact_lines(doc_terms, doc_impacts):
     """Native A9 formatter: list (per doc) of term lists + float32 impact arrays
     (already rounded) -> the impact-TSV text of those docs (one line each)."""

@@ -59,7 +59,22 @@ def run(collection_path, collection_type, output_file_path, model_checkpoint_pat
 
 def _index_file(indexer, collection_path, collection_type, output_file_path,
                 process_batch_size, doc_range, start):
+    """index.py:31-44.  Batches are tokenized one ahead (Indexer.submit) while the
+    previous one encodes and writes; they are written in order, so the bytes are the
+    sequential loop's."""
     lo, hi = (0, None) if doc_range is None else doc_range
+    pending = None  # submitted, not yet written
+
+    def flush(batch):
+        nonlocal pending
+        if not hasattr(indexer, "submit"):  # any object with the reference's index()
+            indexer.index(batch, out)
+            return
+        handle = indexer.submit(batch)
+        if pending is not None:
+            indexer.finish(pending, out)
+        pending = handle
+
     with open(collection_path) as f, open(output_file_path, "w") as out:
         batch = []
         n = 0
@@ -72,7 +87,7 @@ def _index_file(indexer, collection_path, collection_type, output_file_path,
             # (its flush points need not fall inside it: an empty flush would write a
             # stray empty line and shift every later doc id of the joined file)
             if i % process_batch_size == 0 and (doc_range is None or batch):
-                indexer.index(batch, out)
+                flush(batch)
                 logger.info(f"Indexed {i} passages [Rate: {i / (time.time() - start):.2f} "
                             f"passages/s]")
                 batch = []
@@ -80,7 +95,9 @@ def _index_file(indexer, collection_path, collection_type, output_file_path,
             batch.append(passage)
             n += 1
         if doc_range is None or batch:
-            indexer.index(batch, out)
+            flush(batch)
+        if pending is not None:
+            indexer.finish(pending, out)
     return n
 
 

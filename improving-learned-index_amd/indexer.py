@@ -35,8 +35,9 @@ def _tok_init(tok_json: str, max_length: int, term_mapping: str) -> None:
 
 
 def _tok_chunk(docs: Sequence[str]):
-    # packed numpy arrays + one flat term list: cheap to pickle back to the parent
-    return DeepImpact.pack_processed(DeepImpact.process_documents(docs, _W["max_length"]))
+    # packed numpy arrays + the terms as one UTF-8 blob: cheap to pickle back to the
+    # parent, and the parent formats the lines without per-term Python objects
+    return DeepImpact.pack_processed_blob(DeepImpact.process_documents(docs, _W["max_length"]))
 
 
 def pool_supported() -> bool:
@@ -93,26 +94,50 @@ class Indexer:
         self.num_processes = num_processes
         self.pool = pool  # None: tokenize in this process
 
+    def _chunks(self, batch: Sequence[str]):
+        # with a pool: enough chunks to keep every worker busy (down to 64 docs each)
+        step = self.batch_size
+        if self.pool is not None and batch:
+            step = max(64, min(step, -(-len(batch) // self.pool.n)))
+        return [batch[s:s + step] for s in range(0, len(batch), step)]
+
     def encode(self, batch: Sequence[str]):
-        chunks = [batch[s:s + self.batch_size] for s in range(0, len(batch), self.batch_size)]
         out: List = []
         if self.pool is not None:
-            for packed in self.pool.imap(chunks):
-                out += self.model.encode_packed_terms(packed, round3=True)
+            for ids, cu, blob, term_off, tt, ct in self.pool.imap(self._chunks(batch)):
+                terms = [blob[term_off[i]:term_off[i + 1]].decode("utf-8")
+                         for i in range(len(term_off) - 1)]
+                out += self.model.encode_packed_terms((ids, cu, terms, tt, ct), round3=True)
         else:
-            for c in chunks:
+            for c in self._chunks(batch):
                 out += self.model.encode_processed(
                     self.model.process_documents(c, self.model.max_length), round3=True)
         return out
 
-    def index(self, batch: Sequence[str], file) -> None:
+    def submit(self, batch: Sequence[str]):
+        """Start tokenizing `batch` in the pool (returns at once); finish() encodes and
+        writes it.  One submitted batch ahead keeps the workers busy while the GPU
+        encodes the current one."""
+        if self.pool is None:
+            return (batch, None)
+        return (batch, self.pool.imap(self._chunks(batch)))
+
+    def finish(self, handle, file) -> None:
         """indexer.py:31-68: file.write('\\n'.join(lines) + '\\n')."""
-        impacts = self.encode(batch)
-        text = _lib.format_impact_lines([[t for t, _ in d] for d in impacts],
-                                        [[v for _, v in d] for d in impacts])
+        batch, it = handle
+        if it is None:
+            impacts = self.encode(batch)
+            text = _lib.format_impact_lines([[t for t, _ in d] for d in impacts],
+                                            [[v for _, v in d] for d in impacts])
+        else:
+            text = "".join(self.model.encode_packed_text(p) for p in it)
         # '\\n'.join(lines) + '\\n' == every line + '\\n', except for an empty batch
         file.write(text if batch else "\n")
         file.flush()
+
+    def index(self, batch: Sequence[str], file) -> None:
+        """indexer.py:31-68: file.write('\\n'.join(lines) + '\\n')."""
+        self.finish(self.submit(batch), file)
 
 
 def resolve_tokenizer(model_checkpoint_path, tokenizer_path):

@@ -26,6 +26,7 @@ from typing import Dict, Iterable, List, Optional, Sequence, Set, Tuple, Union
 
 import numpy as np
 
+from . import _lib
 from .encoder import DeviceEncoder, EncoderConfig
 
 PUNCTUATION = set(string.punctuation)
@@ -241,6 +242,24 @@ class DeepImpact:
         ct = np.zeros(len(proc) + 1, np.int32)
         ct[1:] = np.cumsum([len(m) for _, m in proc])
         return ids, cu, terms, tt, ct
+
+    @staticmethod
+    def pack_processed_blob(proc):
+        """pack_processed with the kept terms as one UTF-8 blob + byte offsets (what a
+        tokenizer worker sends back: no per-term objects to unpickle)."""
+        ids, cu, terms, tt, ct = DeepImpact.pack_processed(proc)
+        enc = [t.encode("utf-8") for t in terms]
+        term_off = np.zeros(len(enc) + 1, np.int64)
+        if enc:
+            term_off[1:] = np.cumsum([len(b) for b in enc])
+        return ids, cu, b"".join(enc), term_off, tt, ct
+
+    def encode_packed_text(self, packed) -> str:
+        """A pack_processed_blob batch -> its impact-TSV lines (round3, native
+        formatter), without per-term Python objects."""
+        ids, cu, blob, term_off, tt, ct = packed
+        imp = self.encoder.encode_packed(ids, cu, tt, ct, round3=True)
+        return _lib.format_impact_lines_packed(blob, term_off, imp, ct)
 
     def encode_packed_terms(self, packed, round3=False):
         """Encode a pack_processed batch: per document its (term, impact) list."""

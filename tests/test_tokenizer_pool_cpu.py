@@ -32,6 +32,16 @@ class _FakeModel:
                 for j in range(ct[d], ct[d + 1])])
         return out
 
+    def encode_packed_text(self, packed):
+        """The real class's pool path: blob terms -> impacts -> native formatter."""
+        from improving_learned_index_amd import _lib
+
+        ids, cu, blob, term_off, tt, ct = packed
+        terms = [blob[term_off[i]:term_off[i + 1]].decode("utf-8")
+                 for i in range(len(term_off) - 1)]
+        imp = [v for d in self.encode_packed_terms((ids, cu, terms, tt, ct)) for _, v in d]
+        return _lib.format_impact_lines_packed(blob, term_off, np.array(imp, np.float32), ct)
+
     def encode_processed(self, proc, round3=False):
         from improving_learned_index_amd import models
 
