@@ -17,6 +17,7 @@
 namespace di {
 template <typename T>
 void launch_gemm(int epi, const GemmArgs &g, hipStream_t s);
+void launch_gemm256(int epi, const GemmArgs &g, hipStream_t s);
 }
 using namespace di;
 
@@ -204,6 +205,51 @@ int main(int argc, char **argv) {
                     printf("sweep %-5s ablate=%d gm=%2d stagger=%5d  %.3f ms  %.0f TF\n", names[i],
                            abl, gm, stg, ms, flops / ms / 1e9);
                 }
+            }
+        }
+    }
+    // split-bf16 (bf16x3) shapes: A / B as split rows (random bits; timing only).
+    // ablate 6: no GELU, no stores (the K loop and the epilogue's reads)
+    {
+        struct SC {
+            const char *name;
+            int M, N, K, epi;
+        };
+        const SC sc[] = {{"x3_qkv", 206426, 2304, 768, EPI_BIAS},
+                         {"x3_o", 206426, 768, 768, EPI_BIAS_RESID},
+                         {"x3_ffn1", 206426, 3072, 768, EPI_BIAS_GELU},
+                         {"x3_ffn2", 100000, 768, 3072, EPI_BIAS_RESID}};
+        hipEvent_t a0, a1;
+        CK(hipEventCreate(&a0));
+        CK(hipEventCreate(&a1));
+        for (const SC &c : sc) {
+            for (int abl : {0, 6}) {
+                GemmArgs g{};
+                g.A = A;
+                g.B = B;
+                g.bias = bias;
+                g.resid = O2;
+                g.out = O1;
+                g.M = c.M;
+                g.N = c.N;
+                g.K = c.K;
+                g.ld_out = c.epi == EPI_BIAS_RESID ? c.N : 2 * c.N;
+                g.a_rows = (c.M + 255) / 256 * 256;
+                g.hidden = 768;
+                g.tune_gm = c.K == 3072 ? 4 : 8;
+                g.split = 1;
+                g.ablate = abl;
+                for (int w = 0; w < 2; ++w) launch_gemm256(c.epi, g, 0);
+                CK(hipEventRecord(a0, 0));
+                for (int w = 0; w < 10; ++w) launch_gemm256(c.epi, g, 0);
+                CK(hipEventRecord(a1, 0));
+                CK(hipEventSynchronize(a1));
+                float ms;
+                CK(hipEventElapsedTime(&ms, a0, a1));
+                ms /= 10;
+                const double fl = 2.0 * c.M * c.N * c.K;
+                printf("split %-8s ablate=%d  %.3f ms  %.0f TF fp32-eq  %.0f TF bf16-MFMA\n", c.name,
+                       abl, ms, fl / ms / 1e9, 3 * fl / ms / 1e9);
             }
         }
     }
