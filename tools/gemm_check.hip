@@ -187,12 +187,12 @@ int main(int argc, char **argv) {
         for (int i = 0; i < 4; ++i) {
             const Case &c = bench[i];
             const double flops = 2.0 * c.M * c.N * c.K;
-            for (int abl : {0, 1, 2, 4, 6}) {
+            for (int abl : {0, 6, 102, 104, 116}) {  // 1xx: full epilogue, tile group xx
                 for (int stg : {0}) {
-                    const int gm = 8;
+                    const int gm = abl >= 100 ? abl - 100 : 8;
                     GemmArgs g = args(c, O1, V1, true);
                     g.tune_gm = gm;
-                    g.ablate = abl;
+                    g.ablate = abl >= 100 ? 0 : abl;
                     (void)stg;
                     for (int w = 0; w < 2; ++w) launch_gemm<bf16>(c.epi, g, 0);
                     CK(hipEventRecord(a0, 0));
@@ -223,7 +223,7 @@ int main(int argc, char **argv) {
         CK(hipEventCreate(&a0));
         CK(hipEventCreate(&a1));
         for (const SC &c : sc) {
-            for (int abl : {0, 6}) {
+            for (int abl : {0, 6, 100, 102, 104, 116}) {  // 1xx: full epilogue, tile group xx
                 GemmArgs g{};
                 g.A = A;
                 g.B = B;
@@ -236,9 +236,9 @@ int main(int argc, char **argv) {
                 g.ld_out = c.epi == EPI_BIAS_RESID ? c.N : 2 * c.N;
                 g.a_rows = (c.M + 255) / 256 * 256;
                 g.hidden = 768;
-                g.tune_gm = c.K == 3072 ? 4 : 8;
+                g.tune_gm = abl >= 100 ? abl - 100 : (c.K == 3072 ? 4 : 8);
                 g.split = 1;
-                g.ablate = abl;
+                g.ablate = abl >= 100 ? 0 : abl;
                 for (int w = 0; w < 2; ++w) launch_gemm256(c.epi, g, 0);
                 CK(hipEventRecord(a0, 0));
                 for (int w = 0; w < 10; ++w) launch_gemm256(c.epi, g, 0);
@@ -248,7 +248,7 @@ int main(int argc, char **argv) {
                 CK(hipEventElapsedTime(&ms, a0, a1));
                 ms /= 10;
                 const double fl = 2.0 * c.M * c.N * c.K;
-                printf("split %-8s ablate=%d  %.3f ms  %.0f TF fp32-eq  %.0f TF bf16-MFMA\n", c.name,
+                printf("split %-8s ablate=%3d  %.3f ms  %.0f TF fp32-eq  %.0f TF bf16-MFMA\n", c.name,
                        abl, ms, fl / ms / 1e9, 3 * fl / ms / 1e9);
             }
         }
