@@ -38,6 +38,27 @@ V_TERMS = 200_000
 N_QUERIES = 6980  # MS MARCO dev.small
 
 
+def _gloo():
+    return dist.is_initialized() and dist.get_backend() == "gloo"
+
+
+def all_gather_dev(out, inp):
+    """all_gather_into_tensor on device tensors (host-staged under gloo)."""
+    if _gloo():
+        o = torch.empty(out.shape, dtype=out.dtype)
+        torch.cuda.synchronize()
+        dist.all_gather_into_tensor(o, inp.cpu())
+        out.copy_(o)
+    else:
+        dist.all_gather_into_tensor(out, inp)
+
+
+def max_over_ranks(x: float) -> float:
+    t = torch.tensor([x], dtype=torch.float64, device="cpu" if _gloo() else "cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
@@ -104,8 +125,8 @@ def retrieve_leg(args, rank, world, dev, n_docs=DOCS_PER_SHARD, check_queries=0)
         ix.search_device(d_terms, d_cu, nq, k, out_doc, out_score, out_n, out_key,
                          flags | (_lib.DI_F_TIMING if timing else 0))
         if world > 1:
-            dist.all_gather_into_tensor(g_key, out_key)
-            dist.all_gather_into_tensor(g_n, out_n)
+            all_gather_dev(g_key, out_key)
+            all_gather_dev(g_n, out_n)
             _lib.topk_merge_device(g_key, g_n, nq, world, k, m_key, m_n, device=dev,
                                    stream=stream.cuda_stream,
                                    flags=flags | _lib.DI_F_LISTS_MAJOR)
@@ -144,9 +165,7 @@ def retrieve_leg(args, rank, world, dev, n_docs=DOCS_PER_SHARD, check_queries=0)
                 raise SystemExit(f"bench parity check failed on query {i} ({n_docs} docs)")
         log(f"[rank 0] {n_docs}-doc shard: the first {check_queries} queries equal the oracle")
     if world > 1:
-        t = torch.tensor([el], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
+        el = max_over_ranks(el)
 
     # correctness spot check of the timed outputs against the oracle (rank 0, N=1)
     lens = np.diff(term_off)
@@ -316,9 +335,7 @@ def encode_leg(args, rank, world, dev, precision="bf16"):
     el = time.perf_counter() - t1
     enc.sync()
     if world > 1:
-        t = torch.tensor([el], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
+        el = max_over_ranks(el)
     kernels = {}
     for name in ("embed_ln", "gemm_qkv", "attention", "gemm_o", "ln", "gemm_ffn1", "gemm_ffn2",
                  "row_ln", "head", "gather_terms"):
@@ -522,8 +539,14 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        # one rank per GPU over RCCL; more ranks than GPUs (a 1-GPU rehearsal of the
+        # multi-rank path) share the devices over gloo with host-staged collectives
+        n_dev = max(1, torch.cuda.device_count())
+        torch.cuda.set_device(local % n_dev)
+        if world <= n_dev:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
     else:
         torch.cuda.set_device(0)
     dev = torch.cuda.current_device()
