@@ -16,6 +16,7 @@ cores, bounded sample, rank 0 at N=1 only).
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
 import sys
@@ -379,6 +380,9 @@ def encode_leg(args, rank, world, dev, precision="bf16"):
         "tokens_per_step": int(cu[-1]),
         "kernels": kernels,
         "gemm_tflops": {k: round(v[2], 1) for k, v in per_launch.items()},
+        # digest of the last step's impacts: kernel changes that claim bit-identical
+        # outputs are checked by comparing it across builds (seeded weights and docs)
+        "out_sha1": hashlib.sha1(out.cpu().numpy().tobytes()).hexdigest(),
         "model_tflops": round(model_flops * args.steps / el / 1e12 * 1.0, 1),
         "model_flops_frac": round(model_flops * args.steps / el / 1e12 / peak, 4),
         "roofline": {"kernel": f"{pmc_name} ({dom})", "bound": "mfma",
@@ -605,7 +609,7 @@ def main():
     }
     if enc_res is not None:
         out["encode"] = {k: enc_res[k] for k in ("tokens_per_step", "kernels", "gemm_tflops",
-                                                 "model_tflops", "model_flops_frac")}
+                                                 "model_tflops", "model_flops_frac", "out_sha1")}
     if x3_res is not None:
         out["encode_fp32_faithful"] = {
             "value": round(x3_res["value"], 2), "unit": "docs/s", "dtype": "bf16x3",
@@ -614,7 +618,7 @@ def main():
                          "the fp32 reference (tests/test_encoder_bf16x3_gpu.py)",
             "ms_per_step": round(x3_res["ms_per_step"], 4),
             **{k: x3_res[k] for k in ("kernels", "gemm_tflops", "model_tflops",
-                                      "model_flops_frac", "roofline")}}
+                                      "model_flops_frac", "roofline", "out_sha1")}}
     if ret_res is not None:
         out["retrieve"] = {"value": round(ret_res["value"], 2), "unit": "queries/s",
                            "ms_per_step": round(ret_res["ms_per_step"], 4),

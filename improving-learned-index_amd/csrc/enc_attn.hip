@@ -697,10 +697,22 @@ struct Att3 {
     static constexpr int LDS = DB ? 2 * BUF : BUF;
 };
 
-__device__ __forceinline__ uint2 ds_read_tr_b16(uint32_t addr) {
-    uint2 r;
-    asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(addr));
-    return r;
+// K / V image swizzle: the 16-byte slot j of key row r is stored at slot
+// j ^ att3_swz(r).  Bit 2 folds in row bit 3 so that the fragment reads are
+// conflict-free: a ds_read_b128 lane group (16 lanes, rows 8 (c >> 2) + (c & 3) + 4 t
+// of two lane groups g) and a ds_read_b64_tr_b16 lane group (32 lanes, rows
+// 8 g + 4 h2 + q of two g) each see every bank once.  Bits 0-4 of a fragment row
+// never depend on the 32-key chunk, so per lane every read address is a per-pair base
+// plus key0 * 128 plus an immediate (see kb / vb below).
+__device__ __forceinline__ int att3_swz(int r) { return (r & 7) ^ ((r >> 1) & 4); }
+
+// f(integral_constant<K>) for K = K0, K0 + 1, .. < N until f returns true
+template <int K, int N, class F>
+__device__ __forceinline__ void att3_chunks(F &f) {
+    if constexpr (K < N) {
+        if (f(std::integral_constant<int, K>{})) return;
+        att3_chunks<K + 1, N>(f);
+    }
 }
 
 // The key loop is instantiated per tile count (1 or 2) and runs both tiles' S^T
@@ -726,21 +738,22 @@ attention_v3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
     const uint32_t lds_base =
         (uint32_t)(uintptr_t)((__attribute__((address_space(3))) unsigned char *)lds);
 
-    // LDS-DMA of pair p's K (rows < round8(n)) and V (rows < round32(n)) into buffer b
+    // LDS-DMA of pair p's K and V rows < round32(n) into buffer b (rows past n repeat
+    // row n - 1; their scores are masked).  Slot j of row r lands at j ^ att3_swz(r).
     auto stage = [&](int p, int b) {
         const int doc = p / n_heads, h = p % n_heads;
         const int tok0 = cu_seqlens[doc], n = cu_seqlens[doc + 1] - tok0;
-        const int nk8 = (n + 7) >> 3, nv8 = ((n + 31) & ~31) >> 3;  // 8-row pieces
-        const int r_in = lane >> 3;                                    // row within a piece
-        const int chunk = ((lane & 7) ^ r_in) * 8;  // source chunk (elements), swizzled
-        const bf16 *kbase = qkv + (int64_t)tok0 * ld + H + h * ATT_D + chunk;
-        const bf16 *vbase = qkv + (int64_t)tok0 * ld + 2 * H + h * ATT_D + chunk;
+        const int nk8 = ((n + 31) & ~31) >> 3, nv8 = nk8;  // 8-row pieces
+        const int r_in = lane >> 3;                         // row within a piece
+        const bf16 *kbase = qkv + (int64_t)tok0 * ld + H + h * ATT_D;
+        const bf16 *vbase = qkv + (int64_t)tok0 * ld + 2 * H + h * ATT_D;
         unsigned char *buf = lds + b * Att3<DB>::BUF;
         for (int pc = wave; pc < nk8 + nv8; pc += ATT3_WAVES) {
             const bool is_k = pc < nk8;
             const int piece = is_k ? pc : pc - nk8;
             const int r = min(piece * 8 + r_in, n - 1);
-            const bf16 *src = (is_k ? kbase : vbase) + (int64_t)r * ld;
+            const int chunk = ((lane & 7) ^ att3_swz(piece * 8 + r_in)) * 8;  // source slot
+            const bf16 *src = (is_k ? kbase : vbase) + (int64_t)r * ld + chunk;
             unsigned char *dst = buf + (is_k ? 0 : Att3<DB>::ROWS * 128) + piece * 1024;
             __builtin_amdgcn_global_load_lds((const void *)src, (lds_void *)dst, 16, 0, 0);
         }
@@ -749,9 +762,29 @@ attention_v3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
     bf16x8 ones;
 #pragma unroll
     for (int e = 0; e < 8; ++e) ones[e] = (bf16)1.0f;
-    const int krel = 8 * (c >> 2) + (c & 3);
-    // ds_read_b64_tr_b16 lane role inside its 16-lane group: row q, column quad p
-    const int tq = c >> 2, tp = c & 3;
+    // Per-lane fragment offsets within an image (key0 = 0; see att3_swz).
+    // K, S^T tile t, head-dim chunk ch: row krel + 4 t, slot 4 ch + g, stored at
+    // (g ^ (c & 3)) | ((ch ^ t ^ b3) << 2)  ->  koff[ch ^ t] + 512 t.
+    uint32_t koff[2];
+    {
+        const int krel = 8 * (c >> 2) + (c & 3), b3 = (c >> 2) & 1;
+#pragma unroll
+        for (int x = 0; x < 2; ++x) koff[x] = krel * 128 + ((g ^ (c & 3)) << 4) + ((x ^ b3) << 6);
+    }
+    // V^T by ds_read_b64_tr_b16, lane 4 q + p of a 16-lane group: row 8 g + 4 h2 + q,
+    // columns 16 dt + 4 p..+3 = slot 2 dt + (p >> 1), half p & 1, stored at slot
+    // u0 | ((u1 ^ dt0) << 1) | ((dt1 ^ h2 ^ g0) << 2) with u = (p >> 1) ^ q
+    //   ->  voff[dt & 1][(dt >> 1) ^ h2] + 512 h2.
+    uint32_t voff[2][2];
+    {
+        const int tq = c >> 2, tp = c & 3, u = (tp >> 1) ^ tq;
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+            for (int bb = 0; bb < 2; ++bb)
+                voff[a][bb] = (8 * g + tq) * 128 + 8 * (tp & 1) +
+                              16 * ((u & 1) | (((u >> 1) ^ a) << 1) | ((bb ^ (g & 1)) << 2));
+    }
 
     // Q of pair p comes one pair ahead (inline-asm global loads: the compiler sees no
     // pending load, so it neither waits nor drains the K/V prefetch for them), into the
@@ -767,79 +800,75 @@ attention_v3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
         t_cnt = base + (wave < extra ? 1 : 0);
         t_first = wave * base + min(wave, extra);
     };
-    // Q row addresses of pair pp for this wave's tiles: [i][qt][ch]
-    auto q_srcs = [&](int pp, const bf16 *(&src)[2][QTB][2]) {
+    // Q row addresses of pair pp for this wave's tile group i (tiles t_first + 2 i,
+    // + 2 i + 1): [qt][ch]
+    auto q_srcs = [&](int pp, int i, const bf16 *(&src)[QTB][2]) {
         const int dd = pp / n_heads, hh = pp % n_heads;
         const int t0 = cu_seqlens[dd], nn = cu_seqlens[dd + 1] - t0;
         const int qs0 = qsel ? cu_qsel[dd] : 0, nq = qsel ? cu_qsel[dd + 1] - qs0 : nn;
         int t_first, t_cnt;
         tiles_of(nq, t_first, t_cnt);
+        const int q_base = (t_first + 2 * i) * 16;
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            const int q_base = (t_first + 2 * i) * 16;
+        for (int qt = 0; qt < QTB; ++qt) {
+            const int qi = max(min(q_base + 16 * qt + c, nq - 1), 0);
+            const int qloc = qsel ? (nq > 0 ? min(max(qsel[qs0 + qi], 0), max(nn - 1, 0)) : 0)
+                                  : qi;
+            const int qrow = t0 + qloc;
 #pragma unroll
-            for (int qt = 0; qt < QTB; ++qt) {
-                const int qi = max(min(q_base + 16 * qt + c, nq - 1), 0);
-                const int qloc = qsel ? (nq > 0 ? min(max(qsel[qs0 + qi], 0), max(nn - 1, 0)) : 0)
-                                      : qi;
-                const int qrow = t0 + qloc;
-#pragma unroll
-                for (int ch = 0; ch < 2; ++ch)
-                    src[i][qt][ch] = qkv + (int64_t)qrow * ld + hh * ATT_D + ch * 32 + 8 * g;
-            }
+            for (int ch = 0; ch < 2; ++ch)
+                src[qt][ch] = qkv + (int64_t)qrow * ld + hh * ATT_D + ch * 32 + 8 * g;
         }
     };
-    auto load_q = [&](int pp, uint4 (&qd)[2][QTB][2]) {  // DB: one pair ahead
-        const bf16 *src[2][QTB][2];
-        q_srcs(pp, src);
+    // DB: tile group 0 of the next pair, one pair ahead
+    auto load_q = [&](int pp, uint4 (&qd)[QTB][2]) {
+        const bf16 *src[QTB][2];
+        q_srcs(pp, 0, src);
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+        for (int qt = 0; qt < QTB; ++qt)
 #pragma unroll
-            for (int qt = 0; qt < QTB; ++qt)
-#pragma unroll
-                for (int ch = 0; ch < 2; ++ch)
-                    asm volatile("global_load_dwordx4 %0, %1, off"
-                                 : "=v"(qd[i][qt][ch])
-                                 : "v"(src[i][qt][ch])
-                                 : "memory");
+            for (int ch = 0; ch < 2; ++ch)
+                asm volatile("global_load_dwordx4 %0, %1, off"
+                             : "=v"(qd[qt][ch])
+                             : "v"(src[qt][ch])
+                             : "memory");
     };
-    // !DB: this pair's Q, loaded together with the wait for them and the K / V
-    // staging (one asm statement: the outputs exist only after the wait, so no copy
-    // of a register still being loaded can be scheduled above it)
-    auto load_q_wait = [&](int pp, uint4 (&qd)[2][QTB][2]) {
-        static_assert(QTB == 2, "load_q_wait: 8 loads");
-        const bf16 *src[2][QTB][2];
-        q_srcs(pp, src);
+    // tile group i of pair pp now, loaded together with the wait for them (one asm
+    // statement: the outputs exist only after the wait, so no copy of a register
+    // still being loaded can be scheduled above it).  The wait also retires any K / V
+    // staging in flight (!DB: this pair's; DB, group 1: the next pair's, by then
+    // mostly landed).
+    auto load_q_wait = [&](int pp, int i, uint4 (&qd)[QTB][2]) {
+        static_assert(QTB == 2, "load_q_wait: 4 loads");
+        const bf16 *src[QTB][2];
+        q_srcs(pp, i, src);
         asm volatile(
-            "global_load_dwordx4 %0, %8, off\n\t"
-            "global_load_dwordx4 %1, %9, off\n\t"
-            "global_load_dwordx4 %2, %10, off\n\t"
-            "global_load_dwordx4 %3, %11, off\n\t"
-            "global_load_dwordx4 %4, %12, off\n\t"
-            "global_load_dwordx4 %5, %13, off\n\t"
-            "global_load_dwordx4 %6, %14, off\n\t"
-            "global_load_dwordx4 %7, %15, off\n\t"
+            "global_load_dwordx4 %0, %4, off\n\t"
+            "global_load_dwordx4 %1, %5, off\n\t"
+            "global_load_dwordx4 %2, %6, off\n\t"
+            "global_load_dwordx4 %3, %7, off\n\t"
             "s_waitcnt vmcnt(0)"
-            : "=&v"(qd[0][0][0]), "=&v"(qd[0][0][1]), "=&v"(qd[0][1][0]), "=&v"(qd[0][1][1]),
-              "=&v"(qd[1][0][0]), "=&v"(qd[1][0][1]), "=&v"(qd[1][1][0]), "=&v"(qd[1][1][1])
-            : "v"(src[0][0][0]), "v"(src[0][0][1]), "v"(src[0][1][0]), "v"(src[0][1][1]),
-              "v"(src[1][0][0]), "v"(src[1][0][1]), "v"(src[1][1][0]), "v"(src[1][1][1])
+            : "=&v"(qd[0][0]), "=&v"(qd[0][1]), "=&v"(qd[1][0]), "=&v"(qd[1][1])
+            : "v"(src[0][0]), "v"(src[0][1]), "v"(src[1][0]), "v"(src[1][1])
             : "memory");
     };
-    auto run_pair = [&](int p, int b, uint4 (&qc)[2][QTB][2], uint4 (&qn)[2][QTB][2]) {
+    // qn: tile group 0 of pair p (DB: loaded one pair ahead, in flight); qc: the copy
+    // the key loops read, made after the wait (so qn can take the next pair's loads)
+    auto run_pair = [&](int p, int b, uint4 (&qc)[QTB][2], uint4 (&qn)[QTB][2])
+                        __attribute__((always_inline)) {
         if (!DB) {
             stage(p, 0);
-            load_q_wait(p, qc);  // (also retires the staging)
+            load_q_wait(p, 0, qn);  // (also retires the staging)
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // K/V and Q of this pair
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+        for (int qt = 0; qt < QTB; ++qt)
 #pragma unroll
-            for (int qt = 0; qt < QTB; ++qt)
-#pragma unroll
-                for (int ch = 0; ch < 2; ++ch)  // the loaded values exist from here on
-                    asm volatile("" : "+v"(qc[i][qt][ch].x), "+v"(qc[i][qt][ch].y),
-                                 "+v"(qc[i][qt][ch].z), "+v"(qc[i][qt][ch].w));
+            for (int ch = 0; ch < 2; ++ch) {  // the loaded values exist from here on
+                asm volatile("" : "+v"(qn[qt][ch].x), "+v"(qn[qt][ch].y), "+v"(qn[qt][ch].z),
+                             "+v"(qn[qt][ch].w));
+                qc[qt][ch] = qn[qt][ch];
+            }
         __syncthreads();
         const int doc = p / n_heads, h = p % n_heads;
         const int tok0 = cu_seqlens[doc], n = cu_seqlens[doc + 1] - tok0;
@@ -854,59 +883,86 @@ attention_v3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
 
         const uint32_t kim = lds_base + b * Att3<DB>::BUF;
         const uint32_t vim = kim + Att3<DB>::ROWS * 128;
-        // K fragments (2 S^T tiles x 2 head-dim chunks) and V^T fragments of the
-        // 32-key chunk at key0, read from the LDS images (asm: see below)
-        // The 12 reads and their lgkmcnt(0) are ONE asm statement: its outputs exist
-        // only after the wait, so no copy of a register still being loaded can be
-        // scheduled above it (separate asm reads plus "+v" redefinitions after the
-        // wait do not guarantee that: the compiler may copy a tied input early).
-        auto read_kv = [&](int key0, uint4 (&kf)[2][2], bf16x8 (&vf)[4]) {
-            uint32_t ka[2][2], va[4][2];
+        // Per-pair fragment bases (opaque to the compiler, so that it keeps one set
+        // live instead of precomputing every buffer / chunk combination).
+        uint32_t kb[2], vb[2][2];
 #pragma unroll
-            for (int t = 0; t < 2; ++t) {
-                const int r = min(key0 + krel + 4 * t, n - 1);
+        for (int x = 0; x < 2; ++x) {
+            kb[x] = kim + koff[x];
+            asm volatile("" : "+v"(kb[x]));
+        }
 #pragma unroll
-                for (int ch = 0; ch < 2; ++ch) ka[t][ch] = kim + r * 128 + (((ch * 4 + g) ^ (r & 7)) << 4);
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+            for (int bb = 0; bb < 2; ++bb) {
+                vb[a][bb] = vim + voff[a][bb];
+                asm volatile("" : "+v"(vb[a][bb]));
             }
-#pragma unroll
-            for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-                for (int h2 = 0; h2 < 2; ++h2) {
-                    const int r = key0 + 8 * g + 4 * h2 + tq;
-                    const int chv = 2 * dt + (tp >> 1);
-                    va[dt][h2] = vim + r * 128 + ((chv ^ (r & 7)) << 4) + 8 * (tp & 1);
-                }
-            uint2 hv[4][2];
+        // Fragment reads of the 32-key chunk at KEY0 (compile time: the row offset is
+        // the instruction's immediate, no address arithmetic per chunk).  Inline asm:
+        // the compiler must not drain the next pair's LDS-DMA with vmcnt(0) before
+        // them.  Issue and wait are separate statements; the wait names every register
+        // still being written ("+v"), so nothing touches one earlier
+        // (tools/asm_wait_scan.py checks the assembly).
+        auto read_k = [&](int key0, bf16x8 (&kf)[2][2]) {  // [t][ch]
+            const uint32_t k0 = kb[0] + key0 * 128, k1 = kb[1] + key0 * 128;
             asm volatile(
-                "ds_read_b128 %0, %12\n\t"
-                "ds_read_b128 %1, %13\n\t"
-                "ds_read_b128 %2, %14\n\t"
-                "ds_read_b128 %3, %15\n\t"
-                "ds_read_b64_tr_b16 %4, %16\n\t"
-                "ds_read_b64_tr_b16 %5, %17\n\t"
-                "ds_read_b64_tr_b16 %6, %18\n\t"
-                "ds_read_b64_tr_b16 %7, %19\n\t"
-                "ds_read_b64_tr_b16 %8, %20\n\t"
-                "ds_read_b64_tr_b16 %9, %21\n\t"
-                "ds_read_b64_tr_b16 %10, %22\n\t"
-                "ds_read_b64_tr_b16 %11, %23\n\t"
-                "s_waitcnt lgkmcnt(0)"
-                : "=&v"(kf[0][0]), "=&v"(kf[0][1]), "=&v"(kf[1][0]), "=&v"(kf[1][1]),
-                  "=&v"(hv[0][0]), "=&v"(hv[0][1]), "=&v"(hv[1][0]), "=&v"(hv[1][1]),
-                  "=&v"(hv[2][0]), "=&v"(hv[2][1]), "=&v"(hv[3][0]), "=&v"(hv[3][1])
-                : "v"(ka[0][0]), "v"(ka[0][1]), "v"(ka[1][0]), "v"(ka[1][1]), "v"(va[0][0]),
-                  "v"(va[0][1]), "v"(va[1][0]), "v"(va[1][1]), "v"(va[2][0]), "v"(va[2][1]),
-                  "v"(va[3][0]), "v"(va[3][1])
+                "ds_read_b128 %0, %4\n\t"
+                "ds_read_b128 %1, %5\n\t"
+                "ds_read_b128 %2, %5 offset:512\n\t"
+                "ds_read_b128 %3, %4 offset:512"
+                : "=&v"(kf[0][0]), "=&v"(kf[0][1]), "=&v"(kf[1][0]), "=&v"(kf[1][1])
+                : "v"(k0), "v"(k1)
                 : "memory");
-            __builtin_amdgcn_sched_barrier(0);  // no MFMA above the wait (rule 18)
-#pragma unroll
-            for (int dt = 0; dt < 4; ++dt) {
-                const uint4 v4 = make_uint4(hv[dt][0].x, hv[dt][0].y, hv[dt][1].x, hv[dt][1].y);
-                __builtin_memcpy(&vf[dt], &v4, 16);
-            }
         };
-        // merged key loop over NQ (1 or 2) query tiles starting at q_base
-        auto key_loop = [&](auto nq_c, const uint4 (&qf)[QTB][2], int q_base) {
+        auto read_v = [&](int key0, uint2 (&hv)[4][2]) {  // [dt][h2]
+            const uint32_t v00 = vb[0][0] + key0 * 128, v01 = vb[0][1] + key0 * 128,
+                           v10 = vb[1][0] + key0 * 128, v11 = vb[1][1] + key0 * 128;
+            asm volatile(
+                "ds_read_b64_tr_b16 %0, %8\n\t"
+                "ds_read_b64_tr_b16 %1, %9 offset:512\n\t"
+                "ds_read_b64_tr_b16 %2, %10\n\t"
+                "ds_read_b64_tr_b16 %3, %11 offset:512\n\t"
+                "ds_read_b64_tr_b16 %4, %9\n\t"
+                "ds_read_b64_tr_b16 %5, %8 offset:512\n\t"
+                "ds_read_b64_tr_b16 %6, %11\n\t"
+                "ds_read_b64_tr_b16 %7, %10 offset:512"
+                : "=&v"(hv[0][0]), "=&v"(hv[0][1]), "=&v"(hv[1][0]), "=&v"(hv[1][1]),
+                  "=&v"(hv[2][0]), "=&v"(hv[2][1]), "=&v"(hv[3][0]), "=&v"(hv[3][1])
+                : "v"(v00), "v"(v01), "v"(v10), "v"(v11)
+                : "memory");
+        };
+        // counted waits naming the registers they retire ("+v"): LDS reads complete in
+        // issue order, so lgkmcnt(N) retires all but the newest N
+        auto wait_k = [&](bf16x8 (&kf)[2][2]) {  // K in flight, then the 8 V reads
+            asm volatile("s_waitcnt lgkmcnt(8)"
+                         : "+v"(kf[0][0]), "+v"(kf[0][1]), "+v"(kf[1][0]), "+v"(kf[1][1])
+                         :
+                         : "memory");
+        };
+        auto wait_v = [&](uint2 (&hv)[4][2], int) {  // V, then the 4 K reads
+            asm volatile("s_waitcnt lgkmcnt(4)"
+                         : "+v"(hv[0][0]), "+v"(hv[0][1]), "+v"(hv[1][0]), "+v"(hv[1][1]),
+                           "+v"(hv[2][0]), "+v"(hv[2][1]), "+v"(hv[3][0]), "+v"(hv[3][1])
+                         :
+                         : "memory");
+        };
+        auto wait_all = [&](bf16x8 (&kf)[2][2], uint2 (&hv)[4][2]) {
+            asm volatile("s_waitcnt lgkmcnt(0)"
+                         : "+v"(kf[0][0]), "+v"(kf[0][1]), "+v"(kf[1][0]), "+v"(kf[1][1]),
+                           "+v"(hv[0][0]), "+v"(hv[0][1]), "+v"(hv[1][0]), "+v"(hv[1][1]),
+                           "+v"(hv[2][0]), "+v"(hv[2][1]), "+v"(hv[3][0]), "+v"(hv[3][1])
+                         :
+                         : "memory");
+        };
+        // merged key loop over NQ (1 or 2) query tiles starting at q_base, software
+        // pipelined one chunk deep: step k issues S^T(k + 1) = K(k + 1) Q^T on the
+        // matrix pipe, then computes P(k) (VALU) beside it, then O^T += V^T(k) P^T(k);
+        // the LDS reads of K(k + 2) and V(k + 1) are in flight meanwhile.  Every
+        // product and every f32 operation is the one of the unpipelined loop, in the
+        // same order (bit-identical).
+        auto key_loop = [&](auto nq_c, const uint4 (&qf)[QTB][2], int q_base)
+                            __attribute__((always_inline)) {
             constexpr int NQ = decltype(nq_c)::value;
             float m[NQ], msc[NQ];
             f32x4 o[NQ][4], l[NQ];
@@ -918,11 +974,12 @@ attention_v3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
 #pragma unroll
                 for (int dt = 0; dt < 4; ++dt) o[qt][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
             }
-            for (int key0 = 0; key0 < n; key0 += 32) {
-                uint4 kf[2][2];
-                bf16x8 vf[4];
-                read_kv(key0, kf, vf);
-                f32x4 s[NQ][2];
+            bf16x8 qv[NQ][2];  // B operands Q^T
+#pragma unroll
+            for (int qt = 0; qt < NQ; ++qt)
+#pragma unroll
+                for (int ch = 0; ch < 2; ++ch) __builtin_memcpy(&qv[qt][ch], &qf[qt][ch], 16);
+            auto qk = [&](const bf16x8 (&kf)[2][2], f32x4 (&s)[NQ][2]) {
 #pragma unroll
                 for (int qt = 0; qt < NQ; ++qt)
 #pragma unroll
@@ -932,16 +989,10 @@ attention_v3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
 #pragma unroll
                     for (int qt = 0; qt < NQ; ++qt)
 #pragma unroll
-                        for (int t = 0; t < 2; ++t) mma_chunk(kf[t][ch], qf[qt][ch], s[qt][t], bf16{});
-                if (key0 + 32 > n) {
-#pragma unroll
-                    for (int qt = 0; qt < NQ; ++qt)
-#pragma unroll
                         for (int t = 0; t < 2; ++t)
-#pragma unroll
-                            for (int r = 0; r < 4; ++r)
-                                if (key0 + 8 * g + 4 * t + r >= n) s[qt][t][r] = -INFINITY;
-                }
+                            s[qt][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[t][ch], qv[qt][ch], s[qt][t], 0, 0, 0);
+            };
+            auto rescale = [&](f32x4 (&s)[NQ][2]) {
                 bool need[NQ], need_any = false;
 #pragma unroll
                 for (int qt = 0; qt < NQ; ++qt) {
@@ -953,9 +1004,17 @@ attention_v3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
                     for (int qt = 0; qt < NQ; ++qt)
                         if (__any(need[qt])) softmax_rescale(s[qt], m[qt], msc[qt], o[qt], l[qt]);
                 }
+            };
+            auto pv = [&](const f32x4 (&s)[NQ][2], const uint2 (&hv)[4][2]) {
                 bf16x8 pb[NQ];
 #pragma unroll
                 for (int qt = 0; qt < NQ; ++qt) softmax_p(s[qt], msc[qt], pb[qt]);
+                bf16x8 vf[4];
+#pragma unroll
+                for (int dt = 0; dt < 4; ++dt) {
+                    const uint4 v4 = make_uint4(hv[dt][0].x, hv[dt][0].y, hv[dt][1].x, hv[dt][1].y);
+                    __builtin_memcpy(&vf[dt], &v4, 16);
+                }
 #pragma unroll
                 for (int qt = 0; qt < NQ; ++qt) {
 #pragma unroll
@@ -964,6 +1023,61 @@ attention_v3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
                             __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf[dt], pb[qt], o[qt][dt], 0, 0, 0);
                     l[qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pb[qt], l[qt], 0, 0, 0);
                 }
+            };
+            // step at key0 (not the last chunk): s = S^T(key0) issued, kn = K(key0 + 32)
+            // in flight, reloaded in place with K(key0 + 64) once the S^T products have
+            // read it (MFMA A operands are read at issue; one chunk past the end reads
+            // stale rows of the image, never used); sn receives S^T(key0 + 32).  V(key0)
+            // is read inside the step (its latency hides behind the S^T products and the
+            // softmax).
+            auto step = [&](int key0, f32x4 (&s)[NQ][2], f32x4 (&sn)[NQ][2], bf16x8 (&kn)[2][2]) {
+                rescale(s);
+                uint2 hv[4][2];
+                read_v(key0, hv);
+                wait_k(kn);
+                qk(kn, sn);
+                read_k(key0 + 64, kn);
+                wait_v(hv, 0);
+                pv(s, hv);
+            };
+            // the last chunk: masked keys; kn (K one chunk past the end) is named by
+            // the wait
+            auto last = [&](int key0, f32x4 (&s)[NQ][2], bf16x8 (&kn)[2][2]) {
+                if (key0 + 32 > n) {
+#pragma unroll
+                    for (int qt = 0; qt < NQ; ++qt)
+#pragma unroll
+                        for (int t = 0; t < 2; ++t)
+#pragma unroll
+                            for (int r = 0; r < 4; ++r)
+                                if (key0 + 8 * g + 4 * t + r >= n) s[qt][t][r] = -INFINITY;
+                }
+                rescale(s);
+                uint2 hv[4][2];
+                read_v(key0, hv);
+                wait_all(kn, hv);
+                pv(s, hv);
+            };
+            bf16x8 kf[2][2];
+            f32x4 sa[NQ][2], sb[NQ][2];
+            read_k(0, kf);
+            asm volatile("s_waitcnt lgkmcnt(0)"
+                         : "+v"(kf[0][0]), "+v"(kf[0][1]), "+v"(kf[1][0]), "+v"(kf[1][1])
+                         :
+                         : "memory");
+            qk(kf, sa);
+            read_k(32, kf);
+            // two steps per iteration, so S^T alternates between sa and sb without copies
+            int key0 = 0;
+            for (; key0 + 64 < n; key0 += 64) {
+                step(key0, sa, sb, kf);
+                step(key0 + 32, sb, sa, kf);
+            }
+            if (key0 + 32 < n) {
+                step(key0, sa, sb, kf);
+                last(key0 + 32, sb, kf);
+            } else {
+                last(key0, sa, kf);
             }
 #pragma unroll
             for (int qt = 0; qt < NQ; ++qt) {
@@ -981,34 +1095,28 @@ attention_v3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
                 }
             }
         };
-        {
-#pragma unroll
-            for (int i = 0; i < 2; ++i) {
-                if (2 * i >= t_cnt) continue;
-                const int q_base = (t_first + 2 * i) * 16;
-                if (t_cnt - 2 * i >= 2)
-                    key_loop(std::integral_constant<int, 2>{}, qc[i], q_base);
-                else
-                    key_loop(std::integral_constant<int, 1>{}, qc[i], q_base);
-            }
+        // this wave's tiles, two at a time (documents past 8 x 32 queries, x 16 with
+        // qsel, take a second group, its Q loaded here)
+        for (int i = 0; 2 * i < t_cnt;) {
+            if (t_cnt - 2 * i >= 2)
+                key_loop(std::integral_constant<int, 2>{}, qc, (t_first + 2 * i) * 16);
+            else
+                key_loop(std::integral_constant<int, 1>{}, qc, (t_first + 2 * i) * 16);
+            if (2 * ++i >= t_cnt) break;
+            load_q_wait(p, i, qc);
         }
-        __syncthreads();  // every wave is done with buffer b before it is restaged
+        // !DB: every wave is done with the buffer before the next pair restages it (DB:
+        // the barrier at the top of the next pair orders buffer b's restaging, which
+        // is issued after it, behind every wave's reads of this pair)
+        if (!DB) __syncthreads();
     };
-    uint4 qa[2][QTB][2], qb2[2][QTB][2];
+    uint4 qc[QTB][2], qn[QTB][2];
     int p = blockIdx.x, b = 0;
     if (DB && p < n_pairs) {
         stage(p, 0);
-        load_q(p, qa);
+        load_q(p, qn);
     }
-    while (p < n_pairs) {
-        run_pair(p, b, qa, qb2);
-        p += gridDim.x;
-        b ^= (DB ? 1 : 0);
-        if (p >= n_pairs) break;
-        run_pair(p, b, qb2, qa);
-        p += gridDim.x;
-        b ^= (DB ? 1 : 0);
-    }
+    for (; p < n_pairs; p += gridDim.x, b ^= (DB ? 1 : 0)) run_pair(p, b, qc, qn);
 }
 
 bool attention_v3_ok(int max_len, int H) { return max_len <= 512 && H % ATT_D == 0; }
