@@ -632,9 +632,8 @@ void launch_attention_x3(const bf16 *qkv, const int32_t *cu_seqlens, int n_docs,
 // full max / rescale path runs on the first chunk and rarely after.
 // p = exp2(s * sc - m * sc) by the raw v_exp_f32 (inputs <= 8; underflow to 0 is
 // what softmax wants).
-__device__ __forceinline__ bool softmax_need(const f32x4 (&s)[2], float m) {
-    constexpr float sc = 0.125f * 1.4426950408889634f;
-    const float lim = m + 8.0f / sc;
+// lim = m + 8 / sc (kept by the caller, moved only with m)
+__device__ __forceinline__ bool softmax_need(const f32x4 (&s)[2], float lim) {
     bool need = false;
 #pragma unroll
     for (int t = 0; t < 2; ++t)
@@ -738,24 +737,31 @@ attention_v3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
     const uint32_t lds_base =
         (uint32_t)(uintptr_t)((__attribute__((address_space(3))) unsigned char *)lds);
 
-    // LDS-DMA of pair p's K and V rows < round32(n) into buffer b (rows past n repeat
-    // row n - 1; their scores are masked).  Slot j of row r lands at j ^ att3_swz(r).
+    // pair -> (doc, head): p / n_heads by a multiply-high (exact for p < 2^32 / n_heads)
+    const uint32_t heads_magic = 0xFFFFFFFFu / (uint32_t)n_heads + 1u;
+    auto doc_of = [&](int pp) { return (int)__umulhi((uint32_t)pp, heads_magic); };
+
+    // LDS-DMA of pair p's K and V rows < round32(n) into buffer b, through a buffer
+    // resource spanning the document's rows only: rows past n read zeros (their scores
+    // are masked, their probabilities 0).  Slot j of row r lands at j ^ att3_swz(r); a
+    // wave's pieces are all of one parity (pieces wave, wave + 8, ..; n8 is even), so
+    // the swizzle is a per-lane constant: r_in ^ ((wave & 1) << 2).
     auto stage = [&](int p, int b) {
-        const int doc = p / n_heads, h = p % n_heads;
+        const int doc = doc_of(p), h = p - doc * n_heads;
         const int tok0 = cu_seqlens[doc], n = cu_seqlens[doc + 1] - tok0;
-        const int nk8 = ((n + 31) & ~31) >> 3, nv8 = nk8;  // 8-row pieces
-        const int r_in = lane >> 3;                         // row within a piece
-        const bf16 *kbase = qkv + (int64_t)tok0 * ld + H + h * ATT_D;
-        const bf16 *vbase = qkv + (int64_t)tok0 * ld + 2 * H + h * ATT_D;
+        const int n8 = ((n + 31) & ~31) >> 3;  // 8-row pieces of K, and of V
+        const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(
+            (void *)(qkv + (int64_t)tok0 * ld), (short)0, n * ld * 2, 0x00020000);
+        const int r_in = lane >> 3;  // row within a piece
+        const uint32_t voff = r_in * ld * 2 + (H + h * ATT_D) * 2 +
+                              (((lane & 7) ^ r_in ^ ((wave & 1) << 2)) << 4);
         unsigned char *buf = lds + b * Att3<DB>::BUF;
-        for (int pc = wave; pc < nk8 + nv8; pc += ATT3_WAVES) {
-            const bool is_k = pc < nk8;
-            const int piece = is_k ? pc : pc - nk8;
-            const int r = min(piece * 8 + r_in, n - 1);
-            const int chunk = ((lane & 7) ^ att3_swz(piece * 8 + r_in)) * 8;  // source slot
-            const bf16 *src = (is_k ? kbase : vbase) + (int64_t)r * ld + chunk;
-            unsigned char *dst = buf + (is_k ? 0 : Att3<DB>::ROWS * 128) + piece * 1024;
-            __builtin_amdgcn_global_load_lds((const void *)src, (lds_void *)dst, 16, 0, 0);
+        for (int pc = wave; pc < 2 * n8; pc += ATT3_WAVES) {
+            const bool is_k = pc < n8;
+            const int piece = is_k ? pc : pc - n8;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                rsrc, (lds_void *)(buf + (is_k ? 0 : Att3<DB>::ROWS * 128) + piece * 1024), 16,
+                voff + piece * 8 * ld * 2 + (is_k ? 0 : H * 2), 0, 0, 0);
         }
     };
 
@@ -803,7 +809,7 @@ attention_v3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
     // Q row addresses of pair pp for this wave's tile group i (tiles t_first + 2 i,
     // + 2 i + 1): [qt][ch]
     auto q_srcs = [&](int pp, int i, const bf16 *(&src)[QTB][2]) {
-        const int dd = pp / n_heads, hh = pp % n_heads;
+        const int dd = doc_of(pp), hh = pp - dd * n_heads;
         const int t0 = cu_seqlens[dd], nn = cu_seqlens[dd + 1] - t0;
         const int qs0 = qsel ? cu_qsel[dd] : 0, nq = qsel ? cu_qsel[dd + 1] - qs0 : nn;
         int t_first, t_cnt;
@@ -870,7 +876,7 @@ attention_v3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
                 qc[qt][ch] = qn[qt][ch];
             }
         __syncthreads();
-        const int doc = p / n_heads, h = p % n_heads;
+        const int doc = doc_of(p), h = p - doc * n_heads;
         const int tok0 = cu_seqlens[doc], n = cu_seqlens[doc + 1] - tok0;
         const int qs0 = qsel ? cu_qsel[doc] : 0, nq = qsel ? cu_qsel[doc + 1] - qs0 : n;
         const int out0 = qsel ? qs0 : tok0;  // ctx row of query 0
@@ -898,38 +904,43 @@ attention_v3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
                 vb[a][bb] = vim + voff[a][bb];
                 asm volatile("" : "+v"(vb[a][bb]));
             }
-        // Fragment reads of the 32-key chunk at KEY0 (compile time: the row offset is
-        // the instruction's immediate, no address arithmetic per chunk).  Inline asm:
-        // the compiler must not drain the next pair's LDS-DMA with vmcnt(0) before
-        // them.  Issue and wait are separate statements; the wait names every register
-        // still being written ("+v"), so nothing touches one earlier
-        // (tools/asm_wait_scan.py checks the assembly).
-        auto read_k = [&](int key0, bf16x8 (&kf)[2][2]) {  // [t][ch]
+        // Fragment reads of the 32-key chunk at key0 + SUB: key0 (a multiple of 64, one
+        // address add per two chunks) in the address, SUB (compile time) and the row
+        // parts in the instruction's immediate.  Inline asm: the compiler must not drain
+        // the next pair's LDS-DMA with vmcnt(0) before them.  Issue and wait are
+        // separate statements; the wait names every register still being written
+        // ("+v"), so nothing touches one earlier (tools/asm_wait_scan.py checks the
+        // assembly).
+        using C0 = std::integral_constant<int, 0>;
+        using C32 = std::integral_constant<int, 32>;
+        auto read_k = [&](int key0, auto sub_c, bf16x8 (&kf)[2][2]) {  // [t][ch]
+            constexpr int OFF = decltype(sub_c)::value * 128;
             const uint32_t k0 = kb[0] + key0 * 128, k1 = kb[1] + key0 * 128;
             asm volatile(
-                "ds_read_b128 %0, %4\n\t"
-                "ds_read_b128 %1, %5\n\t"
-                "ds_read_b128 %2, %5 offset:512\n\t"
-                "ds_read_b128 %3, %4 offset:512"
+                "ds_read_b128 %0, %4 offset:%6\n\t"
+                "ds_read_b128 %1, %5 offset:%6\n\t"
+                "ds_read_b128 %2, %5 offset:%7\n\t"
+                "ds_read_b128 %3, %4 offset:%7"
                 : "=&v"(kf[0][0]), "=&v"(kf[0][1]), "=&v"(kf[1][0]), "=&v"(kf[1][1])
-                : "v"(k0), "v"(k1)
+                : "v"(k0), "v"(k1), "i"(OFF), "i"(OFF + 512)
                 : "memory");
         };
-        auto read_v = [&](int key0, uint2 (&hv)[4][2]) {  // [dt][h2]
+        auto read_v = [&](int key0, auto sub_c, uint2 (&hv)[4][2]) {  // [dt][h2]
+            constexpr int OFF = decltype(sub_c)::value * 128;
             const uint32_t v00 = vb[0][0] + key0 * 128, v01 = vb[0][1] + key0 * 128,
                            v10 = vb[1][0] + key0 * 128, v11 = vb[1][1] + key0 * 128;
             asm volatile(
-                "ds_read_b64_tr_b16 %0, %8\n\t"
-                "ds_read_b64_tr_b16 %1, %9 offset:512\n\t"
-                "ds_read_b64_tr_b16 %2, %10\n\t"
-                "ds_read_b64_tr_b16 %3, %11 offset:512\n\t"
-                "ds_read_b64_tr_b16 %4, %9\n\t"
-                "ds_read_b64_tr_b16 %5, %8 offset:512\n\t"
-                "ds_read_b64_tr_b16 %6, %11\n\t"
-                "ds_read_b64_tr_b16 %7, %10 offset:512"
+                "ds_read_b64_tr_b16 %0, %8 offset:%12\n\t"
+                "ds_read_b64_tr_b16 %1, %9 offset:%13\n\t"
+                "ds_read_b64_tr_b16 %2, %10 offset:%12\n\t"
+                "ds_read_b64_tr_b16 %3, %11 offset:%13\n\t"
+                "ds_read_b64_tr_b16 %4, %9 offset:%12\n\t"
+                "ds_read_b64_tr_b16 %5, %8 offset:%13\n\t"
+                "ds_read_b64_tr_b16 %6, %11 offset:%12\n\t"
+                "ds_read_b64_tr_b16 %7, %10 offset:%13"
                 : "=&v"(hv[0][0]), "=&v"(hv[0][1]), "=&v"(hv[1][0]), "=&v"(hv[1][1]),
                   "=&v"(hv[2][0]), "=&v"(hv[2][1]), "=&v"(hv[3][0]), "=&v"(hv[3][1])
-                : "v"(v00), "v"(v01), "v"(v10), "v"(v11)
+                : "v"(v00), "v"(v01), "v"(v10), "v"(v11), "i"(OFF), "i"(OFF + 512)
                 : "memory");
         };
         // counted waits naming the registers they retire ("+v"): LDS reads complete in
@@ -964,12 +975,13 @@ attention_v3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
         auto key_loop = [&](auto nq_c, const uint4 (&qf)[QTB][2], int q_base)
                             __attribute__((always_inline)) {
             constexpr int NQ = decltype(nq_c)::value;
-            float m[NQ], msc[NQ];
+            float m[NQ], msc[NQ], lim[NQ];
             f32x4 o[NQ][4], l[NQ];
 #pragma unroll
             for (int qt = 0; qt < NQ; ++qt) {
                 m[qt] = -INFINITY;
                 msc[qt] = -INFINITY;
+                lim[qt] = -INFINITY;
                 l[qt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
                 for (int dt = 0; dt < 4; ++dt) o[qt][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -996,13 +1008,16 @@ attention_v3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
                 bool need[NQ], need_any = false;
 #pragma unroll
                 for (int qt = 0; qt < NQ; ++qt) {
-                    need[qt] = softmax_need(s[qt], m[qt]);
+                    need[qt] = softmax_need(s[qt], lim[qt]);
                     need_any |= need[qt];
                 }
                 if (__any(need_any)) {  // rare after the first chunk
 #pragma unroll
                     for (int qt = 0; qt < NQ; ++qt)
-                        if (__any(need[qt])) softmax_rescale(s[qt], m[qt], msc[qt], o[qt], l[qt]);
+                        if (__any(need[qt])) {
+                            softmax_rescale(s[qt], m[qt], msc[qt], o[qt], l[qt]);
+                            lim[qt] = m[qt] + 8.0f / (0.125f * 1.4426950408889634f);
+                        }
                 }
             };
             auto pv = [&](const f32x4 (&s)[NQ][2], const uint2 (&hv)[4][2]) {
@@ -1024,60 +1039,63 @@ attention_v3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
                     l[qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pb[qt], l[qt], 0, 0, 0);
                 }
             };
-            // step at key0 (not the last chunk): s = S^T(key0) issued, kn = K(key0 + 32)
-            // in flight, reloaded in place with K(key0 + 64) once the S^T products have
-            // read it (MFMA A operands are read at issue; one chunk past the end reads
-            // stale rows of the image, never used); sn receives S^T(key0 + 32).  V(key0)
-            // is read inside the step (its latency hides behind the S^T products and the
-            // softmax).
-            auto step = [&](int key0, f32x4 (&s)[NQ][2], f32x4 (&sn)[NQ][2], bf16x8 (&kn)[2][2]) {
+            // step at chunk key0 + SUB (not the last chunk): s = S^T(chunk) issued,
+            // kn = K(chunk + 32) in flight, reloaded in place with K(chunk + 64) once the
+            // S^T products have read it (MFMA A operands are read at issue; one chunk
+            // past the end reads stale rows of the image, never used); sn receives
+            // S^T(chunk + 32).  V(chunk) is read inside the step (its latency hides
+            // behind the S^T products and the softmax).
+            auto step = [&](int key0, auto sub_c, f32x4 (&s)[NQ][2], f32x4 (&sn)[NQ][2],
+                            bf16x8 (&kn)[2][2]) {
                 rescale(s);
                 uint2 hv[4][2];
-                read_v(key0, hv);
+                read_v(key0, sub_c, hv);
                 wait_k(kn);
                 qk(kn, sn);
-                read_k(key0 + 64, kn);
+                read_k(key0, std::integral_constant<int, decltype(sub_c)::value + 64>{}, kn);
                 wait_v(hv, 0);
                 pv(s, hv);
             };
             // the last chunk: masked keys; kn (K one chunk past the end) is named by
             // the wait
-            auto last = [&](int key0, f32x4 (&s)[NQ][2], bf16x8 (&kn)[2][2]) {
-                if (key0 + 32 > n) {
+            auto last = [&](int key0, auto sub_c, f32x4 (&s)[NQ][2], bf16x8 (&kn)[2][2]) {
+                const int kc = key0 + decltype(sub_c)::value;
+                if (kc + 32 > n) {
 #pragma unroll
                     for (int qt = 0; qt < NQ; ++qt)
 #pragma unroll
                         for (int t = 0; t < 2; ++t)
 #pragma unroll
                             for (int r = 0; r < 4; ++r)
-                                if (key0 + 8 * g + 4 * t + r >= n) s[qt][t][r] = -INFINITY;
+                                if (kc + 8 * g + 4 * t + r >= n) s[qt][t][r] = -INFINITY;
                 }
                 rescale(s);
                 uint2 hv[4][2];
-                read_v(key0, hv);
+                read_v(key0, sub_c, hv);
                 wait_all(kn, hv);
                 pv(s, hv);
             };
             bf16x8 kf[2][2];
             f32x4 sa[NQ][2], sb[NQ][2];
-            read_k(0, kf);
+            read_k(0, C0{}, kf);
             asm volatile("s_waitcnt lgkmcnt(0)"
                          : "+v"(kf[0][0]), "+v"(kf[0][1]), "+v"(kf[1][0]), "+v"(kf[1][1])
                          :
                          : "memory");
             qk(kf, sa);
-            read_k(32, kf);
-            // two steps per iteration, so S^T alternates between sa and sb without copies
+            read_k(0, C32{}, kf);
+            // two steps per iteration: S^T alternates between sa and sb without copies,
+            // and the second step's addresses are the first's plus an immediate
             int key0 = 0;
             for (; key0 + 64 < n; key0 += 64) {
-                step(key0, sa, sb, kf);
-                step(key0 + 32, sb, sa, kf);
+                step(key0, C0{}, sa, sb, kf);
+                step(key0, C32{}, sb, sa, kf);
             }
             if (key0 + 32 < n) {
-                step(key0, sa, sb, kf);
-                last(key0 + 32, sb, kf);
+                step(key0, C0{}, sa, sb, kf);
+                last(key0, C32{}, sb, kf);
             } else {
-                last(key0, sa, kf);
+                last(key0, C0{}, sa, kf);
             }
 #pragma unroll
             for (int qt = 0; qt < NQ; ++qt) {
@@ -1133,6 +1151,8 @@ void launch_attention_v3(const bf16 *qkv, const int32_t *cu_seqlens, int n_docs,
         return v > 0 ? v : 256;
     }();
     const int n_heads = H / ATT_D, n_pairs = n_docs * n_heads;
+    // the kernel's pair -> document multiply-high is exact for pairs < 2^32 / n_heads
+    DI_REQUIRE((int64_t)n_pairs * n_heads < (1ll << 32), DI_ERANGE, "attention v3: %d pairs", n_pairs);
     const int grid = std::min(n_pairs, n_cu);
     auto launch = [&](auto kern, int lds_bytes) {
         DI_HIP(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
