@@ -262,7 +262,7 @@ attention_kernel(const T *__restrict__ qk, const T *__restrict__ vt,
 // (global_load_lds, every wave one 1 KiB piece of K and one of V) while chunk i is
 // computed, so every K / V byte is read from memory once per pass for the workgroup.
 //   K and V images (8 KiB each): key row r = the head's 256 B [ch0 hi | ch0 lo | ch1 hi
-//   | ch1 lo] (16-byte slots), slot j stored at j ^ (r & 15).
+//   | ch1 lo] (16-byte slots), slot j stored at j ^ ax_swz(r).
 //   S^T fragment row c of tile t = key 8 (c >> 2) + 4 t + (c & 3), so lane group g holds
 //   the consecutive keys 8 g..8 g + 7 of P^T (as attention_v3_kernel); the O^T A
 //   operand (V^T) is read from the V rows with ds_read_b64_tr_b16.
@@ -270,6 +270,13 @@ attention_kernel(const T *__restrict__ qk, const T *__restrict__ vt,
 // (the compiler would otherwise drain the in-flight prefetch with vmcnt(0) before an
 // LDS read it cannot tell apart from the DMA's destination).
 constexpr int AX_WAVES = 8, AX_QT = 2, AX_KC = 64;  // keys per staged chunk (2 x 32)
+// Image swizzle: slot j of key row r at j ^ ax_swz(r), ax_swz(r) = r0 r1 r3 in bits 1-3.
+// A ds_read_b128 lane group (16 lanes: rows c&3 + 8 (c>>2) + 4 t, slot bit 0 = g) and a
+// ds_read_b64_tr_b16 lane group (32 lanes: rows q + 8 g + 4 h2, slot bit 0 = p>>1)
+// then reach 16 distinct slots (every 256-byte row starts at bank 0): conflict-free
+// (r & 15 conflicts 2-way on both).  Row bit 5 (the 32-key sub-chunk) is not used, so
+// the sub-chunk stays an immediate offset.
+__device__ __forceinline__ int ax_swz(int r) { return ((r & 3) << 1) | (r & 8); }
 constexpr int AX_IMG = AX_KC * 256, AX_STAGE = 2 * AX_IMG;
 constexpr int AX_LDS = 2 * AX_STAGE;
 
@@ -323,7 +330,7 @@ attention_x3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
 #pragma unroll
         for (int pc = 0; pc < 2; ++pc) {
             const int row = u.tok0 + min(ci * AX_KC + sr + 4 * pc, u.n - 1);
-            const int j = (lane & 15) ^ ((sr + 4 * pc) & 15);
+            const int j = (lane & 15) ^ ax_swz(sr + 4 * pc);
             __builtin_amdgcn_global_load_lds(
                 (const void *)(kg + row * ld + j * 8),
                 (lds_void *)(lds + b * AX_STAGE + wave * 2048 + pc * 1024), 16, 0, 0);
@@ -357,7 +364,7 @@ attention_x3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
 #pragma unroll
             for (int pt = 0; pt < 2; ++pt) {
                 const int r = 8 * (c >> 2) + 4 * t + (c & 3), j = ch * 8 + pt * 4 + g;
-                ka[t][ch][pt] = lds_base + r * 256 + ((j ^ (r & 15)) << 4);
+                ka[t][ch][pt] = lds_base + r * 256 + ((j ^ ax_swz(r)) << 4);
             }
     // [dt][hi, lo][h2]: ds_read_b64_tr_b16 roles -- lane 4 q + p of a 16-lane group
     // addresses key row 8 g + 4 h2 + q, columns 16 dt + 4 p..+3 (one 8-byte half slot);
@@ -372,7 +379,7 @@ attention_x3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
                 const int q = c >> 2, pp = c & 3;
                 const int r = 8 * g + 4 * h2 + q;
                 const int j = (dt >> 1) * 8 + pt * 4 + 2 * (dt & 1) + (pp >> 1);
-                va[dt][pt][h2] = lds_base + AX_IMG + r * 256 + ((j ^ (r & 15)) << 4) + 8 * (pp & 1);
+                va[dt][pt][h2] = lds_base + AX_IMG + r * 256 + ((j ^ ax_swz(r)) << 4) + 8 * (pp & 1);
             }
 
     Unit cu;
