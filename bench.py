@@ -286,8 +286,8 @@ def flops_per_doc(n, H=768, L=12, t=None):
 
 
 def prune_last_layer():
-    """The bf16 term-output encode computes the last layer on the kept terms' rows only
-    (bit-identical impacts)."""
+    """The term-output encode (bf16 and bf16x3) computes the last layer on the kept
+    terms' rows only (bit-identical impacts)."""
     return True
 
 
@@ -347,7 +347,7 @@ def encode_leg(args, rank, world, dev, precision="bf16"):
     # O / FFN1 / FFN2 on the T term rows (QKV on all M)
     T = float(ct[-1])
     split = precision == "bf16x3"
-    prune = prune_last_layer() and not split  # the split forward computes every row
+    prune = prune_last_layer()
     Mp = ((L - 1) * M + T) / L if prune else M
     gemm_flops = {"gemm_qkv": 2 * M * H * 3 * H, "gemm_o": 2 * Mp * H * H,
                   "gemm_ffn1": 2 * Mp * H * F, "gemm_ffn2": 2 * Mp * F * H}

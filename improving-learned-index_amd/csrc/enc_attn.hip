@@ -282,7 +282,11 @@ constexpr int AX_LDS = 2 * AX_STAGE;
 
 __global__ void __launch_bounds__(64 * AX_WAVES)
 attention_x3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu_seqlens, int H,
-                    int n_heads, int n_pairs, bf16 *__restrict__ ctx_split) {
+                    int n_heads, int n_pairs, bf16 *__restrict__ ctx_split,
+                    const int32_t *__restrict__ qsel, const int32_t *__restrict__ cu_qsel) {
+    // qsel (optional, the pruned last layer): only the query rows qsel[cu_qsel[d] ..)
+    // (doc-local token indices) of document d are computed, into ctx rows cu_qsel[d] + i;
+    // keys and values are every token of the document either way.
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     typedef __attribute__((address_space(3))) void lds_void;
     const int tid = threadIdx.x, lane = tid & 63;
@@ -298,7 +302,7 @@ attention_x3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
     // next unit's Q and first K / V chunk load while the current unit's last chunk
     // computes.
     struct Unit {
-        int pair, pass, tok0, n, h;
+        int pair, pass, tok0, n, h, q0, nq;  // q0: ctx row of query 0; nq: queries
     };
     auto make_unit = [&](int pr, int pass, Unit &u) {
         const int doc = pr / n_heads;
@@ -307,17 +311,19 @@ attention_x3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
         u.h = pr % n_heads;
         u.tok0 = cu_seqlens[doc];
         u.n = cu_seqlens[doc + 1] - u.tok0;
+        u.q0 = qsel ? cu_qsel[doc] : u.tok0;
+        u.nq = qsel ? cu_qsel[doc + 1] - u.q0 : u.n;
     };
-    // the unit after `u` with at least one token, or false
+    // the unit after `u` with at least one token and one query, or false
     auto next_unit = [&](const Unit &u, Unit &nu) {
-        if ((u.pass + 1) * PASS_Q < u.n) {
+        if ((u.pass + 1) * PASS_Q < u.nq) {
             nu = u;
             nu.pass = u.pass + 1;
             return true;
         }
         for (int pr = u.pair + (int)gridDim.x; pr < n_pairs; pr += (int)gridDim.x) {
             make_unit(pr, 0, nu);
-            if (nu.n > 0) return true;
+            if (nu.n > 0 && nu.nq > 0) return true;
         }
         return false;
     };
@@ -346,7 +352,9 @@ attention_x3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
         const bf16 *qbase = qkv + split_col(u.h * ATT_D) + 8 * g;
 #pragma unroll
         for (int qt = 0; qt < AX_QT; ++qt) {
-            const int qrow = u.tok0 + min(q_base + 16 * qt + c, u.n - 1);
+            const int qi = min(q_base + 16 * qt + c, u.nq - 1);
+            const int qloc = qsel ? min(max(qsel[u.q0 + qi], 0), u.n - 1) : qi;
+            const int qrow = u.tok0 + qloc;
 #pragma unroll
             for (int ch = 0; ch < 2; ++ch) {
                 const bf16 *src = qbase + qrow * ld + ch * 64;
@@ -387,7 +395,7 @@ attention_x3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
         int pr = blockIdx.x;
         for (; pr < n_pairs; pr += (int)gridDim.x) {
             make_unit(pr, 0, cu);
-            if (cu.n > 0) break;
+            if (cu.n > 0 && cu.nq > 0) break;
         }
         if (pr >= n_pairs) return;
     }
@@ -396,9 +404,9 @@ attention_x3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
     stage(cu, 0, 0);
     int b = 0;  // stage buffer of the next chunk to compute
     for (;;) {
-        const int n = cu.n, tok0 = cu.tok0, h = cu.h;
+        const int n = cu.n, h = cu.h, q0 = cu.q0, nq = cu.nq;
         const int q_base = cu.pass * PASS_Q + wave * (AX_QT * 16);
-        const bool has_q = q_base < n;
+        const bool has_q = q_base < nq;
         const int n_chunks = (n + AX_KC - 1) / AX_KC;
         Unit nu;
         const bool more = next_unit(cu, nu);
@@ -585,8 +593,8 @@ attention_x3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
                 l += __shfl_xor(l, 32, 64);
                 const float inv = 1.0f / l;
                 const int q = q_base + 16 * qt + c;
-                if (q < n) {
-                    bf16 *out = ctx_split + (int64_t)(tok0 + q) * 2 * H;
+                if (q < nq) {
+                    bf16 *out = ctx_split + (int64_t)(q0 + q) * 2 * H;
 #pragma unroll
                     for (int dt = 0; dt < 4; ++dt) {
                         bf16x4 hv, lv;
@@ -619,7 +627,8 @@ attention_x3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
 }
 
 void launch_attention_x3(const bf16 *qkv, const int32_t *cu_seqlens, int n_docs, int H,
-                         bf16 *ctx_split, hipStream_t s) {
+                         bf16 *ctx_split, hipStream_t s, const int32_t *qsel,
+                         const int32_t *cu_qsel) {
     DI_REQUIRE(H % ATT_D == 0, DI_EINVAL, "hidden %d is not a multiple of the head dim 64", H);
     if (n_docs == 0) return;
     const int n_heads = H / ATT_D;
@@ -627,7 +636,7 @@ void launch_attention_x3(const bf16 *qkv, const int32_t *cu_seqlens, int n_docs,
     DI_REQUIRE(n_pairs < (1ll << 31), DI_ERANGE, "attention grid too large");
     const int grid = (int)std::min<int64_t>(n_pairs, n_cu());  // persistent, one per CU
     hipLaunchKernelGGL(attention_x3_kernel, dim3(grid), dim3(64 * AX_WAVES), AX_LDS, s, qkv,
-                       cu_seqlens, H, n_heads, (int)n_pairs, ctx_split);
+                       cu_seqlens, H, n_heads, (int)n_pairs, ctx_split, qsel, cu_qsel);
     check_launch("attention_x3");
 }
 

@@ -97,6 +97,39 @@ __device__ __forceinline__ void gelu_erf8(float (&v)[8]) {
 #undef DI_C2
 }
 
+// GELU for bf16 outputs: x * sigmoid(x P(x^2)) with P a cubic fitted to
+// logit(Phi(x)) / x (the tanh form's quadratic refined), as x / (1 + 2^(x P'(x^2))),
+// P' = -P log2(e).  |error| <= 1.1e-4 absolute and <= 6.6e-4 relative to max(|gelu|,
+// 1e-3) -- a third of a bf16 output's rounding step -- in 7 packed ops and 4
+// transcendentals per pair (gelu_erf8: 16 packed, 4 max/min, 2 transcendentals).
+// Large |x|: 2^(+inf) -> rcp 0 -> -0 (x < 0), 2^(-inf) = 0 -> x (x > 0), as gelu.
+// Only the bf16 epilogues use it; the fp32-faithful (split) outputs keep gelu_erf8.
+__device__ __forceinline__ void gelu_bf16_8(float (&v)[8]) {
+#define DI_C2(c) f32x2{c, c}
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const f32x2 x = f32x2{v[2 * i], v[2 * i + 1]};
+        const f32x2 x2 = x * x;
+        f32x2 p = __builtin_elementwise_fma(x2, DI_C2(-5.821808827022323e-06f),
+                                            DI_C2(0.001257223659195006f));
+        p = __builtin_elementwise_fma(x2, p, DI_C2(-0.10838031768798828f));
+        p = __builtin_elementwise_fma(x2, p, DI_C2(-2.29897403717041f));
+        const f32x2 z = x * p;
+        const f32x2 d = f32x2{__builtin_amdgcn_exp2f(z.x), __builtin_amdgcn_exp2f(z.y)} +
+                        DI_C2(1.0f);
+        const f32x2 y = x * f32x2{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+        v[2 * i] = y.x;
+        v[2 * i + 1] = y.y;
+    }
+#undef DI_C2
+}
+
+__device__ __forceinline__ float gelu_bf16(float x) {
+    float v[8] = {x, x, x, x, x, x, x, x};
+    gelu_bf16_8(v);
+    return v[0];
+}
+
 // GEMM epilogues
 enum GemmEpi : int {
     EPI_BIAS = 0,        // out(T) = acc + bias

@@ -204,7 +204,7 @@ __global__ void __launch_bounds__(G_THREADS) gemm_nt_kernel(GemmArgs g) {
                     for (int j = 0; j < 4; ++j) {
                         const int lr = mt * 16 + (lane >> 4) * 4 + j;  // row within the pass
                         float v = acc[mt][nt][j] + bias_v[nt];
-                        if constexpr (EPI == EPI_BIAS_GELU) v = gelu_erf(v);
+                        if constexpr (EPI == EPI_BIAS_GELU) v = std::is_same<T, bf16>::value ? gelu_bf16(v) : gelu_erf(v);
                         *reinterpret_cast<StT *>(ot + lr * RS + lc * SE) = from_f32<StT>(v);
                     }
                 }

@@ -586,7 +586,10 @@ __global__ void __launch_bounds__(G2_T) gemm256_kernel(GemmArgs g) {
                             v[e] = fmaf(ra[mt], acc[mt][2 * h + (e >> 2)][e & 3],
                                         fmaf(rb[mt], cs2[h][e], bias_v[h][e]));
                         if constexpr (EPI == EPI_FOLD_GELU) {
-                            if (!(g.ablate & 2)) gelu_erf8(v);
+                            if (!(g.ablate & 2)) {
+                                if (g.ablate & 8) gelu_erf8(v);  // (A/B: the erf form)
+                                else gelu_bf16_8(v);
+                            }
                         }
                         bf16x8 o;
 #pragma unroll
@@ -621,7 +624,10 @@ __global__ void __launch_bounds__(G2_T) gemm256_kernel(GemmArgs g) {
                                                          : acc[mt][2 * h + (e >> 2)][e & 3] +
                                                                bias_v[h][e];
                         if constexpr (EPI == EPI_BIAS_GELU) {
-                            if (!(g.ablate & 2)) gelu_erf8(v);
+                            if (!(g.ablate & 2)) {
+                                if (SPLIT || (g.ablate & 8)) gelu_erf8(v);
+                                else gelu_bf16_8(v);
+                            }
                         }
                         if (g.ablate & 4) continue;
                         char *op = ob + (int64_t)mt * 16 * g.ld_out * ESZ + h * HSTEP + olo;

@@ -32,7 +32,8 @@ void launch_attention(const T *qk, const T *vt, const int32_t *cu_seqlens, int n
                       bf16 *ctx_split = nullptr);
 void launch_gemm256(int epi, const GemmArgs &g, hipStream_t s);
 void launch_attention_x3(const bf16 *qkv, const int32_t *cu_seqlens, int n_docs, int H,
-                         bf16 *ctx_split, hipStream_t s);
+                         bf16 *ctx_split, hipStream_t s, const int32_t *qsel = nullptr,
+                         const int32_t *cu_qsel = nullptr);
 void launch_embed_ln_split(const int32_t *ids, const int32_t *cu, int n_docs, int M, int H,
                            const float *word, const float *pos, const float *type0,
                            const float *gamma, const float *beta, float eps, int pos_offset,
@@ -583,8 +584,13 @@ void forward_folded(di_encoder *e, const int32_t *d_ids, const int32_t *d_cu, in
 // bf16 products too (attention_x3_kernel; f32 softmax), LayerNorms in f32 from f32
 // pre-LN rows.  Activations that feed a GEMM or the attention products are split
 // rows (Q | K and V^T included); the pre-LN rows are f32.
+// Pruned last layer (d_tt != nullptr), as forward_folded: after the last QKV projection
+// only the terms' first-token rows are computed (attention queries, O / FFN GEMMs,
+// LayerNorms, head), packed -- the same arithmetic per kept row, bit-identical impacts.
 void forward_split(di_encoder *e, const int32_t *d_ids, const int32_t *d_cu, int n_docs,
-                   int64_t M, int max_len, bool timing, hipStream_t s) {
+                   int64_t M, int max_len, bool timing, hipStream_t s,
+                   const int32_t *d_tt = nullptr, const int32_t *d_ct = nullptr,
+                   int64_t n_terms = 0) {
     const auto &c = e->cfg;
     const int H = c.hidden, F = c.intermediate;
     const int pos_offset = (c.variant == DI_VARIANT_XLMR) ? c.pad_id + 1 : 0;
@@ -621,15 +627,29 @@ void forward_split(di_encoder *e, const int32_t *d_ids, const int32_t *d_cu, int
             TimedLaunch tl(e->timer, timing, "gemm_qkv", s);
             launch_gemm256(EPI_BIAS, g, s);
         }
+        const bool prune = last && d_tt != nullptr;
+        const int64_t Mr = prune ? n_terms : M;  // rows from here on
+        bf16 *Xr = X;                             // the O GEMM's residual rows
         {
             TimedLaunch tl(e->timer, timing, "attention", s);
-            launch_attention_x3(e->qk.as<bf16>(), d_cu, n_docs, H, ctx, s);
+            launch_attention_x3(e->qk.as<bf16>(), d_cu, n_docs, H, ctx, s,
+                                prune ? d_tt : nullptr, prune ? d_ct : nullptr);
         }
-        g = base();
+        if (prune) {  // the terms' residual rows, packed into Hff (free until FFN1)
+            TimedLaunch tl(e->timer, timing, "gather_rows", s);
+            Xr = e->Hff.as<bf16>();
+            launch_gather_term_rows(X, nullptr, d_cu, d_ct, d_tt, n_docs, 2 * H, Xr, nullptr, s);
+        }
+        auto base_r = [&]() {
+            GemmArgs gr = base();
+            gr.M = (int)Mr;
+            return gr;
+        };
+        g = base_r();
         g.A = ctx;
         g.B = L.w_o.p;
         g.bias = L.b_o.as<float>();
-        g.resid = X;
+        g.resid = Xr;
         g.out = pre;
         g.N = H;
         g.K = H;
@@ -640,10 +660,10 @@ void forward_split(di_encoder *e, const int32_t *d_ids, const int32_t *d_cu, int
         }
         {
             TimedLaunch tl(e->timer, timing, "ln", s);
-            launch_ln_split(pre, (int)M, H, L.ln1_g.as<float>(), L.ln1_b.as<float>(),
+            launch_ln_split(pre, (int)Mr, H, L.ln1_g.as<float>(), L.ln1_b.as<float>(),
                             c.layer_norm_eps, X1, nullptr, 0.f, c.activation, nullptr, s);
         }
-        g = base();
+        g = base_r();
         g.A = X1;
         g.B = L.w_i.p;
         g.bias = L.b_i.as<float>();
@@ -655,7 +675,7 @@ void forward_split(di_encoder *e, const int32_t *d_ids, const int32_t *d_cu, int
             TimedLaunch tl(e->timer, timing, "gemm_ffn1", s);
             launch_gemm256(EPI_BIAS_GELU, g, s);
         }
-        g = base();
+        g = base_r();
         g.A = e->Hff.p;
         g.B = L.w_out.p;
         g.bias = L.b_out.as<float>();
@@ -671,7 +691,7 @@ void forward_split(di_encoder *e, const int32_t *d_ids, const int32_t *d_cu, int
         }
         {
             TimedLaunch tl(e->timer, timing, "ln", s);
-            launch_ln_split(pre, (int)M, H, L.ln2_g.as<float>(), L.ln2_b.as<float>(),
+            launch_ln_split(pre, (int)Mr, H, L.ln2_g.as<float>(), L.ln2_b.as<float>(),
                             c.layer_norm_eps, last ? nullptr : X,
                             last ? e->head_w.as<float>() : nullptr, e->head_b, c.activation,
                             last ? e->impact.as<float>() : nullptr, s);
@@ -885,12 +905,13 @@ int di_encode(di_encoder *e, const int32_t *tok_ids, const int32_t *cu_seqlens, 
             d_tt = (const int32_t *)stage_in(term_tok, (size_t)n_terms * 4, dev, e->tt, s);
             d_cut = (const int32_t *)stage_in(cu_terms, (size_t)(n_docs + 1) * 4, dev, e->cut, s);
         }
-        // pruned last layer (bf16 folded path, term output)
-        const bool prune = !token_out && e->esz == 2 && e->folded &&
+        // pruned last layer (bf16 folded and bf16x3 paths, term output)
+        const bool prune = !token_out && (e->split || (e->esz == 2 && e->folded)) &&
                            n_terms <= n_tokens;  // (packed term rows fit the row buffers)
         if (n_tokens > 0) {
             if (e->split)
-                forward_split(e, d_ids, d_cu, n_docs, n_tokens, max_len, timing, s);
+                forward_split(e, d_ids, d_cu, n_docs, n_tokens, max_len, timing, s,
+                              prune ? d_tt : nullptr, prune ? d_cut : nullptr, n_terms);
             else if (e->esz == 2)
                 if (e->folded)
                     forward_folded(e, d_ids, d_cu, n_docs, n_tokens, max_len, timing, s,

@@ -106,6 +106,33 @@ def test_bf16x3_ragged_batches_match_torch_oracle(E, base, lens):
     np.testing.assert_allclose(got, want, rtol=RTOL, atol=1e-6)
 
 
+def test_bf16x3_pruned_last_layer_is_bitexact(E, base):
+    """Term output computes the last layer only for the terms' first-token rows (queries
+    of the attention, O / FFN GEMMs, LayerNorms, head); each kept row's arithmetic is
+    unchanged, so the impacts must equal the full per-token forward gathered at those
+    rows, bit for bit -- ragged documents past one 256-query pass, a document without
+    terms, terms in any order and repeated."""
+    fx, sd = base
+    enc = E.DeviceEncoder(sd, _cfg(E, fx), precision="bf16x3")
+    rng = np.random.default_rng(12)
+    lens = [512, 300, 2, 64, 9, 180, 120, 33]
+    pad, mask = _random_batch(rng, lens, 250002)
+    ids, cu = _pack(pad.tolist(), mask.tolist())
+    tok = enc.encode_packed(ids, cu, token_impacts=True)
+    tt, ct = [], [0]
+    for d, n in enumerate(lens):
+        k = 0 if d == 2 else (n if d == 0 else int(rng.integers(1, n + 1)))
+        pos = rng.choice(n, size=k, replace=False)
+        if d == 3:
+            pos = np.concatenate([pos, pos[:2]])  # repeated token positions
+        tt += pos.tolist()
+        ct.append(len(tt))
+    tt, ct = np.array(tt, np.int32), np.array(ct, np.int32)
+    want = np.array([tok[cu[d] + tt[j]] for d in range(len(lens)) for j in range(ct[d], ct[d + 1])],
+                    np.float32)
+    np.testing.assert_array_equal(enc.encode_packed(ids, cu, tt, ct), want)
+
+
 def _outlier_sd(sd):
     """Outlier LayerNorm channels in every LayerNorm: large beta and gamma on three
     channels, so the residual stream carries rows with |mean| / sigma >> 1."""

@@ -187,7 +187,7 @@ int main(int argc, char **argv) {
         for (int i = 0; i < 4; ++i) {
             const Case &c = bench[i];
             const double flops = 2.0 * c.M * c.N * c.K;
-            for (int abl : {0, 6, 102, 104, 116}) {  // 1xx: full epilogue, tile group xx
+            for (int abl : {0, 6, 8, 102, 104, 116}) {  // 1xx: full epilogue, tile group xx; 8: erf GELU
                 for (int stg : {0}) {
                     const int gm = abl >= 100 ? abl - 100 : 8;
                     GemmArgs g = args(c, O1, V1, true);
