@@ -70,8 +70,7 @@ __device__ __forceinline__ void g2_store(bf16 *p, const bf16x8 &v) {
 // EPI_RESID_STATS stores with its row statistics, before the prefetch: none in flight.
 template <int EPI, bool SPLIT>
 constexpr int g2_stores() {
-    return EPI == EPI_RESID_STATS ? 0
-           : (SPLIT && EPI != EPI_FOLD && EPI != EPI_FOLD_GELU) ? 32 : 16;
+    return EPI == EPI_RESID_STATS ? 0 : SPLIT ? 32 : 16;
 }
 
 #define G2_BAR() asm volatile("s_barrier" ::: "memory")
@@ -475,31 +474,57 @@ __global__ void __launch_bounds__(G2_T) gemm256_kernel(GemmArgs g) {
                         rs[mt] = p.y;
                     }
                 }
-                const char *rbase = static_cast<const char *>(g.resid) + (row_w * N + col_w) * 2;
-                const uint32_t rlo = lane_off(N, 2);
-                char *ob = static_cast<char *>(g.out) + (row_w * g.ld_out + col_w) * 2;
+                // (SPLIT: resid and out are split rows, stride 2N, every 32 columns 32 hi
+                // then 32 lo; the statistics are those of hi + lo, the value the
+                // consumer GEMMs read)
+                const int rld = SPLIT ? 2 * N : N;
+                constexpr int HS = SPLIT ? 128 : 64;  // bytes per 32 columns
+                const char *rbase = static_cast<const char *>(g.resid) +
+                                    (row_w * rld + (SPLIT ? 2 * col_w : col_w)) * 2;
+                const uint32_t rlo = lane_off(rld, 2);
+                char *ob = static_cast<char *>(g.out) +
+                           (row_w * g.ld_out + (SPLIT ? 2 * col_w : col_w)) * 2;
                 const uint32_t olo = lane_off(g.ld_out, 2);
 #pragma unroll
                 for (int mt = 0; mt < 8; ++mt) {
                     if (!FULL && row_l + mt * 16 >= M) continue;
 #pragma unroll
                     for (int h = 0; h < 2; ++h) {
-                        const bf16x8 rv = *reinterpret_cast<const bf16x8 *>(
-                            rbase + (int64_t)mt * 16 * N * 2 + h * 64 + rlo);
-                        bf16x8 o;
+                        const char *rp = rbase + (int64_t)mt * 16 * rld * 2 + h * HS + rlo;
+                        float r[8];
+                        if constexpr (SPLIT) {
+                            const bf16x8 rh = *reinterpret_cast<const bf16x8 *>(rp);
+                            const bf16x8 rl = *reinterpret_cast<const bf16x8 *>(rp + 64);
+#pragma unroll
+                            for (int e = 0; e < 8; ++e) r[e] = (float)rh[e] + (float)rl[e];
+                        } else {
+                            const bf16x8 rv = *reinterpret_cast<const bf16x8 *>(rp);
+#pragma unroll
+                            for (int e = 0; e < 8; ++e) r[e] = (float)rv[e];
+                        }
+                        bf16x8 o, ol;
 #pragma unroll
                         for (int e = 0; e < 8; ++e) {
-                            const float res = fmaf(gm[h][e], fmaf(rr[mt], (float)rv[e], rs[mt]), bt[h][e]);
-                            o[e] = (bf16)(acc[mt][2 * h + (e >> 2)][e & 3] + bias_v[h][e] + res);
-                            const float yb = (float)o[e];
+                            const float res = fmaf(gm[h][e], fmaf(rr[mt], r[e], rs[mt]), bt[h][e]);
+                            const float y = acc[mt][2 * h + (e >> 2)][e & 3] + bias_v[h][e] + res;
+                            float yb;
+                            if constexpr (SPLIT) {
+                                o[e] = split_hi(y);
+                                ol[e] = split_lo(y);
+                                yb = (float)o[e] + (float)ol[e];
+                            } else {
+                                o[e] = (bf16)y;
+                                yb = (float)o[e];
+                            }
                             ss[mt] += yb;
                             sq[mt] = fmaf(yb, yb, sq[mt]);
                             sd[mt] = fmaf(yb, wg[h][e], sd[mt]);
                         }
-                        if (!(g.ablate & 4))
-                            g2_store(reinterpret_cast<bf16 *>(ob + (int64_t)mt * 16 * g.ld_out * 2 +
-                                                              h * 64 + olo),
-                                     o);
+                        if (!(g.ablate & 4)) {
+                            char *op = ob + (int64_t)mt * 16 * g.ld_out * 2 + h * HS + olo;
+                            g2_store(reinterpret_cast<bf16 *>(op), o);
+                            if constexpr (SPLIT) g2_store(reinterpret_cast<bf16 *>(op + 64), ol);
+                        }
                     }
                 }
                 // partials: the 4 lane groups (lanes l, l^16, l^32, l^48 share a row),
@@ -572,7 +597,10 @@ __global__ void __launch_bounds__(G2_T) gemm256_kernel(GemmArgs g) {
                 // LN folded into this GEMM: y = r acc - r mu s + c  (per row r, mu; per
                 // column s, c); row-major order: both 64-byte halves of a row's 128-byte
                 // segment are stored by consecutive instructions
-                char *ob = static_cast<char *>(g.out) + (row_w * g.ld_out + col_w) * 2;
+                // (SPLIT: A holds split rows of the un-normalised x, the output split rows)
+                constexpr int HS = SPLIT ? 128 : 64;  // bytes per 32 columns
+                char *ob = static_cast<char *>(g.out) +
+                           (row_w * g.ld_out + (SPLIT ? 2 * col_w : col_w)) * 2;
                 const uint32_t olo = lane_off(g.ld_out, 2);
 #pragma unroll
                 for (int mt = 0; mt < 8; ++mt) {
@@ -587,17 +615,24 @@ __global__ void __launch_bounds__(G2_T) gemm256_kernel(GemmArgs g) {
                                         fmaf(rb[mt], cs2[h][e], bias_v[h][e]));
                         if constexpr (EPI == EPI_FOLD_GELU) {
                             if (!(g.ablate & 2)) {
-                                if (g.ablate & 8) gelu_erf8(v);  // (A/B: the erf form)
+                                if (SPLIT || (g.ablate & 8)) gelu_erf8(v);  // (A/B: the erf form)
                                 else gelu_bf16_8(v);
                             }
                         }
-                        bf16x8 o;
+                        if (g.ablate & 4) continue;
+                        char *op = ob + (int64_t)mt * 16 * g.ld_out * 2 + h * HS + olo;
+                        if constexpr (SPLIT) {
+                            bf16x8 hv, lv;
 #pragma unroll
-                        for (int e = 0; e < 8; ++e) o[e] = (bf16)v[e];
-                        if (!(g.ablate & 4))
-                            g2_store(reinterpret_cast<bf16 *>(ob + (int64_t)mt * 16 * g.ld_out * 2 +
-                                                              h * 64 + olo),
-                                     o);
+                            for (int e = 0; e < 8; ++e) hv[e] = split_hi(v[e]), lv[e] = split_lo(v[e]);
+                            g2_store(reinterpret_cast<bf16 *>(op), hv);
+                            g2_store(reinterpret_cast<bf16 *>(op + 64), lv);
+                        } else {
+                            bf16x8 o;
+#pragma unroll
+                            for (int e = 0; e < 8; ++e) o[e] = (bf16)v[e];
+                            g2_store(reinterpret_cast<bf16 *>(op), o);
+                        }
                     }
                 }
             } else if constexpr (RS) {
@@ -678,8 +713,7 @@ __global__ void __launch_bounds__(G2_T) gemm256_kernel(GemmArgs g) {
 // Shapes the 8-phase kernel takes; everything else goes to the 128x128 kernel.
 bool gemm256_ok(int epi, const GemmArgs &g) {
     const int64_t m_pad = ((int64_t)g.M + G2_TILE - 1) / G2_TILE * G2_TILE;
-    if (g.split && !(epi == EPI_BIAS || epi == EPI_BIAS_GELU || epi == EPI_BIAS_RESID))
-        return false;
+    if (g.split && epi == EPI_QKV) return false;
     // (SPLIT: K tiles of 32 logical k, K % 64 == 0 keeps their count even)
     return g.N % G2_TILE == 0 && g.K % (g.split ? 64 : 128) == 0 && g.K >= 128 &&
            g.a_rows >= m_pad &&
@@ -711,6 +745,9 @@ void launch_gemm256(int epi, const GemmArgs &g, hipStream_t s) {
             G2_SCASE(EPI_BIAS)
             G2_SCASE(EPI_BIAS_GELU)
             G2_SCASE(EPI_BIAS_RESID)
+            G2_SCASE(EPI_FOLD)
+            G2_SCASE(EPI_FOLD_GELU)
+            G2_SCASE(EPI_RESID_STATS)
 #undef G2_SCASE
             default:
                 fail(DI_EINVAL, "bad split GEMM epilogue");

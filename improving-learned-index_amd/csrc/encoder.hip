@@ -156,10 +156,12 @@ struct HostTensor {
 void fold_upload(DevBuf &w_dst, DevBuf &s_dst, DevBuf &c_dst,
                  const std::vector<const HostTensor *> &w_parts,
                  const std::vector<const HostTensor *> &b_parts, int K, const HostTensor *gamma,
-                 const HostTensor *beta) {
+                 const HostTensor *beta, bool split = false) {
+    // split: W' as split rows (upload_split3's layout), s summed from hi + lo (the
+    // weights the split GEMM multiplies by)
     int64_t rows = 0;
     for (auto *p : w_parts) rows += p->numel() / K;
-    std::vector<uint16_t> w((size_t)(rows * K));
+    std::vector<uint16_t> w((size_t)(rows * K * (split ? 2 : 1)));
     std::vector<float> sv((size_t)rows), cv((size_t)rows);
     std::vector<float> gm((size_t)K), bt((size_t)K);
     for (int k = 0; k < K; ++k) {
@@ -173,9 +175,17 @@ void fold_upload(DevBuf &w_dst, DevBuf &s_dst, DevBuf &c_dst,
             double s = 0.0, c = 0.0;
             for (int k = 0; k < K; ++k) {
                 const float wv = p->at(i * K + k);
-                const uint16_t wb = f32_to_bf16_bits(wv * gm[(size_t)k]);
-                w[(size_t)(r * K + k)] = wb;
-                s += (double)bf16_bits_to_f32(wb);
+                const float wg = wv * gm[(size_t)k];
+                const uint16_t wb = f32_to_bf16_bits(wg);
+                if (split) {
+                    const uint16_t lo = f32_to_bf16_bits(wg - bf16_bits_to_f32(wb));
+                    w[(size_t)(r * 2 * K + split_col(k))] = wb;
+                    w[(size_t)(r * 2 * K + split_col(k) + 32)] = lo;
+                    s += (double)bf16_bits_to_f32(wb) + (double)bf16_bits_to_f32(lo);
+                } else {
+                    w[(size_t)(r * K + k)] = wb;
+                    s += (double)bf16_bits_to_f32(wb);
+                }
                 c += (double)wv * (double)bt[(size_t)k];
             }
             sv[(size_t)r] = (float)s;
@@ -419,7 +429,7 @@ void forward(di_encoder *e, const int32_t *d_ids, const int32_t *d_cu, int n_doc
     }
 }
 
-// bf16 forward with every LayerNorm after the embeddings folded into its consumers
+// bf16 / bf16x3 forward with every LayerNorm after the embeddings folded into its consumers
 // (EPI_FOLD* / EPI_RESID_STATS, see enc_common.h): no LayerNorm pass over the
 // activations.  Buffers: X holds the layer input (the normalised embeddings, then
 // the un-normalised FFN output P2 of the previous layer), X1 the attention-block
@@ -437,18 +447,34 @@ void forward_folded(di_encoder *e, const int32_t *d_ids, const int32_t *d_cu, in
     const auto &c = e->cfg;
     const int H = c.hidden, F = c.intermediate;
     const int pos_offset = (c.variant == DI_VARIANT_XLMR) ? c.pad_id + 1 : 0;
-    DI_REQUIRE(attention_v3_ok(max_len, H), DI_EINVAL, "max_len %d > 512", max_len);
+    // sp (bf16x3): activations are split rows (row stride 2W), GEMMs split-bf16,
+    // attention attention_x3_kernel
+    const bool sp = e->split;
+    const int W2 = sp ? 2 : 1;
+    if (!sp) DI_REQUIRE(attention_v3_ok(max_len, H), DI_EINVAL, "max_len %d > 512", max_len);
     bf16 *X = e->X.as<bf16>(), *X1 = e->X1.as<bf16>();
     float4 *st1 = e->stats1.as<float4>(), *st2 = e->stats2.as<float4>();
     float2 *rl1 = e->rln1.as<float2>(), *rl2 = e->rln2.as<float2>();
     const int ld = (int)e->cap_rows, n_part = H / gemm_stats_cols();
     {
         TimedLaunch tl(e->timer, timing, "embed_ln", s);
-        launch_embed_ln<bf16>(d_ids, d_cu, n_docs, (int)M, H, e->word.as<bf16>(),
-                              e->pos.as<bf16>(), e->type0.as<bf16>(), e->emb_g.as<float>(),
-                              e->emb_b.as<float>(), c.layer_norm_eps, pos_offset, c.vocab_size,
-                              c.max_positions, X, e->err.as<int32_t>(), s);
+        if (sp)
+            launch_embed_ln_split(d_ids, d_cu, n_docs, (int)M, H, e->word.as<float>(),
+                                  e->pos.as<float>(), e->type0.as<float>(), e->emb_g.as<float>(),
+                                  e->emb_b.as<float>(), c.layer_norm_eps, pos_offset,
+                                  c.vocab_size, c.max_positions, X, e->err.as<int32_t>(), s);
+        else
+            launch_embed_ln<bf16>(d_ids, d_cu, n_docs, (int)M, H, e->word.as<bf16>(),
+                                  e->pos.as<bf16>(), e->type0.as<bf16>(), e->emb_g.as<float>(),
+                                  e->emb_b.as<float>(), c.layer_norm_eps, pos_offset,
+                                  c.vocab_size, c.max_positions, X, e->err.as<int32_t>(), s);
     }
+    auto gemm = [&](int epi, const GemmArgs &g) {
+        if (sp)
+            launch_gemm256(epi, g, s);
+        else
+            launch_gemm<bf16>(epi, g, s);
+    };
     auto base = [&]() {
         GemmArgs g{};
         // tile-order group: 8 M-tiles (measured +4% QKV, +1% O / FFN1 over 4); FFN2
@@ -461,6 +487,7 @@ void forward_folded(di_encoder *e, const int32_t *d_ids, const int32_t *d_cu, in
         g.n_part = n_part;
         g.ln_h = H;
         g.ln_eps = c.layer_norm_eps;
+        g.split = sp ? 1 : 0;
         return g;
     };
     for (size_t l = 0; l < e->layers.size(); ++l) {
@@ -475,7 +502,7 @@ void forward_folded(di_encoder *e, const int32_t *d_ids, const int32_t *d_cu, in
         g.out = e->qk.p;
         g.N = 3 * H;
         g.K = H;
-        g.ld_out = 3 * H;
+        g.ld_out = 3 * H * W2;
         if (P) {
             g.row_ln = rl2;
             g.col_s = L.s_qkv.as<float>();
@@ -483,7 +510,7 @@ void forward_folded(di_encoder *e, const int32_t *d_ids, const int32_t *d_cu, in
         }
         {
             TimedLaunch tl(e->timer, timing, "gemm_qkv", s);
-            launch_gemm<bf16>(P ? EPI_FOLD : EPI_BIAS, g, s);
+            gemm(P ? EPI_FOLD : EPI_BIAS, g);
         }
         const bool prune = last && d_tt != nullptr;
         const int64_t Mr = prune ? n_terms : M;  // rows from here on
@@ -491,13 +518,18 @@ void forward_folded(di_encoder *e, const int32_t *d_ids, const int32_t *d_cu, in
         const float2 *rl2r = rl2;
         {
             TimedLaunch tl(e->timer, timing, "attention", s);
-            launch_attention_v3(e->qk.as<bf16>(), d_cu, n_docs, max_len, H, e->ctx.as<bf16>(), s,
-                                prune ? d_tt : nullptr, prune ? d_ct : nullptr);
+            if (sp)
+                launch_attention_x3(e->qk.as<bf16>(), d_cu, n_docs, H, e->ctx.as<bf16>(), s,
+                                    prune ? d_tt : nullptr, prune ? d_ct : nullptr);
+            else
+                launch_attention_v3(e->qk.as<bf16>(), d_cu, n_docs, max_len, H,
+                                    e->ctx.as<bf16>(), s, prune ? d_tt : nullptr,
+                                    prune ? d_ct : nullptr);
         }
         if (prune) {  // the terms' residual rows (and LN2 parameters), packed: Hff / rl1
             TimedLaunch tl(e->timer, timing, "gather_rows", s);  // are free until later
             Xr = e->Hff.as<bf16>();
-            launch_gather_term_rows(X, P ? rl2 : nullptr, d_cu, d_ct, d_tt, n_docs, H, Xr,
+            launch_gather_term_rows(X, P ? rl2 : nullptr, d_cu, d_ct, d_tt, n_docs, H * W2, Xr,
                                     rl1, s);
             rl2r = rl1;
         }
@@ -515,7 +547,7 @@ void forward_folded(di_encoder *e, const int32_t *d_ids, const int32_t *d_cu, in
         g.out = X1;
         g.N = H;
         g.K = H;
-        g.ld_out = H;
+        g.ld_out = H * W2;
         g.stats_out = st1;
         if (P) {
             g.row_ln = rl2r;
@@ -524,7 +556,7 @@ void forward_folded(di_encoder *e, const int32_t *d_ids, const int32_t *d_cu, in
         }
         {
             TimedLaunch tl(e->timer, timing, "gemm_o", s);
-            launch_gemm<bf16>(EPI_RESID_STATS, g, s);
+            gemm(EPI_RESID_STATS, g);
         }
         {
             TimedLaunch tl(e->timer, timing, "row_ln", s);
@@ -537,13 +569,13 @@ void forward_folded(di_encoder *e, const int32_t *d_ids, const int32_t *d_cu, in
         g.out = e->Hff.p;
         g.N = F;
         g.K = H;
-        g.ld_out = F;
+        g.ld_out = F * W2;
         g.row_ln = rl1;
         g.col_s = L.s_i.as<float>();
         g.col_c = L.c_i.as<float>();
         {
             TimedLaunch tl(e->timer, timing, "gemm_ffn1", s);
-            launch_gemm<bf16>(EPI_FOLD_GELU, g, s);
+            gemm(EPI_FOLD_GELU, g);
         }
         // FFN2: P2 = Hff W_out^T + b_out + LN1(P1) -> X, stats2 (+ head dot, last layer)
         g = base_r();
@@ -554,7 +586,7 @@ void forward_folded(di_encoder *e, const int32_t *d_ids, const int32_t *d_cu, in
         g.out = X;
         g.N = H;
         g.K = F;
-        g.ld_out = H;
+        g.ld_out = H * W2;
         g.tune_gm = 4;
         g.row_ln = rl1;
         g.res_gamma = L.ln1_g.as<float>();
@@ -563,7 +595,7 @@ void forward_folded(di_encoder *e, const int32_t *d_ids, const int32_t *d_cu, in
         g.head_wg = last ? e->head_wg.as<float>() : nullptr;
         {
             TimedLaunch tl(e->timer, timing, "gemm_ffn2", s);
-            launch_gemm<bf16>(EPI_RESID_STATS, g, s);
+            gemm(EPI_RESID_STATS, g);
         }
         if (!last) {
             TimedLaunch tl(e->timer, timing, "row_ln", s);
@@ -788,7 +820,9 @@ int di_encoder_create(const di_encoder_cfg *cfg, const di_tensor *w, int32_t n_w
         upload(e->emb_g, {get("embeddings.LayerNorm.weight", {H})}, 0, true, 4);
         upload(e->emb_b, {get("embeddings.LayerNorm.bias", {H})}, 0, true, 4);
         // LayerNorm folding: bf16 with shapes the 256-tile GEMM takes (DI_NO_LN_FOLD: off)
-        e->folded = e->esz == 2 && H % 256 == 0 && F % 256 == 0 && H <= 1024 &&
+        // (bf16x3 too: the GEMMs then read split rows of the un-normalised x, 2^-17
+        // relative, and no LayerNorm pass runs)
+        e->folded = (e->esz == 2 || e->split) && H % 256 == 0 && F % 256 == 0 && H <= 1024 &&
                     std::getenv("DI_NO_LN_FOLD") == nullptr;
         const HostTensor *prev_g2 = nullptr, *prev_b2 = nullptr;  // LN2 of layer l-1
         for (int l = 0; l < c.layers; ++l) {
@@ -801,10 +835,11 @@ int di_encoder_create(const di_encoder_cfg *cfg, const di_tensor *w, int32_t n_w
             const std::vector<const HostTensor *> bqkv = {
                 get(p + "attention.self.query.bias", {H}), get(p + "attention.self.key.bias", {H}),
                 get(p + "attention.self.value.bias", {H})};
-            if (e->split)
+            if (e->folded && l > 0)  // layer 0 reads the (normalised) embedding output
+                fold_upload(L->w_qkv, L->s_qkv, L->c_qkv, wqkv, bqkv, H, prev_g2, prev_b2,
+                            e->split);
+            else if (e->split)
                 upload_split3(L->w_qkv, wqkv, (int)H);
-            else if (e->folded && l > 0)  // layer 0 reads the (normalised) embedding output
-                fold_upload(L->w_qkv, L->s_qkv, L->c_qkv, wqkv, bqkv, H, prev_g2, prev_b2);
             else
                 upload(L->w_qkv, wqkv, 0, false, e->esz);
             upload(L->b_qkv, bqkv, 0, true, 4);
@@ -818,12 +853,12 @@ int di_encoder_create(const di_encoder_cfg *cfg, const di_tensor *w, int32_t n_w
             upload(L->ln1_b, {get(p + "attention.output.LayerNorm.bias", {H})}, 0, true, 4);
             const HostTensor *wi = get(p + "intermediate.dense.weight", {F, H});
             const HostTensor *bi = get(p + "intermediate.dense.bias", {F});
-            if (e->split)
-                upload_split3(L->w_i, {wi}, (int)H);
-            else if (e->folded)
+            if (e->folded)
                 fold_upload(L->w_i, L->s_i, L->c_i, {wi}, {bi}, H,
                             get(p + "attention.output.LayerNorm.weight", {H}),
-                            get(p + "attention.output.LayerNorm.bias", {H}));
+                            get(p + "attention.output.LayerNorm.bias", {H}), e->split);
+            else if (e->split)
+                upload_split3(L->w_i, {wi}, (int)H);
             else
                 upload(L->w_i, {wi}, 0, false, e->esz);
             upload(L->b_i, {bi}, 0, true, 4);
@@ -909,9 +944,12 @@ int di_encode(di_encoder *e, const int32_t *tok_ids, const int32_t *cu_seqlens, 
         const bool prune = !token_out && (e->split || (e->esz == 2 && e->folded)) &&
                            n_terms <= n_tokens;  // (packed term rows fit the row buffers)
         if (n_tokens > 0) {
-            if (e->split)
+            if (e->split && !e->folded)
                 forward_split(e, d_ids, d_cu, n_docs, n_tokens, max_len, timing, s,
                               prune ? d_tt : nullptr, prune ? d_cut : nullptr, n_terms);
+            else if (e->split)
+                forward_folded(e, d_ids, d_cu, n_docs, n_tokens, max_len, timing, s,
+                               prune ? d_tt : nullptr, prune ? d_cut : nullptr, n_terms);
             else if (e->esz == 2)
                 if (e->folded)
                     forward_folded(e, d_ids, d_cu, n_docs, n_tokens, max_len, timing, s,
