@@ -361,12 +361,10 @@ def encode_leg(args, rank, world, dev, precision="bf16"):
     # PMC names (bf16 xlm-roberta-base runs the LayerNorm-folded forward): EPI 5 = folded
     # QKV, 6 = folded FFN1 + GELU, 7 = residual + row statistics (O and FFN2 share it)
     # gemm256_kernel<EPI, SPLIT>: EPI 5 = LN-folded, 6 = folded + GELU, 7 = residual +
-    # statistics (bf16); split: 0 = bias (QKV), 1 = bias + GELU, 2 = residual
-    pmc_name = {"gemm_qkv": "gemm256_kernel<5,false>", "gemm_ffn1": "gemm256_kernel<6,false>",
-                "gemm_o": "gemm256_kernel<7,false>", "gemm_ffn2": "gemm256_kernel<7,false>"}[dom]
-    if split:
-        pmc_name = {"gemm_qkv": "gemm256_kernel<0,true>", "gemm_ffn1": "gemm256_kernel<1,true>",
-                    "gemm_o": "gemm256_kernel<2,true>", "gemm_ffn2": "gemm256_kernel<2,true>"}[dom]
+    # statistics; bf16x3 folds its LayerNorms the same way (SPLIT = true)
+    pmc_name = {"gemm_qkv": "gemm256_kernel<5,%s>", "gemm_ffn1": "gemm256_kernel<6,%s>",
+                "gemm_o": "gemm256_kernel<7,%s>",
+                "gemm_ffn2": "gemm256_kernel<7,%s>"}[dom] % ("true" if split else "false")
     traffic, src = load_pmc_traffic(pmc_name, "encode_x3" if split else "encode")
     # bf16x3: algorithmic (fp32) FLOPs against the split scheme's own peak -- three
     # bf16 MFMA products per fp32 product, 2500 / 3 TF/s (the f32 MFMA peak is 157.3)
