@@ -571,7 +571,9 @@ def main():
     big = {}
     for leg, nd in (("retrieve_shard", 1_100_000), ("retrieve_full", 8_800_000)):
         if leg in legs:
-            big[leg], _ = retrieve_leg(args, rank, world, dev, n_docs=nd, check_queries=20)
+            # (profiling ablations of the scorer, DI_PROFILE_ABLATE, change its results)
+            big[leg], _ = retrieve_leg(args, rank, world, dev, n_docs=nd,
+                                       check_queries=0 if os.environ.get("DI_PROFILE_ABLATE") else 20)
             torch.cuda.empty_cache()
     primary = next((r for r in (enc_res, x3_res, ret_res) + tuple(big.values()) + (e2e_res,)
                     if r is not None), None)

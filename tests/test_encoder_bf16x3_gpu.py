@@ -263,3 +263,52 @@ def test_bf16x3_end_to_end_quantized_and_metrics(E, base):
     text_flip, q_flip, m = res["bf16x3"]
     assert q_flip <= 2e-3, q_flip
     assert m == m_ref
+
+
+def _bench_batch(n_docs, seed, max_len=300, vocab=250002):
+    """The bench's configs[1] encode batch: n_i = clip(round(N(200, 60)),
+    8, 300), ids uniform [5, V) with <s> first, words of 1 + Geom(0.3) tokens, ~0.7 of
+    them kept as terms (their first tokens)."""
+    rng = np.random.default_rng(seed)
+    lens = np.clip(np.rint(rng.normal(200, 60, n_docs)), 8, max_len).astype(np.int32)
+    cu = np.zeros(n_docs + 1, np.int32)
+    cu[1:] = np.cumsum(lens)
+    ids = rng.integers(5, vocab, int(cu[-1])).astype(np.int32)
+    ids[cu[:-1]] = 0
+    tt, ct = [], [0]
+    for n in lens:
+        starts = [1]
+        while True:
+            nxt = starts[-1] + int(rng.geometric(0.3))
+            if nxt >= n - 1:
+                break
+            starts.append(nxt)
+        keep = [s for s in starts if rng.random() < 0.7]
+        tt += keep
+        ct.append(ct[-1] + len(keep))
+    return ids, cu, np.array(tt, np.int32), np.array(ct, np.int32)
+
+
+@pytest.mark.parametrize("precision", ["bf16x3", "bf16"])
+def test_full_size_batch_is_batch_invariant(E, base, precision):
+    """Size-independent property at the bench's full size (8192 docs, ~1.6 M tokens,
+    round3 term output): every row's arithmetic is independent of the other documents
+    (GEMM rows, per-document attention, per-row LayerNorm statistics), so 64 documents
+    re-encoded on their own give bit-identical impacts to their slices of the full batch."""
+    fx, sd = base
+    enc = E.DeviceEncoder(sd, _cfg(E, fx), precision=precision)
+    ids, cu, tt, ct = _bench_batch(8192, 7)
+    full = enc.encode_packed(ids, cu, tt, ct, round3=True)
+    assert full.shape[0] == ct[-1] and np.isfinite(full).all()
+    pick = np.sort(np.random.default_rng(3).choice(8192, 64, replace=False))
+    sids, scu, stt, sct = [], [0], [], [0]
+    want = []
+    for d in pick:
+        sids.append(ids[cu[d]:cu[d + 1]])
+        scu.append(scu[-1] + int(cu[d + 1] - cu[d]))
+        stt.append(tt[ct[d]:ct[d + 1]])
+        sct.append(sct[-1] + int(ct[d + 1] - ct[d]))
+        want.append(full[ct[d]:ct[d + 1]])
+    got = enc.encode_packed(np.concatenate(sids), np.array(scu, np.int32), np.concatenate(stt),
+                            np.array(sct, np.int32), round3=True)
+    np.testing.assert_array_equal(got, np.concatenate(want))
