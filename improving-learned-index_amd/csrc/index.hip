@@ -1360,8 +1360,9 @@ void build_index(di_index *ix, const int64_t *term_off, int64_t n_terms, const u
     // 128..255, ..., class 7 = value 1), classes in order, so that "every posting with
     // value >= 2^(7-c)" is a prefix of the sublist: seg[(t*nb + b)*8 + c] = its length
     // (di_index_set_min_impact prunes with it; class 7 = the whole sublist = exact).
-    // Inside a class, postings are dealt round-robin from their 32 LDS bank buckets
-    // (doc_in_block mod 32): the scorer's lanes read consecutive postings and update
+    // Inside a class, postings are dealt from their 32 LDS bank buckets (doc_in_block
+    // mod 32, distinct banks per aligned 32-posting block where the class allows, see
+    // emit_group): the scorer's lanes read consecutive postings and update
     // acc[doc_in_block], and a 32-lane group of a ds_read_b32 / ds_write_b32 conflicts
     // on equal banks.  Any order is exact: a doc occurs once per term, and its key
     // (first term, value there) does not depend on the order inside the term.
@@ -1401,27 +1402,39 @@ void build_index(di_index *ix, const int64_t *term_off, int64_t n_terms, const u
                 }
                 tmp.resize(n);
                 for (size_t i = 0; i < n; ++i) tmp[cls_pos[cls_of(in[i])]++] = in[i];
-                uint32_t c0 = 0;
+                // The scorer's lanes take the group's postings in rounds from its start,
+                // and a 32-lane group of its ds_read_b32 / ds_write_b32 is one aligned
+                // block of 32 positions: each position takes, from its class, a posting
+                // whose bank is not yet used in the current block (bank cursor carried
+                // on across sweeps and class boundaries), else any.  Restarting every
+                // class at bank 0 put most of a long term's per-wave runs (~8 postings
+                // per class) into conflicts at every class boundary.
+                uint32_t c0 = 0, used = 0;
+                int cursor = 0;
+                const int64_t o_start = o;
                 for (int c = 0; c < 8; ++c) {
                     const uint32_t c1 = c0 + cls_cnt[c];
                     std::fill(bucket_cnt.begin(), bucket_cnt.end(), 0);
                     for (uint32_t i = c0; i < c1; ++i) bucket_cnt[(tmp[i] >> 8) & 31]++;
-                    uint32_t r = 0;
+                    uint32_t r = 0, avail = 0;
                     for (int k = 0; k < 32; ++k) {
                         head[k] = r;
                         r += bucket_cnt[k];
+                        if (bucket_cnt[k]) avail |= 1u << k;
                     }
                     bk.resize(c1 - c0);
                     fill = head;
                     for (uint32_t i = c0; i < c1; ++i) bk[fill[(tmp[i] >> 8) & 31]++] = tmp[i];
-                    for (bool any = true; any;) {
-                        any = false;
-                        for (int k = 0; k < 32; ++k)
-                            if (bucket_cnt[k]) {
-                                packed[o++] = bk[head[k]++];
-                                --bucket_cnt[k];
-                                any = true;
-                            }
+                    for (uint32_t i = c0; i < c1; ++i) {
+                        if (((o - o_start) & 31) == 0) used = 0;
+                        uint32_t cand = avail & ~used;
+                        if (!cand) cand = avail;  // every bank left is taken in this block
+                        const uint32_t rot = cursor ? (cand >> cursor) | (cand << (32 - cursor)) : cand;
+                        const int k = (__builtin_ctz(rot) + cursor) & 31;
+                        packed[o++] = bk[head[k]++];
+                        if (--bucket_cnt[k] == 0) avail &= ~(1u << k);
+                        used |= 1u << k;
+                        cursor = (k + 1) & 31;
                     }
                     if (cum) cum[c] = (uint16_t)(o - s0);
                     c0 = c1;
