@@ -397,15 +397,30 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
             bounds(j, t);
         }
     }
+    // The query's shared threshold histogram (qhist, below) is copied by LDS-DMA into
+    // the selection histogram (idle until the selection) here, so its round trip
+    // overlaps the scatter and the selection reads it from LDS; the fast selection
+    // path zeroes the histogram itself when it runs.  (Early termination reads it
+    // before its scatter, from global memory.)
+    uint32_t *qh = qhist ? qhist + (int64_t)q * QH_BINS : nullptr;
+    const bool qpre = qh != nullptr && !et;
+    static_assert(QH_BINS == 4 * SC_THREADS && QH_BINS <= HIST_BINS, "qhist prefetch");
+    if (qpre) {
+        typedef __attribute__((address_space(3))) void lds_void;
+        __builtin_amdgcn_global_load_lds((const void *)(qh + 4 * tid),
+                                         (lds_void *)(sh.u.hist + wave * 256), 16, 0, 0);
+    }
     {
         uint4 *a4 = reinterpret_cast<uint4 *>(sh.acc);
         const int n4 = (n_local + 3) >> 2;
         for (int i = tid; i < n4; i += SC_THREADS) a4[i] = make_uint4(0, 0, 0, 0);
-        if (fast) reinterpret_cast<uint4 *>(sh.u.hist)[tid] = make_uint4(0, 0, 0, 0);
+        if (fast && !qpre) reinterpret_cast<uint4 *>(sh.u.hist)[tid] = make_uint4(0, 0, 0, 0);
         // (the 64 spare bins past them are written, never read: no zeroing needed)
     }
     __syncthreads();
     if (sh.bad) {
+        // (the histogram copy lands before the next item touches the histogram)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (tid == 0) *cn = -1;
         return;
     }
@@ -416,14 +431,20 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
     // 4095 and above).  read_tq -> the largest s with >= k counted candidates scoring
     // >= s: at least k docs score >= s, so the final k-th score is >= s.  A stale
     // (smaller) count still gives a valid lower bound.  Block-wide (barriers).
-    uint32_t *qh = qhist ? qhist + (int64_t)q * QH_BINS : nullptr;
     auto read_tq = [&]() -> uint32_t {
-        // thread t: bins 4t..4t+3 (relaxed atomic loads: other CUs add to them)
+        // thread t: bins 4t..4t+3 (relaxed atomic loads: other CUs add to them; or the
+        // LDS copy made at the item's start)
         uint32_t hv[4], c = 0;
+        if (qpre) {
+            const uint4 h = reinterpret_cast<const uint4 *>(sh.u.hist)[tid];
+            hv[0] = h.x, hv[1] = h.y, hv[2] = h.z, hv[3] = h.w;
+            c = h.x + h.y + h.z + h.w;
+        } else {
 #pragma unroll
-        for (int e = 0; e < 4; ++e)
-            c += (hv[e] = __hip_atomic_load(&qh[4 * tid + e], __ATOMIC_RELAXED,
-                                            __HIP_MEMORY_SCOPE_AGENT));
+            for (int e = 0; e < 4; ++e)
+                c += (hv[e] = __hip_atomic_load(&qh[4 * tid + e], __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT));
+        }
         uint32_t sfx = wave_suffix_sum(c);
         if (lane == 0) sh.wsum[wave] = sfx;
         if (tid == 0) sh.tq = 0;
@@ -645,7 +666,8 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
         // term boundary: this term's LDS writes land before any wave reads the next
         if (j + 1 < nt) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the asm LDS writes
+    // the asm LDS writes; the threshold histogram's LDS-DMA copy
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __syncthreads();
 
     stamp(1);  // scatter
@@ -723,6 +745,10 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
         // branch-free: an untouched doc (w = 0) counts into a per-lane spare bin past
         // the 4096 score bins (no same-address conflicts), never read
         const uint32_t spare = HIST_BINS + (uint32_t)lane;
+        if (qpre) {  // the threshold copy was read (read_tq's barriers): zero the bins
+            reinterpret_cast<uint4 *>(hist)[tid] = make_uint4(0, 0, 0, 0);
+            __syncthreads();
+        }
         sweep_words(sh.acc, n_local, tid, [&](uint32_t w, int) {
             atomicAdd(&hist[w ? (w >> 16) : spare], 1u);
         });
