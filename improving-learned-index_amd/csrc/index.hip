@@ -358,45 +358,6 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
         hi[j] = min_cls >= 7 ? term_start[t] + bo[1]
                              : lo[j] + seg[((int64_t)t * nb + b) * 8 + min_cls];
     };
-    if (wl) {
-        for (int e = tid; e < nt * WSEG; e += SC_THREADS) {
-            const int j = e / WSEG, w = e % WSEG;
-            const uint32_t t = q_terms[q0 + j];
-            if (t >= n_terms) {  // invalid id (device-pointer callers are not pre-checked)
-                if (w == 0) {
-                    sh.bad = 1;
-                    lo[j] = hi[j] = 0;
-                }
-                continue;
-            }
-            const uint32_t id = lid[(int64_t)t * nb + b];
-            if (w == 0) bounds(j, t);
-            if (id == 0xFFFFFFFFu) {
-                if (et && w < 8) sh.segj[j][w] = seg[((int64_t)t * nb + b) * 8 + w];
-                continue;
-            }
-            const uint16_t *m = wmeta + (int64_t)id * (WSEG * 8);
-            const uint32_t s0 = w ? m[(w - 1) * 8 + 7] : 0u;
-            const uint32_t e0 = m[w * 8 + min(min_cls, 7)];
-            if (et) {
-#pragma unroll
-                for (int c = 0; c < 8; ++c) sh.wt.wcls[j][w][c] = m[w * 8 + c];
-            } else {
-                sh.wt.wtab[j][w] = (s0 << 16) | e0;
-            }
-            if (w == 0) atomicOr(&sh.lmask[j >> 5], 1u << (j & 31));
-        }
-    } else {
-        for (int j = tid; j < nt; j += SC_THREADS) {
-            const uint32_t t = q_terms[q0 + j];
-            if (t >= n_terms) {
-                sh.bad = 1;
-                lo[j] = hi[j] = 0;
-                continue;
-            }
-            bounds(j, t);
-        }
-    }
     // The query's shared threshold histogram (qhist, below) is copied by LDS-DMA into
     // the selection histogram (idle until the selection) here, so its round trip
     // overlaps the scatter and the selection reads it from LDS; the fast selection
@@ -410,12 +371,76 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
         __builtin_amdgcn_global_load_lds((const void *)(qh + 4 * tid),
                                          (lds_void *)(sh.u.hist + wave * 256), 16, 0, 0);
     }
-    {
+    // zeroing of the accumulators (and the fast path's histogram): LDS stores only,
+    // placed where the setup's global loads are in flight
+    auto zero = [&]() {
         uint4 *a4 = reinterpret_cast<uint4 *>(sh.acc);
         const int n4 = (n_local + 3) >> 2;
         for (int i = tid; i < n4; i += SC_THREADS) a4[i] = make_uint4(0, 0, 0, 0);
         if (fast && !qpre) reinterpret_cast<uint4 *>(sh.u.hist)[tid] = make_uint4(0, 0, 0, 0);
         // (the 64 spare bins past them are written, never read: no zeroing needed)
+    };
+    if (wl) {
+        // nt * WSEG <= SC_THREADS: one (term j, wave segment w) per thread.  The term id
+        // and the loads that depend only on it (sublist id, bounds) are issued, the
+        // accumulators zeroed while they are in flight, then the per-wave runs read.
+        static_assert(WTERMS * WSEG <= SC_THREADS, "one setup entry per thread");
+        const int e = tid;
+        const bool act = e < nt * WSEG;
+        const int j = act ? e / WSEG : 0, w = e % WSEG;
+        const uint32_t t = act ? q_terms[q0 + j] : 0u;
+        const bool tok = act && t < n_terms;  // (device-pointer callers are not pre-checked)
+        uint32_t id = 0xFFFFFFFFu, bo0 = 0, bo1 = 0, sgc = 0;
+        int64_t ts = 0;
+        if (tok) {
+            id = lid[(int64_t)t * nb + b];
+            if (w == 0) {
+                const uint32_t *bo = blk_off + (int64_t)t * (nb + 1) + b;
+                ts = term_start[t];
+                bo0 = bo[0];
+                if (min_cls >= 7)
+                    bo1 = bo[1];
+                else
+                    sgc = seg[((int64_t)t * nb + b) * 8 + min_cls];
+            }
+        }
+        zero();
+        if (act && !tok) {  // invalid term id
+            if (w == 0) {
+                sh.bad = 1;
+                lo[j] = hi[j] = 0;
+            }
+        } else if (act) {
+            if (w == 0) {
+                lo[j] = ts + bo0;
+                hi[j] = min_cls >= 7 ? ts + bo1 : lo[j] + sgc;
+            }
+            if (id == 0xFFFFFFFFu) {
+                if (et && w < 8) sh.segj[j][w] = seg[((int64_t)t * nb + b) * 8 + w];
+            } else {
+                const uint16_t *m = wmeta + (int64_t)id * (WSEG * 8);
+                const uint32_t s0 = w ? m[(w - 1) * 8 + 7] : 0u;
+                const uint32_t e0 = m[w * 8 + min(min_cls, 7)];
+                if (et) {
+#pragma unroll
+                    for (int c = 0; c < 8; ++c) sh.wt.wcls[j][w][c] = m[w * 8 + c];
+                } else {
+                    sh.wt.wtab[j][w] = (s0 << 16) | e0;
+                }
+                if (w == 0) atomicOr(&sh.lmask[j >> 5], 1u << (j & 31));
+            }
+        }
+    } else {
+        for (int j = tid; j < nt; j += SC_THREADS) {
+            const uint32_t t = q_terms[q0 + j];
+            if (t >= n_terms) {
+                sh.bad = 1;
+                lo[j] = hi[j] = 0;
+                continue;
+            }
+            bounds(j, t);
+        }
+        zero();
     }
     __syncthreads();
     if (sh.bad) {
