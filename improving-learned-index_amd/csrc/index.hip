@@ -294,6 +294,57 @@ __device__ __forceinline__ void scatter_apply_own(const uint32_t (&cur)[UU], uin
 // accumulated here and printed by di_index_search.
 __device__ unsigned long long g_sb_phase[8];
 
+// Per (item, query term) setup record, resolved for every item in bulk by
+// item_setup_kernel before the scorer: the scorer's setup then reads one record per
+// (term, wave segment) instead of walking the dependent chain query term -> sublist
+// id -> per-wave runs (three global round trips per item, ~1/6 of the kernel).
+struct ItemRec {
+    int64_t lo, hi;        // the term's sublist [lo, hi) in this block (min_cls prefix)
+    uint32_t wtab[WSEG];   // per-wave layout: run of wave w = start << 16 | end
+    uint32_t flags;        // IR_LONG: per-wave layout; IR_BAD: invalid term id
+    uint32_t pad[3];
+};
+constexpr uint32_t IR_LONG = 1, IR_BAD = 2;
+
+// Items (query q, block b) as the scorer numbers them (item = b * n_q + q); records
+// only for queries of 1..WTERMS terms (the scorer's per-wave form), WTERMS per item.
+__global__ void __launch_bounds__(128)
+item_setup_kernel(const int64_t *__restrict__ term_start, const uint32_t *__restrict__ blk_off,
+                  const uint16_t *__restrict__ seg, const uint32_t *__restrict__ lid,
+                  const uint16_t *__restrict__ wmeta, int min_cls, int nb, int64_t n_terms,
+                  const uint32_t *__restrict__ q_terms, const int32_t *__restrict__ cu_q, int n_q,
+                  ItemRec *__restrict__ rec) {
+    const int item = blockIdx.x, q = item % n_q, b = item / n_q;
+    const int q0 = cu_q[q], nt = cu_q[q + 1] - q0;
+    if (nt > WTERMS || nt <= 0) return;
+    ItemRec *r = rec + (int64_t)item * WTERMS;
+    for (int e = threadIdx.x; e < nt * WSEG; e += blockDim.x) {
+        const int j = e / WSEG, w = e % WSEG;
+        const uint32_t t = q_terms[q0 + j];
+        if (t >= n_terms) {  // invalid id (device-pointer callers are not pre-checked)
+            if (w == 0) {
+                r[j].lo = r[j].hi = 0;
+                r[j].flags = IR_BAD;
+            }
+            continue;
+        }
+        const uint32_t id = lid[(int64_t)t * nb + b];
+        if (w == 0) {
+            const uint32_t *bo = blk_off + (int64_t)t * (nb + 1) + b;
+            const int64_t lo = term_start[t] + bo[0];
+            r[j].lo = lo;
+            r[j].hi = min_cls >= 7 ? term_start[t] + bo[1]
+                                   : lo + seg[((int64_t)t * nb + b) * 8 + min_cls];
+            r[j].flags = id != 0xFFFFFFFFu ? IR_LONG : 0u;
+        }
+        if (id != 0xFFFFFFFFu) {
+            const uint16_t *m = wmeta + (int64_t)id * (WSEG * 8);
+            const uint32_t s0 = w ? m[(w - 1) * 8 + 7] : 0u;
+            r[j].wtab[w] = (s0 << 16) | m[w * 8 + min(min_cls, 7)];
+        }
+    }
+}
+
 // One work item = (query q, doc block b): accumulate, select the block's top-k.
 __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
                                            const uint32_t *__restrict__ post,
@@ -307,7 +358,8 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
                                            const int32_t *__restrict__ cu_q, int k,
                                            uint64_t *__restrict__ cand_key,
                                            int32_t *__restrict__ cand_n,
-                                           uint32_t *__restrict__ qhist, int ablate) {
+                                           uint32_t *__restrict__ qhist, int ablate,
+                                           const ItemRec *__restrict__ ir) {
     int64_t *lo = sh.v.bounds[0], *hi = sh.v.bounds[1];
 
     // opaque per item: keeps the per-thread index arithmetic of the sweeps from being
@@ -380,7 +432,33 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
         if (fast && !qpre) reinterpret_cast<uint4 *>(sh.u.hist)[tid] = make_uint4(0, 0, 0, 0);
         // (the 64 spare bins past them are written, never read: no zeroing needed)
     };
-    if (wl) {
+    if (wl && ir != nullptr && !et) {
+        // the item's records (item_setup_kernel): one (term j, wave segment w) per thread
+        const int e = tid;
+        const bool act = e < nt * WSEG;
+        const int j = act ? e / WSEG : 0, w = e % WSEG;
+        uint32_t f = 0, wt = 0;
+        int64_t rlo = 0, rhi = 0;
+        if (act) {
+            const ItemRec &R = ir[j];
+            f = R.flags;
+            wt = R.wtab[w];
+            if (w == 0) {
+                rlo = R.lo;
+                rhi = R.hi;
+            }
+        }
+        zero();
+        if (act) {
+            if (w == 0) {
+                lo[j] = rlo;
+                hi[j] = rhi;
+                if (f & IR_BAD) sh.bad = 1;
+                if (f & IR_LONG) atomicOr(&sh.lmask[j >> 5], 1u << (j & 31));
+            }
+            if (f & IR_LONG) sh.wt.wtab[j][w] = wt;
+        }
+    } else if (wl) {
         // nt * WSEG <= SC_THREADS: one (term j, wave segment w) per thread.  The term id
         // and the loads that depend only on it (sublist id, bounds) are issued, the
         // accumulators zeroed while they are in flight, then the per-wave runs read.
@@ -1026,7 +1104,7 @@ score_blocks_kernel(const uint32_t *__restrict__ post, const int64_t *__restrict
                     uint32_t n_docs, uint32_t doc_lo, const uint32_t *__restrict__ q_terms,
                     const int32_t *__restrict__ cu_q, int k, uint64_t *__restrict__ cand_key,
                     int32_t *__restrict__ cand_n, int n_items, int n_q,
-                    uint32_t *__restrict__ qhist, int ablate) {
+                    uint32_t *__restrict__ qhist, int ablate, const ItemRec *__restrict__ rec) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     ScoreShared &sh = *reinterpret_cast<ScoreShared *>(smem);
     if ((uint32_t)(uintptr_t)((__attribute__((address_space(3))) unsigned char *)smem) != 0) {
@@ -1040,7 +1118,7 @@ score_blocks_kernel(const uint32_t *__restrict__ post, const int64_t *__restrict
     for (int item = blockIdx.x; item < n_items; item += gridDim.x) {
         score_item(sh, item % n_q, item / n_q, post, term_start, blk_off, seg, lid, wmeta,
                    min_cls, nb, block_docs, n_terms, n_docs, doc_lo, q_terms, cu_q, k, cand_key,
-                   cand_n, qhist, ablate);
+                   cand_n, qhist, ablate, rec ? rec + (int64_t)item * WTERMS : nullptr);
         __syncthreads();  // every wave is done with the LDS of this item
     }
 }
@@ -1310,6 +1388,7 @@ struct di_index {
     std::vector<uint16_t> wmeta;     // per-wave class ends of the long sublists
     DevBuf post, term_start, blk_off, seg_dev, lid_dev, wmeta_dev;
     DevBuf ws_q, ws_cu, ws_ck, ws_cn, ws_doc, ws_score, ws_n, ws_key, ws_thr;
+    DevBuf ws_rec;  // ItemRec per (item, term slot): item_setup_kernel -> score_blocks
     // per-query threshold shared across blocks: -1 = auto (on from 8 blocks: at 4 blocks it
     // measured 2.31 vs 2.14 ms per 6980-query batch, at 34 / 269 blocks 16.9 vs 19.5 and
     // 130 vs 161 ms, merge 0.5 vs 7.1 and 1.4 vs 74 ms); DI_SCORE_THRESHOLD=0 / 1 forces
@@ -1724,6 +1803,9 @@ int di_index_search(di_index *ix, const uint32_t *q_terms, const int32_t *cu_q, 
         ix->ws_ck.reserve((size_t)chunk * per_q);
         ix->ws_cn.reserve((size_t)chunk * nb * 4);
         ix->ws_thr.reserve((size_t)chunk * QH_BINS * 4);
+        // (only the records of real terms are written / read: ~6 per query)
+        const bool use_rec = !(ix->ablate & 1024);  // (profiling: the in-kernel chain)
+        if (use_rec) ix->ws_rec.reserve((size_t)chunk * nb * WTERMS * sizeof(ItemRec));
         const uint32_t *dq = (const uint32_t *)stage_in(
             q_terms, (size_t)nterms_total * 4, dev, ix->ws_q, s);
         const int32_t *dcu =
@@ -1750,8 +1832,16 @@ int di_index_search(di_index *ix, const uint32_t *q_terms, const int32_t *cu_q, 
             } else {
                 const bool thr = nb > 1 && (ix->shared_thr < 0 ? nb >= 8 : ix->shared_thr == 1);
                 if (thr) DI_HIP(hipMemsetAsync(ix->ws_thr.p, 0, (size_t)nq * QH_BINS * 4, s));
-                TimedLaunch tl(ix->timer, timing, "score_blocks", s);
+                TimedLaunch tl(ix->timer, timing, "score_blocks", s);  // (both kernels)
                 const int n_items = nq * nb;
+                if (use_rec) {
+                    hipLaunchKernelGGL(item_setup_kernel, dim3(n_items), dim3(128), 0, s,
+                                       ix->term_start.as<int64_t>(), ix->blk_off.as<uint32_t>(),
+                                       ix->seg_dev.as<uint16_t>(), ix->lid_dev.as<uint32_t>(),
+                                       ix->wmeta_dev.as<uint16_t>(), ix->min_cls, nb,
+                                       ix->n_terms, dq, dcu + q0, nq, ix->ws_rec.as<ItemRec>());
+                    check_launch("item_setup");
+                }
                 hipLaunchKernelGGL(score_blocks_kernel, dim3(std::min(n_items, n_cu())),
                                    dim3(SC_THREADS), sizeof(ScoreShared), s,
                                    ix->post.as<uint32_t>(), ix->term_start.as<int64_t>(),
@@ -1760,7 +1850,8 @@ int di_index_search(di_index *ix, const uint32_t *q_terms, const int32_t *cu_q, 
                                    ix->min_cls, nb, ix->block_docs, ix->n_terms,
                                    ix->n_docs, ix->doc_lo, dq, dcu + q0, k,
                                    ix->ws_ck.as<uint64_t>(), ix->ws_cn.as<int32_t>(), n_items,
-                                   nq, thr ? ix->ws_thr.as<uint32_t>() : nullptr, ix->ablate);
+                                   nq, thr ? ix->ws_thr.as<uint32_t>() : nullptr, ix->ablate,
+                                   use_rec ? ix->ws_rec.as<ItemRec>() : nullptr);
                 check_launch("score_blocks");
             }
             {
