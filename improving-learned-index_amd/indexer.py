@@ -106,6 +106,9 @@ class TokenizerPool:
         self.close()
 
 
+DEVICE_DOCS = 4096  # documents per device call when tokenizer chunks are merged
+
+
 class Indexer:
     def __init__(self, model: DeepImpact, model_batch_size: int = 32, num_processes: int = 8,
                  pool: Optional[TokenizerPool] = None):
@@ -152,7 +155,18 @@ class Indexer:
             text = _lib.format_impact_lines([[t for t, _ in d] for d in impacts],
                                             [[v for _, v in d] for d in impacts])
         else:
-            text = "".join(self.model.encode_packed_text(p) for p in it)
+            # the workers' chunks are merged into device batches of up to DEVICE_DOCS
+            # documents (a 100-doc chunk leaves most of the GPU idle), in order
+            parts, n, out = [], 0, []
+            for p in it:
+                parts.append(p)
+                n += len(p[1]) - 1
+                if n >= DEVICE_DOCS:
+                    out.append(self.model.encode_packed_text(DeepImpact.merge_packed_blobs(parts)))
+                    parts, n = [], 0
+            if parts:
+                out.append(self.model.encode_packed_text(DeepImpact.merge_packed_blobs(parts)))
+            text = "".join(out)
         # '\\n'.join(lines) + '\\n' == every line + '\\n', except for an empty batch
         file.write(text if batch else "\n")
         file.flush()

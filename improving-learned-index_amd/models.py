@@ -254,6 +254,27 @@ class DeepImpact:
             term_off[1:] = np.cumsum([len(b) for b in enc])
         return ids, cu, b"".join(enc), term_off, tt, ct
 
+    @staticmethod
+    def merge_packed_blobs(parts):
+        """Concatenate pack_processed_blob batches (in order) into one: the tokenizer
+        workers' small chunks become one device batch (batch sizes never change the
+        impacts: every row's arithmetic is independent of the other documents)."""
+        if len(parts) == 1:
+            return parts[0]
+        ids = np.concatenate([p[0] for p in parts])
+        tt = np.concatenate([p[4] for p in parts])
+        cu, term_off, ct = [np.zeros(1, np.int32)], [np.zeros(1, np.int64)], [np.zeros(1, np.int32)]
+        o_tok = o_byte = o_term = 0
+        for p in parts:
+            cu.append(p[1][1:] + np.int32(o_tok))
+            term_off.append(p[3][1:] + np.int64(o_byte))
+            ct.append(p[5][1:] + np.int32(o_term))
+            o_tok += int(p[1][-1])
+            o_byte += int(p[3][-1])
+            o_term += int(p[5][-1])
+        return (ids, np.concatenate(cu).astype(np.int32), b"".join(p[2] for p in parts),
+                np.concatenate(term_off).astype(np.int64), tt, np.concatenate(ct).astype(np.int32))
+
     def encode_packed_text(self, packed) -> str:
         """A pack_processed_blob batch -> its impact-TSV lines (round3, native
         formatter), without per-term Python objects."""

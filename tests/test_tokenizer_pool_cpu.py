@@ -124,3 +124,21 @@ def test_bert_legacy_term_mapping(restore_class, max_length):
     (_, wmap), = M.DeepImpact.process_documents([doc], max_length)
     if max_length == 6:
         assert wmap == {"hello": 1, "world": 2, "unbelievable": 4}
+
+
+def test_merged_chunks_equal_one_packed_batch(restore_class):
+    """The pool path merges the workers' chunks into device batches
+    (DeepImpact.merge_packed_blobs): the merge must equal packing the whole batch at
+    once (ids, cu_seqlens, term blob and offsets, term token indices, cu_terms)."""
+    D = restore_class.DeepImpact
+    D.set_tokenizer(GOLDEN / "tokenizer.json")
+    texts = json.loads((GOLDEN / "encoder_xlmr_small.json").read_text())["texts"]
+    docs = [texts[i % len(texts)] + f" w{i}, x:{i} é" * (i % 3) for i in range(41)] + [""]
+    whole = D.pack_processed_blob(D.process_documents(docs, 512))
+    parts = [D.pack_processed_blob(D.process_documents(docs[i:i + 6], 512))
+             for i in range(0, len(docs), 6)]
+    merged = D.merge_packed_blobs(parts)
+    assert merged[2] == whole[2]
+    for i in (0, 1, 3, 4, 5):
+        assert merged[i].dtype == whole[i].dtype
+        np.testing.assert_array_equal(merged[i], whole[i])
