@@ -1804,8 +1804,11 @@ int di_index_search(di_index *ix, const uint32_t *q_terms, const int32_t *cu_q, 
         ix->ws_cn.reserve((size_t)chunk * nb * 4);
         ix->ws_thr.reserve((size_t)chunk * QH_BINS * 4);
         // (only the records of real terms are written / read: ~6 per query)
-        const bool use_rec = !(ix->ablate & 1024);  // (profiling: the in-kernel chain)
-        if (use_rec) ix->ws_rec.reserve((size_t)chunk * nb * WTERMS * sizeof(ItemRec));
+        // (bounded: WTERMS slots per item; a search whose records would pass 2 GiB -- a
+        // small k leaves chunks of many queries -- walks the chain in the scorer instead)
+        const size_t rec_bytes = (size_t)chunk * nb * WTERMS * sizeof(ItemRec);
+        const bool use_rec = !(ix->ablate & 1024) && rec_bytes <= (size_t(1) << 31);
+        if (use_rec) ix->ws_rec.reserve(rec_bytes);
         const uint32_t *dq = (const uint32_t *)stage_in(
             q_terms, (size_t)nterms_total * 4, dev, ix->ws_q, s);
         const int32_t *dcu =
