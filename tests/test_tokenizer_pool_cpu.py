@@ -142,3 +142,15 @@ def test_merged_chunks_equal_one_packed_batch(restore_class):
     for i in (0, 1, 3, 4, 5):
         assert merged[i].dtype == whole[i].dtype
         np.testing.assert_array_equal(merged[i], whole[i])
+
+
+def test_worker_threads_follow_the_cpu_share(monkeypatch):
+    """Each tokenizer worker's thread pool is sized from the process's CPU share
+    (OMP_NUM_THREADS when set, as on the GPU box) over the worker count, 2..4."""
+    from improving_learned_index_amd import indexer
+
+    monkeypatch.setenv("OMP_NUM_THREADS", "16")
+    assert indexer.worker_threads(16) == 2
+    assert indexer.worker_threads(2) == 4
+    monkeypatch.setenv("OMP_NUM_THREADS", "64")
+    assert indexer.worker_threads(16) == min(4, max(2, min(64, len(__import__("os").sched_getaffinity(0))) // 16))
