@@ -20,7 +20,8 @@ DI_F_DEVICE_PTRS = 0x1
 DI_F_ASYNC = 0x2
 DI_F_TIMING = 0x4
 DI_F_LISTS_MAJOR = 0x8
-DI_MAX_QUERY_TERMS = 256
+DI_SHORT_QUERY_TERMS = 256  # longer queries: wide merge keys (include/deepimpact.h)
+DI_MAX_QUERY_TERMS = 4096
 DI_MAX_TOPK = 4096
 
 _ERRNAMES = {-1: "DI_EINVAL", -2: "DI_ENOMEM", -3: "DI_EHIP", -4: "DI_ERANGE",
@@ -250,12 +251,21 @@ def topk_merge_device(keys, counts, n_q, n_lists, k, out_key, out_n, device=0, s
                               ptr(out_n), device, ctypes.c_void_p(stream), flags))
 
 
-def key_doc(keys):
+def key_doc(keys, wide=False):
+    """Doc of quantized-index merge keys (di_key_doc / di_key_doc_wide); wide: the
+    keys of a query of more than DI_SHORT_QUERY_TERMS known terms."""
+    if wide:
+        return (np.uint64(0xFFFFFF) - (keys & np.uint64(0xFFFFFF))).astype(np.uint32)
     return (np.uint64(0xFFFFFFFF) - (keys & np.uint64(0xFFFFFFFF))).astype(np.uint32)
 
 
-def key_score(keys):
-    return (keys >> np.uint64(48)).astype(np.uint32)
+def key_score(keys, wide=False):
+    return (keys >> np.uint64(44 if wide else 48)).astype(np.uint32)
+
+
+def is_wide(n_terms: int) -> bool:
+    """Does a query of n_terms known terms get wide merge keys?"""
+    return n_terms > DI_SHORT_QUERY_TERMS
 
 
 def format_impact_lines_packed(blob: bytes, term_off, impacts, cu_terms) -> str:

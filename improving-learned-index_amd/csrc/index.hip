@@ -46,7 +46,7 @@ constexpr int MAX_BLOCK_DOCS = 32768;  // LDS accumulators per workgroup (128 Ki
 constexpr int SC_THREADS = 1024;
 constexpr int SC_WAVES = SC_THREADS / 64;
 constexpr int SC_PER_THREAD = MAX_BLOCK_DOCS / SC_THREADS;  // 32
-constexpr int MAX_TERMS = DI_MAX_QUERY_TERMS;
+constexpr int MAX_TERMS = DI_SHORT_QUERY_TERMS;  // the 32-bit word's query terms
 // Long sublists (>= WLONG_MIN postings in a block) carry a per-wave layout (build pass
 // 3): wave w scatters only the docs of its segment, and runs of long terms need no
 // barrier.  Queries with more than WTERMS terms use the all-wave form only.
@@ -345,6 +345,166 @@ item_setup_kernel(const int64_t *__restrict__ term_start, const uint32_t *__rest
     }
 }
 
+// ---------------------------------------------------------------------------
+// Long queries: DI_SHORT_QUERY_TERMS < known terms <= DI_MAX_QUERY_TERMS.  The 32-bit
+// word holds neither their sums (255 x 4096 > 2^16) nor their first-touch index (> 255),
+// so an item (query, block) of such a query accumulates 64-bit words
+//     score(20) | (4095 - j)(12) | v_j(8)                       (bits 39..0)
+// -- ordered exactly like the short word: score, then first touch -- over half blocks
+// of LH_DOCS docs (128 KiB of LDS, the accumulator array of ScoreShared), and its
+// candidates carry the wide merge key  word << 24 | (0xFFFFFF - doc)  (docs < 2^24).
+// The first half's candidates wait in the item's output list; the second half's
+// selection runs over the union (the waiting keys held in registers, LH_HELD per
+// thread) and rewrites the list, so a long item emits one list of <= k keys like a
+// short one and the merge is unchanged (it decodes wide keys per query, see
+// merge_topk_kernel).  Terms go in chunks of MAX_TERMS bounds, a barrier per term.
+// Rare (no MS MARCO query comes close), so simple: one posting per lane per load.
+constexpr int LONG_TERMS = DI_MAX_QUERY_TERMS;
+constexpr int LH_DOCS = 16384;
+constexpr int LH_PER_THREAD = LH_DOCS / SC_THREADS;  // 16
+constexpr int LH_HELD = DI_MAX_TOPK / SC_THREADS;    // 4
+static_assert(MAX_BLOCK_DOCS <= 2 * LH_DOCS, "two halves cover a block");
+static_assert(LONG_TERMS <= 4096, "12-bit first-touch index");
+
+__device__ __forceinline__ void score_long_item(
+    int q, int b, const uint32_t *__restrict__ post, const int64_t *__restrict__ term_start,
+    const uint32_t *__restrict__ blk_off, const uint16_t *__restrict__ seg, int min_cls, int nb,
+    int block_docs, int64_t n_terms, uint32_t n_docs, uint32_t doc_lo,
+    const uint32_t *__restrict__ q_terms, const int32_t *__restrict__ cu_q, int k,
+    uint64_t *__restrict__ ck, int32_t *__restrict__ cn) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    ScoreShared &sh = *reinterpret_cast<ScoreShared *>(smem);
+    static_assert(sizeof(sh.acc) >= LH_DOCS * sizeof(uint64_t), "half-block words fit");
+    uint64_t *acc = reinterpret_cast<uint64_t *>(sh.acc);
+    int64_t *lo = sh.v.bounds[0], *hi = sh.v.bounds[1];
+    const int tid = threadIdx.x;
+    const int64_t block_first = (int64_t)b * block_docs;
+    const int n_local = (int)min((int64_t)block_docs, (int64_t)n_docs - block_first);
+    const int q0 = cu_q[q], nt = cu_q[q + 1] - q0;
+    if (n_local <= 0) {
+        if (tid == 0) *cn = 0;
+        return;
+    }
+    if ((uint64_t)doc_lo + n_docs > (1ull << 24)) {  // the wide key holds 24-bit docs
+        if (tid == 0) *cn = -1;
+        return;
+    }
+    const uint32_t vmin = 1u << (7 - min(min_cls, 7));  // impact pruning: values >= vmin
+    uint64_t held[LH_HELD] = {0, 0, 0, 0};
+    uint32_t n_held = 0;
+    for (int hb = 0; hb < n_local; hb += LH_DOCS) {
+        const int hn = min(LH_DOCS, n_local - hb);
+        const uint32_t gbase = doc_lo + (uint32_t)(block_first + hb);
+        {
+            uint4 *a4 = reinterpret_cast<uint4 *>(acc);
+            for (int i = tid; i < (hn + 1) / 2; i += SC_THREADS) a4[i] = make_uint4(0, 0, 0, 0);
+        }
+        if (tid == 0) sh.bad = 0;
+        for (int c0 = 0; c0 < nt; c0 += MAX_TERMS) {
+            const int cnt = min(MAX_TERMS, nt - c0);
+            __syncthreads();  // zeroing done / the previous chunk's bounds no longer read
+            for (int j = tid; j < cnt; j += SC_THREADS) {
+                const uint32_t t = q_terms[q0 + c0 + j];
+                if (t >= n_terms) {
+                    sh.bad = 1;
+                    lo[j] = hi[j] = 0;
+                    continue;
+                }
+                // the whole sublist: a long sublist is laid out per wave segment (classes
+                // in order inside each), so the class prefix is not one range -- pruning
+                // (min_cls < 7) filters by value in the scatter instead
+                const uint32_t *bo = blk_off + (int64_t)t * (nb + 1) + b;
+                lo[j] = term_start[t] + bo[0];
+                hi[j] = term_start[t] + bo[1];
+            }
+            __syncthreads();
+            if (sh.bad) {
+                if (tid == 0) *cn = -1;
+                return;
+            }
+            for (int jj = 0; jj < cnt; ++jj) {
+                const uint64_t fb = (uint64_t)(4095 - (c0 + jj)) << 8;
+                const int64_t L = lo[jj], H = hi[jj];
+                for (int64_t p0 = L; p0 < H; p0 += 4 * SC_THREADS) {
+                    uint32_t r[4];
+                    scatter_load<4>(post + p0, H - p0, tid, r);  // past the end: doc 32768, v 0
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const uint32_t d = ((r[u] ^ POST_X) >> 8) - (uint32_t)hb;
+                        const uint64_t v = r[u] & 255u;
+                        if (d < (uint32_t)hn && v >= vmin) {  // a doc occurs once per term
+                            const uint64_t w = acc[d];
+                            acc[d] = w ? w + (v << 20) : (v << 20) | fb | v;
+                        }
+                    }
+                }
+                __syncthreads();  // term boundary
+            }
+        }
+        // ---- selection over this half's touched words + the held keys -------------
+        auto key_of = [&](uint64_t w, int idx) {
+            return (w << 24) | (uint64_t)(0xFFFFFFu - (gbase + (uint32_t)idx));
+        };
+        uint64_t prefix = 0, mask = 0;
+        uint32_t need = (uint32_t)k;
+        for (int shift = 56; shift >= 0; shift -= 8) {
+            radix_clear<SC_THREADS, SC_WAVES>(sh.u.rs);
+            __syncthreads();
+            RunLen rl;
+            for (int i = 0; i < LH_PER_THREAD; ++i) {
+                const int idx = i * SC_THREADS + tid;
+                const uint64_t w = idx < hn ? acc[idx] : 0ull;
+                if (w) {
+                    const uint64_t x = key_of(w, idx);
+                    if ((x & mask) == prefix) rl.add(sh.u.rs, (uint32_t)(x >> shift) & 255u);
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < LH_HELD; ++i)
+                if ((uint32_t)(i * SC_THREADS + tid) < n_held && (held[i] & mask) == prefix)
+                    rl.add(sh.u.rs, (uint32_t)(held[i] >> shift) & 255u);
+            rl.flush(sh.u.rs);
+            __syncthreads();
+            radix_pick<SC_THREADS, SC_WAVES>(sh.u.rs, need);
+            if (shift == 56 && sh.u.rs.total <= (uint32_t)k) {  // every key is a candidate
+                prefix = 0;
+                break;
+            }
+            prefix |= (uint64_t)sh.u.rs.bin << shift;
+            mask |= (uint64_t)255 << shift;
+            need -= sh.u.rs.above;
+        }
+        // keys are unique: the keys >= prefix are exactly min(k, total) (prefix = the
+        // k-th largest key, or 0 when there are at most k)
+        if (tid == 0) sh.emit = 0;
+        __syncthreads();
+        for (int i = 0; i < LH_PER_THREAD; ++i) {
+            const int idx = i * SC_THREADS + tid;
+            const uint64_t w = idx < hn ? acc[idx] : 0ull;
+            const uint64_t x = w ? key_of(w, idx) : 0ull;
+            uint32_t pos;
+            if (wave_append(w != 0 && x >= prefix, &sh.emit, pos) && pos < (uint32_t)k) ck[pos] = x;
+        }
+#pragma unroll
+        for (int i = 0; i < LH_HELD; ++i) {
+            const bool ok = (uint32_t)(i * SC_THREADS + tid) < n_held && held[i] >= prefix;
+            uint32_t pos;
+            if (wave_append(ok, &sh.emit, pos) && pos < (uint32_t)k) ck[pos] = held[i];
+        }
+        __syncthreads();
+        n_held = min(sh.emit, (uint32_t)k);
+        if (hb + LH_DOCS < n_local) {  // the next half: hold this list (written above)
+#pragma unroll
+            for (int i = 0; i < LH_HELD; ++i) {
+                const uint32_t p = (uint32_t)(i * SC_THREADS + tid);
+                held[i] = p < n_held ? ck[p] : 0ull;
+            }
+        }
+        __syncthreads();  // the list is held before the next selection rewrites it
+    }
+    if (tid == 0) *cn = (int32_t)n_held;
+}
+
 // One work item = (query q, doc block b): accumulate, select the block's top-k.
 __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
                                            const uint32_t *__restrict__ post,
@@ -359,7 +519,8 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
                                            uint64_t *__restrict__ cand_key,
                                            int32_t *__restrict__ cand_n,
                                            uint32_t *__restrict__ qhist, int ablate,
-                                           const ItemRec *__restrict__ ir) {
+                                           const ItemRec *__restrict__ ir,
+                                           uint32_t *__restrict__ long_flag) {
     int64_t *lo = sh.v.bounds[0], *hi = sh.v.bounds[1];
 
     // opaque per item: keeps the per-thread index arithmetic of the sweeps from being
@@ -373,6 +534,13 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
     uint64_t *ck = cand_key + ((int64_t)q * nb + b) * k;
     int32_t *cn = cand_n + (int64_t)q * nb + b;
 
+    if (nt > MAX_TERMS && nt <= LONG_TERMS) {  // score_long_kernel's item (it runs next)
+        if (tid == 0) {
+            *cn = 0;
+            *long_flag = 1;
+        }
+        return;
+    }
     if (nt > MAX_TERMS || nt < 0 || n_local <= 0) {
         if (tid == 0) *cn = (nt > MAX_TERMS || nt < 0) ? -1 : 0;
         return;
@@ -1104,7 +1272,8 @@ score_blocks_kernel(const uint32_t *__restrict__ post, const int64_t *__restrict
                     uint32_t n_docs, uint32_t doc_lo, const uint32_t *__restrict__ q_terms,
                     const int32_t *__restrict__ cu_q, int k, uint64_t *__restrict__ cand_key,
                     int32_t *__restrict__ cand_n, int n_items, int n_q,
-                    uint32_t *__restrict__ qhist, int ablate, const ItemRec *__restrict__ rec) {
+                    uint32_t *__restrict__ qhist, int ablate, const ItemRec *__restrict__ rec,
+                    uint32_t *__restrict__ long_flag) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     ScoreShared &sh = *reinterpret_cast<ScoreShared *>(smem);
     if ((uint32_t)(uintptr_t)((__attribute__((address_space(3))) unsigned char *)smem) != 0) {
@@ -1118,8 +1287,55 @@ score_blocks_kernel(const uint32_t *__restrict__ post, const int64_t *__restrict
     for (int item = blockIdx.x; item < n_items; item += gridDim.x) {
         score_item(sh, item % n_q, item / n_q, post, term_start, blk_off, seg, lid, wmeta,
                    min_cls, nb, block_docs, n_terms, n_docs, doc_lo, q_terms, cu_q, k, cand_key,
-                   cand_n, qhist, ablate, rec ? rec + (int64_t)item * WTERMS : nullptr);
+                   cand_n, qhist, ablate, rec ? rec + (int64_t)item * WTERMS : nullptr,
+                   long_flag);
         __syncthreads();  // every wave is done with the LDS of this item
+    }
+}
+
+// The items of the long queries (score_long_item), after score_blocks_kernel on the
+// same stream: it gave them no candidates and raised *long_flag (0: every workgroup
+// leaves at once).  Persistent: every workgroup lists the long queries of each round of
+// SC_THREADS queries in query order (a block scan: the same list in every workgroup)
+// and takes its share of their (query, block) items.
+__global__ void __launch_bounds__(SC_THREADS)
+score_long_kernel(const uint32_t *__restrict__ post, const int64_t *__restrict__ term_start,
+                  const uint32_t *__restrict__ blk_off, const uint16_t *__restrict__ seg,
+                  int min_cls, int nb, int block_docs, int64_t n_terms, uint32_t n_docs,
+                  uint32_t doc_lo, const uint32_t *__restrict__ q_terms,
+                  const int32_t *__restrict__ cu_q, int k, uint64_t *__restrict__ cand_key,
+                  int32_t *__restrict__ cand_n, int n_q, const uint32_t *__restrict__ long_flag) {
+    if (__builtin_amdgcn_readfirstlane(*long_flag) == 0) return;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    ScoreShared &sh = *reinterpret_cast<ScoreShared *>(smem);
+    static_assert(sizeof(sh.wt) >= SC_THREADS * sizeof(uint32_t), "round list fits");
+    uint32_t *list = &sh.wt.wtab[0][0];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    for (int r0 = 0; r0 < n_q; r0 += SC_THREADS) {
+        const int q = r0 + tid;
+        int nt = 0;
+        if (q < n_q) nt = cu_q[q + 1] - cu_q[q];
+        const uint32_t is_long = nt > MAX_TERMS && nt <= LONG_TERMS ? 1u : 0u;
+        const uint32_t incl = wave_prefix_sum(is_long);
+        if (lane == 63) sh.wsum[wave] = incl;
+        __syncthreads();
+        uint32_t base = incl - is_long, n = 0;
+        for (int w2 = 0; w2 < SC_WAVES; ++w2) {
+            const uint32_t x = sh.wsum[w2];
+            if (w2 < wave) base += x;
+            n += x;
+        }
+        if (is_long) list[base] = (uint32_t)q;
+        __syncthreads();
+        const int n_items = (int)n * nb;
+        for (int it = blockIdx.x; it < n_items; it += gridDim.x) {
+            const int lq = (int)list[it % n], b = it / n;
+            score_long_item(lq, b, post, term_start, blk_off, seg, min_cls, nb, block_docs,
+                            n_terms, n_docs, doc_lo, q_terms, cu_q, k,
+                            cand_key + ((int64_t)lq * nb + b) * k, cand_n + (int64_t)lq * nb + b);
+            __syncthreads();  // the item's LDS (and the list) stay consistent
+        }
+        __syncthreads();  // the list and wsum are rewritten by the next round
     }
 }
 
@@ -1155,7 +1371,7 @@ merge_topk_kernel(const uint64_t *__restrict__ keys, const int32_t *__restrict__
                   int64_t q_stride, int64_t cq_stride, int cap,
                   uint64_t *__restrict__ out_key, uint32_t *__restrict__ out_doc,
                   uint32_t *__restrict__ out_score, int32_t *__restrict__ out_n, int mode,
-                  int select) {
+                  int select, const int32_t *__restrict__ cu_q) {
     // key i of list l of query q: keys[q*q_stride + l*list_stride + i]
     // its count:                  counts[q*cq_stride + l*cnt_stride]
     constexpr int WAVES = THREADS / 64;
@@ -1287,11 +1503,14 @@ merge_topk_kernel(const uint64_t *__restrict__ keys, const int32_t *__restrict__
         __syncthreads();
         total = take;
     }
+    // a long query's keys are wide (score_long_item)
+    const bool wide = mode == DECODE_QUANT && cu_q && cu_q[q + 1] - cu_q[q] > MAX_TERMS;
     auto emit = [&](int i, uint64_t x) {  // output rank i
         if (ok) ok[i] = x;
         if (mode == DECODE_QUANT) {
-            out_doc[(int64_t)q * k + i] = 0xFFFFFFFFu - (uint32_t)x;
-            out_score[(int64_t)q * k + i] = (uint32_t)(x >> 48);
+            out_doc[(int64_t)q * k + i] =
+                wide ? 0xFFFFFFu - (uint32_t)(x & 0xFFFFFFu) : 0xFFFFFFFFu - (uint32_t)x;
+            out_score[(int64_t)q * k + i] = (uint32_t)(x >> (wide ? 44 : 48));
         } else if (mode == DECODE_SPARSE) {
             out_doc[(int64_t)q * k + i] = 0xFFFFFFu - (uint32_t)(x & 0xFFFFFFu);
             out_score[(int64_t)q * k + i] = (uint32_t)(x >> 32);  // f32 bits
@@ -1389,6 +1608,7 @@ struct di_index {
     DevBuf post, term_start, blk_off, seg_dev, lid_dev, wmeta_dev;
     DevBuf ws_q, ws_cu, ws_ck, ws_cn, ws_doc, ws_score, ws_n, ws_key, ws_thr;
     DevBuf ws_rec;  // ItemRec per (item, term slot): item_setup_kernel -> score_blocks
+    DevBuf ws_long;  // score_blocks -> score_long_kernel: the batch has long queries
     // per-query threshold shared across blocks: -1 = auto (on from 8 blocks: at 4 blocks it
     // measured 2.31 vs 2.14 ms per 6980-query batch, at 34 / 269 blocks 16.9 vs 19.5 and
     // 130 vs 161 ms, merge 0.5 vs 7.1 and 1.4 vs 74 ms); DI_SCORE_THRESHOLD=0 / 1 forces
@@ -1625,6 +1845,9 @@ void enable_big_lds() {
     DI_HIP(hipFuncSetAttribute((const void *)score_blocks_kernel,
                                hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)sizeof(ScoreShared)));
+    DI_HIP(hipFuncSetAttribute((const void *)score_long_kernel,
+                               hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)sizeof(ScoreShared)));
     DI_HIP(hipFuncSetAttribute((const void *)merge_topk_kernel<1024>,
                                hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)(sizeof(MergeHead<1024>) + MG_LDS_KEYS * 8)));
@@ -1638,7 +1861,8 @@ void enable_big_lds() {
 
 void launch_merge(const uint64_t *keys, const int32_t *counts, int n_q, int n_lists, int k_in,
                   int k, uint64_t *out_key, uint32_t *out_doc, uint32_t *out_score,
-                  int32_t *out_n, int mode, hipStream_t s, bool lists_major = false) {
+                  int32_t *out_n, int mode, hipStream_t s, bool lists_major = false,
+                  const int32_t *cu_q = nullptr) {
     if (n_q == 0) return;
     int64_t ls = k_in, cs = 1, qs = (int64_t)n_lists * k_in, cqs = n_lists;
     if (lists_major) {
@@ -1665,17 +1889,17 @@ void launch_merge(const uint64_t *keys, const int32_t *counts, int n_q, int n_li
         size_t lds = sizeof(MergeHead<256>) + (size_t)cap * 8 + sel_lds;
         hipLaunchKernelGGL(merge_topk_kernel<256>, dim3(n_q), dim3(256), lds, s, keys, counts,
                            n_lists, k_in, k, ls, cs, qs, cqs, cap, out_key, out_doc, out_score,
-                           out_n, mode, select);
+                           out_n, mode, select, cu_q);
     } else if (mt == 512) {
         size_t lds = sizeof(MergeHead<512>) + (size_t)cap * 8 + sel_lds;
         hipLaunchKernelGGL(merge_topk_kernel<512>, dim3(n_q), dim3(512), lds, s, keys, counts,
                            n_lists, k_in, k, ls, cs, qs, cqs, cap, out_key, out_doc, out_score,
-                           out_n, mode, select);
+                           out_n, mode, select, cu_q);
     } else {
         size_t lds = sizeof(MergeHead<1024>) + (size_t)cap * 8 + sel_lds;
         hipLaunchKernelGGL(merge_topk_kernel<1024>, dim3(n_q), dim3(1024), lds, s, keys,
                            counts, n_lists, k_in, k, ls, cs, qs, cqs, cap, out_key, out_doc,
-                           out_score, out_n, mode, select);
+                           out_score, out_n, mode, select, cu_q);
     }
     check_launch("merge_topk");
 }
@@ -1790,6 +2014,11 @@ int di_index_search(di_index *ix, const uint32_t *q_terms, const int32_t *cu_q, 
                 DI_REQUIRE(c >= 0, DI_EINVAL, "cu_q not monotone at %d", q);
                 DI_REQUIRE(c <= DI_MAX_QUERY_TERMS, DI_ERANGE,
                            "query %d has %d terms (limit %d)", q, c, DI_MAX_QUERY_TERMS);
+                DI_REQUIRE(c <= DI_SHORT_QUERY_TERMS ||
+                               (uint64_t)ix->doc_lo + ix->n_docs <= (1ull << 24),
+                           DI_ERANGE,
+                           "query %d has %d terms: queries over %d terms need shard docs < 2^24",
+                           q, c, DI_SHORT_QUERY_TERMS);
             }
             nterms_total = cu_q[n_q];
             for (int64_t i = 0; i < nterms_total; ++i)
@@ -1803,6 +2032,7 @@ int di_index_search(di_index *ix, const uint32_t *q_terms, const int32_t *cu_q, 
         ix->ws_ck.reserve((size_t)chunk * per_q);
         ix->ws_cn.reserve((size_t)chunk * nb * 4);
         ix->ws_thr.reserve((size_t)chunk * QH_BINS * 4);
+        ix->ws_long.reserve(4);
         // (only the records of real terms are written / read: ~6 per query)
         // (bounded: WTERMS slots per item; a search whose records would pass 2 GiB -- a
         // small k leaves chunks of many queries -- walks the chain in the scorer instead)
@@ -1835,6 +2065,7 @@ int di_index_search(di_index *ix, const uint32_t *q_terms, const int32_t *cu_q, 
             } else {
                 const bool thr = nb > 1 && (ix->shared_thr < 0 ? nb >= 8 : ix->shared_thr == 1);
                 if (thr) DI_HIP(hipMemsetAsync(ix->ws_thr.p, 0, (size_t)nq * QH_BINS * 4, s));
+                DI_HIP(hipMemsetAsync(ix->ws_long.p, 0, 4, s));
                 TimedLaunch tl(ix->timer, timing, "score_blocks", s);  // (both kernels)
                 const int n_items = nq * nb;
                 if (use_rec) {
@@ -1854,14 +2085,24 @@ int di_index_search(di_index *ix, const uint32_t *q_terms, const int32_t *cu_q, 
                                    ix->n_docs, ix->doc_lo, dq, dcu + q0, k,
                                    ix->ws_ck.as<uint64_t>(), ix->ws_cn.as<int32_t>(), n_items,
                                    nq, thr ? ix->ws_thr.as<uint32_t>() : nullptr, ix->ablate,
-                                   use_rec ? ix->ws_rec.as<ItemRec>() : nullptr);
+                                   use_rec ? ix->ws_rec.as<ItemRec>() : nullptr,
+                                   ix->ws_long.as<uint32_t>());
                 check_launch("score_blocks");
+                hipLaunchKernelGGL(score_long_kernel, dim3(std::min(n_items, n_cu())),
+                                   dim3(SC_THREADS), sizeof(ScoreShared), s,
+                                   ix->post.as<uint32_t>(), ix->term_start.as<int64_t>(),
+                                   ix->blk_off.as<uint32_t>(), ix->seg_dev.as<uint16_t>(),
+                                   ix->min_cls, nb, ix->block_docs, ix->n_terms, ix->n_docs,
+                                   ix->doc_lo, dq, dcu + q0, k, ix->ws_ck.as<uint64_t>(),
+                                   ix->ws_cn.as<int32_t>(), nq, ix->ws_long.as<uint32_t>());
+                check_launch("score_long");
             }
             {
                 TimedLaunch tl(ix->timer, timing, "merge_topk", s);
                 launch_merge(ix->ws_ck.as<uint64_t>(), ix->ws_cn.as<int32_t>(), nq, nb, k, k,
                              dkey ? dkey + (int64_t)q0 * k : nullptr, ddoc + (int64_t)q0 * k,
-                             dscore + (int64_t)q0 * k, dn + q0, DECODE_QUANT, s);
+                             dscore + (int64_t)q0 * k, dn + q0, DECODE_QUANT, s, false,
+                             dcu + q0);
             }
         }
         if (!dev) {

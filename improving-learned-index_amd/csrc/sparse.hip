@@ -36,7 +36,7 @@ constexpr int SP_DOCS = 16384;
 constexpr int SP_THREADS = 1024;
 constexpr int SP_WAVES = SP_THREADS / 64;
 constexpr int SP_PER_THREAD = SP_DOCS / SP_THREADS;  // 16
-constexpr int SP_MAX_TERMS = DI_MAX_QUERY_TERMS;
+constexpr int SP_MAX_TERMS = 256;  // term bounds per chunk (LDS)
 
 struct SparseShared {
     float acc[SP_DOCS];          // 64 KiB
@@ -406,7 +406,8 @@ sparse_merge64_kernel(const Key96 *__restrict__ cand, const int32_t *__restrict_
 
 void launch_merge(const uint64_t *keys, const int32_t *counts, int n_q, int n_lists, int k_in,
                   int k, uint64_t *out_key, uint32_t *out_doc, uint32_t *out_score,
-                  int32_t *out_n, int mode, hipStream_t s, bool lists_major);
+                  int32_t *out_n, int mode, hipStream_t s, bool lists_major,
+                  const int32_t *cu_q);
 void enable_big_lds();
 
 }  // namespace di
@@ -582,7 +583,7 @@ int di_sparse_search(di_sparse *sp, const uint32_t *q_terms, const int32_t *cu_q
             TimedLaunch tl(sp->timer, timing, "merge_topk", s);
             launch_merge(sp->ws_ck.as<uint64_t>(), sp->ws_cn.as<int32_t>(), nq, nb, k, k,
                          dkey ? dkey + (int64_t)q0 * k : nullptr, ddoc + (int64_t)q0 * k,
-                         dsc + (int64_t)q0 * k, dn + q0, 1 /*DECODE_SPARSE*/, s, false);
+                         dsc + (int64_t)q0 * k, dn + q0, 1 /*DECODE_SPARSE*/, s, false, nullptr);
         }
         if (!dev) {
             DI_HIP(hipMemcpyAsync(out_doc, ddoc, (size_t)n_q * k * 4, hipMemcpyDeviceToHost, s));

@@ -103,10 +103,18 @@ def global_max(local_max: float, group=None, device=None) -> float:
     return float(t.item())
 
 
-def decode_quant_keys(keys: np.ndarray, n: int) -> List[Tuple[int, int]]:
+def decode_quant_keys(keys: np.ndarray, n: int, n_terms: int = 0) -> List[Tuple[int, int]]:
+    """(doc, score) list of one query's merged keys.  n < 0 is a query the scorer
+    rejected on some shard (a kernel limit, include/deepimpact.h): raise, never emit
+    the keys.  n_terms: the query's known terms (wide keys above DI_SHORT_QUERY_TERMS)."""
+    if n < 0:
+        raise RuntimeError("DI_ERANGE: the scorer rejected a query (out_n = -1: more than "
+                           "DI_MAX_QUERY_TERMS terms, or a long query on a shard past doc 2^24)")
     k = keys[:n].astype(np.uint64)
-    docs = (np.uint64(0xFFFFFFFF) - (k & np.uint64(0xFFFFFFFF))).astype(np.int64)
-    scores = (k >> np.uint64(48)).astype(np.int64)
+    wide = n_terms > 256  # DI_SHORT_QUERY_TERMS
+    m, sh = (np.uint64(0xFFFFFF), np.uint64(44)) if wide else (np.uint64(0xFFFFFFFF), np.uint64(48))
+    docs = (m - (k & m)).astype(np.int64)
+    scores = (k >> sh).astype(np.int64)
     return list(zip(docs.tolist(), scores.tolist()))
 
 
@@ -182,7 +190,7 @@ class ShardedRetriever:
 
     def search(self, queries) -> List[List[Tuple[int, int]]]:
         mk, mn = self.search_keys(queries)
-        return [decode_quant_keys(mk[i], int(mn[i])) for i in range(len(mn))]
+        return [decode_quant_keys(mk[i], int(mn[i]), len(queries[i])) for i in range(len(mn))]
 
 
 def exchange_merge_device(index, queries, k: int, device: int, flags: int = 0):

@@ -76,7 +76,8 @@ class Ranker:
                 dist.broadcast_object_list(ids, src=0)
                 keys, n = parallel.exchange_merge_device(
                     self.index.device_index, ids[0], self.top_k, self.device)
-                results = [parallel.decode_quant_keys(keys[i], int(n[i]))
+                # (raises on a query some shard rejected, out_n < 0)
+                results = [parallel.decode_quant_keys(keys[i], int(n[i]), len(ids[0][i]))
                            for i in range(len(chunk))]
             else:
                 results = self.index.score_batch(terms, self.top_k)

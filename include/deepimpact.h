@@ -47,7 +47,9 @@ extern "C" {
 #define DI_F_LISTS_MAJOR 0x8u /* di_topk_merge: keys are [list][query][k]       */
 
 /* Limits of the retrieval kernels (documented in DESIGN.md). */
-#define DI_MAX_QUERY_TERMS 256   /* known terms per query (first-touch key, u16 score) */
+#define DI_SHORT_QUERY_TERMS 256 /* queries up to this many known terms use the compact key */
+#define DI_MAX_QUERY_TERMS 4096  /* known terms per query of the quantized scorer; longer
+                                    than DI_SHORT_QUERY_TERMS: wide keys, shard docs < 2^24 */
 #define DI_MAX_TOPK 4096
 #define DI_MAX_SPARSE_QUERY_TERMS 4096 /* float search: known terms per query (chunked) */
 #define DI_MAX_SPARSE_DOCS 16777215u /* float index: doc ids embedded in 24 bits   */
@@ -100,7 +102,11 @@ int di_index_load_reference(const char *dir, uint32_t doc_lo, uint32_t doc_hi, i
  * the top-k (doc, score) pairs are written in the reference's order -- score
  * descending, ties in first-touch order -- to out_doc/out_score[q*k ...] and the
  * count to out_n[q].  out_key (may be NULL) receives the 64-bit merge keys used
- * to combine shards (di_topk_merge).                                             */
+ * to combine shards (di_topk_merge; wide keys for queries of more than
+ * DI_SHORT_QUERY_TERMS terms, see di_key_doc_wide).  A query over a kernel limit
+ * (more than DI_MAX_QUERY_TERMS terms; a long query on a shard reaching doc 2^24;
+ * an unknown term id) fails the call with DI_ERANGE / DI_EINVAL for host pointers,
+ * and gets out_n[q] = -1 with DI_F_DEVICE_PTRS (the caller must check).          */
 int di_index_search(di_index *ix, const uint32_t *q_terms, const int32_t *cu_q, int32_t n_q,
                     int32_t k, uint32_t *out_doc, uint32_t *out_score, int32_t *out_n,
                     uint64_t *out_key, uint32_t flags);
@@ -268,9 +274,15 @@ int di_synth_postings(int64_t n_docs, int32_t v_terms, uint64_t seed, int32_t ma
                       int32_t draws, double zipf_a, int64_t *term_off, uint32_t *pdoc,
                       uint8_t *pval, int64_t cap, int64_t *n_post, double *max_impact);
 
-/* Decoding of a quantized-index merge key. */
+/* Decoding of a quantized-index merge key.  A query of at most DI_SHORT_QUERY_TERMS
+ * known terms: score(16) | (255 - first term)(8) | its value(8) | ~doc(32).  A longer
+ * one (wide key): score(20) | (4095 - first term)(12) | its value(8) | (0xFFFFFF - doc)(24).
+ * Within one query every key has the same form and keys order exactly like the
+ * reference ranking (score desc, then first touch). */
 static inline uint32_t di_key_doc(uint64_t key) { return 0xFFFFFFFFu - (uint32_t)key; }
 static inline uint32_t di_key_score(uint64_t key) { return (uint32_t)(key >> 48); }
+static inline uint32_t di_key_doc_wide(uint64_t key) { return 0xFFFFFFu - (uint32_t)(key & 0xFFFFFFu); }
+static inline uint32_t di_key_score_wide(uint64_t key) { return (uint32_t)(key >> 44); }
 
 #ifdef __cplusplus
 }

@@ -141,7 +141,7 @@ typedef struct {
 
 static void score_one(const int64_t *term_off, const uint32_t *pdoc, const uint8_t *pval,
                       const uint32_t *qt, int nt, int k, uint32_t *acc, uint32_t *touched,
-                      uint16_t *ftk, uint32_t *od, uint32_t *os, int32_t *on, uint64_t *ok) {
+                      uint32_t *ftk, uint32_t *od, uint32_t *os, int32_t *on, uint64_t *ok) {
     int64_t nt_touch = 0;
     uint32_t max_score = 0;
     for (int j = 0; j < nt; ++j) {
@@ -152,8 +152,8 @@ static void score_one(const int64_t *term_off, const uint32_t *pdoc, const uint8
             uint32_t d = pdoc[p];
             if (acc[d] == 0) {
                 touched[nt_touch++] = d;
-                /* first-touch key: earlier term, then larger value (list order) */
-                ftk[d] = (uint16_t)(((255 - j) << 8) | v);
+                /* first touch: term index j and its value there (list order) */
+                ftk[d] = ((uint32_t)j << 8) | v;
             }
             acc[d] += v;
             if (acc[d] > max_score) max_score = acc[d];
@@ -177,9 +177,15 @@ static void score_one(const int64_t *term_off, const uint32_t *pdoc, const uint8
         if (pos < kk) {
             od[pos] = d;
             os[pos] = acc[d];
-            /* the shard-merge key of the HIP path (include/deepimpact.h) */
-            if (ok) ok[pos] = ((uint64_t)acc[d] << 48) | ((uint64_t)ftk[d] << 32) |
-                              (uint64_t)(0xFFFFFFFFu - d);
+            /* the shard-merge key of the HIP path (include/deepimpact.h di_key_*):
+             * compact up to 256 query terms, wide beyond */
+            const uint64_t j = ftk[d] >> 8, v = ftk[d] & 255u;
+            if (ok && nt <= 256)
+                ok[pos] = ((uint64_t)acc[d] << 48) | ((255 - j) << 40) | (v << 32) |
+                          (uint64_t)(0xFFFFFFFFu - d);
+            else if (ok)
+                ok[pos] = ((uint64_t)acc[d] << 44) | ((4095 - j) << 32) | (v << 24) |
+                          (uint64_t)(0xFFFFFFu - d);
         }
     }
     *on = kk;
@@ -198,7 +204,7 @@ OR_API int or_score(const int64_t *term_off, const uint32_t *pdoc, const uint8_t
     {
         uint32_t *acc = (uint32_t *)calloc((size_t)n_docs + 1, sizeof(uint32_t));
         uint32_t *touched = (uint32_t *)malloc(((size_t)n_docs + 1) * sizeof(uint32_t));
-        uint16_t *ftk = (uint16_t *)malloc(((size_t)n_docs + 1) * sizeof(uint16_t));
+        uint32_t *ftk = (uint32_t *)malloc(((size_t)n_docs + 1) * sizeof(uint32_t));
 #ifdef _OPENMP
 #pragma omp for schedule(dynamic, 1)
 #endif

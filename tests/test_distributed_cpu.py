@@ -149,6 +149,38 @@ def test_sharded_search_golden_index():
     assert [[[int(d), int(s)] for d, s in qq] for qq in out[0][0]] == gold["top1000"]
 
 
+def test_sharded_long_queries_match_single_shard(tmp_path):
+    """Queries of more than 256 known terms carry wide keys (include/deepimpact.h); the
+    sharded exchange decodes them per query length and equals the unsharded ranking."""
+    docs = _random_docs(900, 700, seed=5)
+    vocab, term_off, pdoc, pval = oracle.build_index(docs)
+    oracle.write_index(tmp_path, vocab, term_off, pdoc, pval)
+    ix = oracle.Index(tmp_path)
+    rng = np.random.default_rng(9)
+    queries = [[int(t) for t in rng.choice(len(vocab), size=int(rng.integers(257, 600)),
+                                           replace=False)] for _ in range(6)]
+    queries += [[int(t) for t in rng.choice(len(vocab), size=3, replace=False)]]
+    full = ix.score_ids(queries, 1000)
+    out = _run(2, str(tmp_path), queries, 1000)
+    for r in range(2):
+        assert [[(int(d), int(s)) for d, s in qq] for qq in out[r][0]] == \
+            [[(int(d), int(s)) for d, s in qq] for qq in full]
+
+
+def test_decode_quant_keys():
+    """Compact and wide key layouts; a rejected query (n < 0) raises instead of
+    emitting keys (the sharded rank path used to write k - 1 garbage lines)."""
+    compact = np.array([(300 << 48) | (250 << 40) | (7 << 32) | (0xFFFFFFFF - 123456789)],
+                       np.uint64)
+    assert parallel.decode_quant_keys(compact, 1, 5) == [(123456789, 300)]
+    wide = np.array([(70000 << 44) | (4000 << 32) | (7 << 24) | (0xFFFFFF - 8_800_000)],
+                    np.uint64)
+    assert parallel.decode_quant_keys(wide, 1, 300) == [(8_800_000, 70000)]
+    assert parallel.decode_quant_keys(wide, 0, 300) == []
+    with pytest.raises(RuntimeError):
+        parallel.decode_quant_keys(compact, -1, 5)
+
+
 def _quant_worker(rank, world, port, src, out, max_val, q):
     try:
         import torch.distributed as dist

@@ -312,3 +312,37 @@ def test_full_size_batch_is_batch_invariant(E, base, precision):
     got = enc.encode_packed(np.concatenate(sids), np.array(scu, np.int32), np.concatenate(stt),
                             np.array(sct, np.int32), round3=True)
     np.testing.assert_array_equal(got, np.concatenate(want))
+
+
+def test_flip_rates_at_bench_scale(E, base):
+    """The bench's full configs[1] batch (8192 docs, ~1.6 M tokens, ~344 k terms):
+    bf16x3 (and bf16) against the library's fp32 mode -- itself within ~1e-5 of the fp32
+    oracle (test_encoder_gpu) -- through the reference's text path: round(., 3)
+    (indexer.py:62-68; a "text flip" = the impact text differs) and the 8-bit quantizer
+    (quantize.py:27-47, each run with its own max like quantize_file; a "quantized
+    flip" = the integer differs, 0 = dropped included).  Bar: bf16x3 quantized flips
+    <= 1e-3 of the terms.  The rates are printed for DESIGN.md."""
+    fx, sd = base
+    ids, cu, tt, ct = _bench_batch(8192, 7)
+    r = {}
+    for prec in ("fp32", "bf16x3", "bf16"):
+        enc = E.DeviceEncoder(sd, _cfg(E, fx), precision=prec)
+        r[prec] = enc.encode_packed(ids, cu, tt, ct, round3=True)
+        del enc
+    assert r["fp32"].shape[0] == ct[-1] > 300_000
+
+    def quant(v):
+        d = v.astype(np.float64)
+        return np.trunc(d * (255.0 / float(d.max()))).astype(np.int64)
+
+    q32 = quant(r["fp32"])
+    rates = {}
+    for prec in ("bf16x3", "bf16"):
+        text = float(np.mean(r[prec].view(np.uint32) != r["fp32"].view(np.uint32)))
+        qf = float(np.mean(quant(r[prec]) != q32))
+        rel = np.abs(r[prec].astype(np.float64) - r["fp32"]) / np.maximum(np.abs(r["fp32"]), 1e-3)
+        rates[prec] = (text, qf, float(rel.max()))
+    print(f"flip rates over {int(ct[-1])} terms (vs fp32 mode): " + "; ".join(
+        f"{p}: text {t:.3e} quantized {q:.3e} max rel (rounded) {m:.2e}"
+        for p, (t, q, m) in rates.items()))
+    assert rates["bf16x3"][1] <= 1e-3, rates

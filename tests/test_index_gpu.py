@@ -119,11 +119,116 @@ def test_shards_merge_equals_single(L, synth):
                         L.key_score(mk[i, :mn[i]]).tolist())) == w
 
 
+def _long_queries(v_terms, n, seed, lo=257, hi=1200):
+    """Queries of lo..hi distinct known terms (zipf-ordered draws: the frequent terms
+    come early, as in a real long query; the rest fills up with random terms)."""
+    rng = np.random.default_rng(seed)
+    qs = []
+    for _ in range(n):
+        nt = int(rng.integers(lo, hi + 1))
+        z = np.minimum(rng.zipf(1.2, 2 * nt), v_terms) - 1
+        q = list(dict.fromkeys(int(x) for x in z))
+        seen = set(q)
+        rest = [int(x) for x in rng.permutation(v_terms) if int(x) not in seen]
+        qs.append((q + rest)[:nt])
+    return qs
+
+
+@pytest.mark.parametrize("k", [1, 10, 1000, 4096])
+def test_long_queries_match_oracle(L, synth, k):
+    """Queries of 257..1200 known terms (score_long_kernel: 64-bit words over half
+    blocks, wide keys) in one batch with short ones: the reference's ranking exactly
+    (InvertedIndex.score has no term limit, inverted_index.py:55-62)."""
+    term_off, pdoc, pval, ora = synth
+    dev = L.DeviceIndex.from_postings(term_off, pdoc, pval)
+    qs = _long_queries(5000, 10, seed=k) + _queries(5000, 30, seed=k)
+    qs = [qs[i] for i in np.random.default_rng(k).permutation(len(qs))]
+    assert max(len(q) for q in qs) > 256
+    got = dev.search(qs, k)
+    want = ora.score_ids(qs, k, n_threads=8)
+    for i, (g, w) in enumerate(zip(got, want)):
+        assert g == w, (i, len(qs[i]), len(g), len(w))
+    # pruned (min_impact) long queries too
+    dev.set_min_impact(16)
+    keep = pval >= 16
+    cnt = np.array([int(keep[term_off[t]:term_off[t + 1]].sum()) for t in range(len(term_off) - 1)])
+    pr = oracle.Index.__new__(oracle.Index)
+    pr.term_off = np.concatenate([[0], np.cumsum(cnt)]).astype(np.int64)
+    pr.pdoc, pr.pval, pr.n_docs = pdoc[keep], pval[keep], ora.n_docs
+    assert dev.search(qs, k) == pr.score_ids(qs, k, n_threads=8)
+
+
+def test_long_query_shards_merge_equals_single(L, synth):
+    """Wide keys of long queries merge across doc-id shards exactly like the compact
+    ones (di_topk_merge is key-order only) and decode with key_doc/key_score(wide)."""
+    term_off, pdoc, pval, ora = synth
+    k = 700
+    qs = _long_queries(5000, 6, seed=3, lo=257, hi=900) + _queries(5000, 6, seed=4)
+    full = L.DeviceIndex.from_postings(term_off, pdoc, pval)
+    _, _, n_full, key_full = full.search_csr(*L.csr(qs), k, with_keys=True)
+    _, okeys, on = ora.score_ids(qs, k, n_threads=8, with_keys=True)
+    cuts = [0, 33_333, ora.n_docs]
+    keys = np.zeros((len(qs), 2, k), np.uint64)
+    counts = np.zeros((len(qs), 2), np.int32)
+    for s in range(2):
+        sh = L.DeviceIndex.from_postings(term_off, pdoc, pval, cuts[s], cuts[s + 1])
+        _, _, n, key = sh.search_csr(*L.csr(qs), k, with_keys=True)
+        keys[:, s, :], counts[:, s] = key, n
+    mk, mn = L.topk_merge(keys, counts, k)
+    assert (mn == n_full).all() and (mn == on).all()
+    for i, q in enumerate(qs):
+        wide = L.is_wide(len(q))
+        assert (mk[i, :mn[i]] == key_full[i, :n_full[i]]).all()
+        assert (mk[i, :mn[i]] == okeys[i, :on[i]]).all()  # the oracle's own keys
+        w = ora.score_ids([q], k)[0]
+        assert list(zip(L.key_doc(mk[i, :mn[i]], wide).tolist(),
+                        L.key_score(mk[i, :mn[i]], wide).tolist())) == w
+
+
+def test_device_path_flags_rejected_queries(L, synth):
+    """DI_F_DEVICE_PTRS (the sharded rank CLI, bench) skips the host checks: a query
+    over a kernel limit must come back as out_n = -1 -- never as keys -- and the other
+    queries of the batch stay exact."""
+    import torch
+
+    term_off, pdoc, pval, ora = synth
+    dev = L.DeviceIndex.from_postings(term_off, pdoc, pval)
+    qs = [[1, 2, 3], list(range(4097)), [7], list(range(300)), [5000]]  # 4097 terms; bad id
+    flat, cu = L.csr(qs)
+    k = 10
+    d_t = torch.from_numpy(flat.astype(np.int32)).cuda()
+    d_cu = torch.from_numpy(cu).cuda()
+    od = torch.empty(len(qs) * k, dtype=torch.int32, device="cuda")
+    osc = torch.empty_like(od)
+    on = torch.empty(len(qs), dtype=torch.int32, device="cuda")
+    ok = torch.empty(len(qs) * k, dtype=torch.int64, device="cuda")
+    dev.search_device(d_t, d_cu, len(qs), k, od, osc, on, ok)
+    n = on.cpu().numpy()
+    assert n[1] == -1 and n[4] == -1
+    want = ora.score_ids([qs[0], qs[2], qs[3]], k)
+    od, osc = od.cpu().numpy(), osc.cpu().numpy()
+    for i, w in zip((0, 2, 3), want):
+        assert list(zip(od[i * k:i * k + n[i]].tolist(), osc[i * k:i * k + n[i]].tolist())) == w
+    from improving_learned_index_amd import parallel
+
+    with pytest.raises(RuntimeError):
+        parallel.decode_quant_keys(ok.cpu().numpy().view(np.uint64)[k:2 * k], int(n[1]), 4097)
+
+
 def test_limits_and_errors(L, synth):
     term_off, pdoc, pval, _ = synth
     dev = L.DeviceIndex.from_postings(term_off, pdoc, pval)
     with pytest.raises(L.DIError) as e:
-        dev.search([list(range(257))], 10)
+        dev.search([list(range(4097))], 10)  # DI_MAX_QUERY_TERMS
+    assert e.value.code == -4
+    assert len(dev.search([list(range(257))], 10)[0]) == 10  # no 256-term limit any more
+    # a long query needs 24-bit docs (wide key): a shard reaching doc 2^24 rejects it
+    far = L.DeviceIndex.from_postings(np.array([0, 1, 2], np.int64),
+                                      np.array([(1 << 24) + 3, 5], np.uint32),
+                                      np.array([9, 4], np.uint8))
+    assert far.search([[0, 1]], 10) == [[((1 << 24) + 3, 9), (5, 4)]]
+    with pytest.raises(L.DIError) as e:
+        far.search([[0, 1] * 129], 10)
     assert e.value.code == -4
     with pytest.raises(L.DIError):
         dev.search([[5000]], 10)  # unknown term id

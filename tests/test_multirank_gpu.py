@@ -117,3 +117,44 @@ def test_rank_cli_two_ranks_equals_one():
         _torchrun("rank", args + ["--output_path", str(td / "one7.tsv"), "--top_k", "7"],
                   world=0)
         _same_run((td / "three.tsv").read_text(), (td / "one7.tsv").read_text())
+
+
+def test_rank_cli_long_queries_two_ranks_equals_one():
+    """Queries of 257..700 known terms through the sharded rank CLI (device pointers,
+    wide keys, all-gather, GPU merge): the same run file as one process, which
+    test_index_gpu pins to the oracle.  (The 256-term limit of round 2 made this path
+    write garbage lines; now a rejected query raises instead, see test_index_gpu.)"""
+    import numpy as np
+
+    rng = np.random.default_rng(17)
+    n_terms = 900
+    with tempfile.TemporaryDirectory() as td:
+        td = Path(td)
+        lines = []
+        for d in range(4000):
+            ts = rng.choice(n_terms, size=int(rng.integers(0, 40)), replace=False)
+            lines.append(", ".join(f"\u2581w{t}: {int(rng.integers(1, 256))}" for t in ts))
+        (td / "coll.quantized").write_text("\n".join(lines) + "\n", encoding="utf-8")
+        from improving_learned_index_amd.inverted_index import InvertedIndexCreator
+
+        InvertedIndexCreator(td / "coll.quantized", td / "index").run()
+        qs = [rng.choice(n_terms, size=int(rng.integers(257, 700)), replace=False)
+              for _ in range(5)]
+        qs += [rng.choice(n_terms, size=4, replace=False) for _ in range(5)]
+        qf = td / "queries.tsv"
+        qf.write_text("".join(f"q{i}\t{' '.join(f'w{t}' for t in q)}\n"
+                              for i, q in enumerate(qs)))
+        args = ["--index_path", str(td / "index"), "--queries_path", str(qf),
+                "--tokenizer_path", str(GOLDEN / "tokenizer.json")]
+        _torchrun("rank", args + ["--output_path", str(td / "one.tsv")], world=0)
+        _torchrun("rank", args + ["--output_path", str(td / "two.tsv")])
+        one = (td / "one.tsv").read_text()
+        _same_run((td / "two.tsv").read_text(), one)
+        per_q = {}
+        for line in one.splitlines():
+            qid, doc, rank_, score = line.split("\t")
+            per_q.setdefault(qid, []).append((int(doc), int(score)))
+        for i in range(5):  # the long queries hit far more than 1000 docs
+            assert len(per_q[f"q{i}"]) == 1000
+            sc = [s_ for _, s_ in per_q[f"q{i}"]]
+            assert sc == sorted(sc, reverse=True) and sc[0] > 255
