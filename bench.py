@@ -35,8 +35,15 @@ from improving_learned_index_amd import synthetic as S  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md); 6.3 TB/s measured copy
 DOCS_PER_SHARD = 100_000
-V_TERMS = 200_000
 N_QUERIES = 6980  # MS MARCO dev.small
+REF_QUANTIZE_DOCS_S = 7003.0  # reference quantize_file, 1 core (SURVEY §6 / BASELINE.md)
+REF_CREATE_DOCS_S = 4726.0    # reference InvertedIndexCreator.run, 1 core (same)
+
+
+def v_terms(n_docs):
+    """the vocabulary scales with the collection, V = 2 N (the 100k-doc
+    slice keeps BASELINE.md's V = 200k)."""
+    return 2 * n_docs
 
 
 def _gloo():
@@ -87,20 +94,21 @@ def retrieve_leg(args, rank, world, dev, n_docs=DOCS_PER_SHARD, check_queries=0)
     check_queries > 0: the first that many queries are checked against the oracle's
     C scorer right after the timed loop."""
     t0 = time.time()
+    V = v_terms(n_docs)
     if n_docs == DOCS_PER_SHARD:
-        cu, term, imp = S.msmarco_like_docs(DOCS_PER_SHARD, V_TERMS, seed=1234 + rank)
+        cu, term, imp = S.msmarco_like_docs(DOCS_PER_SHARD, V, seed=1234 + rank)
         q, _ = S.quantize_like_reference(imp)
-        term_off, pdoc, pval = S.postings_reference_order(cu, term, q, V_TERMS)
+        term_off, pdoc, pval = S.postings_reference_order(cu, term, q, V)
         del cu, term, imp, q
     else:
-        term_off, pdoc, pval, _ = S.synth_postings(n_docs, V_TERMS, seed=4321 + rank)
+        term_off, pdoc, pval, _ = S.synth_postings(n_docs, V, seed=4321 + rank)
     t_gen = time.time() - t0
     doc_lo = rank * n_docs
     if doc_lo:
         pdoc = pdoc + np.uint32(doc_lo)
     ix = _lib.DeviceIndex.from_postings(term_off, pdoc, pval, doc_lo, doc_lo + n_docs,
                                         device=dev)
-    queries = S.msmarco_like_queries(args.queries, V_TERMS, seed=1234)
+    queries = S.msmarco_like_queries(args.queries, V, seed=1234)
     flat, cuq = _lib.csr(queries)
     log(f"[rank {rank}] shard index: {ix.info()} generated in {t_gen:.1f}s, built in "
         f"{time.time() - t0 - t_gen:.1f}s")
@@ -148,6 +156,10 @@ def retrieve_leg(args, rank, world, dev, n_docs=DOCS_PER_SHARD, check_queries=0)
         dist.barrier()
     el = time.perf_counter() - t0
     ix.sync()
+    # a query the scorer rejected (out_n < 0: a kernel limit) invalidates the leg
+    n_min = int((m_n if world > 1 else out_n).min().item()) if nq else 0
+    if n_min < 0:
+        raise SystemExit(f"scorer rejected a query (out_n = {n_min}): the leg is invalid")
     ms_sb, n_sb = ix.timing("score_blocks")
     ms_mg, n_mg = ix.timing("merge_topk")
     if check_queries and rank == 0:
@@ -176,7 +188,8 @@ def retrieve_leg(args, rank, world, dev, n_docs=DOCS_PER_SHARD, check_queries=0)
         "value": nq * args.steps / el,
         "ms_per_step": 1000.0 * el / args.steps,
         "postings_per_query": post_per_launch / nq,
-        "docs": n_docs, "postings": int(ix.info()["n_postings"]), "blocks": ix.info()["n_blocks"],
+        "docs": n_docs, "v_terms": V, "postings": int(ix.info()["n_postings"]),
+        "blocks": ix.info()["n_blocks"],
         "kernel_ms": {"score_blocks": ms_sb / max(n_sb, 1), "merge_topk": ms_mg / max(n_mg, 1)},
         "kernel_ms_per_step": {"score_blocks": ms_sb / max(args.steps, 1),
                                "merge_topk": ms_mg / max(args.steps, 1)},
@@ -198,7 +211,11 @@ def retrieve_leg(args, rank, world, dev, n_docs=DOCS_PER_SHARD, check_queries=0)
         traffic *= n_sb / max(args.steps, 1)
     res["roofline"] = {
         "kernel": "score_blocks_kernel",
-        "bound": "hbm",
+        # priced against HBM by the algorithmic bytes, but the counters show the popular
+        # lists served from L2 / MALL (PMC traffic below) and the LDS scatter's latency
+        # and bank conflicts as the limit
+        "bound": "lds",
+        "priced_against": "hbm",
         "achieved": round(achieved, 1),
         "peak": HBM_PEAK_GBS,
         "unit": "GB/s",
@@ -513,6 +530,65 @@ def index_e2e_leg(args, dev):
                     "docs run as 256-doc device chunks)"}
 
 
+def text_legs(args):
+    """A10 + A11 at one 8-way shard of configs[2] (1.1 M docs, V = 2 N): the impact TSV
+    the index CLI writes (synthetic, the retrieve legs' generator, native writer) ->
+    quantize_file (di_quantize_file: threaded parse, fp64 GPU quantize, threaded
+    format) -> InvertedIndexCreator.run (di_build_reference_index: threaded parse /
+    vocabulary / bucketing / per-term value sort, byte-identical files).  Each timed
+    region is the whole call, file read and write included, as the reference's rates
+    (7.0 k / 4.7 k docs/s, 1 core) are.  Host threads: DI_HOST_THREADS or
+    OMP_NUM_THREADS (16 on the GPU box).  Checked: the index holds exactly the
+    generator's postings (di_synth_postings, same seed)."""
+    import ctypes
+    import shutil
+    import tempfile
+
+    from improving_learned_index_amd.inverted_index import create_index
+    from improving_learned_index_amd.quantize import quantize_file
+
+    n = args.text_docs
+    V = v_terms(n)
+    td = Path(tempfile.mkdtemp(dir="/tmp"))
+    try:
+        t0 = time.perf_counter()
+        n_pairs = S.synth_impact_tsv(td / "collection.index", n, V, seed=4321)
+        t_gen = time.perf_counter() - t0
+        in_bytes = (td / "collection.index").stat().st_size
+        t0 = time.perf_counter()
+        quantize_file(td / "collection.index", td / "collection.quantized")
+        t_q = time.perf_counter() - t0
+        (td / "collection.index").unlink()
+        q_bytes = (td / "collection.quantized").stat().st_size
+        t0 = time.perf_counter()
+        create_index(td / "collection.quantized", td / "index")
+        t_c = time.perf_counter() - t0
+        dat = (td / "index" / "inverted_index.dat").stat().st_size
+        term_off = np.zeros(V + 1, np.int64)
+        n_post = ctypes.c_int64(0)
+        _lib.check(_lib.lib().di_synth_postings(n, V, 4321, 100, 200, 1.2,
+                                                term_off.ctypes.data_as(ctypes.c_void_p), None,
+                                                None, 0, ctypes.byref(n_post), None))
+        if dat != 5 * n_post.value:
+            raise SystemExit(f"text legs: index holds {dat // 5} postings, the generator "
+                             f"{n_post.value}")
+    finally:
+        shutil.rmtree(td, ignore_errors=True)
+    threads = int(os.environ.get("DI_HOST_THREADS") or os.environ.get("OMP_NUM_THREADS") or
+                  (os.cpu_count() or 1))
+    log(f"text legs: {n} docs, gen {t_gen:.1f}s, quantize {t_q:.2f}s, create {t_c:.2f}s")
+    common = {"docs": n, "v_terms": V, "terms": int(n_pairs), "host_threads": min(threads, 64)}
+    return {
+        "quantize": {"value": round(n / t_q, 1), "unit": "docs/s", "seconds": round(t_q, 3),
+                     "input_bytes": int(in_bytes), "output_bytes": int(q_bytes),
+                     "reference_cpu_docs_s": REF_QUANTIZE_DOCS_S,
+                     "vs_reference_cpu": round(n / t_q / REF_QUANTIZE_DOCS_S, 1), **common},
+        "index_create": {"value": round(n / t_c, 1), "unit": "docs/s", "seconds": round(t_c, 3),
+                         "postings": int(dat // 5), "reference_cpu_docs_s": REF_CREATE_DOCS_S,
+                         "vs_reference_cpu": round(n / t_c / REF_CREATE_DOCS_S, 1), **common},
+    }
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -530,10 +606,13 @@ def main():
                     help="index_e2e leg: --model_batch_size (reference default 32)")
     ap.add_argument("--e2e-process-batch", type=int, default=1600,
                     help="index_e2e leg: --process_batch_size (reference default 1600)")
-    ap.add_argument("--legs", default="encode,encode_x3,retrieve,retrieve_shard,index_e2e",
-                    help="encode (bf16, configs[1]), encode_x3 (fp32-faithful bf16x3), retrieve "
-                         "(100k-doc shard, configs[1]), retrieve_shard (1.1M docs: one 8-way shard "
-                         "of configs[2]), retrieve_full (8.8M docs on one GPU, configs[2]), "
+    ap.add_argument("--text-docs", type=int, default=1_100_000,
+                    help="text legs (quantize, index_create): docs of the impact TSV")
+    ap.add_argument("--legs", default="encode_x3,encode,retrieve,retrieve_shard,text,index_e2e",
+                    help="encode_x3 (fp32-faithful bf16x3: the headline), encode (bf16 throughput "
+                         "mode), retrieve (100k-doc shard, configs[1]), retrieve_shard (1.1M docs: "
+                         "one 8-way shard of configs[2]), retrieve_full (8.8M docs on one GPU, "
+                         "configs[2]), text (quantize + index_create of a 1.1M-doc impact TSV), "
                          "index_e2e (index.py's path end to end, tokenizer workers included)")
     args = ap.parse_args()
 
@@ -561,13 +640,14 @@ def main():
     legs = set(args.legs.split(","))
     enc_res = ret_res = None
     x3_res = None
+    if "encode_x3" in legs:
+        x3_res, x3_ctx = encode_leg(args, rank, world, dev, precision="bf16x3")
     if "encode" in legs:
         enc_res, enc_ctx = encode_leg(args, rank, world, dev)
-    if "encode_x3" in legs:
-        x3_res, _ = encode_leg(args, rank, world, dev, precision="bf16x3")
     if "retrieve" in legs:
         ret_res, ret_ctx = retrieve_leg(args, rank, world, dev)
     e2e_res = index_e2e_leg(args, dev) if "index_e2e" in legs and world == 1 else None
+    text_res = text_legs(args) if "text" in legs and rank == 0 else None
     big = {}
     for leg, nd in (("retrieve_shard", 1_100_000), ("retrieve_full", 8_800_000)):
         if leg in legs:
@@ -575,7 +655,10 @@ def main():
             big[leg], _ = retrieve_leg(args, rank, world, dev, n_docs=nd,
                                        check_queries=0 if os.environ.get("DI_PROFILE_ABLATE") else 20)
             torch.cuda.empty_cache()
-    primary = next((r for r in (enc_res, x3_res, ret_res) + tuple(big.values()) + (e2e_res,)
+    # the headline is the fp32-faithful encode (bf16x3: the reference computes in fp32,
+    # indexer.py:46); the bf16 throughput mode is a side line (it flips a third of the
+    # quantized integers)
+    primary = next((r for r in (x3_res, enc_res, ret_res) + tuple(big.values()) + (e2e_res,)
                     if r is not None), None)
     if primary is None:
         raise SystemExit("no bench leg selected")
@@ -590,11 +673,12 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "bf16" if enc_res is not None else ("bf16x3" if x3_res is not None else "u8"),
+        "dtype": "bf16x3" if primary is x3_res else ("bf16" if primary is enc_res else "u8"),
         "data": "synthetic (seeded generators of BASELINE.md §2 / SURVEY §8d); random-init "
                 "xlm-roberta-base weights",
-        "config": {"workload": "configs[1]: MS MARCO passage 100k-doc slice shape, bf16 encode "
-                               "(xlm-roberta-base DeepImpact) + top-1000 retrieve of 6980 "
+        "config": {"workload": "configs[1]: MS MARCO passage 100k-doc slice shape, encode "
+                               "(xlm-roberta-base DeepImpact, fp32-faithful split-bf16 "
+                               "'bf16x3'; bf16 beside it) + top-1000 retrieve of 6980 "
                                "dev.small-shaped queries",
                    "docs_per_step_per_gpu": args.docs, "max_length": args.max_len,
                    "docs_per_shard": DOCS_PER_SHARD, "queries": args.queries, "k": args.k,
@@ -608,8 +692,14 @@ def main():
         "cpu_baseline": None,
     }
     if enc_res is not None:
-        out["encode"] = {k: enc_res[k] for k in ("tokens_per_step", "kernels", "gemm_tflops",
-                                                 "model_tflops", "model_flops_frac", "out_sha1")}
+        out["encode_bf16"] = {
+            "value": round(enc_res["value"], 2), "unit": "docs/s", "dtype": "bf16",
+            "precision": "bf16 MFMA, LayerNorms folded: NOT fp32-faithful -- it flips a third "
+                         "of the 8-bit quantized integers of the fp32 reference "
+                         "(tests/test_encoder_bf16x3_gpu.py::test_flip_rates_at_bench_scale)",
+            "ms_per_step": round(enc_res["ms_per_step"], 4),
+            **{k: enc_res[k] for k in ("tokens_per_step", "kernels", "gemm_tflops", "model_tflops",
+                                       "model_flops_frac", "roofline", "out_sha1")}}
     if x3_res is not None:
         out["encode_fp32_faithful"] = {
             "value": round(x3_res["value"], 2), "unit": "docs/s", "dtype": "bf16x3",
@@ -629,6 +719,8 @@ def main():
                            "cpu_baseline": None}
     if e2e_res is not None:
         out["index_e2e"] = e2e_res
+    if text_res is not None:
+        out.update(text_res)
     for leg, r in big.items():
         out[leg] = {"value": round(r["value"], 2), "unit": "queries/s",
                     "docs_per_shard": r["docs"], "postings": r["postings"], "blocks": r["blocks"],
@@ -637,12 +729,13 @@ def main():
                     "kernel_ms": r["kernel_ms"], "kernel_ms_per_step": r["kernel_ms_per_step"],
                     "launches_per_step": r["launches_per_step"], "roofline": r["roofline"]}
     if rank == 0 and world == 1 and not args.no_cpu:
-        if enc_res is not None:
-            out["cpu_baseline"] = cpu_baseline_encode(args, *enc_ctx)
+        if x3_res is not None or enc_res is not None:
+            cb = cpu_baseline_encode(args, *(x3_ctx if x3_res is not None else enc_ctx))
+            out["cpu_baseline"] = cb
         if ret_res is not None:
             cb = cpu_baseline_retrieve(args, *ret_ctx)
             out["retrieve"]["cpu_baseline"] = cb
-            if enc_res is None:
+            if x3_res is None and enc_res is None:
                 out["cpu_baseline"] = cb
     if rank == 0:
         print(json.dumps(out), flush=True)

@@ -77,6 +77,8 @@ SIGNATURES = {
     "di_sparse_destroy": (ctypes.c_int, [P]),
     "di_synth_postings": (ctypes.c_int, [I64, I32, U64, I32, I32, ctypes.c_double, P, P, P, I64,
                                          P, P]),
+    "di_synth_impact_tsv": (ctypes.c_int, [ctypes.c_char_p, I64, I32, U64, I32, I32,
+                                           ctypes.c_double, P]),
 }
 
 _LIB = None

@@ -54,6 +54,35 @@ void parallel_for(int64_t n, F &&f) {
     for (auto &x : th) x.join();
 }
 
+// parallel_for over n chunks whose bodies may throw di::Error: f(chunk, thread).  The
+// lowest-index failing chunk's error (code and message -- di_last_error is thread-local)
+// is rethrown on the calling thread, the one a serial loop would have raised first.
+template <class F>
+void parallel_chunks(int64_t n, F &&f) {
+    std::vector<int> code((size_t)std::max<int64_t>(n, 1), 0);
+    std::vector<std::string> msg((size_t)std::max<int64_t>(n, 1));
+    parallel_for(n, [&](int64_t lo, int64_t hi, int t) {
+        for (int64_t c = lo; c < hi; ++c) {
+            try {
+                f(c, t);
+            } catch (const Error &e) {
+                code[(size_t)c] = e.code;
+                msg[(size_t)c] = last_error();
+                return;  // (later chunks of this thread come after the failure)
+            } catch (...) {
+                code[(size_t)c] = DI_ENOMEM;
+                msg[(size_t)c] = "host allocation failed";
+                return;
+            }
+        }
+    });
+    for (int64_t c = 0; c < n; ++c)
+        if (code[(size_t)c]) {
+            set_error("%s", msg[(size_t)c].c_str());
+            throw Error{code[(size_t)c]};
+        }
+}
+
 [[noreturn]] inline void fail(int code, const char *msg) {
     set_error("%s", msg);
     throw Error{code};

@@ -7,27 +7,26 @@
 // Device layout ("doc-blocked, impact-ordered postings"):
 //   docs of a shard are cut into nb = ceil(n_docs / 32768) equal blocks (a multiple
 //   of 64 docs each, at most 32768); every term's postings are grouped by block
-//   (block-major, then the reference order value-desc/doc-asc).  One posting = one
-//   u32: (doc_in_block << 8) | value.
-//   term_start[t] (i64) + blk_off[t*(NB+1)+b] (u32) locate the sublist (t, b).
+//   (block-major; inside a block by impact class, bank-dealt).  One posting = one
+//   u32: (doc_in_block << 8) | value.  A sparse term -> block table locates the
+//   (term, block) sublists (SubIndex).
 //
-// score_blocks: one 1024-thread workgroup per (query, block).  The block's
-//   32768 accumulators live in LDS (128 KiB).  Terms are applied in query
-//   order with a barrier between terms; inside a term every doc occurs once,
-//   so plain LDS read-modify-write is race free and no atomics are needed.
-//   Each LDS word is   score(16) | (255 - j)(8) | v_j(8)
-//   where j is the first query term that touched the doc and v_j its value
-//   there: comparing words reproduces the reference's order exactly -- score
-//   descending, then first-touch order (term order, then impact desc inside
-//   that term's list, then doc asc).  A block-wide radix select keeps the
-//   block's top-k (ties in the last digit by doc ascending).  With <= 16 query
-//   terms the k-th score comes from one 4096-bin score histogram instead, and the
-//   docs tied at it are ordered from a compact list.
-// merge_topk: one workgroup per query sorts the <= NB*k block candidates by
-//   the 64-bit key  word(32) | ~doc(32)  and writes doc/score/key.
+// score_blocks: one 1024-thread workgroup per (query, block) item, persistent.  The
+//   block's accumulators live in LDS: packed 16-bit scores (LDS atomic adds, no
+//   return) and 16-bit first-touch keys (plain stores, terms applied in reverse query
+//   order so the first term's key is the last written).  A doc's word
+//   score(16) | (255 - j)(8) | v_j(8)  (j = the first query term touching it, v_j its
+//   value there) orders docs exactly like the reference -- score descending, then
+//   first-touch order (term order, then impact desc inside that term's list, then doc
+//   asc).  Selection: a per-query threshold shared across blocks, a 4096-bin score
+//   histogram (<= 16 query terms) or a block-wide radix select.
+// score_long: queries of more than 256 terms (64-bit words, wide keys).
+// merge_topk: one workgroup per query selects the <= NB*k block candidates by the
+//   64-bit key  word(32) | ~doc(32)  and writes doc/score/key.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstddef>
 #include <cstdlib>
 #include <cstring>
 #include <fstream>
@@ -42,14 +41,15 @@
 
 namespace di {
 
-constexpr int MAX_BLOCK_DOCS = 32768;  // LDS accumulators per workgroup (128 KiB)
+constexpr int MAX_BLOCK_DOCS = 32768;  // docs per block (one workgroup's accumulators)
 constexpr int SC_THREADS = 1024;
 constexpr int SC_WAVES = SC_THREADS / 64;
-constexpr int SC_PER_THREAD = MAX_BLOCK_DOCS / SC_THREADS;  // 32
-constexpr int MAX_TERMS = DI_SHORT_QUERY_TERMS;  // the 32-bit word's query terms
+constexpr int SC_PER_THREAD = MAX_BLOCK_DOCS / SC_THREADS;  // 32 docs per thread in a sweep
+constexpr int MAX_TERMS = DI_SHORT_QUERY_TERMS;  // query terms of the compact word
 // Long sublists (>= WLONG_MIN postings in a block) carry a per-wave layout (build pass
-// 3): wave w scatters only the docs of its segment, and runs of long terms need no
-// barrier.  Queries with more than WTERMS terms use the all-wave form only.
+// 3): wave w scatters only the docs of its segment.  Queries of at most WTERMS terms
+// run every term that way (short terms: every wave reads the sublist, applies its own
+// docs); longer ones run the all-wave form, a barrier per term.
 constexpr int WSEG = SC_WAVES;
 constexpr int WLONG_MIN = 1024;
 constexpr int WTERMS = 64;
@@ -60,14 +60,43 @@ constexpr int FAST_TERMS = 16;
 constexpr int HIST_BINS = 4096;
 constexpr int TIE_CAP = HIST_BINS;
 constexpr int QH_BINS = 4096;  // per-query candidate-score histogram (shared threshold)
-// Safe early termination (score-at-a-time over the impact classes, see score_item):
-// queries of at most ET_TERMS terms with the per-wave layout.
-constexpr int ET_TERMS = FAST_TERMS;
+// Long queries (score_long_item): 64-bit words over half blocks.
+constexpr int LONG_TERMS = DI_MAX_QUERY_TERMS;
+constexpr int LH_DOCS = 16384;
+constexpr int LH_PER_THREAD = LH_DOCS / SC_THREADS;  // 16
+constexpr int LH_HELD = DI_MAX_TOPK / SC_THREADS;    // 4
+static_assert(MAX_BLOCK_DOCS <= 2 * LH_DOCS, "two halves cover a block");
+static_assert(LONG_TERMS <= 4096, "12-bit first-touch index");
+
+// Accumulators of one block (LDS, from address 0):
+//   sc[w]  packed 16-bit scores, doc 2w in the low half, 2w + 1 in the high half
+//          (a score is at most 255 x 256 < 2^16: no carry between the halves), then
+//          one dummy word per lane;
+//   ft[d]  the doc's first-touch key (255 - j) << 8 | v_j (j = the first query term
+//          touching it, v_j its value there), then two dummy slots per lane.
+// The scatter never reads them: a posting is ds_add_u32 (v << 16 (d & 1)) to sc[d / 2]
+// plus a plain ds_write_b16 of its term's key to ft[d], with the terms applied in
+// REVERSE query order -- the last write is the first term's, and a doc's writes all
+// come from one wave in program order (the per-wave layout) or from terms separated by
+// barriers (all-wave form).  No load -> read -> write chain per posting.
+// The selection works on the scores and reads a key only for what it emits or ranks:
+//   word(d) = score(16) | (255 - j)(8) | v_j(8)
+// orders docs exactly like the reference (score desc, then first touch: term order,
+// then the term list's value-desc / doc-asc order).
+constexpr int SC_WORDS = MAX_BLOCK_DOCS / 2 + 64;
+constexpr int FT_SLOTS = MAX_BLOCK_DOCS + 128;
+constexpr uint32_t FT_BASE = SC_WORDS * 4;  // LDS byte address of ft[0]
 
 struct ScoreShared {
-    uint32_t acc[MAX_BLOCK_DOCS + 64];  // 128 KiB (+ the scatter's dummy words)
     union {
-        RadixScratch<SC_WAVES> rs;  // general radix path
+        struct {
+            uint32_t sc[SC_WORDS];
+            uint16_t ft[FT_SLOTS];
+        } a;
+        uint64_t w64[LH_DOCS];  // long-query items: the 64-bit words of a half block
+    } acc;
+    union {
+        RadixScratch<SC_WAVES> rs;      // general radix path
         uint32_t hist[HIST_BINS + 64];  // fast path: score histogram (+ spare bins), then the tie list
     } u;
     union {
@@ -79,19 +108,58 @@ struct ScoreShared {
     uint32_t n_tie;  // tie-list cursor
     uint32_t bad;
     uint32_t thr, above, ties, bin, bin_above;
-    uint32_t tq;  // the query's shared threshold as this item read it
-    uint32_t lmask[WTERMS / 32];      // terms (j < WTERMS) with a per-wave layout in this block
-    union {
-        uint32_t wtab[WTERMS][WSEG];       // their per-wave runs: start << 16 | end (in the sublist)
-        uint16_t wcls[ET_TERMS][WSEG][8];  // early termination: per-wave class ends (wmeta)
-    } wt;
-    uint16_t segj[ET_TERMS][8];            // early termination: short terms' class ends (seg)
+    uint32_t tq;                   // the query's shared threshold as this item read it
+    uint32_t lmask[WTERMS / 32];   // terms (j < WTERMS) with a per-wave layout in this block
+    uint32_t wtab[WTERMS][WSEG];   // their per-wave runs: start << 16 | end (in the sublist)
 };
+static_assert(offsetof(ScoreShared, acc) == 0 && sizeof(ScoreShared().acc.a) ==
+                  SC_WORDS * 4 + FT_SLOTS * 2, "accumulator layout");
+static_assert(sizeof(ScoreShared().acc) >= LH_DOCS * sizeof(uint64_t), "half-block words fit");
 static_assert(sizeof(RadixScratch<SC_WAVES>) >= (HIST_BINS + 64) * 4,
               "histogram (+ 64 spare bins) overlays the radix scratch");
+static_assert(sizeof(ScoreShared().wtab) >= SC_THREADS * 4, "score_long_kernel's query list");
 
-// One radix pass over the block's words (i-major: lanes read consecutive words,
-// conflict-free).  KeyF: word,index -> key;  Pred: word,index,key -> bool.
+__device__ __forceinline__ uint32_t score_of(const ScoreShared &sh, int idx) {
+    return (sh.acc.a.sc[idx >> 1] >> ((idx & 1) << 4)) & 0xFFFFu;
+}
+__device__ __forceinline__ uint32_t word_at(const ScoreShared &sh, int idx) {
+    return (score_of(sh, idx) << 16) | sh.acc.a.ft[idx];
+}
+
+// Sweep of the block's scores: f(s, idx) for idx < round4(n_local), 4 consecutive docs
+// per lane per ds_read_b64 (lane-consecutive: conflict-free), 4 reads in flight before
+// any is used.  Scores past the zeroed range come as 0; f runs in wave-uniform control
+// flow (it may ballot).
+template <class F>
+__device__ __forceinline__ void sweep_scores(const ScoreShared &sh, int n_local, int tid, F f) {
+    const uint2 *s2 = reinterpret_cast<const uint2 *>(sh.acc.a.sc);
+    const int n4 = (n_local + 3) >> 2;
+    constexpr int G = 4;
+    for (int i0 = 0; i0 < SC_PER_THREAD / 4; i0 += G) {
+        if (i0 * SC_THREADS >= n4) break;  // (uniform)
+        uint2 x[G];
+#pragma unroll
+        for (int i = 0; i < G; ++i) {
+            // q4 < 8192 always lies inside the array: load unconditionally, then drop
+            // what lies past the zeroed range
+            const int q4 = (i0 + i) * SC_THREADS + tid;
+            const uint2 y = s2[q4];
+            x[i].x = q4 < n4 ? y.x : 0u;
+            x[i].y = q4 < n4 ? y.y : 0u;
+        }
+#pragma unroll
+        for (int i = 0; i < G; ++i) {
+            const int base = 4 * ((i0 + i) * SC_THREADS + tid);
+            f(x[i].x & 0xFFFFu, base);
+            f(x[i].x >> 16, base + 1);
+            f(x[i].y & 0xFFFFu, base + 2);
+            f(x[i].y >> 16, base + 3);
+        }
+    }
+}
+
+// One radix pass over the block's full words (i-major: lanes read consecutive docs).
+// KeyF: word,index -> key;  Pred: word,index,key -> bool.
 template <class KeyF, class Pred>
 __device__ __forceinline__ void score_radix_pass(ScoreShared &sh, int n_local, int shift,
                                                  uint32_t need, KeyF key, Pred pred) {
@@ -102,7 +170,8 @@ __device__ __forceinline__ void score_radix_pass(ScoreShared &sh, int n_local, i
     for (int i = 0; i < SC_PER_THREAD; ++i) {
         int idx = i * SC_THREADS + threadIdx.x;
         if (idx < n_local) {
-            uint32_t w = sh.acc[idx];
+            const uint32_t s = score_of(sh, idx);
+            const uint32_t w = s ? (s << 16) | sh.acc.a.ft[idx] : 0u;
             uint32_t kk = key(w, idx);
             if (pred(w, idx, kk)) rl.add(sh.u.rs, (kk >> shift) & 255u);
         }
@@ -112,54 +181,14 @@ __device__ __forceinline__ void score_radix_pass(ScoreShared &sh, int n_local, i
     radix_pick<SC_THREADS, SC_WAVES>(sh.u.rs, need);
 }
 
-// Sweep of the block's accumulator words: f(w, idx) for idx < round4(n_local), 4
-// consecutive words per lane per ds_read_b128, 4 reads in flight before any is
-// used (a read-then-use loop is LDS-latency bound).  Words past the zeroed range
-// come as 0; f runs in wave-uniform control flow (it may ballot).
-template <class F>
-__device__ __forceinline__ void sweep_words(const uint32_t *acc, int n_local, int tid, F f) {
-    const uint4 *a4 = reinterpret_cast<const uint4 *>(acc);
-    const int n4 = (n_local + 3) >> 2;
-    constexpr int G = 4;  // uint4 reads in flight per lane
-    for (int i0 = 0; i0 < SC_PER_THREAD / 4; i0 += G) {
-        if (i0 * SC_THREADS >= n4) break;  // (uniform)
-        uint4 x[G];
-#pragma unroll
-        for (int i = 0; i < G; ++i) {
-            // q4 < 8192 always lies inside the array: load unconditionally (no branch),
-            // then drop what lies past the zeroed range
-            const int q4 = (i0 + i) * SC_THREADS + tid;
-            const uint4 y = a4[q4];
-            x[i].x = q4 < n4 ? y.x : 0u;
-            x[i].y = q4 < n4 ? y.y : 0u;
-            x[i].z = q4 < n4 ? y.z : 0u;
-            x[i].w = q4 < n4 ? y.w : 0u;
-        }
-#pragma unroll
-        for (int i = 0; i < G; ++i) {
-            const int base = 4 * ((i0 + i) * SC_THREADS + tid);
-            f(x[i].x, base);
-            f(x[i].y, base + 1);
-            f(x[i].z, base + 2);
-            f(x[i].w, base + 3);
-        }
-    }
-}
-
-// Block-wide stable compaction over the accumulator words into two lists:
-// cls(w, idx) -> bit 0: list A, bit 1: list B.  One counting sweep, one exclusive
-// block scan of the packed per-thread counts, one writing sweep calling
-// out(list, pos, w, idx) -- no atomics.  Returns the packed totals (A | B << 16;
-// each list holds at most 32768).  Ends with a barrier.
-template <class Cls, class Out, class St = void (*)(int)>
-__device__ __forceinline__ uint32_t compact_words(ScoreShared &sh, int n_local, int tid, Cls cls,
-                                                  Out out, St st = nullptr) {
+// Block-wide stable compaction over the scores into one list: cls(s, idx) -> take?
+// One counting sweep, one exclusive block scan of the per-thread counts, one writing
+// sweep calling out(pos, s, idx) -- no atomics.  Returns the total.  Ends with a barrier.
+template <class Cls, class Out>
+__device__ __forceinline__ uint32_t compact_scores(ScoreShared &sh, int n_local, int tid, Cls cls,
+                                                   Out out) {
     uint32_t cnt = 0;
-    sweep_words(sh.acc, n_local, tid, [&](uint32_t w, int idx) {
-        const uint32_t c = cls(w, idx);
-        cnt += (c & 1u) + ((c & 2u) << 15);
-    });
-    if constexpr (!std::is_same<St, void (*)(int)>::value) st(6);
+    sweep_scores(sh, n_local, tid, [&](uint32_t s, int idx) { cnt += cls(s, idx) ? 1u : 0u; });
     const int lane = tid & 63, wave = tid >> 6;
     const uint32_t incl = wave_prefix_sum(cnt);
     if (lane == 63) sh.wsum[wave] = incl;
@@ -170,13 +199,10 @@ __device__ __forceinline__ uint32_t compact_words(ScoreShared &sh, int n_local, 
         if (w2 < wave) base += x;
         total += x;
     }
-    uint32_t pa = base & 0xFFFFu, pb = base >> 16;
-    if constexpr (!std::is_same<St, void (*)(int)>::value) st(7);
-    sweep_words(sh.acc, n_local, tid, [&](uint32_t w, int idx) {
-        const uint32_t c = cls(w, idx);
-        if (c & 1u) out(0, pa++, w, idx);
-        if (c & 2u) out(1, pb++, w, idx);
-    });
+    if (cnt)  // (most lanes emit nothing: skip their second sweep)
+        sweep_scores(sh, n_local, tid, [&](uint32_t s, int idx) {
+            if (cls(s, idx)) out(base++, s, idx);
+        });
     __syncthreads();
     return total;
 }
@@ -196,16 +222,13 @@ __device__ __forceinline__ bool wave_append(bool take, uint32_t *cursor, uint32_
 }
 
 // Device posting words are ((doc_in_block << 8) | value) XOR POST_X.  A buffer load
-// past the descriptor's range returns 0, which decodes to doc MAX_BLOCK_DOCS -- the
-// dummy accumulator word after the block -- with value 0: the padding lanes of a
-// round need no clamp, no select and no branch (their update lands in the dummy).
+// past the descriptor's range returns 0, which decodes to doc MAX_BLOCK_DOCS with value
+// 0: the padding lanes of a round go to their lane's dummy accumulators.
 constexpr uint32_t POST_X = (uint32_t)MAX_BLOCK_DOCS << 8;
 
-// One scatter round over postings p[0 .. min(avail, UU * SC_THREADS)) (lane-
-// consecutive, UU per lane; p and avail wave-uniform): all loads first -- buffer loads
-// bounds-checked by the hardware, a 32-bit lane offset and no per-posting address
-// arithmetic -- then the LDS reads, then the writes.  A doc occurs once per term, so
-// the read-modify-write needs no atomics.
+// One scatter round's loads: postings p[0 .. min(avail, UU * NT)) (lane-consecutive,
+// UU per lane; p and avail wave-uniform), buffer loads bounds-checked by the hardware
+// with a 32-bit lane offset.
 template <int UU, int NT = SC_THREADS>
 __device__ __forceinline__ void scatter_load(const uint32_t *p, int64_t avail, int tid,
                                              uint32_t (&cur)[UU]) {
@@ -220,73 +243,47 @@ __device__ __forceinline__ void scatter_load(const uint32_t *p, int64_t avail, i
     for (int u = 0; u < UU; ++u)
         cur[u] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, (tid + u * NT) * 4, 0, 0);
 }
-// The word update.  Term order (MAXF false): touched w + (v << 16), first touch
-// (v << 16) | first_bits | v -- both one 24-bit multiply-add (v < 256, first_bits =
-// (255 - j) << 8: no carries).  Out of term order (MAXF, early termination): the
-// score adds up and the low half keeps the smallest term index, max of the old low
-// half and first_bits | v (distinct j: the larger is the earlier term and its value).
-template <bool MAXF>
-__device__ __forceinline__ uint32_t word_update(uint32_t w, uint32_t v, uint32_t first_bits) {
-    if constexpr (MAXF) {
-        return ((w & 0xFFFF0000u) + (v << 16)) | max(w & 0xFFFFu, first_bits | v);
-    } else {
-        const uint32_t t = __umul24(v, 0x10000u) + w;
-        const uint32_t f = __umul24(v, 0x10001u) + first_bits;
-        return w ? t : f;
-    }
-}
 
-template <int UU, bool MAXF = false>
-__device__ __forceinline__ void scatter_apply(uint32_t *acc, const uint32_t (&cur)[UU],
-                                              uint32_t first_bits) {
-    // LDS byte addresses formed here and the accesses in inline asm (the compiler's own
-    // form adds the array's zero base once more per posting); the reads are retired by
-    // the explicit wait, the writes by the caller's term barrier / final wait.
-    // (acc is the first member of the kernel's only LDS object, the dynamic segment at
-    // LDS address 0: score_blocks_kernel checks that once)
-    (void)acc;
-    uint32_t w[UU], a[UU];
+// The round's LDS updates: per posting one ds_add_u32 of its value into its doc's half
+// of sc and one ds_write_b16 of the term's key | value into ft -- no return values, so
+// a wave issues them back to back.  Docs outside [dlo, dlo + dn) (OWN: another wave's
+// docs; and the padding lanes' doc MAX_BLOCK_DOCS) update the lane's dummies.  (sc is
+// the first member of the kernel's only LDS object, the dynamic segment at LDS address
+// 0: score_blocks_kernel checks that once.)
+// FILT: only values >= vmin (impact pruning over a whole sublist, see score_item).
+// MODE (profiling A/B only, results wrong): 1 no key store, 2 read + write instead of
+// the atomic add (racy), 3 both.
+template <int UU, bool FILT = false, int MODE = 0>
+__device__ __forceinline__ void scatter_apply(const uint32_t (&cur)[UU], uint32_t key,
+                                              uint32_t dlo, uint32_t dn, uint32_t dummy_sc,
+                                              uint32_t dummy_ft, uint32_t vmin = 0) {
+    uint32_t a_sc[UU], a_ft[UU], inc[UU], kv[UU];
 #pragma unroll
     for (int u = 0; u < UU; ++u) {
-        a[u] = ((cur[u] ^ POST_X) >> 8) << 2;
-        asm volatile("ds_read_b32 %0, %1" : "=v"(w[u]) : "v"(a[u]) : "memory");
+        const uint32_t x = cur[u] ^ POST_X;
+        const uint32_t d = x >> 8, v = x & 255u;
+        const bool ok = d - dlo < dn && (!FILT || v >= vmin);
+        a_sc[u] = ok ? (d >> 1) << 2 : dummy_sc;
+        a_ft[u] = ok ? FT_BASE + (d << 1) : dummy_ft;
+        inc[u] = v << ((d & 1u) << 4);
+        kv[u] = key | v;
+        if constexpr (!(MODE & 2))
+            asm volatile("ds_add_u32 %0, %1" ::"v"(a_sc[u]), "v"(inc[u]) : "memory");
+        if constexpr (!(MODE & 1))
+            asm volatile("ds_write_b16 %0, %1" ::"v"(a_ft[u]), "v"(kv[u]) : "memory");
     }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    // the compiler sees the asm reads' results as ready at once: redefine them after
-    // the wait, and fence the scheduler, so that no use is hoisted above it
+    if constexpr ((MODE & 2) != 0) {
+        uint32_t w[UU];
 #pragma unroll
-    for (int u = 0; u < UU; ++u) asm volatile("" : "+v"(w[u]));
-    __builtin_amdgcn_sched_barrier(0);
+        for (int u = 0; u < UU; ++u)
+            asm volatile("ds_read_b32 %0, %1" : "=v"(w[u]) : "v"(a_sc[u]) : "memory");
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
-    for (int u = 0; u < UU; ++u) {
-        const uint32_t v = cur[u] & 255u;
-        asm volatile("ds_write_b32 %0, %1" ::"v"(a[u]), "v"(word_update<MAXF>(w[u], v, first_bits))
-                     : "memory");
-    }
-}
-
-// scatter_apply restricted to the docs [dlo, dhi) of one wave (a short term, whose
-// sublist every wave reads in full): the other postings (and the padding) update a
-// per-lane dummy word past the block instead.
-template <int UU, bool MAXF = false>
-__device__ __forceinline__ void scatter_apply_own(const uint32_t (&cur)[UU], uint32_t first_bits,
-                                                  uint32_t dlo, uint32_t dn, uint32_t dummy) {
-    uint32_t w[UU], a[UU];
+        for (int u = 0; u < UU; ++u) asm volatile("" : "+v"(w[u]));
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int u = 0; u < UU; ++u) {
-        const uint32_t d = (cur[u] ^ POST_X) >> 8;
-        a[u] = (d - dlo < dn) ? d << 2 : dummy;
-        asm volatile("ds_read_b32 %0, %1" : "=v"(w[u]) : "v"(a[u]) : "memory");
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-    for (int u = 0; u < UU; ++u) asm volatile("" : "+v"(w[u]));
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int u = 0; u < UU; ++u) {
-        const uint32_t v = cur[u] & 255u;
-        asm volatile("ds_write_b32 %0, %1" ::"v"(a[u]), "v"(word_update<MAXF>(w[u], v, first_bits))
-                     : "memory");
+        for (int u = 0; u < UU; ++u)
+            asm volatile("ds_write_b32 %0, %1" ::"v"(a_sc[u]), "v"(w[u] + inc[u]) : "memory");
     }
 }
 
@@ -294,10 +291,48 @@ __device__ __forceinline__ void scatter_apply_own(const uint32_t (&cur)[UU], uin
 // accumulated here and printed by di_index_search.
 __device__ unsigned long long g_sb_phase[8];
 
+// The (term, block) sublists: sparse per term -- the entries of term t are
+// [tb_start[t], tb_start[t+1]), one per block holding postings of t, in block order
+// (eblk), at postings [epos[e], epos[e+1]); seg[8e + c] = end of impact class c inside
+// the sublist; lid[e] = its long id (per-wave layout) or ~0.  A term present in every
+// block is indexed directly; otherwise a binary search over its entries' blocks.
+struct SubIndex {
+    const uint32_t *tb_start;
+    const uint16_t *eblk;
+    const uint32_t *epos;
+    const uint16_t *seg;
+    const uint32_t *lid;
+    const uint16_t *wmeta;
+};
+
+// entry of (term t, block b), or -1 when t has no posting in b
+__device__ __forceinline__ int64_t find_entry(const SubIndex &si, int nb, uint32_t t, int b) {
+    const uint32_t e0 = si.tb_start[t], e1 = si.tb_start[t + 1];
+    if (e1 - e0 == (uint32_t)nb) return (int64_t)e0 + b;
+    uint32_t lo = e0, hi = e1;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (si.eblk[mid] < (uint32_t)b) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo < e1 && si.eblk[lo] == (uint32_t)b ? (int64_t)lo : -1;
+}
+
+// [lo, hi) of entry e scored at impact-class prefix min_cls (7: the whole sublist)
+__device__ __forceinline__ void entry_bounds(const SubIndex &si, int64_t e, int min_cls,
+                                             int64_t &lo, int64_t &hi) {
+    if (e < 0) {
+        lo = hi = 0;
+        return;
+    }
+    lo = si.epos[e];
+    hi = min_cls >= 7 ? (int64_t)si.epos[e + 1] : lo + si.seg[e * 8 + min_cls];
+}
+
 // Per (item, query term) setup record, resolved for every item in bulk by
 // item_setup_kernel before the scorer: the scorer's setup then reads one record per
-// (term, wave segment) instead of walking the dependent chain query term -> sublist
-// id -> per-wave runs (three global round trips per item, ~1/6 of the kernel).
+// (term, wave segment) instead of walking the dependent chain query term -> entry ->
+// per-wave runs (several global round trips per item).
 struct ItemRec {
     int64_t lo, hi;        // the term's sublist [lo, hi) in this block (min_cls prefix)
     uint32_t wtab[WSEG];   // per-wave layout: run of wave w = start << 16 | end
@@ -309,9 +344,7 @@ constexpr uint32_t IR_LONG = 1, IR_BAD = 2;
 // Items (query q, block b) as the scorer numbers them (item = b * n_q + q); records
 // only for queries of 1..WTERMS terms (the scorer's per-wave form), WTERMS per item.
 __global__ void __launch_bounds__(128)
-item_setup_kernel(const int64_t *__restrict__ term_start, const uint32_t *__restrict__ blk_off,
-                  const uint16_t *__restrict__ seg, const uint32_t *__restrict__ lid,
-                  const uint16_t *__restrict__ wmeta, int min_cls, int nb, int64_t n_terms,
+item_setup_kernel(SubIndex si, int min_cls, int nb, int64_t n_terms,
                   const uint32_t *__restrict__ q_terms, const int32_t *__restrict__ cu_q, int n_q,
                   ItemRec *__restrict__ rec) {
     const int item = blockIdx.x, q = item % n_q, b = item / n_q;
@@ -328,17 +361,17 @@ item_setup_kernel(const int64_t *__restrict__ term_start, const uint32_t *__rest
             }
             continue;
         }
-        const uint32_t id = lid[(int64_t)t * nb + b];
+        const int64_t en = find_entry(si, nb, t, b);
+        const uint32_t id = en >= 0 ? si.lid[en] : 0xFFFFFFFFu;
         if (w == 0) {
-            const uint32_t *bo = blk_off + (int64_t)t * (nb + 1) + b;
-            const int64_t lo = term_start[t] + bo[0];
+            int64_t lo, hi;
+            entry_bounds(si, en, min_cls, lo, hi);
             r[j].lo = lo;
-            r[j].hi = min_cls >= 7 ? term_start[t] + bo[1]
-                                   : lo + seg[((int64_t)t * nb + b) * 8 + min_cls];
+            r[j].hi = hi;
             r[j].flags = id != 0xFFFFFFFFu ? IR_LONG : 0u;
         }
         if (id != 0xFFFFFFFFu) {
-            const uint16_t *m = wmeta + (int64_t)id * (WSEG * 8);
+            const uint16_t *m = si.wmeta + (int64_t)id * (WSEG * 8);
             const uint32_t s0 = w ? m[(w - 1) * 8 + 7] : 0u;
             r[j].wtab[w] = (s0 << 16) | m[w * 8 + min(min_cls, 7)];
         }
@@ -346,36 +379,25 @@ item_setup_kernel(const int64_t *__restrict__ term_start, const uint32_t *__rest
 }
 
 // ---------------------------------------------------------------------------
-// Long queries: DI_SHORT_QUERY_TERMS < known terms <= DI_MAX_QUERY_TERMS.  The 32-bit
-// word holds neither their sums (255 x 4096 > 2^16) nor their first-touch index (> 255),
-// so an item (query, block) of such a query accumulates 64-bit words
+// Long queries: DI_SHORT_QUERY_TERMS < known terms <= DI_MAX_QUERY_TERMS.  The packed
+// score does not hold their sums (255 x 4096 > 2^16) nor the key their first-touch index
+// (> 255), so an item (query, block) of such a query accumulates 64-bit words
 //     score(20) | (4095 - j)(12) | v_j(8)                       (bits 39..0)
 // -- ordered exactly like the short word: score, then first touch -- over half blocks
-// of LH_DOCS docs (128 KiB of LDS, the accumulator array of ScoreShared), and its
-// candidates carry the wide merge key  word << 24 | (0xFFFFFF - doc)  (docs < 2^24).
-// The first half's candidates wait in the item's output list; the second half's
-// selection runs over the union (the waiting keys held in registers, LH_HELD per
-// thread) and rewrites the list, so a long item emits one list of <= k keys like a
-// short one and the merge is unchanged (it decodes wide keys per query, see
-// merge_topk_kernel).  Terms go in chunks of MAX_TERMS bounds, a barrier per term.
-// Rare (no MS MARCO query comes close), so simple: one posting per lane per load.
-constexpr int LONG_TERMS = DI_MAX_QUERY_TERMS;
-constexpr int LH_DOCS = 16384;
-constexpr int LH_PER_THREAD = LH_DOCS / SC_THREADS;  // 16
-constexpr int LH_HELD = DI_MAX_TOPK / SC_THREADS;    // 4
-static_assert(MAX_BLOCK_DOCS <= 2 * LH_DOCS, "two halves cover a block");
-static_assert(LONG_TERMS <= 4096, "12-bit first-touch index");
-
+// of LH_DOCS docs (128 KiB of LDS, the accumulators of ScoreShared), and its candidates
+// carry the wide merge key  word << 24 | (0xFFFFFF - doc)  (docs < 2^24).  The first
+// half's candidates wait in the item's output list; the second half's selection runs
+// over the union (the waiting keys held in registers, LH_HELD per thread) and rewrites
+// the list, so a long item emits one list of <= k keys like a short one and the merge
+// is unchanged (it decodes wide keys per query, see merge_topk_kernel).  Terms go in
+// chunks of MAX_TERMS bounds, a barrier per term.  Rare (no MS MARCO query comes close),
+// so simple: one posting per lane per load, a read-modify-write per posting.
 __device__ __forceinline__ void score_long_item(
-    int q, int b, const uint32_t *__restrict__ post, const int64_t *__restrict__ term_start,
-    const uint32_t *__restrict__ blk_off, const uint16_t *__restrict__ seg, int min_cls, int nb,
-    int block_docs, int64_t n_terms, uint32_t n_docs, uint32_t doc_lo,
+    ScoreShared &sh, int q, int b, const uint32_t *__restrict__ post, const SubIndex &si,
+    int min_cls, int nb, int block_docs, int64_t n_terms, uint32_t n_docs, uint32_t doc_lo,
     const uint32_t *__restrict__ q_terms, const int32_t *__restrict__ cu_q, int k,
     uint64_t *__restrict__ ck, int32_t *__restrict__ cn) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    ScoreShared &sh = *reinterpret_cast<ScoreShared *>(smem);
-    static_assert(sizeof(sh.acc) >= LH_DOCS * sizeof(uint64_t), "half-block words fit");
-    uint64_t *acc = reinterpret_cast<uint64_t *>(sh.acc);
+    uint64_t *acc = sh.acc.w64;
     int64_t *lo = sh.v.bounds[0], *hi = sh.v.bounds[1];
     const int tid = threadIdx.x;
     const int64_t block_first = (int64_t)b * block_docs;
@@ -413,9 +435,7 @@ __device__ __forceinline__ void score_long_item(
                 // the whole sublist: a long sublist is laid out per wave segment (classes
                 // in order inside each), so the class prefix is not one range -- pruning
                 // (min_cls < 7) filters by value in the scatter instead
-                const uint32_t *bo = blk_off + (int64_t)t * (nb + 1) + b;
-                lo[j] = term_start[t] + bo[0];
-                hi[j] = term_start[t] + bo[1];
+                entry_bounds(si, find_entry(si, nb, t, b), 7, lo[j], hi[j]);
             }
             __syncthreads();
             if (sh.bad) {
@@ -507,14 +527,10 @@ __device__ __forceinline__ void score_long_item(
 
 // One work item = (query q, doc block b): accumulate, select the block's top-k.
 __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
-                                           const uint32_t *__restrict__ post,
-                                           const int64_t *__restrict__ term_start,
-                                           const uint32_t *__restrict__ blk_off,
-                                           const uint16_t *__restrict__ seg,
-                                           const uint32_t *__restrict__ lid,
-                                           const uint16_t *__restrict__ wmeta, int min_cls, int nb,
-                                           int block_docs, int64_t n_terms, uint32_t n_docs,
-                                           uint32_t doc_lo, const uint32_t *__restrict__ q_terms,
+                                           const uint32_t *__restrict__ post, const SubIndex &si,
+                                           int min_cls, int nb, int block_docs, int64_t n_terms,
+                                           uint32_t n_docs, uint32_t doc_lo,
+                                           const uint32_t *__restrict__ q_terms,
                                            const int32_t *__restrict__ cu_q, int k,
                                            uint64_t *__restrict__ cand_key,
                                            int32_t *__restrict__ cand_n,
@@ -563,44 +579,35 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
     }
     __syncthreads();
 
-    // sublist bounds for this block and, with the per-wave layout, the long terms' runs
-    // (one pass: the loads of both depend only on the term id, so they overlap);
-    // ablate bit 128: all-wave form only
-    const bool wl = nt <= WTERMS && !(ablate & 128);
-    // with the per-wave layout, short terms too are scattered by each wave over its own
-    // docs (ablate bit 256: the barrier form for them): then no term needs a barrier
-    const bool own_short = wl && !(ablate & 256);
-    // safe early termination (ablate bit 512: off, profiling / A-B)
-    const bool et = own_short && nt <= ET_TERMS && qhist != nullptr && !(ablate & 512);
-    auto bounds = [&](int j, uint32_t t) {
-        const uint32_t *bo = blk_off + (int64_t)t * (nb + 1) + b;
-        lo[j] = term_start[t] + bo[0];
-        hi[j] = min_cls >= 7 ? term_start[t] + bo[1]
-                             : lo[j] + seg[((int64_t)t * nb + b) * 8 + min_cls];
-    };
+    // per-wave form (every term applied by each wave to its own docs: no barriers)
+    const bool wl = nt <= WTERMS;
     // The query's shared threshold histogram (qhist, below) is copied by LDS-DMA into
     // the selection histogram (idle until the selection) here, so its round trip
     // overlaps the scatter and the selection reads it from LDS; the fast selection
-    // path zeroes the histogram itself when it runs.  (Early termination reads it
-    // before its scatter, from global memory.)
+    // path zeroes the histogram itself when it runs.
     uint32_t *qh = qhist ? qhist + (int64_t)q * QH_BINS : nullptr;
-    const bool qpre = qh != nullptr && !et;
     static_assert(QH_BINS == 4 * SC_THREADS && QH_BINS <= HIST_BINS, "qhist prefetch");
-    if (qpre) {
+    if (qh) {
         typedef __attribute__((address_space(3))) void lds_void;
         __builtin_amdgcn_global_load_lds((const void *)(qh + 4 * tid),
                                          (lds_void *)(sh.u.hist + wave * 256), 16, 0, 0);
     }
     // zeroing of the accumulators (and the fast path's histogram): LDS stores only,
-    // placed where the setup's global loads are in flight
+    // placed where the setup's global loads are in flight.  Scores and keys up to
+    // round4(n_local) docs (the sweeps' range).
+    const int n4z = (n_local + 3) >> 2;
     auto zero = [&]() {
-        uint4 *a4 = reinterpret_cast<uint4 *>(sh.acc);
-        const int n4 = (n_local + 3) >> 2;
-        for (int i = tid; i < n4; i += SC_THREADS) a4[i] = make_uint4(0, 0, 0, 0);
-        if (fast && !qpre) reinterpret_cast<uint4 *>(sh.u.hist)[tid] = make_uint4(0, 0, 0, 0);
+        uint4 *s4 = reinterpret_cast<uint4 *>(sh.acc.a.sc);
+        uint4 *f4 = reinterpret_cast<uint4 *>(sh.acc.a.ft);
+        const int nz = (n4z + 1) >> 1;  // uint4 per array: 8 scores / 8 keys each
+        for (int i = tid; i < nz; i += SC_THREADS) {
+            s4[i] = make_uint4(0, 0, 0, 0);
+            f4[i] = make_uint4(0, 0, 0, 0);
+        }
+        if (fast && !qh) reinterpret_cast<uint4 *>(sh.u.hist)[tid] = make_uint4(0, 0, 0, 0);
         // (the 64 spare bins past them are written, never read: no zeroing needed)
     };
-    if (wl && ir != nullptr && !et) {
+    if (wl && ir != nullptr) {
         // the item's records (item_setup_kernel): one (term j, wave segment w) per thread
         const int e = tid;
         const bool act = e < nt * WSEG;
@@ -624,11 +631,11 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
                 if (f & IR_BAD) sh.bad = 1;
                 if (f & IR_LONG) atomicOr(&sh.lmask[j >> 5], 1u << (j & 31));
             }
-            if (f & IR_LONG) sh.wt.wtab[j][w] = wt;
+            if (f & IR_LONG) sh.wtab[j][w] = wt;
         }
     } else if (wl) {
-        // nt * WSEG <= SC_THREADS: one (term j, wave segment w) per thread.  The term id
-        // and the loads that depend only on it (sublist id, bounds) are issued, the
+        // nt * WSEG <= SC_THREADS: one (term j, wave segment w) per thread.  The entry
+        // lookup and the loads that depend on it (bounds, long id) are issued, the
         // accumulators zeroed while they are in flight, then the per-wave runs read.
         static_assert(WTERMS * WSEG <= SC_THREADS, "one setup entry per thread");
         const int e = tid;
@@ -636,19 +643,12 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
         const int j = act ? e / WSEG : 0, w = e % WSEG;
         const uint32_t t = act ? q_terms[q0 + j] : 0u;
         const bool tok = act && t < n_terms;  // (device-pointer callers are not pre-checked)
-        uint32_t id = 0xFFFFFFFFu, bo0 = 0, bo1 = 0, sgc = 0;
-        int64_t ts = 0;
+        int64_t en = -1, blo = 0, bhi = 0;
+        uint32_t id = 0xFFFFFFFFu;
         if (tok) {
-            id = lid[(int64_t)t * nb + b];
-            if (w == 0) {
-                const uint32_t *bo = blk_off + (int64_t)t * (nb + 1) + b;
-                ts = term_start[t];
-                bo0 = bo[0];
-                if (min_cls >= 7)
-                    bo1 = bo[1];
-                else
-                    sgc = seg[((int64_t)t * nb + b) * 8 + min_cls];
-            }
+            en = find_entry(si, nb, t, b);
+            if (en >= 0) id = si.lid[en];
+            if (w == 0) entry_bounds(si, en, min_cls, blo, bhi);
         }
         zero();
         if (act && !tok) {  // invalid term id
@@ -658,25 +658,19 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
             }
         } else if (act) {
             if (w == 0) {
-                lo[j] = ts + bo0;
-                hi[j] = min_cls >= 7 ? ts + bo1 : lo[j] + sgc;
+                lo[j] = blo;
+                hi[j] = bhi;
             }
-            if (id == 0xFFFFFFFFu) {
-                if (et && w < 8) sh.segj[j][w] = seg[((int64_t)t * nb + b) * 8 + w];
-            } else {
-                const uint16_t *m = wmeta + (int64_t)id * (WSEG * 8);
+            if (id != 0xFFFFFFFFu) {
+                const uint16_t *m = si.wmeta + (int64_t)id * (WSEG * 8);
                 const uint32_t s0 = w ? m[(w - 1) * 8 + 7] : 0u;
-                const uint32_t e0 = m[w * 8 + min(min_cls, 7)];
-                if (et) {
-#pragma unroll
-                    for (int c = 0; c < 8; ++c) sh.wt.wcls[j][w][c] = m[w * 8 + c];
-                } else {
-                    sh.wt.wtab[j][w] = (s0 << 16) | e0;
-                }
+                sh.wtab[j][w] = (s0 << 16) | m[w * 8 + min(min_cls, 7)];
                 if (w == 0) atomicOr(&sh.lmask[j >> 5], 1u << (j & 31));
             }
         }
     } else {
+        // all-wave form: whole sublists (a long one is laid out per wave segment, so its
+        // class prefix is not one range); impact pruning filters by value (FILT below)
         for (int j = tid; j < nt; j += SC_THREADS) {
             const uint32_t t = q_terms[q0 + j];
             if (t >= n_terms) {
@@ -684,7 +678,7 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
                 lo[j] = hi[j] = 0;
                 continue;
             }
-            bounds(j, t);
+            entry_bounds(si, find_entry(si, nb, t, b), 7, lo[j], hi[j]);
         }
         zero();
     }
@@ -703,19 +697,10 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
     // >= s: at least k docs score >= s, so the final k-th score is >= s.  A stale
     // (smaller) count still gives a valid lower bound.  Block-wide (barriers).
     auto read_tq = [&]() -> uint32_t {
-        // thread t: bins 4t..4t+3 (relaxed atomic loads: other CUs add to them; or the
-        // LDS copy made at the item's start)
-        uint32_t hv[4], c = 0;
-        if (qpre) {
-            const uint4 h = reinterpret_cast<const uint4 *>(sh.u.hist)[tid];
-            hv[0] = h.x, hv[1] = h.y, hv[2] = h.z, hv[3] = h.w;
-            c = h.x + h.y + h.z + h.w;
-        } else {
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-                c += (hv[e] = __hip_atomic_load(&qh[4 * tid + e], __ATOMIC_RELAXED,
-                                                __HIP_MEMORY_SCOPE_AGENT));
-        }
+        // thread t: bins 4t..4t+3 (the LDS copy made at the item's start)
+        const uint4 h = reinterpret_cast<const uint4 *>(sh.u.hist)[tid];
+        const uint32_t hv[4] = {h.x, h.y, h.z, h.w};
+        const uint32_t c = h.x + h.y + h.z + h.w;
         uint32_t sfx = wave_suffix_sum(c);
         if (lane == 0) sh.wsum[wave] = sfx;
         if (tid == 0) sh.tq = 0;
@@ -736,208 +721,104 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
         __syncthreads();  // (wsum / tq are reused)
         return r;
     };
-    // ---- scatter: terms in query order, barrier between terms -------------
-    // A term's sublist goes in rounds of 16 postings per lane while 16 k remain, then
-    // 4 per lane while more than 1 k remain, then 1: a short tail does not pay for a
-    // full round of issue (loads, LDS reads and writes of masked lanes).  Each round
-    // has all its loads in flight before any is applied; the 16 waves of the CU
-    // overlap one another's load latency with their LDS work.
-    // The last round of a term also loads the next term's first 4 k postings, before
-    // the term barrier (a raw one: LDS writes retired, loads left in flight), so the
-    // barrier does not expose a load round trip per term.
-    // A long term (per-wave layout) is scattered by each wave over its own doc segment,
-    // rounds of up to 16 postings per lane: no other wave touches those docs, so a run
-    // of long terms needs no barrier between its terms, only at its ends.
-    uint32_t pre[4];
-    bool have_pre = false;
-    auto is_long = [&](int j) { return wl && ((sh.lmask[j >> 5] >> (j & 31)) & 1u); };
+    // ---- scatter: terms in REVERSE query order (the last key written is the first
+    // term's) ----------------------------------------------------------------------
+    // Per-wave form: a long term (per-wave layout) is read by each wave over its own
+    // run; a short one (< WLONG_MIN postings in the block) is read in full by every wave,
+    // which applies the postings of its own docs.  No other wave touches a wave's docs,
+    // so no term needs a barrier.  Rounds of 16 postings per lane while more than 512
+    // remain, then 8 / 4 / 1.
+    // All-wave form (more than WTERMS terms): the block's 1024 lanes split each term's
+    // sublist, rounds of 16 postings per lane while 16 k remain, then 4, then 1; a
+    // barrier between terms (the key writes of term j must land after those of j + 1).
     const uint32_t wseg = ((uint32_t)block_docs + WSEG - 1) / WSEG;
     const uint32_t wdlo = (uint32_t)wave * wseg;
-    const uint32_t wdn = wave == WSEG - 1 ? 0x7FFFFFFFu - wdlo : wseg;  // last: the rest
-    const uint32_t wdummy = (uint32_t)(MAX_BLOCK_DOCS + lane) << 2;
-    // Safe early termination (configs[4]; exact): the query's shared threshold Tq (see
-    // read_tq) is a lower bound of its final k-th score, and the postings of every (term,
-    // block[, wave segment]) sublist are grouped by impact class c (values in
-    // [2^(7-c), 2^(8-c))).  Each wave applies class 0 of every term, then class 1, ...
-    // to its own doc segment (no barriers: no other wave touches those docs); after
-    // class c, every doc of the segment can still gain at most
-    //   R = sum over the terms with postings left (classes > c) of 2^(7-c) - 1,
-    // so when the segment's best partial score + R < Tq no doc of it can reach Tq -- nor
-    // the query's top-k -- and the wave skips the rest of its postings.  Terms touch a
-    // doc out of term order, so the first-touch field keeps the smallest term index
-    // (MAXF updates: max of (255 - j) << 8 | v_j); sums are order-free integers.  Docs
-    // left with partial scores stay below Tq and are never emitted: the Tq path emits
-    // only docs >= Tq, and with more than k of those the block's top-k are all >= Tq.
-    uint32_t tq_et = 0;
-    if (et) tq_et = read_tq();
-    if (et && !(ablate & 1)) {
-        const uint32_t wend = min((uint32_t)n_local, wdlo + wseg);
-        const uint32_t wstart = min(wdlo, wend);
-        auto range = [&](int64_t pos, const int64_t end, const bool lj, const uint32_t fb) {
-            while (pos < end) {
-                const int64_t rem = end - pos;
-                if (rem > 8 * 64) {
-                    uint32_t r[16];
-                    scatter_load<16, 64>(post + pos, rem, lane, r);
-                    if (lj) scatter_apply<16, true>(sh.acc, r, fb);
-                    else scatter_apply_own<16, true>(r, fb, wdlo, wdn, wdummy);
-                    pos += 16 * 64;
-                } else if (rem > 4 * 64) {
-                    uint32_t r[8];
-                    scatter_load<8, 64>(post + pos, rem, lane, r);
-                    if (lj) scatter_apply<8, true>(sh.acc, r, fb);
-                    else scatter_apply_own<8, true>(r, fb, wdlo, wdn, wdummy);
-                    pos = end;
-                } else if (rem > 64) {
-                    uint32_t r[4];
-                    scatter_load<4, 64>(post + pos, rem, lane, r);
-                    if (lj) scatter_apply<4, true>(sh.acc, r, fb);
-                    else scatter_apply_own<4, true>(r, fb, wdlo, wdn, wdummy);
-                    pos = end;
-                } else {
-                    uint32_t r[1];
-                    scatter_load<1, 64>(post + pos, rem, lane, r);
-                    if (lj) scatter_apply<1, true>(sh.acc, r, fb);
-                    else scatter_apply_own<1, true>(r, fb, wdlo, wdn, wdummy);
-                    pos = end;
+    const uint32_t wdn = min(wseg, (uint32_t)MAX_BLOCK_DOCS - min(wdlo, (uint32_t)MAX_BLOCK_DOCS));
+    const uint32_t dummy_sc = (uint32_t)(MAX_BLOCK_DOCS / 2 + lane) << 2;
+    const uint32_t dummy_ft = FT_BASE + ((uint32_t)(MAX_BLOCK_DOCS + 2 * lane) << 1);
+    auto is_long = [&](int j) { return wl && ((sh.lmask[j >> 5] >> (j & 31)) & 1u); };
+    if (!(ablate & 1)) {  // ablate bit 0: skip (profiling)
+        auto per_wave = [&](auto mode) {
+            constexpr int M = decltype(mode)::value;
+            for (int j = nt - 1; j >= 0; --j) {
+                const uint32_t key = (uint32_t)(255 - j) << 8;
+                int64_t pos = lo[j], end = hi[j];
+                if (is_long(j)) {
+                    const uint32_t se = sh.wtab[j][wave];
+                    pos = lo[j] + (se >> 16);
+                    end = lo[j] + (se & 0xFFFFu);
+                }
+                while (pos < end) {
+                    const int64_t rem = end - pos;
+                    if (rem > 8 * 64) {
+                        uint32_t r[16];
+                        scatter_load<16, 64>(post + pos, rem, lane, r);
+                        scatter_apply<16, false, M>(r, key, wdlo, wdn, dummy_sc, dummy_ft);
+                        pos += 16 * 64;
+                    } else if (rem > 4 * 64) {
+                        uint32_t r[8];
+                        scatter_load<8, 64>(post + pos, rem, lane, r);
+                        scatter_apply<8, false, M>(r, key, wdlo, wdn, dummy_sc, dummy_ft);
+                        pos = end;
+                    } else if (rem > 64) {
+                        uint32_t r[4];
+                        scatter_load<4, 64>(post + pos, rem, lane, r);
+                        scatter_apply<4, false, M>(r, key, wdlo, wdn, dummy_sc, dummy_ft);
+                        pos = end;
+                    } else {
+                        uint32_t r[1];
+                        scatter_load<1, 64>(post + pos, rem, lane, r);
+                        scatter_apply<1, false, M>(r, key, wdlo, wdn, dummy_sc, dummy_ft);
+                        pos = end;
+                    }
                 }
             }
         };
-        for (int c = 0; c <= min_cls; ++c) {
-            for (int j = 0; j < nt; ++j) {
-                const bool lj = is_long(j);
-                uint32_t cs, ce;
-                if (lj) {
-                    const uint16_t *e = sh.wt.wcls[j][wave];
-                    cs = c ? e[c - 1] : (wave ? sh.wt.wcls[j][wave - 1][7] : 0u);
-                    ce = e[c];
-                } else {
-                    cs = c ? sh.segj[j][c - 1] : 0u;
-                    ce = sh.segj[j][c];
+        if (wl) {
+            const int m = (ablate >> 11) & 3;  // profiling A/B of the update (ablate 2048 / 4096)
+            if (m == 0) per_wave(std::integral_constant<int, 0>{});
+            else if (m == 1) per_wave(std::integral_constant<int, 1>{});
+            else if (m == 2) per_wave(std::integral_constant<int, 2>{});
+            else per_wave(std::integral_constant<int, 3>{});
+        } else {
+            auto all_wave = [&](auto filt) {
+                constexpr bool F = decltype(filt)::value;
+                const uint32_t vmin = 1u << (7 - min(min_cls, 7));
+                for (int j = nt - 1; j >= 0; --j) {
+                    const uint32_t key = (uint32_t)(255 - j) << 8;
+                    for (int64_t pos = lo[j], end = hi[j]; pos < end;) {
+                        const int64_t rem = end - pos;
+                        if (rem >= 16 * SC_THREADS) {
+                            uint32_t r[16];
+                            scatter_load<16>(post + pos, rem, tid, r);
+                            scatter_apply<16, F>(r, key, 0u, (uint32_t)MAX_BLOCK_DOCS, dummy_sc,
+                                                 dummy_ft, vmin);
+                            pos += 16 * SC_THREADS;
+                        } else if (rem > SC_THREADS) {
+                            uint32_t r[4];
+                            scatter_load<4>(post + pos, rem, tid, r);
+                            scatter_apply<4, F>(r, key, 0u, (uint32_t)MAX_BLOCK_DOCS, dummy_sc,
+                                                dummy_ft, vmin);
+                            pos += 4 * SC_THREADS;
+                        } else {
+                            uint32_t r[1];
+                            scatter_load<1>(post + pos, rem, tid, r);
+                            scatter_apply<1, F>(r, key, 0u, (uint32_t)MAX_BLOCK_DOCS, dummy_sc,
+                                                dummy_ft, vmin);
+                            pos = end;
+                        }
+                    }
+                    // term boundary: this term's key writes land before the next term's
+                    if (j > 0) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
                 }
-                range(lo[j] + cs, lo[j] + ce, lj, (uint32_t)(255 - j) << 8);
-            }
-            if (c < min_cls && tq_et > 0) {
-                const uint32_t cb = (1u << (7 - c)) - 1u;
-                uint32_t rb = 0;
-                for (int j = 0; j < nt; ++j) {
-                    const bool more = is_long(j)
-                                          ? sh.wt.wcls[j][wave][min_cls] > sh.wt.wcls[j][wave][c]
-                                          : sh.segj[j][min_cls] > sh.segj[j][c];
-                    rb += more ? cb : 0u;
-                }
-                if (rb == 0) break;  // nothing left in this segment
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's writes
-                uint32_t mx = 0;
-                for (uint32_t i = wstart + lane; i < wend; i += 64) mx = max(mx, sh.acc[i] >> 16);
-#pragma unroll
-                for (int d = 32; d >= 1; d >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, d, 64));
-                if (mx + rb < tq_et) break;  // the segment is out of the race: skip the rest
-            }
+            };
+            if (min_cls < 7)
+                all_wave(std::true_type{});
+            else
+                all_wave(std::false_type{});
         }
     }
-    for (int j = (ablate & 1) || et ? nt : 0; j < nt; ++j) {  // ablate bit 0: skip (profiling)
-        const uint32_t first_bits = (uint32_t)(255 - j) << 8;
-        const bool lj = is_long(j);
-        if (lj) {
-            const uint32_t se = sh.wt.wtab[j][wave];
-            int64_t pos = lo[j] + (se >> 16);
-            const int64_t end = lo[j] + (se & 0xFFFFu);
-            while (pos < end) {
-                const int64_t rem = end - pos;
-                if (rem > 8 * 64) {
-                    uint32_t r[16];
-                    scatter_load<16, 64>(post + pos, rem, lane, r);
-                    scatter_apply<16>(sh.acc, r, first_bits);
-                    pos += 16 * 64;
-                } else if (rem > 4 * 64) {
-                    uint32_t r[8];
-                    scatter_load<8, 64>(post + pos, rem, lane, r);
-                    scatter_apply<8>(sh.acc, r, first_bits);
-                    pos = end;
-                } else if (rem > 64) {
-                    uint32_t r[4];
-                    scatter_load<4, 64>(post + pos, rem, lane, r);
-                    scatter_apply<4>(sh.acc, r, first_bits);
-                    pos = end;
-                } else {
-                    uint32_t r[1];
-                    scatter_load<1, 64>(post + pos, rem, lane, r);
-                    scatter_apply<1>(sh.acc, r, first_bits);
-                    pos = end;
-                }
-            }
-            if (!own_short && j + 1 < nt && !is_long(j + 1))
-                asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-            continue;
-        }
-        if (own_short) {
-            // a short term (< WLONG_MIN postings in the block): every wave reads the whole
-            // sublist and applies the postings of its own doc segment -- no barrier
-            for (int64_t pos = lo[j], end = hi[j]; pos < end;) {
-                const int64_t rem = end - pos;
-                if (rem > 8 * 64) {
-                    uint32_t r[16];
-                    scatter_load<16, 64>(post + pos, rem, lane, r);
-                    scatter_apply_own<16>(r, first_bits, wdlo, wdn, wdummy);
-                    pos += 16 * 64;
-                } else if (rem > 4 * 64) {
-                    uint32_t r[8];
-                    scatter_load<8, 64>(post + pos, rem, lane, r);
-                    scatter_apply_own<8>(r, first_bits, wdlo, wdn, wdummy);
-                    pos = end;
-                } else if (rem > 64) {
-                    uint32_t r[4];
-                    scatter_load<4, 64>(post + pos, rem, lane, r);
-                    scatter_apply_own<4>(r, first_bits, wdlo, wdn, wdummy);
-                    pos = end;
-                } else {
-                    uint32_t r[1];
-                    scatter_load<1, 64>(post + pos, rem, lane, r);
-                    scatter_apply_own<1>(r, first_bits, wdlo, wdn, wdummy);
-                    pos = end;
-                }
-            }
-            continue;
-        }
-        int64_t pos = lo[j];
-        const int64_t end = hi[j];
-        if (have_pre) {
-            scatter_apply<4>(sh.acc, pre, first_bits);
-            pos = min(end, pos + (int64_t)4 * SC_THREADS);
-            have_pre = false;
-        }
-        const bool next = j + 1 < nt && hi[j + 1] > lo[j + 1] && !is_long(j + 1);
-        auto prefetch_next = [&]() {
-            scatter_load<4>(post + lo[j + 1], hi[j + 1] - lo[j + 1], tid, pre);
-            have_pre = true;
-        };
-        while (pos < end) {
-            const int64_t rem = end - pos;
-            if (rem >= 16 * SC_THREADS) {
-                uint32_t r[16];
-                scatter_load<16>(post + pos, rem, tid, r);
-                if (rem == 16 * SC_THREADS && next) prefetch_next();
-                scatter_apply<16>(sh.acc, r, first_bits);
-                pos += 16 * SC_THREADS;
-            } else if (rem > SC_THREADS) {
-                uint32_t r[4];
-                scatter_load<4>(post + pos, rem, tid, r);
-                if (rem <= 4 * SC_THREADS && next) prefetch_next();
-                scatter_apply<4>(sh.acc, r, first_bits);
-                pos += 4 * SC_THREADS;
-            } else {
-                uint32_t r[1];
-                scatter_load<1>(post + pos, rem, tid, r);
-                if (next) prefetch_next();
-                scatter_apply<1>(sh.acc, r, first_bits);
-                pos = end;
-            }
-        }
-        // term boundary: this term's LDS writes land before any wave reads the next
-        if (j + 1 < nt) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    }
-    // the asm LDS writes; the threshold histogram's LDS-DMA copy
+    // the asm LDS updates; the threshold histogram's LDS-DMA copy
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __syncthreads();
 
@@ -947,12 +828,11 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
         return;
     }
     const uint64_t doc_base = (uint64_t)doc_lo + (uint64_t)block_first;
-    // Candidates are staged in the unused tail of the accumulator array when they fit
-    // there and copied out coalesced (a lane-scattered 8-byte store per candidate slot
-    // costs a store instruction per slot and wave); else they go straight out.
-    const int n4z = (n_local + 3) >> 2;
-    uint64_t *stage = reinterpret_cast<uint64_t *>(sh.acc + 4 * n4z);
-    const bool staged = 2 * k <= MAX_BLOCK_DOCS - 4 * n4z;
+    // Candidates are staged in the unused tail of the score array when they fit there
+    // and copied out coalesced (a lane-scattered 8-byte store per candidate slot costs
+    // a store instruction per slot and wave); else they go straight out.
+    uint64_t *stage = reinterpret_cast<uint64_t *>(sh.acc.a.sc + 2 * n4z);
+    const bool staged = 2 * k <= MAX_BLOCK_DOCS / 2 - 2 * n4z;
     auto cand = [&](uint32_t pos, uint32_t w, int idx) {
         const uint32_t doc = (uint32_t)(doc_base + (uint64_t)idx);
         const uint64_t key = ((uint64_t)w << 32) | (uint64_t)(0xFFFFFFFFu - doc);
@@ -973,12 +853,11 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
         }
     };
     auto emit_all_touched = [&]() {
-        const uint32_t n = compact_words(sh, n_local, tid, [](uint32_t w, int) { return w ? 1u : 0u; },
-                                         [&](int, uint32_t pos, uint32_t w, int idx) {
-                                             cand(pos, w, idx);
-                                         });
-        flush(min(n & 0xFFFFu, (uint32_t)k));
-        if (tid == 0) *cn = (int32_t)min(n & 0xFFFFu, (uint32_t)k);
+        const uint32_t n = compact_scores(
+            sh, n_local, tid, [](uint32_t s, int) { return s != 0; },
+            [&](uint32_t pos, uint32_t s, int idx) { cand(pos, (s << 16) | sh.acc.a.ft[idx], idx); });
+        flush(min(n, (uint32_t)k));
+        if (tid == 0) *cn = (int32_t)min(n, (uint32_t)k);
     };
 
     // Shared per-query threshold.  qhist[q] (when given) counts the scores of every
@@ -989,20 +868,19 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
     // reach Tq they are its only candidates (no histogram, no tie order -- the merge
     // orders them by key); else the full selection below runs.  Items run block-major
     // (all queries' block 0 first), so Tq is close to the final k-th score after the
-    // first blocks and the later blocks emit few candidates.  A stale (smaller) count
-    // still gives a valid lower bound.
+    // first blocks and the later blocks emit few candidates.
     uint32_t Tq = 0;
     if (qh) {
         Tq = read_tq();
         if (Tq > 0) {
-            const uint32_t thr_w = Tq << 16;
-            const uint32_t n = compact_words(
-                sh, n_local, tid, [thr_w](uint32_t w, int) { return w >= thr_w ? 1u : 0u; },
-                [&](int, uint32_t pos, uint32_t w, int idx) { cand(pos, w, idx); });
-            const uint32_t na = n & 0xFFFFu;
-            if (na <= (uint32_t)k) {
-                flush(na);
-                if (tid == 0) *cn = (int32_t)na;
+            const uint32_t n = compact_scores(
+                sh, n_local, tid, [Tq](uint32_t s, int) { return s >= Tq; },
+                [&](uint32_t pos, uint32_t s, int idx) {
+                    cand(pos, (s << 16) | sh.acc.a.ft[idx], idx);
+                });
+            if (n <= (uint32_t)k) {
+                flush(n);
+                if (tid == 0) *cn = (int32_t)n;
                 return;
             }
         }
@@ -1013,16 +891,14 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
     if (fast) {
         // ---- fast path: score histogram -> k-th score T -------------------
         uint32_t *hist = sh.u.hist;
-        // branch-free: an untouched doc (w = 0) counts into a per-lane spare bin past
+        // branch-free: an untouched doc (s = 0) counts into a per-lane spare bin past
         // the 4096 score bins (no same-address conflicts), never read
         const uint32_t spare = HIST_BINS + (uint32_t)lane;
-        if (qpre) {  // the threshold copy was read (read_tq's barriers): zero the bins
+        if (qh) {  // the threshold copy was read (read_tq's barriers): zero the bins
             reinterpret_cast<uint4 *>(hist)[tid] = make_uint4(0, 0, 0, 0);
             __syncthreads();
         }
-        sweep_words(sh.acc, n_local, tid, [&](uint32_t w, int) {
-            atomicAdd(&hist[w ? (w >> 16) : spare], 1u);
-        });
+        sweep_scores(sh, n_local, tid, [&](uint32_t s, int) { atomicAdd(&hist[s ? s : spare], 1u); });
         __syncthreads();
         // thread t owns bins 4t..4t+3; s = touched docs with score >= 4t
         const uint4 h4 = reinterpret_cast<const uint4 *>(hist)[tid];
@@ -1065,30 +941,30 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
         need -= above;
         if (ties == need || ties <= (uint32_t)TIE_CAP) {
             // scores above T are in; the ties at T all go in, or into a list (the
-            // histogram is consumed) as (low 16 bits of the word, 0xFFFF - idx):
-            // unique, and larger = first-touch earlier, then doc smaller.
+            // histogram is consumed) as (key of the doc, 0xFFFF - idx): unique, and
+            // larger = first-touch earlier, then doc smaller.
             // Compaction: one sweep marks each lane's candidates and ties in two
-            // 32-bit masks over its 32 words (4 per ds_read_b128); a block scan of the
-            // counts gives positions; the write loop visits only the marked words
+            // 32-bit masks over its 32 docs (4 per ds_read_b64); a block scan of the
+            // counts gives positions; the write loop visits only the marked docs
             // (~1 per lane), not all 32.
             const bool all_ties = ties == need;
-            const uint32_t thr_a = (all_ties ? T : T + 1) << 16;  // list A: w >= thr_a
+            const uint32_t thr_a = all_ties ? T : T + 1;  // list A: s >= thr_a
             uint32_t *tl = sh.u.hist;
             uint32_t ma = 0, mb = 0;
             {
-                const uint4 *a4 = reinterpret_cast<const uint4 *>(sh.acc);
+                const uint2 *s2 = reinterpret_cast<const uint2 *>(sh.acc.a.sc);
                 const int n4 = (n_local + 3) >> 2;
 #pragma unroll
                 for (int i = 0; i < SC_PER_THREAD / 4; ++i) {
                     const int q4 = i * SC_THREADS + tid;
-                    const uint4 y = a4[q4];  // q4 < 8192: inside the array
+                    const uint2 y = s2[q4];  // q4 < 8192: inside the array
                     const bool ok = q4 < n4;
-                    const uint32_t wv[4] = {y.x, y.y, y.z, y.w};
+                    const uint32_t sv[4] = {y.x & 0xFFFFu, y.x >> 16, y.y & 0xFFFFu, y.y >> 16};
 #pragma unroll
                     for (int e = 0; e < 4; ++e) {
-                        const uint32_t w = ok ? wv[e] : 0u;
-                        ma |= (uint32_t)(w >= thr_a) << (4 * i + e);
-                        mb |= (uint32_t)((w >> 16) == T) << (4 * i + e);
+                        const uint32_t sc = ok ? sv[e] : 0u;
+                        ma |= (uint32_t)(sc >= thr_a) << (4 * i + e);
+                        mb |= (uint32_t)(sc == T) << (4 * i + e);
                     }
                 }
                 if (all_ties) mb = 0;
@@ -1108,13 +984,13 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
                     const int bit = __builtin_ctz(ma);
                     ma &= ma - 1;
                     const int idx = idx_of(bit);
-                    cand(pa++, sh.acc[idx], idx);
+                    cand(pa++, word_at(sh, idx), idx);
                 }
                 while (mb) {
                     const int bit = __builtin_ctz(mb);
                     mb &= mb - 1;
                     const int idx = idx_of(bit);
-                    tl[pb++] = ((sh.acc[idx] & 0xFFFFu) << 16) | (0xFFFFu - (uint32_t)idx);
+                    tl[pb++] = ((uint32_t)sh.acc.a.ft[idx] << 16) | (0xFFFFu - (uint32_t)idx);
                 }
             }
             __syncthreads();
@@ -1251,29 +1127,31 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
         dcut = dprefix;  // keep ties whose (0xFFFF - idx) >= dcut
     }
     __syncthreads();
-    const uint32_t n = compact_words(
+    // (the compaction classifies by score first; the key is read for the score's docs)
+    const uint32_t Ts = T >> 16;
+    const uint32_t n = compact_scores(
         sh, n_local, tid,
-        [T, dcut](uint32_t w, int idx) -> uint32_t {
-            return (w != 0 && (w > T || (w == T && (0xFFFFu - (uint32_t)idx) >= dcut))) ? 1u : 0u;
+        [&](uint32_t s, int idx) -> bool {
+            if (s == 0 || s < Ts) return false;
+            if (s > Ts) return true;
+            const uint32_t w = (s << 16) | sh.acc.a.ft[idx];
+            return w > T || (w == T && (0xFFFFu - (uint32_t)idx) >= dcut);
         },
-        [&](int, uint32_t pos, uint32_t w, int idx) { cand(pos, w, idx); });
+        [&](uint32_t pos, uint32_t s, int idx) { cand(pos, (s << 16) | sh.acc.a.ft[idx], idx); });
     flush((uint32_t)k);
     // exactly k by construction; anything else is a selection bug -> flag it
-    if (tid == 0) *cn = (n & 0xFFFFu) == (uint32_t)k ? k : -2;
+    if (tid == 0) *cn = n == (uint32_t)k ? k : -2;
 }
 
 // Persistent: one workgroup per CU walks the (query, block) items, so the per-
-// workgroup launch cost (16 waves, 150 KiB of LDS) is paid once per CU, not per item.
+// workgroup launch cost (16 waves, 154 KiB of LDS) is paid once per CU, not per item.
 __global__ void __launch_bounds__(SC_THREADS)
-score_blocks_kernel(const uint32_t *__restrict__ post, const int64_t *__restrict__ term_start,
-                    const uint32_t *__restrict__ blk_off, const uint16_t *__restrict__ seg,
-                    const uint32_t *__restrict__ lid, const uint16_t *__restrict__ wmeta,
-                    int min_cls, int nb, int block_docs, int64_t n_terms,
-                    uint32_t n_docs, uint32_t doc_lo, const uint32_t *__restrict__ q_terms,
-                    const int32_t *__restrict__ cu_q, int k, uint64_t *__restrict__ cand_key,
-                    int32_t *__restrict__ cand_n, int n_items, int n_q,
-                    uint32_t *__restrict__ qhist, int ablate, const ItemRec *__restrict__ rec,
-                    uint32_t *__restrict__ long_flag) {
+score_blocks_kernel(const uint32_t *__restrict__ post, SubIndex si, int min_cls, int nb,
+                    int block_docs, int64_t n_terms, uint32_t n_docs, uint32_t doc_lo,
+                    const uint32_t *__restrict__ q_terms, const int32_t *__restrict__ cu_q, int k,
+                    uint64_t *__restrict__ cand_key, int32_t *__restrict__ cand_n, int n_items,
+                    int n_q, uint32_t *__restrict__ qhist, int ablate,
+                    const ItemRec *__restrict__ rec, uint32_t *__restrict__ long_flag) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     ScoreShared &sh = *reinterpret_cast<ScoreShared *>(smem);
     if ((uint32_t)(uintptr_t)((__attribute__((address_space(3))) unsigned char *)smem) != 0) {
@@ -1285,10 +1163,9 @@ score_blocks_kernel(const uint32_t *__restrict__ post, const int64_t *__restrict
     }
     // items block-major: item = b * n_q + q (the shared threshold, see score_item)
     for (int item = blockIdx.x; item < n_items; item += gridDim.x) {
-        score_item(sh, item % n_q, item / n_q, post, term_start, blk_off, seg, lid, wmeta,
-                   min_cls, nb, block_docs, n_terms, n_docs, doc_lo, q_terms, cu_q, k, cand_key,
-                   cand_n, qhist, ablate, rec ? rec + (int64_t)item * WTERMS : nullptr,
-                   long_flag);
+        score_item(sh, item % n_q, item / n_q, post, si, min_cls, nb, block_docs, n_terms,
+                   n_docs, doc_lo, q_terms, cu_q, k, cand_key, cand_n, qhist, ablate,
+                   rec ? rec + (int64_t)item * WTERMS : nullptr, long_flag);
         __syncthreads();  // every wave is done with the LDS of this item
     }
 }
@@ -1299,17 +1176,15 @@ score_blocks_kernel(const uint32_t *__restrict__ post, const int64_t *__restrict
 // SC_THREADS queries in query order (a block scan: the same list in every workgroup)
 // and takes its share of their (query, block) items.
 __global__ void __launch_bounds__(SC_THREADS)
-score_long_kernel(const uint32_t *__restrict__ post, const int64_t *__restrict__ term_start,
-                  const uint32_t *__restrict__ blk_off, const uint16_t *__restrict__ seg,
-                  int min_cls, int nb, int block_docs, int64_t n_terms, uint32_t n_docs,
-                  uint32_t doc_lo, const uint32_t *__restrict__ q_terms,
-                  const int32_t *__restrict__ cu_q, int k, uint64_t *__restrict__ cand_key,
-                  int32_t *__restrict__ cand_n, int n_q, const uint32_t *__restrict__ long_flag) {
+score_long_kernel(const uint32_t *__restrict__ post, SubIndex si, int min_cls, int nb,
+                  int block_docs, int64_t n_terms, uint32_t n_docs, uint32_t doc_lo,
+                  const uint32_t *__restrict__ q_terms, const int32_t *__restrict__ cu_q, int k,
+                  uint64_t *__restrict__ cand_key, int32_t *__restrict__ cand_n, int n_q,
+                  const uint32_t *__restrict__ long_flag) {
     if (__builtin_amdgcn_readfirstlane(*long_flag) == 0) return;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     ScoreShared &sh = *reinterpret_cast<ScoreShared *>(smem);
-    static_assert(sizeof(sh.wt) >= SC_THREADS * sizeof(uint32_t), "round list fits");
-    uint32_t *list = &sh.wt.wtab[0][0];
+    uint32_t *list = &sh.wtab[0][0];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     for (int r0 = 0; r0 < n_q; r0 += SC_THREADS) {
         const int q = r0 + tid;
@@ -1330,9 +1205,9 @@ score_long_kernel(const uint32_t *__restrict__ post, const int64_t *__restrict__
         const int n_items = (int)n * nb;
         for (int it = blockIdx.x; it < n_items; it += gridDim.x) {
             const int lq = (int)list[it % n], b = it / n;
-            score_long_item(lq, b, post, term_start, blk_off, seg, min_cls, nb, block_docs,
-                            n_terms, n_docs, doc_lo, q_terms, cu_q, k,
-                            cand_key + ((int64_t)lq * nb + b) * k, cand_n + (int64_t)lq * nb + b);
+            score_long_item(sh, lq, b, post, si, min_cls, nb, block_docs, n_terms, n_docs,
+                            doc_lo, q_terms, cu_q, k, cand_key + ((int64_t)lq * nb + b) * k,
+                            cand_n + (int64_t)lq * nb + b);
             __syncthreads();  // the item's LDS (and the list) stay consistent
         }
         __syncthreads();  // the list and wsum are rewritten by the next round
@@ -1598,14 +1473,12 @@ struct di_index {
     int device = 0;
     hipStream_t stream = nullptr;
     bool own_stream = false;
-    int64_t n_terms = 0, n_post = 0;
+    int64_t n_terms = 0, n_post = 0, n_ent = 0, n_long = 0;
     uint32_t n_docs = 0, doc_lo = 0;  // shard [doc_lo, doc_lo + n_docs)
     int nb = 0, block_docs = 0;
     int min_cls = 7;                 // impact-class prefix scored (7 = every posting: exact)
-    std::vector<uint16_t> seg;       // host copy of the class offsets (pass 3)
-    std::vector<uint32_t> lid;       // long-sublist ids (pass 3)
-    std::vector<uint16_t> wmeta;     // per-wave class ends of the long sublists
-    DevBuf post, term_start, blk_off, seg_dev, lid_dev, wmeta_dev;
+    // postings and the sparse (term, block) entries (SubIndex)
+    DevBuf post, tb_start, eblk, epos, seg, lid, wmeta, emax;
     DevBuf ws_q, ws_cu, ws_ck, ws_cn, ws_doc, ws_score, ws_n, ws_key, ws_thr;
     DevBuf ws_rec;  // ItemRec per (item, term slot): item_setup_kernel -> score_blocks
     DevBuf ws_long;  // score_blocks -> score_long_kernel: the batch has long queries
@@ -1615,6 +1488,11 @@ struct di_index {
     int shared_thr = -1;
     int ablate = 0;  // DI_PROFILE_ABLATE: profiling only (1 no scatter, 2 no selection, 4 stop at the k-th score)
     Timer timer;
+
+    SubIndex sub() const {
+        return SubIndex{tb_start.as<uint32_t>(), eblk.as<uint16_t>(), epos.as<uint32_t>(),
+                        seg.as<uint16_t>(), lid.as<uint32_t>(), wmeta.as<uint16_t>()};
+    }
 };
 
 namespace {
@@ -1631,9 +1509,23 @@ struct DeviceScope {
     }
 };
 
+template <class T>
+void upload(DevBuf &d, const std::vector<T> &h) {
+    d.reserve(std::max<size_t>(h.size() * sizeof(T), 16));
+    if (!h.empty()) DI_HIP(hipMemcpy(d.p, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice));
+}
+
+// The device index of postings given in the reference file order (term-major, value
+// desc / doc asc): the shard's docs in nb equal blocks; per term only the blocks it has
+// postings in get an entry (the sparse term -> block table: a multi-million-term
+// vocabulary costs its entries, not n_terms x nb).  Every pass runs over term ranges on
+// host_threads() threads (a term owns disjoint output ranges); the result does not
+// depend on the thread count.
 void build_index(di_index *ix, const int64_t *term_off, int64_t n_terms, const uint32_t *pdoc,
                  const uint8_t *pval, uint32_t doc_lo, uint32_t doc_hi) {
     DI_REQUIRE(n_terms >= 0, DI_EINVAL, "n_terms < 0");
+    DI_REQUIRE(n_terms < (int64_t)0xFFFFFFFF, DI_ERANGE, "n_terms %lld >= 2^32",
+               (long long)n_terms);
     DI_REQUIRE(term_off[0] >= 0, DI_EINVAL, "term_off[0] < 0");
     for (int64_t t = 0; t < n_terms; ++t)
         DI_REQUIRE(term_off[t + 1] >= term_off[t], DI_EINVAL, "term_off not monotone at %lld",
@@ -1650,6 +1542,7 @@ void build_index(di_index *ix, const int64_t *term_off, int64_t n_terms, const u
     DI_REQUIRE(doc_hi >= doc_lo, DI_EINVAL, "doc_hi < doc_lo");
     const uint32_t nd = doc_hi - doc_lo;
     const int nb = (int)((nd + MAX_BLOCK_DOCS - 1) / MAX_BLOCK_DOCS);
+    DI_REQUIRE(nb <= 65535, DI_ERANGE, "%u docs in one shard: more than 65535 blocks", nd);
     // equal blocks (no small tail block costing a whole workgroup per query)
     const uint32_t bd =
         nb ? (uint32_t)std::min<uint64_t>(MAX_BLOCK_DOCS, ((nd + nb - 1) / nb + 63) / 64 * 64)
@@ -1659,181 +1552,208 @@ void build_index(di_index *ix, const int64_t *term_off, int64_t n_terms, const u
     ix->doc_lo = doc_lo;
     ix->nb = nb;
     ix->block_docs = (int)bd;
-    const int64_t stride = nb + 1;
-    std::vector<int64_t> tstart(std::max<int64_t>(n_terms, 1), 0);
-    std::vector<uint32_t> boff((size_t)std::max<int64_t>(n_terms * stride, 1), 0);
-    // The three passes run over term ranges on host_threads() threads (every term owns
-    // disjoint output ranges); the result does not depend on the thread count.
-    // pass 1: per (term, block) counts of kept postings
+    const uint32_t NO = 0xFFFFFFFFu;
+
+    // pass 1: per term, kept postings and the blocks holding them
+    std::vector<uint32_t> n_kept((size_t)n_terms + 1, 0), n_ent_t((size_t)n_terms + 1, 0);
     parallel_for(n_terms, [&](int64_t t0, int64_t t1, int) {
-        std::vector<uint32_t> cnt(stride);
+        std::vector<uint32_t> cnt((size_t)std::max(nb, 1), 0);
+        std::vector<int> touched;
         for (int64_t t = t0; t < t1; ++t) {
-            std::fill(cnt.begin(), cnt.end(), 0);
+            uint32_t kept = 0;
+            touched.clear();
             for (int64_t p = term_off[t]; p < term_off[t + 1]; ++p) {
                 if (pval[p] == 0) break;  // inverted_index.py:50-51
-                uint32_t d = pdoc[p];
+                const uint32_t d = pdoc[p];
                 if (d < doc_lo || d >= doc_hi) continue;
-                cnt[(d - doc_lo) / bd]++;
+                const int b = (int)((d - doc_lo) / bd);
+                if (cnt[b]++ == 0) touched.push_back(b);
+                ++kept;
             }
-            uint32_t run = 0;
-            for (int b = 0; b < nb; ++b) {
-                boff[t * stride + b] = run;
-                run += cnt[b];
-            }
-            boff[t * stride + nb] = run;
+            for (int b : touched) cnt[b] = 0;
+            n_kept[t] = kept;
+            n_ent_t[t] = (uint32_t)touched.size();
         }
     });
-    int64_t total = 0;
+    std::vector<uint32_t> tb_start((size_t)n_terms + 1, 0);
+    std::vector<uint64_t> tstart((size_t)n_terms + 1, 0);
+    uint64_t total = 0, n_ent = 0;
     for (int64_t t = 0; t < n_terms; ++t) {
         tstart[t] = total;
-        total += boff[t * stride + nb];
+        tb_start[t] = (uint32_t)n_ent;
+        total += n_kept[t];
+        n_ent += n_ent_t[t];
+        DI_REQUIRE(total < NO && n_ent < NO, DI_ERANGE,
+                   "more than 2^32 postings / (term, block) entries in one shard");
     }
-    ix->n_post = total;
-    std::vector<uint32_t> packed((size_t)std::max<int64_t>(total, 4));
-    // pass 2: place (stable: keeps value-desc/doc-asc inside each block)
+    tstart[n_terms] = total;
+    tb_start[n_terms] = (uint32_t)n_ent;
+    std::vector<uint32_t>().swap(n_kept);
+    std::vector<uint32_t>().swap(n_ent_t);
+    ix->n_post = (int64_t)total;
+    ix->n_ent = (int64_t)n_ent;
+
+    // pass 2: the entries (block, start) and the postings placed by block (stable: the
+    // reference order inside each sublist)
+    std::vector<uint16_t> eblk((size_t)std::max<uint64_t>(n_ent, 1));
+    std::vector<uint32_t> epos((size_t)n_ent + 1);
+    std::vector<uint32_t> packed((size_t)std::max<uint64_t>(total, 4));
     parallel_for(n_terms, [&](int64_t t0, int64_t t1, int) {
-        std::vector<uint32_t> cur(stride);
+        std::vector<uint32_t> cur((size_t)std::max(nb, 1), 0);
+        std::vector<int> touched;
         for (int64_t t = t0; t < t1; ++t) {
-            for (int b = 0; b <= nb; ++b) cur[b] = boff[t * stride + b];
+            touched.clear();
             for (int64_t p = term_off[t]; p < term_off[t + 1]; ++p) {
                 if (pval[p] == 0) break;
-                uint32_t d = pdoc[p];
+                const uint32_t d = pdoc[p];
                 if (d < doc_lo || d >= doc_hi) continue;
-                uint32_t r = d - doc_lo;
-                int b = (int)(r / bd);
-                packed[tstart[t] + cur[b]++] = ((r % bd) << 8) | pval[p];
+                const int b = (int)((d - doc_lo) / bd);
+                if (cur[b]++ == 0) touched.push_back(b);
+            }
+            std::sort(touched.begin(), touched.end());
+            uint32_t run = (uint32_t)tstart[t];
+            uint32_t e = tb_start[t];
+            for (int b : touched) {
+                eblk[e] = (uint16_t)b;
+                epos[e++] = run;
+                const uint32_t c = cur[b];
+                cur[b] = run;  // now the block's write cursor
+                run += c;
+            }
+            for (int64_t p = term_off[t]; p < term_off[t + 1]; ++p) {
+                if (pval[p] == 0) break;
+                const uint32_t d = pdoc[p];
+                if (d < doc_lo || d >= doc_hi) continue;
+                const uint32_t r = d - doc_lo;
+                packed[cur[r / bd]++] = ((r % bd) << 8) | pval[p];
+            }
+            for (int b : touched) cur[b] = 0;
+        }
+    });
+    epos[n_ent] = (uint32_t)total;
+
+    // long sublists (>= WLONG_MIN postings) get ids in entry order
+    std::vector<uint32_t> lid((size_t)std::max<uint64_t>(n_ent, 1), NO);
+    uint32_t n_long = 0;
+    for (uint64_t e = 0; e < n_ent; ++e)
+        if (epos[e + 1] - epos[e] >= (uint32_t)WLONG_MIN) lid[e] = n_long++;
+    ix->n_long = n_long;
+
+    // pass 3: order inside every sublist, the impact-class offsets and the block max.
+    // Postings are grouped by impact class c = 7 - floor(log2 value) (class 0 = values
+    // 128..255, ..., class 7 = value 1), classes in order, so that "every posting with
+    // value >= 2^(7-c)" is a prefix of the sublist: seg[8e + c] = its length
+    // (di_index_set_min_impact prunes with it; class 7 = the whole sublist = exact).
+    // Inside a class, postings are dealt from their 32 LDS bank buckets ((doc_in_block
+    // / 2) mod 32: the bank of both the doc's packed score word and its key slot;
+    // distinct banks per aligned 32-posting block where the class allows, see
+    // emit_group): the scorer's lanes read consecutive postings and update their docs'
+    // words, and a 32-lane group of a ds_add_u32 / ds_write_b16 conflicts on equal
+    // banks.  Any order is exact: a doc occurs once per term, and its key (first term,
+    // value there) does not depend on the order inside the term.
+    // Long sublists are laid out by wave segment first: wave w of the scorer owns the
+    // block's docs [w S, (w + 1) S), S = ceil(bd / 16), and its postings of the sublist
+    // form one run (classes in order, bank-dealt inside), so that no two waves touch one
+    // doc.  wmeta[lid * 128 + 8 w + c] = end of class c of segment w (offset in the
+    // sublist).  emax[e] = the sublist's largest value (block-max metadata).
+    std::vector<uint16_t> seg((size_t)std::max<uint64_t>(n_ent * 8, 8), 0);
+    std::vector<uint16_t> wmeta((size_t)std::max<uint32_t>(n_long, 1) * WSEG * 8, 0);
+    std::vector<uint8_t> emax((size_t)std::max<uint64_t>(n_ent, 1), 0);
+    auto cls_of = [](uint32_t w) { return 7 - (31 - __builtin_clz(w & 255u)); };
+    auto bank_of = [](uint32_t w) { return (w >> 9) & 31u; };  // (doc_in_block / 2) mod 32
+    const uint32_t S = (bd + WSEG - 1) / WSEG;
+    parallel_for(n_terms, [&](int64_t t0, int64_t t1, int) {
+        std::vector<uint32_t> grp, tmp, bk, seg_in, cls_cnt(8), cls_pos(8), bucket_cnt(32),
+            head(32), fill(32);
+        // one group (any order in): classes in order (stable), each dealt round-robin
+        // from its 32 LDS bank buckets into packed[o..]; cum[c] = end of class c
+        // relative to the sublist start s0
+        auto emit_group = [&](const uint32_t *in, size_t n, int64_t &o, int64_t s0,
+                              uint16_t *cum) {
+            std::fill(cls_cnt.begin(), cls_cnt.end(), 0);
+            for (size_t i = 0; i < n; ++i) cls_cnt[cls_of(in[i])]++;
+            uint32_t run = 0;
+            for (int c = 0; c < 8; ++c) {
+                cls_pos[c] = run;
+                run += cls_cnt[c];
+            }
+            tmp.resize(n);
+            for (size_t i = 0; i < n; ++i) tmp[cls_pos[cls_of(in[i])]++] = in[i];
+            // The scorer's lanes take the group's postings in rounds from its start,
+            // and a 32-lane group of its LDS updates is one aligned block of 32
+            // positions: each position takes, from its class, a posting whose bank is
+            // not yet used in the current block (bank cursor carried on across sweeps
+            // and class boundaries), else any.
+            uint32_t c0 = 0, used = 0;
+            int cursor = 0;
+            const int64_t o_start = o;
+            for (int c = 0; c < 8; ++c) {
+                const uint32_t c1 = c0 + cls_cnt[c];
+                std::fill(bucket_cnt.begin(), bucket_cnt.end(), 0);
+                for (uint32_t i = c0; i < c1; ++i) bucket_cnt[bank_of(tmp[i])]++;
+                uint32_t r = 0, avail = 0;
+                for (int k = 0; k < 32; ++k) {
+                    head[k] = r;
+                    r += bucket_cnt[k];
+                    if (bucket_cnt[k]) avail |= 1u << k;
+                }
+                bk.resize(c1 - c0);
+                fill = head;
+                for (uint32_t i = c0; i < c1; ++i) bk[fill[bank_of(tmp[i])]++] = tmp[i];
+                for (uint32_t i = c0; i < c1; ++i) {
+                    if (((o - o_start) & 31) == 0) used = 0;
+                    uint32_t cand = avail & ~used;
+                    if (!cand) cand = avail;  // every bank left is taken in this block
+                    const uint32_t rot = cursor ? (cand >> cursor) | (cand << (32 - cursor)) : cand;
+                    const int k = (__builtin_ctz(rot) + cursor) & 31;
+                    packed[o++] = bk[head[k]++];
+                    if (--bucket_cnt[k] == 0) avail &= ~(1u << k);
+                    used |= 1u << k;
+                    cursor = (k + 1) & 31;
+                }
+                if (cum) cum[c] = (uint16_t)(o - s0);
+                c0 = c1;
+            }
+        };
+        for (int64_t t = t0; t < t1; ++t) {
+            for (uint32_t e = tb_start[t]; e < tb_start[t + 1]; ++e) {
+                const int64_t s0 = epos[e], s1 = epos[e + 1];
+                uint16_t *sg = &seg[(size_t)e * 8];
+                grp.assign(packed.begin() + s0, packed.begin() + s1);
+                uint32_t mx = 0;
+                for (uint32_t x : grp) mx = std::max(mx, x & 255u);
+                emax[e] = (uint8_t)mx;
+                int64_t o = s0;
+                const uint32_t id = lid[e];
+                if (id == NO) {
+                    emit_group(grp.data(), grp.size(), o, s0, sg);
+                    continue;
+                }
+                {  // whole-sublist class counts (seg), then the per-wave layout
+                    uint32_t run = 0, cc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+                    for (uint32_t x : grp) cc[cls_of(x)]++;
+                    for (int c = 0; c < 8; ++c) sg[c] = (uint16_t)(run += cc[c]);
+                }
+                for (int w = 0; w < WSEG; ++w) {
+                    seg_in.clear();
+                    for (uint32_t x : grp)
+                        if (std::min<uint32_t>((x >> 8) / S, WSEG - 1) == (uint32_t)w)
+                            seg_in.push_back(x);
+                    emit_group(seg_in.data(), seg_in.size(), o, s0,
+                               &wmeta[(size_t)id * WSEG * 8 + w * 8]);
+                }
             }
         }
     });
-    // pass 3: order inside every (term, block) sublist, and the impact-class offsets.
-    // Postings are grouped by impact class c = 7 - floor(log2 value) (class 0 = values
-    // 128..255, ..., class 7 = value 1), classes in order, so that "every posting with
-    // value >= 2^(7-c)" is a prefix of the sublist: seg[(t*nb + b)*8 + c] = its length
-    // (di_index_set_min_impact prunes with it; class 7 = the whole sublist = exact).
-    // Inside a class, postings are dealt from their 32 LDS bank buckets (doc_in_block
-    // mod 32, distinct banks per aligned 32-posting block where the class allows, see
-    // emit_group): the scorer's lanes read consecutive postings and update
-    // acc[doc_in_block], and a 32-lane group of a ds_read_b32 / ds_write_b32 conflicts
-    // on equal banks.  Any order is exact: a doc occurs once per term, and its key
-    // (first term, value there) does not depend on the order inside the term.
-    ix->seg.assign((size_t)std::max<int64_t>(n_terms * nb * 8, 1), 0);
-    // Long sublists (>= WLONG_MIN postings) are laid out by wave segment first: wave w
-    // of the scorer owns the block's docs [w S, (w + 1) S), S = ceil(bd / 16), and
-    // its postings of the sublist form one run (classes in order, bank-dealt inside),
-    // so that consecutive long terms need no barrier (no two waves touch one doc).
-    // wmeta[lid * 128 + 8 w + c] = end of class c of segment w (offset in the
-    // sublist), lid[t * nb + b] = the sublist's long id (0xFFFFFFFF: short), ids in
-    // (term, block) order.
-    ix->lid.assign((size_t)std::max<int64_t>(n_terms * nb, 1), 0xFFFFFFFFu);
-    {
-        const int64_t wlong_min = WLONG_MIN;
-        uint32_t n_long = 0;
-        for (int64_t t = 0; t < n_terms; ++t)
-            for (int b = 0; b < nb; ++b)
-                if ((int64_t)(boff[t * stride + b + 1] - boff[t * stride + b]) >= wlong_min)
-                    ix->lid[(size_t)(t * nb + b)] = n_long++;
-        ix->wmeta.assign((size_t)n_long * WSEG * 8, 0);
-        auto cls_of = [](uint32_t w) { return 7 - (31 - __builtin_clz(w & 255u)); };
-        const uint32_t S = (bd + WSEG - 1) / WSEG;
-        parallel_for(n_terms, [&](int64_t t0, int64_t t1, int) {
-            std::vector<uint32_t> grp, tmp, bk, seg_in, cls_cnt(8), cls_pos(8), bucket_cnt(32),
-                head(32), fill(32);
-            // one group (any order in): classes in order (stable), each dealt round-robin
-            // from its 32 LDS bank buckets (doc_in_block mod 32) into packed[o..];
-            // cum[c] = end of class c relative to the sublist start s0
-            auto emit_group = [&](const uint32_t *in, size_t n, int64_t &o, int64_t s0,
-                                  uint16_t *cum) {
-                std::fill(cls_cnt.begin(), cls_cnt.end(), 0);
-                for (size_t i = 0; i < n; ++i) cls_cnt[cls_of(in[i])]++;
-                uint32_t run = 0;
-                for (int c = 0; c < 8; ++c) {
-                    cls_pos[c] = run;
-                    run += cls_cnt[c];
-                }
-                tmp.resize(n);
-                for (size_t i = 0; i < n; ++i) tmp[cls_pos[cls_of(in[i])]++] = in[i];
-                // The scorer's lanes take the group's postings in rounds from its start,
-                // and a 32-lane group of its ds_read_b32 / ds_write_b32 is one aligned
-                // block of 32 positions: each position takes, from its class, a posting
-                // whose bank is not yet used in the current block (bank cursor carried
-                // on across sweeps and class boundaries), else any.  Restarting every
-                // class at bank 0 put most of a long term's per-wave runs (~8 postings
-                // per class) into conflicts at every class boundary.
-                uint32_t c0 = 0, used = 0;
-                int cursor = 0;
-                const int64_t o_start = o;
-                for (int c = 0; c < 8; ++c) {
-                    const uint32_t c1 = c0 + cls_cnt[c];
-                    std::fill(bucket_cnt.begin(), bucket_cnt.end(), 0);
-                    for (uint32_t i = c0; i < c1; ++i) bucket_cnt[(tmp[i] >> 8) & 31]++;
-                    uint32_t r = 0, avail = 0;
-                    for (int k = 0; k < 32; ++k) {
-                        head[k] = r;
-                        r += bucket_cnt[k];
-                        if (bucket_cnt[k]) avail |= 1u << k;
-                    }
-                    bk.resize(c1 - c0);
-                    fill = head;
-                    for (uint32_t i = c0; i < c1; ++i) bk[fill[(tmp[i] >> 8) & 31]++] = tmp[i];
-                    for (uint32_t i = c0; i < c1; ++i) {
-                        if (((o - o_start) & 31) == 0) used = 0;
-                        uint32_t cand = avail & ~used;
-                        if (!cand) cand = avail;  // every bank left is taken in this block
-                        const uint32_t rot = cursor ? (cand >> cursor) | (cand << (32 - cursor)) : cand;
-                        const int k = (__builtin_ctz(rot) + cursor) & 31;
-                        packed[o++] = bk[head[k]++];
-                        if (--bucket_cnt[k] == 0) avail &= ~(1u << k);
-                        used |= 1u << k;
-                        cursor = (k + 1) & 31;
-                    }
-                    if (cum) cum[c] = (uint16_t)(o - s0);
-                    c0 = c1;
-                }
-            };
-            for (int64_t t = t0; t < t1; ++t) {
-                for (int b = 0; b < nb; ++b) {
-                    const int64_t s0 = tstart[t] + boff[t * stride + b];
-                    const int64_t s1 = tstart[t] + boff[t * stride + b + 1];
-                    if (s1 == s0) continue;
-                    uint16_t *sg = &ix->seg[(size_t)(t * nb + b) * 8];
-                    grp.assign(packed.begin() + s0, packed.begin() + s1);
-                    int64_t o = s0;
-                    const uint32_t id = ix->lid[(size_t)(t * nb + b)];
-                    if (id == 0xFFFFFFFFu) {
-                        emit_group(grp.data(), grp.size(), o, s0, sg);
-                        continue;
-                    }
-                    {  // whole-sublist class counts (seg), then the per-wave layout
-                        uint32_t run = 0, cc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-                        for (uint32_t x : grp) cc[cls_of(x)]++;
-                        for (int c = 0; c < 8; ++c) sg[c] = (uint16_t)(run += cc[c]);
-                    }
-                    for (int w = 0; w < WSEG; ++w) {
-                        seg_in.clear();
-                        for (uint32_t x : grp)
-                            if (std::min<uint32_t>((x >> 8) / S, WSEG - 1) == (uint32_t)w)
-                                seg_in.push_back(x);
-                        emit_group(seg_in.data(), seg_in.size(), o, s0,
-                                   &ix->wmeta[(size_t)id * WSEG * 8 + w * 8]);
-                    }
-                }
-            }
-        });
-    }
     for (auto &w : packed) w ^= POST_X;  // device encoding (see POST_X)
-    ix->post.reserve(packed.size() * 4);
-    ix->term_start.reserve(tstart.size() * 8);
-    ix->blk_off.reserve(boff.size() * 4);
-    DI_HIP(hipMemcpy(ix->post.p, packed.data(), packed.size() * 4, hipMemcpyHostToDevice));
-    DI_HIP(hipMemcpy(ix->term_start.p, tstart.data(), tstart.size() * 8, hipMemcpyHostToDevice));
-    DI_HIP(hipMemcpy(ix->blk_off.p, boff.data(), boff.size() * 4, hipMemcpyHostToDevice));
-    ix->seg_dev.reserve(ix->seg.size() * 2);
-    DI_HIP(hipMemcpy(ix->seg_dev.p, ix->seg.data(), ix->seg.size() * 2, hipMemcpyHostToDevice));
-    ix->lid_dev.reserve(ix->lid.size() * 4);
-    DI_HIP(hipMemcpy(ix->lid_dev.p, ix->lid.data(), ix->lid.size() * 4, hipMemcpyHostToDevice));
-    if (ix->wmeta.empty()) ix->wmeta.assign(WSEG * 8, 0);
-    ix->wmeta_dev.reserve(ix->wmeta.size() * 2);
-    DI_HIP(hipMemcpy(ix->wmeta_dev.p, ix->wmeta.data(), ix->wmeta.size() * 2, hipMemcpyHostToDevice));
+    upload(ix->post, packed);
+    upload(ix->tb_start, tb_start);
+    upload(ix->eblk, eblk);
+    upload(ix->epos, epos);
+    upload(ix->seg, seg);
+    upload(ix->lid, lid);
+    upload(ix->wmeta, wmeta);
+    upload(ix->emax, emax);
 }
 
 }  // namespace
@@ -1927,14 +1847,6 @@ int di_index_create(const int64_t *term_off, int64_t n_terms, const uint32_t *pd
         if (const char *ab = std::getenv("DI_PROFILE_ABLATE")) ix->ablate = std::atoi(ab);
         if (const char *st = std::getenv("DI_SCORE_THRESHOLD"))  // (tested both ways)
             ix->shared_thr = st[0] != '0' ? 1 : 0;
-        // safe early termination: opt-in (DI_EARLY_TERMINATION=1; tested both ways).  On
-        // the SURVEY §8d synthetic collection no doc range can be skipped (97.6% of even
-        // 64-doc ranges can still reach the k-th score: tools/et_potential.py), and the
-        // class-major order costs 3x in score_blocks (1.1M docs: 51 vs 17 ms per step)
-        {
-            const char *et = std::getenv("DI_EARLY_TERMINATION");
-            if (!(et && et[0] == '1')) ix->ablate |= 512;
-        }
         build_index(ix.get(), term_off, n_terms, pdoc, pval, doc_lo, doc_hi);
         *out = ix.release();
     });
@@ -2070,17 +1982,13 @@ int di_index_search(di_index *ix, const uint32_t *q_terms, const int32_t *cu_q, 
                 const int n_items = nq * nb;
                 if (use_rec) {
                     hipLaunchKernelGGL(item_setup_kernel, dim3(n_items), dim3(128), 0, s,
-                                       ix->term_start.as<int64_t>(), ix->blk_off.as<uint32_t>(),
-                                       ix->seg_dev.as<uint16_t>(), ix->lid_dev.as<uint32_t>(),
-                                       ix->wmeta_dev.as<uint16_t>(), ix->min_cls, nb,
-                                       ix->n_terms, dq, dcu + q0, nq, ix->ws_rec.as<ItemRec>());
+                                       ix->sub(), ix->min_cls, nb, ix->n_terms, dq, dcu + q0, nq,
+                                       ix->ws_rec.as<ItemRec>());
                     check_launch("item_setup");
                 }
                 hipLaunchKernelGGL(score_blocks_kernel, dim3(std::min(n_items, n_cu())),
                                    dim3(SC_THREADS), sizeof(ScoreShared), s,
-                                   ix->post.as<uint32_t>(), ix->term_start.as<int64_t>(),
-                                   ix->blk_off.as<uint32_t>(), ix->seg_dev.as<uint16_t>(),
-                                   ix->lid_dev.as<uint32_t>(), ix->wmeta_dev.as<uint16_t>(),
+                                   ix->post.as<uint32_t>(), ix->sub(),
                                    ix->min_cls, nb, ix->block_docs, ix->n_terms,
                                    ix->n_docs, ix->doc_lo, dq, dcu + q0, k,
                                    ix->ws_ck.as<uint64_t>(), ix->ws_cn.as<int32_t>(), n_items,
@@ -2090,8 +1998,7 @@ int di_index_search(di_index *ix, const uint32_t *q_terms, const int32_t *cu_q, 
                 check_launch("score_blocks");
                 hipLaunchKernelGGL(score_long_kernel, dim3(std::min(n_items, n_cu())),
                                    dim3(SC_THREADS), sizeof(ScoreShared), s,
-                                   ix->post.as<uint32_t>(), ix->term_start.as<int64_t>(),
-                                   ix->blk_off.as<uint32_t>(), ix->seg_dev.as<uint16_t>(),
+                                   ix->post.as<uint32_t>(), ix->sub(),
                                    ix->min_cls, nb, ix->block_docs, ix->n_terms, ix->n_docs,
                                    ix->doc_lo, dq, dcu + q0, k, ix->ws_ck.as<uint64_t>(),
                                    ix->ws_cn.as<int32_t>(), nq, ix->ws_long.as<uint32_t>());

@@ -4,6 +4,7 @@
 // shortest round-trip repr of a double.  Host code only.
 #pragma once
 
+#include <algorithm>
 #include <charconv>
 #include <cmath>
 #include <cstdint>
@@ -89,9 +90,77 @@ inline void for_each_line(std::string_view buf, F &&f) {
     }
 }
 
+// Cut buf into at most `parts` ranges of whole lines: boundaries right after a line
+// terminator (\n, a \r\n pair, a lone \r), so for_each_line over the ranges in order
+// yields exactly the lines of the whole buffer.  Returns the cut positions (first 0,
+// last buf.size()).
+inline std::vector<size_t> line_chunks(std::string_view buf, int parts) {
+    const size_t n = buf.size();
+    std::vector<size_t> cut{0};
+    auto boundary = [&](size_t b) {  // a line starts at b
+        if (b == 0 || b >= n) return true;
+        const char c = buf[b - 1];
+        return c == '\n' || (c == '\r' && buf[b] != '\n');
+    };
+    for (int p = 1; p < parts; ++p) {
+        size_t b = std::max(cut.back(), n * (size_t)p / (size_t)parts);
+        while (b < n && !boundary(b)) ++b;
+        if (b > cut.back() && b < n) cut.push_back(b);
+    }
+    cut.push_back(n);
+    return cut;
+}
+
 // float(text): strict decimal/inf/nan literal with optional surrounding
 // whitespace.  Digit-group underscores (PEP 515) are accepted as Python does.
+// Fast path (the formats' own numbers): plain [digits][.digits] with a mantissa below
+// 2^53 and at most 22 fraction digits is m / 10^k in one correctly rounded division
+// (both exact doubles: Clinger's fast path) -- the value strtod returns.
 inline bool parse_float(std::string_view s, double *out) {
+    {
+        static constexpr double p10[23] = {1e0,  1e1,  1e2,  1e3,  1e4,  1e5,  1e6,  1e7,
+                                           1e8,  1e9,  1e10, 1e11, 1e12, 1e13, 1e14, 1e15,
+                                           1e16, 1e17, 1e18, 1e19, 1e20, 1e21, 1e22};
+        uint64_t m = 0;
+        int nd = 0, frac = -1;
+        bool fast = !s.empty();
+        for (char c : s) {
+            if (c >= '0' && c <= '9') {
+                if (++nd > 19) {
+                    fast = false;
+                    break;
+                }
+                m = m * 10 + (uint64_t)(c - '0');
+                if (frac >= 0) ++frac;
+            } else if (c == '.' && frac < 0) {
+                frac = 0;
+            } else {
+                fast = false;
+                break;
+            }
+        }
+        const int k = frac < 0 ? 0 : frac;
+        if (fast && nd > 0 && m <= (1ull << 53) && k <= 22) {
+            *out = (double)m / p10[k];
+            return true;
+        }
+        // 54..64-bit mantissas (17-19 digits, e.g. repr of a float32 as a double): one
+        // x87 extended division (64-bit mantissa, m and 10^k exact) rounded to double.
+        // The double rounding is exact unless the extended quotient is itself a midpoint
+        // between two doubles (its low 11 bits 0x400): then strtod decides.
+        // (host code: x86-64 long double; a target without it takes strtod)
+        if constexpr (sizeof(long double) >= 10) {
+            if (fast && nd > 0 && k <= 22) {
+                const long double q = (long double)m / (long double)p10[k];
+                uint64_t mant;  // the x87 format's explicit 64-bit significand (low 8 bytes)
+                std::memcpy(&mant, &q, 8);
+                if ((mant & 0x7FFu) != 0x400u) {
+                    *out = (double)q;
+                    return true;
+                }
+            }
+        }
+    }
     s = strip(s);
     if (s.empty()) return false;
     char buf[128];

@@ -21,6 +21,7 @@
 #include <vector>
 
 #include "di_common.h"
+#include "pytext.h"
 
 namespace {
 
@@ -103,7 +104,86 @@ inline float round3(float x) {
     return (float)(std::nearbyint(t)) / 1000.0f;
 }
 
+// Doc d of the collection: its sorted unique 0-based term ids and float32 impacts
+// (the stream depends on (seed, d) only).
+inline void synth_doc(const Alias &zipf, uint64_t seed, int64_t d, int32_t max_terms,
+                      int32_t draws, std::vector<uint32_t> &buf, std::vector<uint32_t> &terms,
+                      std::vector<float> &imps) {
+    Rng r(seed, (uint64_t)d);
+    buf.resize((size_t)draws);
+    for (int i = 0; i < draws; ++i) buf[(size_t)i] = zipf.sample(r);
+    std::sort(buf.begin(), buf.end());
+    const size_t n = (size_t)(std::unique(buf.begin(), buf.end()) - buf.begin());
+    const size_t m = std::min<size_t>(n, (size_t)max_terms);
+    terms.clear();
+    imps.clear();
+    for (size_t i = 0; i < m; ++i) {
+        const double x = r.normal() * 1.5 - 0.5;
+        terms.push_back(buf[i] - 1);
+        imps.push_back((float)std::log1p(std::exp(x)));
+    }
+}
+
 }  // namespace
+
+// The same collection as di_synth_postings, as the impact TSV the index CLI writes
+// (indexer.py:62-68: ', '.join(f'{term}: {round(impact, 3)}'), one line per doc), the
+// term of id t spelled "\u2581t<t>" (an XLM-R-style Metaspace term).  Bench input of
+// the quantize and index-create legs (A10 / A11).  Threads over doc chunks, written in
+// order; *n_terms_out = the (doc, term) pairs written.
+extern "C" int di_synth_impact_tsv(const char *path, int64_t n_docs, int32_t v_terms,
+                                   uint64_t seed, int32_t max_terms, int32_t draws,
+                                   double zipf_a, int64_t *n_terms_out) {
+    using namespace di;
+    return guard([&] {
+        DI_REQUIRE(path && n_docs >= 0 && v_terms > 0 && max_terms > 0 && draws > 0 &&
+                       zipf_a > 1.0,
+                   DI_EINVAL, "bad argument");
+        const Alias zipf(v_terms, zipf_a);
+        FILE *f = std::fopen(path, "wb");
+        DI_REQUIRE(f, DI_EIO, "cannot create %s", path);
+        const int T = host_threads();
+        const int64_t per = 65536;  // docs per chunk; T chunks formatted at a time
+        int64_t total = 0;
+        bool ok = true;
+        std::vector<std::string> text((size_t)T);
+        std::vector<int64_t> cnt((size_t)T);
+        for (int64_t d0 = 0; d0 < n_docs && ok; d0 += per * T) {
+            parallel_for(T, [&](int64_t lo, int64_t hi, int) {
+                std::vector<uint32_t> buf, terms;
+                std::vector<float> imps;
+                char num[16];
+                for (int64_t c = lo; c < hi; ++c) {
+                    std::string &out = text[(size_t)c];
+                    out.clear();
+                    cnt[(size_t)c] = 0;
+                    const int64_t a = std::min(n_docs, d0 + c * per), b = std::min(n_docs, a + per);
+                    for (int64_t d = a; d < b; ++d) {
+                        synth_doc(zipf, seed, d, max_terms, draws, buf, terms, imps);
+                        for (size_t i = 0; i < terms.size(); ++i) {
+                            if (i) out += ", ";
+                            out += "\xe2\x96\x81t";
+                            const int len = std::snprintf(num, sizeof num, "%u", terms[i]);
+                            out.append(num, (size_t)len);
+                            out += ": ";
+                            py::repr_double((double)round3(imps[i]), out);
+                        }
+                        out += '\n';
+                        cnt[(size_t)c] += (int64_t)terms.size();
+                    }
+                }
+            });
+            for (int c = 0; c < T; ++c) {
+                ok = ok && std::fwrite(text[(size_t)c].data(), 1, text[(size_t)c].size(), f) ==
+                               text[(size_t)c].size();
+                total += cnt[(size_t)c];
+            }
+        }
+        ok = (std::fclose(f) == 0) && ok;
+        DI_REQUIRE(ok, DI_EIO, "short write to %s", path);
+        if (n_terms_out) *n_terms_out = total;
+    });
+}
 
 extern "C" int di_synth_postings(int64_t n_docs, int32_t v_terms, uint64_t seed,
                                  int32_t max_terms, int32_t draws, double zipf_a,
@@ -133,20 +213,16 @@ extern "C" int di_synth_postings(int64_t n_docs, int32_t v_terms, uint64_t seed,
                 vi.reserve((size_t)(d1 - d0) * max_terms);
                 vl.reserve((size_t)(d1 - d0));
                 float mx = 0.0f;
+                std::vector<uint32_t> terms;
+                std::vector<float> imps;
                 for (int64_t d = d0; d < d1; ++d) {
-                    Rng r(seed, (uint64_t)d);
-                    for (int i = 0; i < draws; ++i) buf[(size_t)i] = zipf.sample(r);
-                    std::sort(buf.begin(), buf.end());
-                    const size_t n = (size_t)(std::unique(buf.begin(), buf.end()) - buf.begin());
-                    const size_t m = std::min<size_t>(n, (size_t)max_terms);
-                    for (size_t i = 0; i < m; ++i) {
-                        const double x = r.normal() * 1.5 - 0.5;
-                        const float imp = (float)std::log1p(std::exp(x));
-                        vt.push_back(buf[i] - 1);
-                        vi.push_back(imp);
-                        mx = std::max(mx, round3(imp));
+                    synth_doc(zipf, seed, d, max_terms, draws, buf, terms, imps);
+                    for (size_t i = 0; i < terms.size(); ++i) {
+                        vt.push_back(terms[i]);
+                        vi.push_back(imps[i]);
+                        mx = std::max(mx, round3(imps[i]));
                     }
-                    vl.push_back((uint32_t)m);
+                    vl.push_back((uint32_t)terms.size());
                 }
                 c_max[(size_t)c] = mx;
             }

@@ -12,6 +12,7 @@
 #include <fstream>
 #include <string>
 #include <string_view>
+#include <algorithm>
 #include <vector>
 
 #include "di_common.h"
@@ -63,38 +64,57 @@ std::string read_all(const char *path) {
 
 }  // namespace
 
-// quantize_file: two passes of the reference become parse-once + one GPU kernel.
+// quantize_file: two passes of the reference become parse-once + one GPU kernel.  The
+// parse and the output formatting run on host_threads() threads over ranges of whole
+// lines (the output is the ranges' text in order).
 extern "C" int di_quantize_file(const char *input_path, const char *output_path, double max_val,
                                 int32_t bits, int device, double *max_used) {
     return guard([&] {
         DI_REQUIRE(input_path, DI_EINVAL, "null argument");
-        std::string buf = read_all(input_path);
-        std::vector<std::string_view> terms;
-        std::vector<double> vals;
-        std::vector<int64_t> cu{0};
-        std::vector<std::string_view> pieces, tv;
-        int64_t line_no = 0;
+        const std::string buf = read_all(input_path);
+        const std::vector<size_t> cut = py::line_chunks(buf, 8 * host_threads());
+        const int C = (int)cut.size() - 1;
+        struct Part {
+            std::vector<std::string_view> terms;
+            std::vector<double> vals;
+            std::vector<uint32_t> cu{0};
+            std::string out;
+        };
+        std::vector<Part> P((size_t)std::max(C, 1));
         // for doc_id, line in enumerate(f): for t in line.strip().split(', '):
         //     term, score = t.strip().split(': ')         (quantize.py:21-22, :41-42)
-        py::for_each_line(buf, [&](std::string_view line) {
-            ++line_no;
-            py::split(py::strip(line), ", ", pieces);
-            for (auto t : pieces) {
-                py::split(py::strip(t), ": ", tv);
-                DI_REQUIRE(tv.size() == 2, DI_EFORMAT,
-                           "line %lld: '%.*s' is not 'term: score' (the reference raises "
-                           "ValueError)",
-                           (long long)line_no, (int)std::min<size_t>(t.size(), 200), t.data());
-                double v;
-                DI_REQUIRE(py::parse_float(tv[1], &v), DI_EFORMAT,
-                           "line %lld: could not convert '%.*s' to float", (long long)line_no,
-                           (int)std::min<size_t>(tv[1].size(), 64), tv[1].data());
-                terms.push_back(tv[0]);
-                vals.push_back(v);
-            }
-            cu.push_back((int64_t)terms.size());
+        parallel_chunks(C, [&](int64_t c, int) {
+            Part &pc = P[(size_t)c];
+            std::vector<std::string_view> pieces, tv;
+            py::for_each_line(std::string_view(buf).substr(cut[c], cut[c + 1] - cut[c]),
+                              [&](std::string_view line) {
+                py::split(py::strip(line), ", ", pieces);
+                for (auto t : pieces) {
+                    py::split(py::strip(t), ": ", tv);
+                    DI_REQUIRE(tv.size() == 2, DI_EFORMAT,
+                               "'%.*s' is not 'term: score' (the reference raises ValueError)",
+                               (int)std::min<size_t>(t.size(), 200), t.data());
+                    double v;
+                    DI_REQUIRE(py::parse_float(tv[1], &v), DI_EFORMAT,
+                               "could not convert '%.*s' to float",
+                               (int)std::min<size_t>(tv[1].size(), 64), tv[1].data());
+                    pc.terms.push_back(tv[0]);
+                    pc.vals.push_back(v);
+                }
+                pc.cu.push_back((uint32_t)pc.terms.size());
+            });
         });
-        const int64_t n = (int64_t)vals.size();
+        std::vector<int64_t> off((size_t)C + 1, 0);
+        for (int c = 0; c < C; ++c) off[(size_t)c + 1] = off[(size_t)c] + (int64_t)P[(size_t)c].vals.size();
+        const int64_t n = off[(size_t)C];
+        std::vector<double> vals((size_t)std::max<int64_t>(n, 1));
+        parallel_for(C, [&](int64_t lo, int64_t hi, int) {
+            for (int64_t c = lo; c < hi; ++c) {
+                auto &v = P[(size_t)c].vals;
+                std::copy(v.begin(), v.end(), vals.begin() + off[(size_t)c]);
+                std::vector<double>().swap(v);
+            }
+        });
         int prev = 0;
         DI_HIP(hipGetDevice(&prev));
         DI_HIP(hipSetDevice(device));
@@ -105,7 +125,7 @@ extern "C" int di_quantize_file(const char *input_path, const char *output_path,
         if (n) DI_HIP(hipMemcpy(dv.p, vals.data(), (size_t)n * 8, hipMemcpyHostToDevice));
         launch_quantize_f64(dv.as<double>(), n, max_val, bits, dq.as<int32_t>(),
                             dm.as<unsigned long long>(), nullptr);
-        std::vector<int32_t> q((size_t)n);
+        std::vector<int32_t> q((size_t)std::max<int64_t>(n, 1));
         unsigned long long mb = 0;
         if (n) DI_HIP(hipMemcpy(q.data(), dq.p, (size_t)n * 4, hipMemcpyDeviceToHost));
         DI_HIP(hipMemcpy(&mb, dm.p, 8, hipMemcpyDeviceToHost));
@@ -122,26 +142,36 @@ extern "C" int di_quantize_file(const char *input_path, const char *output_path,
             max_val = m;
         }
         if (max_used) *max_used = max_val;
-        std::string out;
-        out.reserve(buf.size());
-        char num[32];
-        for (size_t d = 0; d + 1 < cu.size(); ++d) {
-            bool first = true;
-            for (int64_t i = cu[d]; i < cu[d + 1]; ++i) {
-                if (q[(size_t)i] <= 0) continue;  // quantize.py:44
-                if (!first) out += ", ";
-                first = false;
-                out.append(terms[(size_t)i].data(), terms[(size_t)i].size());
-                out += ": ";
-                int len = std::snprintf(num, sizeof num, "%d", q[(size_t)i]);
-                out.append(num, (size_t)len);
+        parallel_for(C, [&](int64_t lo, int64_t hi, int) {
+            char num[32];
+            for (int64_t c = lo; c < hi; ++c) {
+                Part &pc = P[(size_t)c];
+                std::string &out = pc.out;
+                out.reserve(cut[c + 1] - cut[c]);
+                const int32_t *qc = q.data() + off[(size_t)c];
+                for (size_t d = 0; d + 1 < pc.cu.size(); ++d) {
+                    bool first = true;
+                    for (uint32_t i = pc.cu[d]; i < pc.cu[d + 1]; ++i) {
+                        if (qc[i] <= 0) continue;  // quantize.py:44
+                        if (!first) out += ", ";
+                        first = false;
+                        out.append(pc.terms[i].data(), pc.terms[i].size());
+                        out += ": ";
+                        const int len = std::snprintf(num, sizeof num, "%d", qc[i]);
+                        out.append(num, (size_t)len);
+                    }
+                    out += '\n';
+                }
             }
-            out += '\n';
-        }
+        });
         FILE *f = std::fopen(output_path, "wb");
         DI_REQUIRE(f, DI_EIO, "cannot create %s", output_path);
-        size_t w = out.empty() ? 0 : std::fwrite(out.data(), 1, out.size(), f);
-        int rc = std::fclose(f);
-        DI_REQUIRE(w == out.size() && rc == 0, DI_EIO, "short write to %s", output_path);
+        bool ok = true;
+        for (int c = 0; c < C; ++c) {
+            const std::string &o = P[(size_t)c].out;
+            ok = ok && (o.empty() || std::fwrite(o.data(), 1, o.size(), f) == o.size());
+        }
+        ok = (std::fclose(f) == 0) && ok;
+        DI_REQUIRE(ok, DI_EIO, "short write to %s", output_path);
     });
 }

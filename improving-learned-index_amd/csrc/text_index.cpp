@@ -4,12 +4,23 @@
 // create.py:12-55) reading the collection through DeepImpactCollection
 // (src/deep_impact/indexing/deep_impact_collection.py:6-33); output is
 // byte-identical: vocab.txt, inverted_index.idx, inverted_index.dat.
+//
+// Every pass runs on host_threads() threads: the collection is cut into ranges of
+// whole lines (parsed in parallel, doc ids = global line numbers), the vocabulary is
+// the union of per-thread term sets merged by hash partition and sorted, the postings
+// are bucketed by term with per-thread write offsets (doc order inside a term), then
+// stable-sorted by value descending per term.  The output does not depend on the
+// thread count.
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
+#include <cstring>
 #include <fstream>
+#include <functional>
 #include <string>
 #include <string_view>
 #include <unordered_map>
+#include <unordered_set>
 #include <vector>
 
 #include "di_common.h"
@@ -31,49 +42,82 @@ std::string read_file(const char *path) {
 
 struct Parsed {
     std::vector<std::string_view> term;  // per posting, doc order
-    std::vector<int64_t> val;            // int(float(text))
-    std::vector<int64_t> cu;             // per doc
+    std::vector<uint16_t> val;           // int(float(text)); 256: outside the 1-byte record
+    std::vector<uint32_t> cu;            // per doc (local)
 };
 
 // DeepImpactCollection.__getitem__: line.strip(); '' -> {}; else
 // {term: float(v) for term, v in (p.split(': ') for p in s.split(', '))}
-// (a dict: a repeated term keeps its first position and its last value).
+// (a dict: a repeated term keeps its first position and its last value).  A line is
+// taken as parsed; then the sorted hashes of its terms show whether any term repeats
+// (rare), and only then is the dict rule applied.
+inline uint64_t fnv1a(std::string_view x) {
+    uint64_t h = 0xCBF29CE484222325ull;
+    for (unsigned char c : x) h = (h ^ c) * 0x100000001B3ull;
+    return h;
+}
+
 void parse_collection(std::string_view buf, Parsed &P) {
     P.cu.push_back(0);
     std::vector<std::string_view> pairs, tv;
-    std::unordered_map<std::string_view, size_t> seen;
-    int64_t line_no = 0;
+    std::vector<std::pair<uint64_t, uint32_t>> hs;
     py::for_each_line(buf, [&](std::string_view line) {
-        ++line_no;
         std::string_view s = py::strip(line);
         if (!py::strip(s).empty()) {
             py::split(s, ", ", pairs);
-            seen.clear();
+            const size_t first = P.term.size();
             for (auto pr : pairs) {
                 py::split(pr, ": ", tv);
                 DI_REQUIRE(tv.size() == 2, DI_EFORMAT,
-                           "line %lld: '%.*s' does not split into term and value (reference "
-                           "raises ValueError)",
-                           (long long)line_no, (int)std::min<size_t>(pr.size(), 200), pr.data());
+                           "'%.*s' does not split into term and value (reference raises "
+                           "ValueError)",
+                           (int)std::min<size_t>(pr.size(), 200), pr.data());
                 double v;
                 DI_REQUIRE(py::parse_float(tv[1], &v), DI_EFORMAT,
-                           "line %lld: could not convert '%.*s' to float", (long long)line_no,
+                           "could not convert '%.*s' to float",
                            (int)std::min<size_t>(tv[1].size(), 64), tv[1].data());
                 DI_REQUIRE(!std::isnan(v) && !std::isinf(v), DI_EFORMAT,
-                           "line %lld: int() of a non-finite value", (long long)line_no);
-                int64_t iv = (int64_t)std::trunc(v);
-                auto it = seen.find(tv[0]);
-                if (it != seen.end()) {
-                    P.val[it->second] = iv;  // dict: last value wins
-                } else {
-                    seen.emplace(tv[0], P.term.size());
-                    P.term.push_back(tv[0]);
-                    P.val.push_back(iv);
+                           "int() of a non-finite value");
+                const double t = std::trunc(v);
+                // (checked on the dict's final values below: a later value of a repeated
+                // term replaces an earlier one)
+                P.term.push_back(tv[0]);
+                P.val.push_back(t >= 0.0 && t <= 255.0 ? (uint16_t)t : (uint16_t)256);
+            }
+            const size_t n = P.term.size() - first;
+            if (n > 1) {
+                hs.resize(n);
+                for (size_t i = 0; i < n; ++i) hs[i] = {fnv1a(P.term[first + i]), (uint32_t)i};
+                std::sort(hs.begin(), hs.end());
+                bool dup = false;
+                for (size_t i = 1; i < n && !dup; ++i)
+                    dup = hs[i].first == hs[i - 1].first &&
+                          P.term[first + hs[i].second] == P.term[first + hs[i - 1].second];
+                if (dup) {  // the dict: first slot, last value
+                    std::unordered_map<std::string_view, size_t> seen;
+                    size_t o = first;
+                    for (size_t i = first; i < first + n; ++i) {
+                        auto it = seen.find(P.term[i]);
+                        if (it != seen.end()) {
+                            P.val[it->second] = P.val[i];
+                        } else {
+                            seen.emplace(P.term[i], o);
+                            P.term[o] = P.term[i];
+                            P.val[o] = P.val[i];
+                            ++o;
+                        }
+                    }
+                    P.term.resize(o);
+                    P.val.resize(o);
                 }
             }
         }
-        P.cu.push_back((int64_t)P.term.size());
+        P.cu.push_back((uint32_t)P.term.size());
     });
+    for (uint16_t v : P.val)
+        DI_REQUIRE(v <= 255, DI_EFORMAT,
+                   "a value does not fit the 1-byte impact record (struct.error in the "
+                   "reference)");
 }
 
 void write_all(const std::string &path, const void *data, size_t n) {
@@ -89,65 +133,157 @@ void write_all(const std::string &path, const void *data, size_t n) {
 extern "C" int di_build_reference_index(const char *collection_path, const char *out_dir) {
     return guard([&] {
         DI_REQUIRE(collection_path && out_dir, DI_EINVAL, "null argument");
-        std::string buf = read_file(collection_path);
-        Parsed P;
-        parse_collection(buf, P);
-        const int64_t n_docs = (int64_t)P.cu.size() - 1;
+        const std::string buf = read_file(collection_path);
+        const int T = host_threads();
+        // 1. parse ranges of whole lines in parallel
+        const std::vector<size_t> cut = py::line_chunks(buf, 8 * T);
+        const int C = (int)cut.size() - 1;
+        std::vector<Parsed> P((size_t)std::max(C, 1));
+        parallel_chunks(C, [&](int64_t c, int) {
+            parse_collection(std::string_view(buf).substr(cut[c], cut[c + 1] - cut[c]),
+                             P[(size_t)c]);
+        });
+        std::vector<int64_t> doc0((size_t)C + 1, 0), occ0((size_t)C + 1, 0);
+        for (int c = 0; c < C; ++c) {
+            doc0[(size_t)c + 1] = doc0[(size_t)c] + (int64_t)P[(size_t)c].cu.size() - 1;
+            occ0[(size_t)c + 1] = occ0[(size_t)c] + (int64_t)P[(size_t)c].term.size();
+        }
+        const int64_t n_docs = doc0[(size_t)C], n_occ = occ0[(size_t)C];
         DI_REQUIRE(n_docs <= 0xFFFFFFFFll, DI_ERANGE, "more than 2^32 documents");
-        // vocab: sorted(set(terms)) -- code-point order == UTF-8 byte order
-        std::unordered_map<std::string_view, uint32_t> ids;
-        ids.reserve(P.term.size() / 8 + 16);
-        std::vector<std::string_view> vocab;
-        for (auto t : P.term)
-            if (ids.emplace(t, 0).second) vocab.push_back(t);
-        std::sort(vocab.begin(), vocab.end());
-        for (size_t i = 0; i < vocab.size(); ++i) ids[vocab[i]] = (uint32_t)i;
-        const size_t V = vocab.size();
-        // postings: per term, docs in order; stable by value descending
-        for (auto v : P.val)
-            DI_REQUIRE(v >= 0 && v <= 255, DI_EFORMAT,
-                       "value %lld does not fit the 1-byte impact record (struct.error in "
-                       "the reference)",
-                       (long long)v);
-        // bucket by term (doc order), then a stable value-descending sort per term
-        std::vector<int64_t> toff(V + 1, 0);
-        std::vector<uint32_t> tid(P.term.size());
-        for (size_t i = 0; i < P.term.size(); ++i) {
-            tid[i] = ids[P.term[i]];
-            toff[tid[i] + 1]++;
-        }
-        for (size_t t = 0; t < V; ++t) toff[t + 1] += toff[t];
-        std::vector<uint32_t> bdoc(P.term.size());
-        std::vector<uint8_t> bval(P.term.size());
-        {
-            std::vector<int64_t> cur(toff.begin(), toff.end() - 1);
-            for (int64_t d = 0; d < n_docs; ++d)
-                for (int64_t i = P.cu[d]; i < P.cu[d + 1]; ++i) {
-                    int64_t pos = cur[tid[i]]++;
-                    bdoc[pos] = (uint32_t)d;
-                    bval[pos] = (uint8_t)P.val[i];
-                }
-        }
-        std::vector<unsigned char> dat(P.term.size() * 5);
-        std::vector<int64_t> vc(257);
-        for (size_t t = 0; t < V; ++t) {
-            const int64_t a = toff[t], b = toff[t + 1];
-            std::fill(vc.begin(), vc.end(), 0);
-            for (int64_t i = a; i < b; ++i) vc[(size_t)(255 - bval[i]) + 1]++;
-            for (int c = 0; c < 256; ++c) vc[c + 1] += vc[c];
-            for (int64_t i = a; i < b; ++i) {
-                int64_t pos = a + vc[(size_t)(255 - bval[i])]++;
-                std::memcpy(&dat[(size_t)pos * 5], &bdoc[i], 4);
-                dat[(size_t)pos * 5 + 4] = bval[i];
+        // 2. vocabulary: sorted(set(terms)) -- code-point order == UTF-8 byte order.
+        // Per-thread sets over contiguous chunk ranges, merged by hash partition.
+        const std::hash<std::string_view> H;
+        std::vector<std::unordered_set<std::string_view>> tset((size_t)T);
+        parallel_for(C, [&](int64_t lo, int64_t hi, int t) {
+            auto &st = tset[(size_t)t];
+            for (int64_t c = lo; c < hi; ++c)
+                for (auto x : P[(size_t)c].term) st.insert(x);
+        });
+        std::vector<std::vector<std::string_view>> part((size_t)T);
+        parallel_for(T, [&](int64_t lo, int64_t hi, int) {
+            for (int64_t p = lo; p < hi; ++p) {
+                std::unordered_set<std::string_view> u;
+                for (auto &st : tset)
+                    for (auto x : st)
+                        if (H(x) % (size_t)T == (size_t)p) u.insert(x);
+                part[(size_t)p].assign(u.begin(), u.end());
             }
+        });
+        std::vector<std::unordered_set<std::string_view>>().swap(tset);
+        std::vector<std::string_view> vocab;
+        for (auto &pp : part) vocab.insert(vocab.end(), pp.begin(), pp.end());
+        std::sort(vocab.begin(), vocab.end());
+        const size_t V = vocab.size();
+        DI_REQUIRE(V < 0xFFFFFFFFull, DI_ERANGE, "more than 2^32 terms");
+        // id lookup: per-partition maps (built in parallel, read-only after)
+        std::vector<std::unordered_map<std::string_view, uint32_t>> idmap((size_t)T);
+        parallel_for(T, [&](int64_t lo, int64_t hi, int) {
+            for (int64_t p = lo; p < hi; ++p) idmap[(size_t)p].reserve(part[(size_t)p].size());
+        });
+        parallel_for(T, [&](int64_t lo, int64_t hi, int) {
+            for (int64_t p = lo; p < hi; ++p)
+                for (auto x : part[(size_t)p]) idmap[(size_t)p].emplace(x, 0u);
+        });
+        parallel_for((int64_t)V, [&](int64_t lo, int64_t hi, int) {
+            for (int64_t i = lo; i < hi; ++i) {
+                auto x = vocab[(size_t)i];
+                idmap[H(x) % (size_t)T].find(x)->second = (uint32_t)i;  // (own slot: no race)
+            }
+        });
+        // 3. term id of every occurrence; per-thread counts per term
+        std::vector<uint32_t> tid((size_t)std::max<int64_t>(n_occ, 1));
+        std::vector<std::vector<uint32_t>> tcnt((size_t)T);
+        parallel_for(C, [&](int64_t lo, int64_t hi, int t) {
+            auto &cnt = tcnt[(size_t)t];
+            cnt.assign(V, 0);
+            for (int64_t c = lo; c < hi; ++c) {
+                const auto &pc = P[(size_t)c];
+                for (size_t i = 0; i < pc.term.size(); ++i) {
+                    auto x = pc.term[i];
+                    const uint32_t id = idmap[H(x) % (size_t)T].find(x)->second;
+                    tid[(size_t)occ0[(size_t)c] + i] = id;
+                    cnt[id]++;
+                }
+            }
+        });
+        std::vector<std::unordered_map<std::string_view, uint32_t>>().swap(idmap);
+        // toff[t] and each thread's write offset per term (doc order inside a term:
+        // threads own ascending doc ranges)
+        std::vector<int64_t> toff(V + 1, 0);
+        std::vector<std::vector<uint32_t>> &tpos = tcnt;  // counts -> offsets in place
+        for (size_t t = 0; t < V; ++t) {
+            int64_t run = toff[t];
+            for (int th = 0; th < T; ++th) {
+                auto &v = tpos[(size_t)th];
+                if (v.empty()) continue;
+                const uint32_t c = v[t];
+                v[t] = (uint32_t)(run - toff[t]);  // offset within the term
+                run += c;
+            }
+            toff[t + 1] = run;
         }
+        std::vector<uint32_t> bdoc((size_t)std::max<int64_t>(n_occ, 1));
+        std::vector<uint8_t> bval((size_t)std::max<int64_t>(n_occ, 1));
+        parallel_for(C, [&](int64_t lo, int64_t hi, int t) {
+            auto &off = tpos[(size_t)t];
+            for (int64_t c = lo; c < hi; ++c) {
+                const auto &pc = P[(size_t)c];
+                for (size_t d = 0; d + 1 < pc.cu.size(); ++d) {
+                    const uint32_t doc = (uint32_t)(doc0[(size_t)c] + (int64_t)d);
+                    for (uint32_t i = pc.cu[d]; i < pc.cu[d + 1]; ++i) {
+                        const uint32_t id = tid[(size_t)occ0[(size_t)c] + i];
+                        const int64_t pos = toff[id] + off[id]++;
+                        bdoc[(size_t)pos] = doc;
+                        bval[(size_t)pos] = (uint8_t)pc.val[i];
+                    }
+                }
+            }
+        });
+        std::vector<std::vector<uint32_t>>().swap(tcnt);
+        std::vector<uint32_t>().swap(tid);
+        // 4. per term: stable sort by value descending (create.py:41) into the records
+        std::vector<unsigned char> dat((size_t)n_occ * 5);
+        parallel_for((int64_t)V, [&](int64_t lo, int64_t hi, int) {
+            std::vector<int64_t> vc(257);
+            std::vector<uint32_t> ord;
+            for (int64_t t = lo; t < hi; ++t) {
+                const int64_t a = toff[(size_t)t], b = toff[(size_t)t + 1];
+                if (b - a <= 32) {  // short list: stable insertion order by value desc
+                    ord.resize((size_t)(b - a));
+                    for (int64_t i = 0; i < b - a; ++i) {
+                        int64_t j = i;
+                        while (j > 0 && bval[(size_t)(a + ord[(size_t)j - 1])] < bval[(size_t)(a + i)]) {
+                            ord[(size_t)j] = ord[(size_t)j - 1];
+                            --j;
+                        }
+                        ord[(size_t)j] = (uint32_t)i;
+                    }
+                    for (int64_t i = 0; i < b - a; ++i) {
+                        const int64_t s = a + ord[(size_t)i];
+                        std::memcpy(&dat[(size_t)(a + i) * 5], &bdoc[(size_t)s], 4);
+                        dat[(size_t)(a + i) * 5 + 4] = bval[(size_t)s];
+                    }
+                    continue;
+                }
+                std::fill(vc.begin(), vc.end(), 0);
+                for (int64_t i = a; i < b; ++i) vc[(size_t)(255 - bval[(size_t)i]) + 1]++;
+                for (int c = 0; c < 256; ++c) vc[(size_t)c + 1] += vc[(size_t)c];
+                for (int64_t i = a; i < b; ++i) {
+                    const int64_t pos = a + vc[(size_t)(255 - bval[(size_t)i])]++;
+                    std::memcpy(&dat[(size_t)pos * 5], &bdoc[(size_t)i], 4);
+                    dat[(size_t)pos * 5 + 4] = bval[(size_t)i];
+                }
+            }
+        });
         std::vector<uint64_t> idx(V * 2);
         for (size_t t = 0; t < V; ++t) {
             idx[2 * t] = (uint64_t)toff[t] * 5;
             idx[2 * t + 1] = (uint64_t)toff[t + 1] * 5;
         }
         std::string vtxt;
-        vtxt.reserve(V * 8);
+        size_t vbytes = 0;
+        for (auto t : vocab) vbytes += t.size() + 1;
+        vtxt.reserve(vbytes);
         for (auto t : vocab) {
             vtxt.append(t.data(), t.size());
             vtxt += '\n';

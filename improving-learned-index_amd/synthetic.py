@@ -92,3 +92,18 @@ def synth_postings(n_docs, v_terms=200_000, seed=1234, max_terms=100, draws=200,
                                   int(draws), float(zipf_a), ptr(term_off), ptr(pdoc), ptr(pval),
                                   cap, ctypes.byref(n), ctypes.byref(m)))
     return term_off, pdoc[:n.value], pval[:n.value], m.value
+
+
+def synth_impact_tsv(path, n_docs, v_terms=200_000, seed=1234, max_terms=100, draws=200,
+                     zipf_a=1.2) -> int:
+    """The synth_postings collection as the impact TSV the index CLI writes (A9 text,
+    terms "\\u2581t<id>"), generated in the library's host code.  Returns the number of
+    (doc, term) pairs written."""
+    import ctypes
+
+    from ._lib import check, lib
+
+    n = ctypes.c_int64(0)
+    check(lib().di_synth_impact_tsv(str(path).encode(), int(n_docs), int(v_terms), int(seed),
+                                    int(max_terms), int(draws), float(zipf_a), ctypes.byref(n)))
+    return n.value

@@ -274,6 +274,12 @@ int di_synth_postings(int64_t n_docs, int32_t v_terms, uint64_t seed, int32_t ma
                       int32_t draws, double zipf_a, int64_t *term_off, uint32_t *pdoc,
                       uint8_t *pval, int64_t cap, int64_t *n_post, double *max_impact);
 
+/* The same seeded collection as the impact TSV of the index CLI (indexer.py:62-68),
+ * term id t spelled "\u2581t<t>": bench input of the quantize / index-create legs.
+ * *n_terms receives the (doc, term) pairs written. */
+int di_synth_impact_tsv(const char *path, int64_t n_docs, int32_t v_terms, uint64_t seed,
+                        int32_t max_terms, int32_t draws, double zipf_a, int64_t *n_terms);
+
 /* Decoding of a quantized-index merge key.  A query of at most DI_SHORT_QUERY_TERMS
  * known terms: score(16) | (255 - first term)(8) | its value(8) | ~doc(32).  A longer
  * one (wide key): score(20) | (4095 - first term)(12) | its value(8) | (0xFFFFFF - doc)(24).

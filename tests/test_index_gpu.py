@@ -253,10 +253,13 @@ def test_zero_values_stop_term_lists(L):
 def test_min_impact_pruning_equals_oracle_on_pruned_postings(L, synth, min_impact):
     """di_index_set_min_impact (BASELINE configs[4] sweep): scoring the postings with
     value >= 2^floor(log2 min_impact) gives exactly the oracle's ranking over those
-    postings (the first-touch tie rule unchanged); 1 restores the exact search."""
+    postings (the first-touch tie rule unchanged); 1 restores the exact search.  Short
+    queries (class prefixes, per-wave runs) and 65..200-term ones (the all-wave form:
+    whole sublists filtered by value)."""
     term_off, pdoc, pval, ora = synth
     dev = L.DeviceIndex.from_postings(term_off, pdoc, pval)
-    qs = _queries(5000, 60, seed=min_impact)
+    qs = _queries(5000, 60, seed=min_impact) + _long_queries(5000, 4, seed=min_impact, lo=65,
+                                                                hi=200)
     thr = 1 << (int(min_impact).bit_length() - 1)
     keep = pval >= thr
     cnt = np.array([int(keep[term_off[t]:term_off[t + 1]].sum()) for t in range(len(term_off) - 1)])
@@ -303,37 +306,66 @@ def test_shared_threshold_off_equals_oracle(L, synth, monkeypatch):
     off = L.DeviceIndex.from_postings(term_off, pdoc, pval)
     assert off.search(qs, 1000) == want
     monkeypatch.setenv("DI_SCORE_THRESHOLD", "1")
-    for et in ("1", "0"):  # safe early termination on / off
-        monkeypatch.setenv("DI_EARLY_TERMINATION", et)
-        on = L.DeviceIndex.from_postings(term_off, pdoc, pval)
-        assert on.search(qs, 1000) == want
-        assert on.search(qs, 7) == ora.score_ids(qs, 7, n_threads=8)
-        assert on.search(qs, 1) == ora.score_ids(qs, 1, n_threads=8)
+    on = L.DeviceIndex.from_postings(term_off, pdoc, pval)
+    assert on.search(qs, 1000) == want
+    assert on.search(qs, 7) == ora.score_ids(qs, 7, n_threads=8)
+    assert on.search(qs, 1) == ora.score_ids(qs, 1, n_threads=8)
+
+
+def test_in_kernel_setup_fallback_equals_oracle(L, synth, monkeypatch):
+    """score_blocks resolves its items' sublists itself when the item_setup_kernel
+    records would pass 2 GiB (e.g. rank --top_k 10 over 8.8 M docs); DI_PROFILE_ABLATE
+    bit 1024 forces that path here: the same exact ranking."""
+    term_off, pdoc, pval, ora = synth
+    qs = _queries(5000, 80, seed=13, long_every=10)
+    monkeypatch.setenv("DI_PROFILE_ABLATE", "1024")
+    dev = L.DeviceIndex.from_postings(term_off, pdoc, pval)
+    for k in (10, 1000):
+        assert dev.search(qs, k) == ora.score_ids(qs, k, n_threads=8)
 
 
 @pytest.fixture(scope="module")
 def million():
     """One 8-way shard of configs[2] (full MS MARCO: 8.8 M docs): 1.1 M docs, 34 LDS
-    blocks, ~100 M postings (the library's threaded generator, same distribution as
-    the 100k bench shard)."""
+    blocks, ~105 M postings, the SURVEY §8d generator with the vocabulary scaled with N
+    (V = 2 N = 2.2 M terms, ~8.7 M (term, block) entries in the sparse table)."""
     from improving_learned_index_amd import synthetic as S
 
-    term_off, pdoc, pval, _ = S.synth_postings(1_100_000, 200_000, seed=99)
+    term_off, pdoc, pval, _ = S.synth_postings(1_100_000, 2_200_000, seed=99)
     ora = oracle.Index.__new__(oracle.Index)
     ora.term_off, ora.pdoc, ora.pval = term_off, pdoc, pval
     ora.n_docs = 1_100_000
     return term_off, pdoc, pval, ora
 
 
-@pytest.mark.parametrize("k,et", [(10, "1"), (1000, "1"), (1000, "0")])
-def test_million_doc_shard_matches_oracle(L, million, k, et, monkeypatch):
-    """34 blocks, shared threshold on; safe early termination (configs[4]) on and off:
-    the exact top-k either way."""
+@pytest.mark.parametrize("k", [10, 1000])
+def test_million_doc_shard_matches_oracle(L, million, k):
+    """34 blocks, scaled vocabulary, shared threshold on: the exact top-k (dev.small-
+    shaped queries, longer ones, and queries of 65..300 terms: the all-wave form and
+    the long-query kernel)."""
     from improving_learned_index_amd import synthetic as S
 
     term_off, pdoc, pval, ora = million
-    monkeypatch.setenv("DI_EARLY_TERMINATION", et)
     dev = L.DeviceIndex.from_postings(term_off, pdoc, pval, 0, ora.n_docs)
     assert dev.info()["n_blocks"] == 34
-    qs = S.msmarco_like_queries(24, 200_000, seed=k) + _queries(200_000, 8, seed=k)
+    qs = S.msmarco_like_queries(24, 2_200_000, seed=k) + _queries(2_200_000, 8, seed=k) + \
+        _long_queries(3000, 3, seed=k, lo=65, hi=300)
     assert dev.search(qs, k) == ora.score_ids(qs, k, n_threads=16)
+
+
+def test_full_msmarco_scaled_vocab_on_one_gpu(L):
+    """configs[2] at full size on one GPU: 8.8 M docs (269 blocks), the vocabulary
+    scaled with N (V = 2 N = 17.6 M terms: a dense term x block table would be 4.7 G
+    entries; the sparse one holds only the nonempty (term, block) pairs), ~0.9 G
+    postings.  It loads, and dev.small-shaped queries equal the oracle."""
+    from improving_learned_index_amd import synthetic as S
+
+    n, v = 8_800_000, 17_600_000
+    term_off, pdoc, pval, _ = S.synth_postings(n, v, seed=7)
+    dev = L.DeviceIndex.from_postings(term_off, pdoc, pval, 0, n)
+    info = dev.info()
+    assert info["n_blocks"] == 269 and info["n_terms"] == v and info["n_docs"] == n
+    ora = oracle.Index.__new__(oracle.Index)
+    ora.term_off, ora.pdoc, ora.pval, ora.n_docs = term_off, pdoc, pval, n
+    qs = S.msmarco_like_queries(16, v, seed=3)
+    assert dev.search(qs, 1000) == ora.score_ids(qs, 1000, n_threads=16)
