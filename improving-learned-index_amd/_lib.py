@@ -93,7 +93,11 @@ def lib():
                 f"{LIB_PATH} is missing: the HIP extension must be built "
                 f"(python -c 'import __graft_entry__; __graft_entry__.build()')")
         L = ctypes.CDLL(str(LIB_PATH))
+        # (DI_LIB_ALLOW_MISSING=1: an older build for an A/B run, tools/ab_scorer.sh)
+        allow_missing = os.environ.get("DI_LIB_ALLOW_MISSING") == "1"
         for name, (res, args) in SIGNATURES.items():
+            if allow_missing and not hasattr(L, name):
+                continue
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args

@@ -12,14 +12,15 @@
 //   (term, block) sublists (SubIndex).
 //
 // score_blocks: one 1024-thread workgroup per (query, block) item, persistent.  The
-//   block's accumulators live in LDS: packed 16-bit scores (LDS atomic adds, no
-//   return) and 16-bit first-touch keys (plain stores, terms applied in reverse query
-//   order so the first term's key is the last written).  A doc's word
+//   block's 32768 accumulators live in LDS (128 KiB), one word per doc
 //   score(16) | (255 - j)(8) | v_j(8)  (j = the first query term touching it, v_j its
-//   value there) orders docs exactly like the reference -- score descending, then
-//   first-touch order (term order, then impact desc inside that term's list, then doc
-//   asc).  Selection: a per-query threshold shared across blocks, a 4096-bin score
-//   histogram (<= 16 query terms) or a block-wide radix select.
+//   value there): comparing words orders docs exactly like the reference -- score
+//   descending, then first-touch order (term order, then impact desc inside that
+//   term's list, then doc asc).  Terms are applied in query order; a doc occurs once
+//   per term and is updated by one wave (per-wave layout) or between term barriers, so
+//   a plain LDS read-modify-write is race free.  Selection: a per-query threshold
+//   shared across blocks, a 4096-bin score histogram (<= 16 query terms) or a
+//   block-wide radix select.
 // score_long: queries of more than 256 terms (64-bit words, wide keys).
 // merge_topk: one workgroup per query selects the <= NB*k block candidates by the
 //   64-bit key  word(32) | ~doc(32)  and writes doc/score/key.
@@ -68,33 +69,11 @@ constexpr int LH_HELD = DI_MAX_TOPK / SC_THREADS;    // 4
 static_assert(MAX_BLOCK_DOCS <= 2 * LH_DOCS, "two halves cover a block");
 static_assert(LONG_TERMS <= 4096, "12-bit first-touch index");
 
-// Accumulators of one block (LDS, from address 0):
-//   sc[w]  packed 16-bit scores, doc 2w in the low half, 2w + 1 in the high half
-//          (a score is at most 255 x 256 < 2^16: no carry between the halves), then
-//          one dummy word per lane;
-//   ft[d]  the doc's first-touch key (255 - j) << 8 | v_j (j = the first query term
-//          touching it, v_j its value there), then two dummy slots per lane.
-// The scatter never reads them: a posting is ds_add_u32 (v << 16 (d & 1)) to sc[d / 2]
-// plus a plain ds_write_b16 of its term's key to ft[d], with the terms applied in
-// REVERSE query order -- the last write is the first term's, and a doc's writes all
-// come from one wave in program order (the per-wave layout) or from terms separated by
-// barriers (all-wave form).  No load -> read -> write chain per posting.
-// The selection works on the scores and reads a key only for what it emits or ranks:
-//   word(d) = score(16) | (255 - j)(8) | v_j(8)
-// orders docs exactly like the reference (score desc, then first touch: term order,
-// then the term list's value-desc / doc-asc order).
-constexpr int SC_WORDS = MAX_BLOCK_DOCS / 2 + 64;
-constexpr int FT_SLOTS = MAX_BLOCK_DOCS + 128;
-constexpr uint32_t FT_BASE = SC_WORDS * 4;  // LDS byte address of ft[0]
-
 struct ScoreShared {
-    union {
-        struct {
-            uint32_t sc[SC_WORDS];
-            uint16_t ft[FT_SLOTS];
-        } a;
-        uint64_t w64[LH_DOCS];  // long-query items: the 64-bit words of a half block
-    } acc;
+    // the block's words score(16) | (255 - j)(8) | v_j(8) (j = the first query term
+    // touching the doc, v_j its value there), + 64 per-lane dummy words; a long-query
+    // item uses the array as LH_DOCS 64-bit words (score_long_item)
+    uint32_t acc[MAX_BLOCK_DOCS + 64];
     union {
         RadixScratch<SC_WAVES> rs;      // general radix path
         uint32_t hist[HIST_BINS + 64];  // fast path: score histogram (+ spare bins), then the tie list
@@ -112,54 +91,12 @@ struct ScoreShared {
     uint32_t lmask[WTERMS / 32];   // terms (j < WTERMS) with a per-wave layout in this block
     uint32_t wtab[WTERMS][WSEG];   // their per-wave runs: start << 16 | end (in the sublist)
 };
-static_assert(offsetof(ScoreShared, acc) == 0 && sizeof(ScoreShared().acc.a) ==
-                  SC_WORDS * 4 + FT_SLOTS * 2, "accumulator layout");
+static_assert(offsetof(ScoreShared, acc) == 0, "accumulators at LDS address 0");
 static_assert(sizeof(ScoreShared().acc) >= LH_DOCS * sizeof(uint64_t), "half-block words fit");
 static_assert(sizeof(RadixScratch<SC_WAVES>) >= (HIST_BINS + 64) * 4,
               "histogram (+ 64 spare bins) overlays the radix scratch");
 static_assert(sizeof(ScoreShared().wtab) >= SC_THREADS * 4, "score_long_kernel's query list");
 
-__device__ __forceinline__ uint32_t score_of(const ScoreShared &sh, int idx) {
-    return (sh.acc.a.sc[idx >> 1] >> ((idx & 1) << 4)) & 0xFFFFu;
-}
-__device__ __forceinline__ uint32_t word_at(const ScoreShared &sh, int idx) {
-    return (score_of(sh, idx) << 16) | sh.acc.a.ft[idx];
-}
-
-// Sweep of the block's scores: f(s, idx) for idx < round4(n_local), 4 consecutive docs
-// per lane per ds_read_b64 (lane-consecutive: conflict-free), 4 reads in flight before
-// any is used.  Scores past the zeroed range come as 0; f runs in wave-uniform control
-// flow (it may ballot).
-template <class F>
-__device__ __forceinline__ void sweep_scores(const ScoreShared &sh, int n_local, int tid, F f) {
-    const uint2 *s2 = reinterpret_cast<const uint2 *>(sh.acc.a.sc);
-    const int n4 = (n_local + 3) >> 2;
-    constexpr int G = 4;
-    for (int i0 = 0; i0 < SC_PER_THREAD / 4; i0 += G) {
-        if (i0 * SC_THREADS >= n4) break;  // (uniform)
-        uint2 x[G];
-#pragma unroll
-        for (int i = 0; i < G; ++i) {
-            // q4 < 8192 always lies inside the array: load unconditionally, then drop
-            // what lies past the zeroed range
-            const int q4 = (i0 + i) * SC_THREADS + tid;
-            const uint2 y = s2[q4];
-            x[i].x = q4 < n4 ? y.x : 0u;
-            x[i].y = q4 < n4 ? y.y : 0u;
-        }
-#pragma unroll
-        for (int i = 0; i < G; ++i) {
-            const int base = 4 * ((i0 + i) * SC_THREADS + tid);
-            f(x[i].x & 0xFFFFu, base);
-            f(x[i].x >> 16, base + 1);
-            f(x[i].y & 0xFFFFu, base + 2);
-            f(x[i].y >> 16, base + 3);
-        }
-    }
-}
-
-// One radix pass over the block's full words (i-major: lanes read consecutive docs).
-// KeyF: word,index -> key;  Pred: word,index,key -> bool.
 template <class KeyF, class Pred>
 __device__ __forceinline__ void score_radix_pass(ScoreShared &sh, int n_local, int shift,
                                                  uint32_t need, KeyF key, Pred pred) {
@@ -170,8 +107,7 @@ __device__ __forceinline__ void score_radix_pass(ScoreShared &sh, int n_local, i
     for (int i = 0; i < SC_PER_THREAD; ++i) {
         int idx = i * SC_THREADS + threadIdx.x;
         if (idx < n_local) {
-            const uint32_t s = score_of(sh, idx);
-            const uint32_t w = s ? (s << 16) | sh.acc.a.ft[idx] : 0u;
+            uint32_t w = sh.acc[idx];
             uint32_t kk = key(w, idx);
             if (pred(w, idx, kk)) rl.add(sh.u.rs, (kk >> shift) & 255u);
         }
@@ -181,14 +117,54 @@ __device__ __forceinline__ void score_radix_pass(ScoreShared &sh, int n_local, i
     radix_pick<SC_THREADS, SC_WAVES>(sh.u.rs, need);
 }
 
-// Block-wide stable compaction over the scores into one list: cls(s, idx) -> take?
-// One counting sweep, one exclusive block scan of the per-thread counts, one writing
-// sweep calling out(pos, s, idx) -- no atomics.  Returns the total.  Ends with a barrier.
-template <class Cls, class Out>
-__device__ __forceinline__ uint32_t compact_scores(ScoreShared &sh, int n_local, int tid, Cls cls,
-                                                   Out out) {
+// Sweep of the block's accumulator words: f(w, idx) for idx < round4(n_local), 4
+// consecutive words per lane per ds_read_b128, 4 reads in flight before any is
+// used (a read-then-use loop is LDS-latency bound).  Words past the zeroed range
+// come as 0; f runs in wave-uniform control flow (it may ballot).
+template <class F>
+__device__ __forceinline__ void sweep_words(const uint32_t *acc, int n_local, int tid, F f) {
+    const uint4 *a4 = reinterpret_cast<const uint4 *>(acc);
+    const int n4 = (n_local + 3) >> 2;
+    constexpr int G = 4;  // uint4 reads in flight per lane
+    for (int i0 = 0; i0 < SC_PER_THREAD / 4; i0 += G) {
+        if (i0 * SC_THREADS >= n4) break;  // (uniform)
+        uint4 x[G];
+#pragma unroll
+        for (int i = 0; i < G; ++i) {
+            // q4 < 8192 always lies inside the array: load unconditionally (no branch),
+            // then drop what lies past the zeroed range
+            const int q4 = (i0 + i) * SC_THREADS + tid;
+            const uint4 y = a4[q4];
+            x[i].x = q4 < n4 ? y.x : 0u;
+            x[i].y = q4 < n4 ? y.y : 0u;
+            x[i].z = q4 < n4 ? y.z : 0u;
+            x[i].w = q4 < n4 ? y.w : 0u;
+        }
+#pragma unroll
+        for (int i = 0; i < G; ++i) {
+            const int base = 4 * ((i0 + i) * SC_THREADS + tid);
+            f(x[i].x, base);
+            f(x[i].y, base + 1);
+            f(x[i].z, base + 2);
+            f(x[i].w, base + 3);
+        }
+    }
+}
+
+// Block-wide stable compaction over the accumulator words into two lists:
+// cls(w, idx) -> bit 0: list A, bit 1: list B.  One counting sweep, one exclusive
+// block scan of the packed per-thread counts, one writing sweep calling
+// out(list, pos, w, idx) -- no atomics.  Returns the packed totals (A | B << 16;
+// each list holds at most 32768).  Ends with a barrier.
+template <class Cls, class Out, class St = void (*)(int)>
+__device__ __forceinline__ uint32_t compact_words(ScoreShared &sh, int n_local, int tid, Cls cls,
+                                                  Out out, St st = nullptr) {
     uint32_t cnt = 0;
-    sweep_scores(sh, n_local, tid, [&](uint32_t s, int idx) { cnt += cls(s, idx) ? 1u : 0u; });
+    sweep_words(sh.acc, n_local, tid, [&](uint32_t w, int idx) {
+        const uint32_t c = cls(w, idx);
+        cnt += (c & 1u) + ((c & 2u) << 15);
+    });
+    if constexpr (!std::is_same<St, void (*)(int)>::value) st(6);
     const int lane = tid & 63, wave = tid >> 6;
     const uint32_t incl = wave_prefix_sum(cnt);
     if (lane == 63) sh.wsum[wave] = incl;
@@ -199,10 +175,13 @@ __device__ __forceinline__ uint32_t compact_scores(ScoreShared &sh, int n_local,
         if (w2 < wave) base += x;
         total += x;
     }
-    if (cnt)  // (most lanes emit nothing: skip their second sweep)
-        sweep_scores(sh, n_local, tid, [&](uint32_t s, int idx) {
-            if (cls(s, idx)) out(base++, s, idx);
-        });
+    uint32_t pa = base & 0xFFFFu, pb = base >> 16;
+    if constexpr (!std::is_same<St, void (*)(int)>::value) st(7);
+    sweep_words(sh.acc, n_local, tid, [&](uint32_t w, int idx) {
+        const uint32_t c = cls(w, idx);
+        if (c & 1u) out(0, pa++, w, idx);
+        if (c & 2u) out(1, pb++, w, idx);
+    });
     __syncthreads();
     return total;
 }
@@ -222,13 +201,16 @@ __device__ __forceinline__ bool wave_append(bool take, uint32_t *cursor, uint32_
 }
 
 // Device posting words are ((doc_in_block << 8) | value) XOR POST_X.  A buffer load
-// past the descriptor's range returns 0, which decodes to doc MAX_BLOCK_DOCS with value
-// 0: the padding lanes of a round go to their lane's dummy accumulators.
+// past the descriptor's range returns 0, which decodes to doc MAX_BLOCK_DOCS -- the
+// dummy accumulator word after the block -- with value 0: the padding lanes of a
+// round need no clamp, no select and no branch (their update lands in the dummy).
 constexpr uint32_t POST_X = (uint32_t)MAX_BLOCK_DOCS << 8;
 
-// One scatter round's loads: postings p[0 .. min(avail, UU * NT)) (lane-consecutive,
-// UU per lane; p and avail wave-uniform), buffer loads bounds-checked by the hardware
-// with a 32-bit lane offset.
+// One scatter round over postings p[0 .. min(avail, UU * SC_THREADS)) (lane-
+// consecutive, UU per lane; p and avail wave-uniform): all loads first -- buffer loads
+// bounds-checked by the hardware, a 32-bit lane offset and no per-posting address
+// arithmetic -- then the LDS reads, then the writes.  A doc occurs once per term, so
+// the read-modify-write needs no atomics.
 template <int UU, int NT = SC_THREADS>
 __device__ __forceinline__ void scatter_load(const uint32_t *p, int64_t avail, int tid,
                                              uint32_t (&cur)[UU]) {
@@ -243,47 +225,69 @@ __device__ __forceinline__ void scatter_load(const uint32_t *p, int64_t avail, i
     for (int u = 0; u < UU; ++u)
         cur[u] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, (tid + u * NT) * 4, 0, 0);
 }
+// The word update: touched w + (v << 16), first touch (v << 16) | first_bits | v --
+// both one 24-bit multiply-add (v < 256, first_bits = (255 - j) << 8: no carries).
+__device__ __forceinline__ uint32_t word_update(uint32_t w, uint32_t v, uint32_t first_bits) {
+    const uint32_t t = __umul24(v, 0x10000u) + w;
+    const uint32_t f = __umul24(v, 0x10001u) + first_bits;
+    return w ? t : f;
+}
 
-// The round's LDS updates: per posting one ds_add_u32 of its value into its doc's half
-// of sc and one ds_write_b16 of the term's key | value into ft -- no return values, so
-// a wave issues them back to back.  Docs outside [dlo, dlo + dn) (OWN: another wave's
-// docs; and the padding lanes' doc MAX_BLOCK_DOCS) update the lane's dummies.  (sc is
-// the first member of the kernel's only LDS object, the dynamic segment at LDS address
-// 0: score_blocks_kernel checks that once.)
-// FILT: only values >= vmin (impact pruning over a whole sublist, see score_item).
-// MODE (profiling A/B only, results wrong): 1 no key store, 2 read + write instead of
-// the atomic add (racy), 3 both.
-template <int UU, bool FILT = false, int MODE = 0>
-__device__ __forceinline__ void scatter_apply(const uint32_t (&cur)[UU], uint32_t key,
-                                              uint32_t dlo, uint32_t dn, uint32_t dummy_sc,
-                                              uint32_t dummy_ft, uint32_t vmin = 0) {
-    uint32_t a_sc[UU], a_ft[UU], inc[UU], kv[UU];
+// FILT (the all-wave form under impact pruning): postings below vmin update the lane's
+// dummy word instead.
+template <int UU, bool FILT = false>
+__device__ __forceinline__ void scatter_apply(uint32_t *acc, const uint32_t (&cur)[UU],
+                                              uint32_t first_bits, uint32_t vmin = 0) {
+    // LDS byte addresses formed here and the accesses in inline asm (the compiler's own
+    // form adds the array's zero base once more per posting); the reads are retired by
+    // the explicit wait, the writes by the caller's term barrier / final wait.
+    // (acc is the first member of the kernel's only LDS object, the dynamic segment at
+    // LDS address 0: score_blocks_kernel checks that once)
+    (void)acc;
+    uint32_t w[UU], a[UU];
 #pragma unroll
     for (int u = 0; u < UU; ++u) {
-        const uint32_t x = cur[u] ^ POST_X;
-        const uint32_t d = x >> 8, v = x & 255u;
-        const bool ok = d - dlo < dn && (!FILT || v >= vmin);
-        a_sc[u] = ok ? (d >> 1) << 2 : dummy_sc;
-        a_ft[u] = ok ? FT_BASE + (d << 1) : dummy_ft;
-        inc[u] = v << ((d & 1u) << 4);
-        kv[u] = key | v;
-        if constexpr (!(MODE & 2))
-            asm volatile("ds_add_u32 %0, %1" ::"v"(a_sc[u]), "v"(inc[u]) : "memory");
-        if constexpr (!(MODE & 1))
-            asm volatile("ds_write_b16 %0, %1" ::"v"(a_ft[u]), "v"(kv[u]) : "memory");
+        a[u] = ((cur[u] ^ POST_X) >> 8) << 2;
+        if constexpr (FILT)
+            a[u] = (cur[u] & 255u) >= vmin ? a[u] : (uint32_t)(MAX_BLOCK_DOCS + lane_id()) << 2;
+        asm volatile("ds_read_b32 %0, %1" : "=v"(w[u]) : "v"(a[u]) : "memory");
     }
-    if constexpr ((MODE & 2) != 0) {
-        uint32_t w[UU];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    // the compiler sees the asm reads' results as ready at once: redefine them after
+    // the wait, and fence the scheduler, so that no use is hoisted above it
 #pragma unroll
-        for (int u = 0; u < UU; ++u)
-            asm volatile("ds_read_b32 %0, %1" : "=v"(w[u]) : "v"(a_sc[u]) : "memory");
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    for (int u = 0; u < UU; ++u) asm volatile("" : "+v"(w[u]));
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int u = 0; u < UU; ++u) asm volatile("" : "+v"(w[u]));
-        __builtin_amdgcn_sched_barrier(0);
+    for (int u = 0; u < UU; ++u) {
+        const uint32_t v = cur[u] & 255u;
+        asm volatile("ds_write_b32 %0, %1" ::"v"(a[u]), "v"(word_update(w[u], v, first_bits))
+                     : "memory");
+    }
+}
+
+// scatter_apply restricted to the docs [dlo, dlo + dn) of one wave (a short term, whose
+// sublist every wave reads in full): the other postings (and the padding) update a
+// per-lane dummy word past the block instead.
+template <int UU>
+__device__ __forceinline__ void scatter_apply_own(const uint32_t (&cur)[UU], uint32_t first_bits,
+                                                  uint32_t dlo, uint32_t dn, uint32_t dummy) {
+    uint32_t w[UU], a[UU];
 #pragma unroll
-        for (int u = 0; u < UU; ++u)
-            asm volatile("ds_write_b32 %0, %1" ::"v"(a_sc[u]), "v"(w[u] + inc[u]) : "memory");
+    for (int u = 0; u < UU; ++u) {
+        const uint32_t d = (cur[u] ^ POST_X) >> 8;
+        a[u] = (d - dlo < dn) ? d << 2 : dummy;
+        asm volatile("ds_read_b32 %0, %1" : "=v"(w[u]) : "v"(a[u]) : "memory");
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int u = 0; u < UU; ++u) asm volatile("" : "+v"(w[u]));
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int u = 0; u < UU; ++u) {
+        const uint32_t v = cur[u] & 255u;
+        asm volatile("ds_write_b32 %0, %1" ::"v"(a[u]), "v"(word_update(w[u], v, first_bits))
+                     : "memory");
     }
 }
 
@@ -397,7 +401,7 @@ __device__ __forceinline__ void score_long_item(
     int min_cls, int nb, int block_docs, int64_t n_terms, uint32_t n_docs, uint32_t doc_lo,
     const uint32_t *__restrict__ q_terms, const int32_t *__restrict__ cu_q, int k,
     uint64_t *__restrict__ ck, int32_t *__restrict__ cn) {
-    uint64_t *acc = sh.acc.w64;
+    uint64_t *acc = reinterpret_cast<uint64_t *>(sh.acc);
     int64_t *lo = sh.v.bounds[0], *hi = sh.v.bounds[1];
     const int tid = threadIdx.x;
     const int64_t block_first = (int64_t)b * block_docs;
@@ -528,9 +532,9 @@ __device__ __forceinline__ void score_long_item(
 // One work item = (query q, doc block b): accumulate, select the block's top-k.
 __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
                                            const uint32_t *__restrict__ post, const SubIndex &si,
-                                           int min_cls, int nb, int block_docs, int64_t n_terms,
-                                           uint32_t n_docs, uint32_t doc_lo,
-                                           const uint32_t *__restrict__ q_terms,
+                                           int min_cls, int nb,
+                                           int block_docs, int64_t n_terms, uint32_t n_docs,
+                                           uint32_t doc_lo, const uint32_t *__restrict__ q_terms,
                                            const int32_t *__restrict__ cu_q, int k,
                                            uint64_t *__restrict__ cand_key,
                                            int32_t *__restrict__ cand_n,
@@ -579,32 +583,29 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
     }
     __syncthreads();
 
-    // per-wave form (every term applied by each wave to its own docs: no barriers)
+    // per-wave form (at most WTERMS terms): every term applied by each wave to its own
+    // docs -- long terms over their per-wave runs, short ones read in full by every wave
+    // -- so no term needs a barrier; longer queries: the all-wave form, a barrier per term
     const bool wl = nt <= WTERMS;
     // The query's shared threshold histogram (qhist, below) is copied by LDS-DMA into
     // the selection histogram (idle until the selection) here, so its round trip
     // overlaps the scatter and the selection reads it from LDS; the fast selection
     // path zeroes the histogram itself when it runs.
     uint32_t *qh = qhist ? qhist + (int64_t)q * QH_BINS : nullptr;
+    const bool qpre = qh != nullptr;
     static_assert(QH_BINS == 4 * SC_THREADS && QH_BINS <= HIST_BINS, "qhist prefetch");
-    if (qh) {
+    if (qpre) {
         typedef __attribute__((address_space(3))) void lds_void;
         __builtin_amdgcn_global_load_lds((const void *)(qh + 4 * tid),
                                          (lds_void *)(sh.u.hist + wave * 256), 16, 0, 0);
     }
     // zeroing of the accumulators (and the fast path's histogram): LDS stores only,
-    // placed where the setup's global loads are in flight.  Scores and keys up to
-    // round4(n_local) docs (the sweeps' range).
-    const int n4z = (n_local + 3) >> 2;
+    // placed where the setup's global loads are in flight
     auto zero = [&]() {
-        uint4 *s4 = reinterpret_cast<uint4 *>(sh.acc.a.sc);
-        uint4 *f4 = reinterpret_cast<uint4 *>(sh.acc.a.ft);
-        const int nz = (n4z + 1) >> 1;  // uint4 per array: 8 scores / 8 keys each
-        for (int i = tid; i < nz; i += SC_THREADS) {
-            s4[i] = make_uint4(0, 0, 0, 0);
-            f4[i] = make_uint4(0, 0, 0, 0);
-        }
-        if (fast && !qh) reinterpret_cast<uint4 *>(sh.u.hist)[tid] = make_uint4(0, 0, 0, 0);
+        uint4 *a4 = reinterpret_cast<uint4 *>(sh.acc);
+        const int n4 = (n_local + 3) >> 2;
+        for (int i = tid; i < n4; i += SC_THREADS) a4[i] = make_uint4(0, 0, 0, 0);
+        if (fast && !qpre) reinterpret_cast<uint4 *>(sh.u.hist)[tid] = make_uint4(0, 0, 0, 0);
         // (the 64 spare bins past them are written, never read: no zeroing needed)
     };
     if (wl && ir != nullptr) {
@@ -670,7 +671,7 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
         }
     } else {
         // all-wave form: whole sublists (a long one is laid out per wave segment, so its
-        // class prefix is not one range); impact pruning filters by value (FILT below)
+        // class prefix is not one range); impact pruning filters by value (vmin below)
         for (int j = tid; j < nt; j += SC_THREADS) {
             const uint32_t t = q_terms[q0 + j];
             if (t >= n_terms) {
@@ -697,10 +698,19 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
     // >= s: at least k docs score >= s, so the final k-th score is >= s.  A stale
     // (smaller) count still gives a valid lower bound.  Block-wide (barriers).
     auto read_tq = [&]() -> uint32_t {
-        // thread t: bins 4t..4t+3 (the LDS copy made at the item's start)
-        const uint4 h = reinterpret_cast<const uint4 *>(sh.u.hist)[tid];
-        const uint32_t hv[4] = {h.x, h.y, h.z, h.w};
-        const uint32_t c = h.x + h.y + h.z + h.w;
+        // thread t: bins 4t..4t+3 (relaxed atomic loads: other CUs add to them; or the
+        // LDS copy made at the item's start)
+        uint32_t hv[4], c = 0;
+        if (qpre) {
+            const uint4 h = reinterpret_cast<const uint4 *>(sh.u.hist)[tid];
+            hv[0] = h.x, hv[1] = h.y, hv[2] = h.z, hv[3] = h.w;
+            c = h.x + h.y + h.z + h.w;
+        } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                c += (hv[e] = __hip_atomic_load(&qh[4 * tid + e], __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT));
+        }
         uint32_t sfx = wave_suffix_sum(c);
         if (lane == 0) sh.wsum[wave] = sfx;
         if (tid == 0) sh.tq = 0;
@@ -721,104 +731,126 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
         __syncthreads();  // (wsum / tq are reused)
         return r;
     };
-    // ---- scatter: terms in REVERSE query order (the last key written is the first
-    // term's) ----------------------------------------------------------------------
-    // Per-wave form: a long term (per-wave layout) is read by each wave over its own
-    // run; a short one (< WLONG_MIN postings in the block) is read in full by every wave,
-    // which applies the postings of its own docs.  No other wave touches a wave's docs,
-    // so no term needs a barrier.  Rounds of 16 postings per lane while more than 512
-    // remain, then 8 / 4 / 1.
-    // All-wave form (more than WTERMS terms): the block's 1024 lanes split each term's
-    // sublist, rounds of 16 postings per lane while 16 k remain, then 4, then 1; a
-    // barrier between terms (the key writes of term j must land after those of j + 1).
+    // ---- scatter: terms in query order, barrier between terms -------------
+    // A term's sublist goes in rounds of 16 postings per lane while 16 k remain, then
+    // 4 per lane while more than 1 k remain, then 1: a short tail does not pay for a
+    // full round of issue (loads, LDS reads and writes of masked lanes).  Each round
+    // has all its loads in flight before any is applied; the 16 waves of the CU
+    // overlap one another's load latency with their LDS work.
+    // The last round of a term also loads the next term's first 4 k postings, before
+    // the term barrier (a raw one: LDS writes retired, loads left in flight), so the
+    // barrier does not expose a load round trip per term.
+    // A long term (per-wave layout) is scattered by each wave over its own doc segment,
+    // rounds of up to 16 postings per lane: no other wave touches those docs, so a run
+    // of long terms needs no barrier between its terms, only at its ends.
+    uint32_t pre[4];
+    bool have_pre = false;
+    auto is_long = [&](int j) { return wl && ((sh.lmask[j >> 5] >> (j & 31)) & 1u); };
     const uint32_t wseg = ((uint32_t)block_docs + WSEG - 1) / WSEG;
     const uint32_t wdlo = (uint32_t)wave * wseg;
-    const uint32_t wdn = min(wseg, (uint32_t)MAX_BLOCK_DOCS - min(wdlo, (uint32_t)MAX_BLOCK_DOCS));
-    const uint32_t dummy_sc = (uint32_t)(MAX_BLOCK_DOCS / 2 + lane) << 2;
-    const uint32_t dummy_ft = FT_BASE + ((uint32_t)(MAX_BLOCK_DOCS + 2 * lane) << 1);
-    auto is_long = [&](int j) { return wl && ((sh.lmask[j >> 5] >> (j & 31)) & 1u); };
-    if (!(ablate & 1)) {  // ablate bit 0: skip (profiling)
-        auto per_wave = [&](auto mode) {
-            constexpr int M = decltype(mode)::value;
-            for (int j = nt - 1; j >= 0; --j) {
-                const uint32_t key = (uint32_t)(255 - j) << 8;
-                int64_t pos = lo[j], end = hi[j];
-                if (is_long(j)) {
-                    const uint32_t se = sh.wtab[j][wave];
-                    pos = lo[j] + (se >> 16);
-                    end = lo[j] + (se & 0xFFFFu);
-                }
-                while (pos < end) {
-                    const int64_t rem = end - pos;
-                    if (rem > 8 * 64) {
-                        uint32_t r[16];
-                        scatter_load<16, 64>(post + pos, rem, lane, r);
-                        scatter_apply<16, false, M>(r, key, wdlo, wdn, dummy_sc, dummy_ft);
-                        pos += 16 * 64;
-                    } else if (rem > 4 * 64) {
-                        uint32_t r[8];
-                        scatter_load<8, 64>(post + pos, rem, lane, r);
-                        scatter_apply<8, false, M>(r, key, wdlo, wdn, dummy_sc, dummy_ft);
-                        pos = end;
-                    } else if (rem > 64) {
-                        uint32_t r[4];
-                        scatter_load<4, 64>(post + pos, rem, lane, r);
-                        scatter_apply<4, false, M>(r, key, wdlo, wdn, dummy_sc, dummy_ft);
-                        pos = end;
-                    } else {
-                        uint32_t r[1];
-                        scatter_load<1, 64>(post + pos, rem, lane, r);
-                        scatter_apply<1, false, M>(r, key, wdlo, wdn, dummy_sc, dummy_ft);
-                        pos = end;
-                    }
+    const uint32_t wdn = wave == WSEG - 1 ? 0x7FFFFFFFu - wdlo : wseg;  // last: the rest
+    const uint32_t wdummy = (uint32_t)(MAX_BLOCK_DOCS + lane) << 2;
+    const uint32_t vmin = 1u << (7 - min(min_cls, 7));  // all-wave form: pruning by value
+    for (int j = (ablate & 1) ? nt : 0; j < nt; ++j) {  // ablate bit 0: skip (profiling)
+        const uint32_t first_bits = (uint32_t)(255 - j) << 8;
+        const bool lj = is_long(j);
+        if (lj) {
+            const uint32_t se = sh.wtab[j][wave];
+            int64_t pos = lo[j] + (se >> 16);
+            const int64_t end = lo[j] + (se & 0xFFFFu);
+            while (pos < end) {
+                const int64_t rem = end - pos;
+                if (rem > 8 * 64) {
+                    uint32_t r[16];
+                    scatter_load<16, 64>(post + pos, rem, lane, r);
+                    scatter_apply<16>(sh.acc, r, first_bits);
+                    pos += 16 * 64;
+                } else if (rem > 4 * 64) {
+                    uint32_t r[8];
+                    scatter_load<8, 64>(post + pos, rem, lane, r);
+                    scatter_apply<8>(sh.acc, r, first_bits);
+                    pos = end;
+                } else if (rem > 64) {
+                    uint32_t r[4];
+                    scatter_load<4, 64>(post + pos, rem, lane, r);
+                    scatter_apply<4>(sh.acc, r, first_bits);
+                    pos = end;
+                } else {
+                    uint32_t r[1];
+                    scatter_load<1, 64>(post + pos, rem, lane, r);
+                    scatter_apply<1>(sh.acc, r, first_bits);
+                    pos = end;
                 }
             }
-        };
-        if (wl) {
-            const int m = (ablate >> 11) & 3;  // profiling A/B of the update (ablate 2048 / 4096)
-            if (m == 0) per_wave(std::integral_constant<int, 0>{});
-            else if (m == 1) per_wave(std::integral_constant<int, 1>{});
-            else if (m == 2) per_wave(std::integral_constant<int, 2>{});
-            else per_wave(std::integral_constant<int, 3>{});
-        } else {
-            auto all_wave = [&](auto filt) {
-                constexpr bool F = decltype(filt)::value;
-                const uint32_t vmin = 1u << (7 - min(min_cls, 7));
-                for (int j = nt - 1; j >= 0; --j) {
-                    const uint32_t key = (uint32_t)(255 - j) << 8;
-                    for (int64_t pos = lo[j], end = hi[j]; pos < end;) {
-                        const int64_t rem = end - pos;
-                        if (rem >= 16 * SC_THREADS) {
-                            uint32_t r[16];
-                            scatter_load<16>(post + pos, rem, tid, r);
-                            scatter_apply<16, F>(r, key, 0u, (uint32_t)MAX_BLOCK_DOCS, dummy_sc,
-                                                 dummy_ft, vmin);
-                            pos += 16 * SC_THREADS;
-                        } else if (rem > SC_THREADS) {
-                            uint32_t r[4];
-                            scatter_load<4>(post + pos, rem, tid, r);
-                            scatter_apply<4, F>(r, key, 0u, (uint32_t)MAX_BLOCK_DOCS, dummy_sc,
-                                                dummy_ft, vmin);
-                            pos += 4 * SC_THREADS;
-                        } else {
-                            uint32_t r[1];
-                            scatter_load<1>(post + pos, rem, tid, r);
-                            scatter_apply<1, F>(r, key, 0u, (uint32_t)MAX_BLOCK_DOCS, dummy_sc,
-                                                dummy_ft, vmin);
-                            pos = end;
-                        }
-                    }
-                    // term boundary: this term's key writes land before the next term's
-                    if (j > 0) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-                }
-            };
-            if (min_cls < 7)
-                all_wave(std::true_type{});
-            else
-                all_wave(std::false_type{});
+            continue;
         }
+        if (wl) {
+            // a short term (< WLONG_MIN postings in the block): every wave reads the whole
+            // sublist and applies the postings of its own doc segment -- no barrier
+            for (int64_t pos = lo[j], end = hi[j]; pos < end;) {
+                const int64_t rem = end - pos;
+                if (rem > 8 * 64) {
+                    uint32_t r[16];
+                    scatter_load<16, 64>(post + pos, rem, lane, r);
+                    scatter_apply_own<16>(r, first_bits, wdlo, wdn, wdummy);
+                    pos += 16 * 64;
+                } else if (rem > 4 * 64) {
+                    uint32_t r[8];
+                    scatter_load<8, 64>(post + pos, rem, lane, r);
+                    scatter_apply_own<8>(r, first_bits, wdlo, wdn, wdummy);
+                    pos = end;
+                } else if (rem > 64) {
+                    uint32_t r[4];
+                    scatter_load<4, 64>(post + pos, rem, lane, r);
+                    scatter_apply_own<4>(r, first_bits, wdlo, wdn, wdummy);
+                    pos = end;
+                } else {
+                    uint32_t r[1];
+                    scatter_load<1, 64>(post + pos, rem, lane, r);
+                    scatter_apply_own<1>(r, first_bits, wdlo, wdn, wdummy);
+                    pos = end;
+                }
+            }
+            continue;
+        }
+        int64_t pos = lo[j];
+        const int64_t end = hi[j];
+        if (have_pre) {
+            scatter_apply<4, true>(sh.acc, pre, first_bits, vmin);
+            pos = min(end, pos + (int64_t)4 * SC_THREADS);
+            have_pre = false;
+        }
+        const bool next = j + 1 < nt && hi[j + 1] > lo[j + 1] && !is_long(j + 1);
+        auto prefetch_next = [&]() {
+            scatter_load<4>(post + lo[j + 1], hi[j + 1] - lo[j + 1], tid, pre);
+            have_pre = true;
+        };
+        while (pos < end) {
+            const int64_t rem = end - pos;
+            if (rem >= 16 * SC_THREADS) {
+                uint32_t r[16];
+                scatter_load<16>(post + pos, rem, tid, r);
+                if (rem == 16 * SC_THREADS && next) prefetch_next();
+                scatter_apply<16, true>(sh.acc, r, first_bits, vmin);
+                pos += 16 * SC_THREADS;
+            } else if (rem > SC_THREADS) {
+                uint32_t r[4];
+                scatter_load<4>(post + pos, rem, tid, r);
+                if (rem <= 4 * SC_THREADS && next) prefetch_next();
+                scatter_apply<4, true>(sh.acc, r, first_bits, vmin);
+                pos += 4 * SC_THREADS;
+            } else {
+                uint32_t r[1];
+                scatter_load<1>(post + pos, rem, tid, r);
+                if (next) prefetch_next();
+                scatter_apply<1, true>(sh.acc, r, first_bits, vmin);
+                pos = end;
+            }
+        }
+        // term boundary: this term's LDS writes land before any wave reads the next
+        if (j + 1 < nt) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     }
-    // the asm LDS updates; the threshold histogram's LDS-DMA copy
+    // the asm LDS writes; the threshold histogram's LDS-DMA copy
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __syncthreads();
 
@@ -828,11 +860,12 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
         return;
     }
     const uint64_t doc_base = (uint64_t)doc_lo + (uint64_t)block_first;
-    // Candidates are staged in the unused tail of the score array when they fit there
-    // and copied out coalesced (a lane-scattered 8-byte store per candidate slot costs
-    // a store instruction per slot and wave); else they go straight out.
-    uint64_t *stage = reinterpret_cast<uint64_t *>(sh.acc.a.sc + 2 * n4z);
-    const bool staged = 2 * k <= MAX_BLOCK_DOCS / 2 - 2 * n4z;
+    // Candidates are staged in the unused tail of the accumulator array when they fit
+    // there and copied out coalesced (a lane-scattered 8-byte store per candidate slot
+    // costs a store instruction per slot and wave); else they go straight out.
+    const int n4z = (n_local + 3) >> 2;
+    uint64_t *stage = reinterpret_cast<uint64_t *>(sh.acc + 4 * n4z);
+    const bool staged = 2 * k <= MAX_BLOCK_DOCS - 4 * n4z;
     auto cand = [&](uint32_t pos, uint32_t w, int idx) {
         const uint32_t doc = (uint32_t)(doc_base + (uint64_t)idx);
         const uint64_t key = ((uint64_t)w << 32) | (uint64_t)(0xFFFFFFFFu - doc);
@@ -853,11 +886,12 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
         }
     };
     auto emit_all_touched = [&]() {
-        const uint32_t n = compact_scores(
-            sh, n_local, tid, [](uint32_t s, int) { return s != 0; },
-            [&](uint32_t pos, uint32_t s, int idx) { cand(pos, (s << 16) | sh.acc.a.ft[idx], idx); });
-        flush(min(n, (uint32_t)k));
-        if (tid == 0) *cn = (int32_t)min(n, (uint32_t)k);
+        const uint32_t n = compact_words(sh, n_local, tid, [](uint32_t w, int) { return w ? 1u : 0u; },
+                                         [&](int, uint32_t pos, uint32_t w, int idx) {
+                                             cand(pos, w, idx);
+                                         });
+        flush(min(n & 0xFFFFu, (uint32_t)k));
+        if (tid == 0) *cn = (int32_t)min(n & 0xFFFFu, (uint32_t)k);
     };
 
     // Shared per-query threshold.  qhist[q] (when given) counts the scores of every
@@ -868,19 +902,20 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
     // reach Tq they are its only candidates (no histogram, no tie order -- the merge
     // orders them by key); else the full selection below runs.  Items run block-major
     // (all queries' block 0 first), so Tq is close to the final k-th score after the
-    // first blocks and the later blocks emit few candidates.
+    // first blocks and the later blocks emit few candidates.  A stale (smaller) count
+    // still gives a valid lower bound.
     uint32_t Tq = 0;
     if (qh) {
         Tq = read_tq();
         if (Tq > 0) {
-            const uint32_t n = compact_scores(
-                sh, n_local, tid, [Tq](uint32_t s, int) { return s >= Tq; },
-                [&](uint32_t pos, uint32_t s, int idx) {
-                    cand(pos, (s << 16) | sh.acc.a.ft[idx], idx);
-                });
-            if (n <= (uint32_t)k) {
-                flush(n);
-                if (tid == 0) *cn = (int32_t)n;
+            const uint32_t thr_w = Tq << 16;
+            const uint32_t n = compact_words(
+                sh, n_local, tid, [thr_w](uint32_t w, int) { return w >= thr_w ? 1u : 0u; },
+                [&](int, uint32_t pos, uint32_t w, int idx) { cand(pos, w, idx); });
+            const uint32_t na = n & 0xFFFFu;
+            if (na <= (uint32_t)k) {
+                flush(na);
+                if (tid == 0) *cn = (int32_t)na;
                 return;
             }
         }
@@ -891,14 +926,16 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
     if (fast) {
         // ---- fast path: score histogram -> k-th score T -------------------
         uint32_t *hist = sh.u.hist;
-        // branch-free: an untouched doc (s = 0) counts into a per-lane spare bin past
+        // branch-free: an untouched doc (w = 0) counts into a per-lane spare bin past
         // the 4096 score bins (no same-address conflicts), never read
         const uint32_t spare = HIST_BINS + (uint32_t)lane;
-        if (qh) {  // the threshold copy was read (read_tq's barriers): zero the bins
+        if (qpre) {  // the threshold copy was read (read_tq's barriers): zero the bins
             reinterpret_cast<uint4 *>(hist)[tid] = make_uint4(0, 0, 0, 0);
             __syncthreads();
         }
-        sweep_scores(sh, n_local, tid, [&](uint32_t s, int) { atomicAdd(&hist[s ? s : spare], 1u); });
+        sweep_words(sh.acc, n_local, tid, [&](uint32_t w, int) {
+            atomicAdd(&hist[w ? (w >> 16) : spare], 1u);
+        });
         __syncthreads();
         // thread t owns bins 4t..4t+3; s = touched docs with score >= 4t
         const uint4 h4 = reinterpret_cast<const uint4 *>(hist)[tid];
@@ -941,30 +978,30 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
         need -= above;
         if (ties == need || ties <= (uint32_t)TIE_CAP) {
             // scores above T are in; the ties at T all go in, or into a list (the
-            // histogram is consumed) as (key of the doc, 0xFFFF - idx): unique, and
-            // larger = first-touch earlier, then doc smaller.
+            // histogram is consumed) as (low 16 bits of the word, 0xFFFF - idx):
+            // unique, and larger = first-touch earlier, then doc smaller.
             // Compaction: one sweep marks each lane's candidates and ties in two
-            // 32-bit masks over its 32 docs (4 per ds_read_b64); a block scan of the
-            // counts gives positions; the write loop visits only the marked docs
+            // 32-bit masks over its 32 words (4 per ds_read_b128); a block scan of the
+            // counts gives positions; the write loop visits only the marked words
             // (~1 per lane), not all 32.
             const bool all_ties = ties == need;
-            const uint32_t thr_a = all_ties ? T : T + 1;  // list A: s >= thr_a
+            const uint32_t thr_a = (all_ties ? T : T + 1) << 16;  // list A: w >= thr_a
             uint32_t *tl = sh.u.hist;
             uint32_t ma = 0, mb = 0;
             {
-                const uint2 *s2 = reinterpret_cast<const uint2 *>(sh.acc.a.sc);
+                const uint4 *a4 = reinterpret_cast<const uint4 *>(sh.acc);
                 const int n4 = (n_local + 3) >> 2;
 #pragma unroll
                 for (int i = 0; i < SC_PER_THREAD / 4; ++i) {
                     const int q4 = i * SC_THREADS + tid;
-                    const uint2 y = s2[q4];  // q4 < 8192: inside the array
+                    const uint4 y = a4[q4];  // q4 < 8192: inside the array
                     const bool ok = q4 < n4;
-                    const uint32_t sv[4] = {y.x & 0xFFFFu, y.x >> 16, y.y & 0xFFFFu, y.y >> 16};
+                    const uint32_t wv[4] = {y.x, y.y, y.z, y.w};
 #pragma unroll
                     for (int e = 0; e < 4; ++e) {
-                        const uint32_t sc = ok ? sv[e] : 0u;
-                        ma |= (uint32_t)(sc >= thr_a) << (4 * i + e);
-                        mb |= (uint32_t)(sc == T) << (4 * i + e);
+                        const uint32_t w = ok ? wv[e] : 0u;
+                        ma |= (uint32_t)(w >= thr_a) << (4 * i + e);
+                        mb |= (uint32_t)((w >> 16) == T) << (4 * i + e);
                     }
                 }
                 if (all_ties) mb = 0;
@@ -984,13 +1021,13 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
                     const int bit = __builtin_ctz(ma);
                     ma &= ma - 1;
                     const int idx = idx_of(bit);
-                    cand(pa++, word_at(sh, idx), idx);
+                    cand(pa++, sh.acc[idx], idx);
                 }
                 while (mb) {
                     const int bit = __builtin_ctz(mb);
                     mb &= mb - 1;
                     const int idx = idx_of(bit);
-                    tl[pb++] = ((uint32_t)sh.acc.a.ft[idx] << 16) | (0xFFFFu - (uint32_t)idx);
+                    tl[pb++] = ((sh.acc[idx] & 0xFFFFu) << 16) | (0xFFFFu - (uint32_t)idx);
                 }
             }
             __syncthreads();
@@ -1127,20 +1164,15 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
         dcut = dprefix;  // keep ties whose (0xFFFF - idx) >= dcut
     }
     __syncthreads();
-    // (the compaction classifies by score first; the key is read for the score's docs)
-    const uint32_t Ts = T >> 16;
-    const uint32_t n = compact_scores(
+    const uint32_t n = compact_words(
         sh, n_local, tid,
-        [&](uint32_t s, int idx) -> bool {
-            if (s == 0 || s < Ts) return false;
-            if (s > Ts) return true;
-            const uint32_t w = (s << 16) | sh.acc.a.ft[idx];
-            return w > T || (w == T && (0xFFFFu - (uint32_t)idx) >= dcut);
+        [T, dcut](uint32_t w, int idx) -> uint32_t {
+            return (w != 0 && (w > T || (w == T && (0xFFFFu - (uint32_t)idx) >= dcut))) ? 1u : 0u;
         },
-        [&](uint32_t pos, uint32_t s, int idx) { cand(pos, (s << 16) | sh.acc.a.ft[idx], idx); });
+        [&](int, uint32_t pos, uint32_t w, int idx) { cand(pos, w, idx); });
     flush((uint32_t)k);
     // exactly k by construction; anything else is a selection bug -> flag it
-    if (tid == 0) *cn = n == (uint32_t)k ? k : -2;
+    if (tid == 0) *cn = (n & 0xFFFFu) == (uint32_t)k ? k : -2;
 }
 
 // Persistent: one workgroup per CU walks the (query, block) items, so the per-
@@ -1644,12 +1676,11 @@ void build_index(di_index *ix, const int64_t *term_off, int64_t n_terms, const u
     // 128..255, ..., class 7 = value 1), classes in order, so that "every posting with
     // value >= 2^(7-c)" is a prefix of the sublist: seg[8e + c] = its length
     // (di_index_set_min_impact prunes with it; class 7 = the whole sublist = exact).
-    // Inside a class, postings are dealt from their 32 LDS bank buckets ((doc_in_block
-    // / 2) mod 32: the bank of both the doc's packed score word and its key slot;
-    // distinct banks per aligned 32-posting block where the class allows, see
-    // emit_group): the scorer's lanes read consecutive postings and update their docs'
-    // words, and a 32-lane group of a ds_add_u32 / ds_write_b16 conflicts on equal
-    // banks.  Any order is exact: a doc occurs once per term, and its key (first term,
+    // Inside a class, postings are dealt from their 32 LDS bank buckets (doc_in_block
+    // mod 32, distinct banks per aligned 32-posting block where the class allows, see
+    // emit_group): the scorer's lanes read consecutive postings and update
+    // acc[doc_in_block], and a 32-lane group of a ds_read_b32 / ds_write_b32 conflicts
+    // on equal banks.  Any order is exact: a doc occurs once per term, and its key (first term,
     // value there) does not depend on the order inside the term.
     // Long sublists are laid out by wave segment first: wave w of the scorer owns the
     // block's docs [w S, (w + 1) S), S = ceil(bd / 16), and its postings of the sublist
@@ -1660,7 +1691,7 @@ void build_index(di_index *ix, const int64_t *term_off, int64_t n_terms, const u
     std::vector<uint16_t> wmeta((size_t)std::max<uint32_t>(n_long, 1) * WSEG * 8, 0);
     std::vector<uint8_t> emax((size_t)std::max<uint64_t>(n_ent, 1), 0);
     auto cls_of = [](uint32_t w) { return 7 - (31 - __builtin_clz(w & 255u)); };
-    auto bank_of = [](uint32_t w) { return (w >> 9) & 31u; };  // (doc_in_block / 2) mod 32
+    auto bank_of = [](uint32_t w) { return (w >> 8) & 31u; };  // doc_in_block mod 32
     const uint32_t S = (bd + WSEG - 1) / WSEG;
     parallel_for(n_terms, [&](int64_t t0, int64_t t1, int) {
         std::vector<uint32_t> grp, tmp, bk, seg_in, cls_cnt(8), cls_pos(8), bucket_cnt(32),

@@ -66,3 +66,34 @@ def test_native_index_builder_rejects_what_the_reference_rejects():
         bad.write_text("▁a: 300\n")  # struct.pack('B', 300) fails in the reference
         with pytest.raises(_lib.DIError):
             create_index(bad, Path(td) / "out")
+
+
+def test_native_index_builder_at_scale_equals_oracle(tmp_path):
+    """The threaded builder (line ranges parsed in parallel, per-thread term sets,
+    per-thread bucket offsets) on a 20k-doc impact TSV from the library's generator,
+    plus lines with repeated terms (dict: first slot, last value), blank and
+    whitespace-only lines and a \\r\\n / lone \\r terminator, against the oracle's build of
+    the same lines -- byte-identical files, for 1 and 8 host threads."""
+    import os
+
+    import oracle
+    from improving_learned_index_amd import synthetic as S
+    from improving_learned_index_amd.inverted_index import create_index
+
+    src = tmp_path / "c.tsv"
+    S.synth_impact_tsv(src, 20_000, 40_000, seed=3)
+    extra = ("▁t7: 3.5, ▁t9: 1.25, ▁t7: 4.75\n\n   \n▁t1: 2.0\r\n"
+             + ", ".join(f"▁t{i % 23}: {i % 7}.5" for i in range(60)) + "\r▁t3: 1.0\n")
+    with open(src, "a", encoding="utf-8", newline="") as f:
+        f.write(extra)
+    vocab, term_off, pdoc, pval = oracle.build_index(oracle.collection_items(src))
+    oracle.write_index(tmp_path / "want", vocab, term_off, pdoc, pval)
+    for threads in ("1", "8"):
+        os.environ["DI_HOST_THREADS"] = threads
+        try:
+            create_index(src, tmp_path / f"got{threads}")
+        finally:
+            del os.environ["DI_HOST_THREADS"]
+        for name in ("vocab.txt", "inverted_index.idx", "inverted_index.dat"):
+            assert (tmp_path / f"got{threads}" / name).read_bytes() == \
+                (tmp_path / "want" / name).read_bytes(), (threads, name)

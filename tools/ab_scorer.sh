@@ -17,9 +17,10 @@ for k in ("retrieve", "retrieve_shard", "retrieve_full"):
 print("  ".join(out), flush=True)
 PY
 }
-run old DEEPIMPACT_HIP_LIB=$PWD/tools/_old/libdeepimpact_hip.so || exit 1
-run new X=0 || exit 1
-run nokey DI_PROFILE_ABLATE=2048 || exit 1
-run rw DI_PROFILE_ABLATE=4096 || exit 1
-run rw_nokey DI_PROFILE_ABLATE=6144 || exit 1
-run noscatter DI_PROFILE_ABLATE=1 || exit 1
+for v in ${VARIANTS:-old new}; do
+    case $v in
+        old) run old DEEPIMPACT_HIP_LIB=$PWD/tools/_old/libdeepimpact_hip.so DI_LIB_ALLOW_MISSING=1 || exit 1 ;;
+        new) run new X=0 || exit 1 ;;
+        ablate*) run $v DI_PROFILE_ABLATE=${v#ablate} || exit 1 ;;
+    esac
+done
