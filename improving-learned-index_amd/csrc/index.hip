@@ -31,6 +31,10 @@
 #include <cstdlib>
 #include <cstring>
 #include <fstream>
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
 #include <memory>
 #include <numeric>
 #include <string>
@@ -1888,39 +1892,88 @@ int di_index_load_reference(const char *dir, uint32_t doc_lo, uint32_t doc_hi, i
     return guard([&] {
         DI_REQUIRE(dir && out, DI_EINVAL, "null argument");
         std::string d(dir);
+        // .idx read whole (16 B per term); .dat mapped: a doc-id shard reads only its
+        // own postings out of it, on host_threads() threads (every rank of a sharded
+        // rank CLI maps the same file: one page-cache copy, no per-rank whole-file copy)
         std::ifstream fi(d + "/inverted_index.idx", std::ios::binary | std::ios::ate);
-        std::ifstream fd(d + "/inverted_index.dat", std::ios::binary | std::ios::ate);
-        DI_REQUIRE(fi && fd, DI_EIO, "cannot open %s/inverted_index.{idx,dat}", dir);
-        size_t isz = (size_t)fi.tellg(), dsz = (size_t)fd.tellg();
+        DI_REQUIRE(fi, DI_EIO, "cannot open %s/inverted_index.idx", dir);
+        const size_t isz = (size_t)fi.tellg();
         DI_REQUIRE(isz % 16 == 0, DI_EFORMAT, "inverted_index.idx size %zu not a multiple of 16",
                    isz);
+        std::vector<uint64_t> idx(isz / 8);
+        fi.seekg(0);
+        fi.read(reinterpret_cast<char *>(idx.data()), (std::streamsize)isz);
+        DI_REQUIRE(fi || isz == 0, DI_EIO, "cannot read %s/inverted_index.idx", dir);
+        const int fd = ::open((d + "/inverted_index.dat").c_str(), O_RDONLY);
+        DI_REQUIRE(fd >= 0, DI_EIO, "cannot open %s/inverted_index.dat", dir);
+        struct stat st;
+        if (::fstat(fd, &st) != 0) {
+            ::close(fd);
+            DI_REQUIRE(false, DI_EIO, "cannot stat %s/inverted_index.dat", dir);
+        }
+        const size_t dsz = (size_t)st.st_size;
+        const unsigned char *dat = nullptr;
+        if (dsz) {
+            void *m = ::mmap(nullptr, dsz, PROT_READ, MAP_SHARED, fd, 0);
+            ::close(fd);
+            DI_REQUIRE(m != MAP_FAILED, DI_EIO, "cannot map %s/inverted_index.dat", dir);
+            dat = static_cast<const unsigned char *>(m);
+        } else {
+            ::close(fd);
+        }
+        struct Unmap {
+            const void *p;
+            size_t n;
+            ~Unmap() {
+                if (p) ::munmap(const_cast<void *>(p), n);
+            }
+        } unmap{dat, dsz};
         DI_REQUIRE(dsz % 5 == 0, DI_EFORMAT, "inverted_index.dat size %zu not a multiple of 5",
                    dsz);
-        std::vector<uint64_t> idx(isz / 8);
-        std::vector<unsigned char> dat(dsz);
-        fi.seekg(0);
-        fd.seekg(0);
-        fi.read(reinterpret_cast<char *>(idx.data()), (std::streamsize)isz);
-        fd.read(reinterpret_cast<char *>(dat.data()), (std::streamsize)dsz);
-        const int64_t nt = (int64_t)(isz / 16), np = (int64_t)(dsz / 5);
-        // postings of term t: records [start/5, end/5) -- create.py:45-51
-        std::vector<int64_t> term_off(nt + 1, 0);
-        std::vector<uint32_t> pdoc;
-        std::vector<uint8_t> pval;
-        pdoc.reserve(np);
-        pval.reserve(np);
+        const int64_t nt = (int64_t)(isz / 16);
         for (int64_t t = 0; t < nt; ++t) {
-            uint64_t s = idx[2 * t], e = idx[2 * t + 1];
+            const uint64_t s = idx[2 * t], e = idx[2 * t + 1];
             DI_REQUIRE(s % 5 == 0 && e % 5 == 0 && s <= e && e <= dsz, DI_EFORMAT,
                        "bad (start,end) for term %lld", (long long)t);
-            for (uint64_t r = s / 5; r < e / 5; ++r) {
-                uint32_t doc;
-                std::memcpy(&doc, &dat[r * 5], 4);
-                pdoc.push_back(doc);
-                pval.push_back(dat[r * 5 + 4]);
-            }
-            term_off[t + 1] = (int64_t)pdoc.size();
         }
+        const uint64_t hi = doc_hi ? doc_hi : 0x100000000ull;
+        // postings of term t: records [start/5, end/5) up to its first 0 value
+        // (create.py:45-51, inverted_index.py:50-51), docs of the shard only
+        auto rec_doc = [&](uint64_t r) {
+            uint32_t doc;
+            std::memcpy(&doc, dat + r * 5, 4);
+            return doc;
+        };
+        std::vector<int64_t> term_off((size_t)nt + 1, 0);
+        parallel_for(nt, [&](int64_t t0, int64_t t1, int) {
+            for (int64_t t = t0; t < t1; ++t) {
+                int64_t c = 0;
+                for (uint64_t r = idx[2 * t] / 5; r < idx[2 * t + 1] / 5; ++r) {
+                    if (dat[r * 5 + 4] == 0) break;
+                    const uint32_t doc = rec_doc(r);
+                    c += doc >= doc_lo && doc < hi;
+                }
+                term_off[(size_t)t + 1] = c;
+            }
+        });
+        for (int64_t t = 0; t < nt; ++t) term_off[(size_t)t + 1] += term_off[(size_t)t];
+        const int64_t np = term_off[(size_t)nt];
+        std::vector<uint32_t> pdoc((size_t)std::max<int64_t>(np, 1));
+        std::vector<uint8_t> pval((size_t)std::max<int64_t>(np, 1));
+        parallel_for(nt, [&](int64_t t0, int64_t t1, int) {
+            for (int64_t t = t0; t < t1; ++t) {
+                int64_t o = term_off[(size_t)t];
+                for (uint64_t r = idx[2 * t] / 5; r < idx[2 * t + 1] / 5; ++r) {
+                    const uint8_t v = dat[r * 5 + 4];
+                    if (v == 0) break;
+                    const uint32_t doc = rec_doc(r);
+                    if (doc >= doc_lo && doc < hi) {
+                        pdoc[(size_t)o] = doc;
+                        pval[(size_t)o++] = v;
+                    }
+                }
+            }
+        });
         int rc = di_index_create(term_off.data(), nt, pdoc.data(), pval.data(), doc_lo, doc_hi,
                                  device, out);
         if (rc != DI_OK) throw Error{rc};

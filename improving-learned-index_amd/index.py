@@ -34,7 +34,7 @@ logger = logging.getLogger("index")
 def run(collection_path, collection_type, output_file_path, model_checkpoint_path,
         num_processes=8, process_batch_size=50 * BATCH_SIZE, model_batch_size=BATCH_SIZE,
         tokenizer_path=None, max_length=None, precision="bf16x3", device=0, variant="xlmr",
-        doc_range=None, pairwise=False):
+        doc_range=None, pairwise=False, first_shard=True):
     if pairwise:
         raise NotImplementedError("DeepPairwiseImpact is outside this build (SURVEY §8f F4)")
     start = time.time()
@@ -51,17 +51,23 @@ def run(collection_path, collection_type, output_file_path, model_checkpoint_pat
         indexer = Indexer(model, model_batch_size=model_batch_size,
                           num_processes=num_processes, pool=pool)
         return _index_file(indexer, collection_path, collection_type, output_file_path,
-                           process_batch_size, doc_range, start)
+                           process_batch_size, doc_range, start, first_shard)
     finally:
         if pool is not None:
             pool.close()
 
 
 def _index_file(indexer, collection_path, collection_type, output_file_path,
-                process_batch_size, doc_range, start):
+                process_batch_size, doc_range, start, first_shard=True):
     """index.py:31-44.  Batches are tokenized one ahead (Indexer.submit) while the
     previous one encodes and writes; they are written in order, so the bytes are the
-    sequential loop's."""
+    sequential loop's.
+
+    A doc-id shard (doc_range) writes its docs' lines only: the joined shards are the
+    single-process file.  The reference's one empty batch -- at line 1 when
+    process_batch_size is 1 (the flush comes before the append), or the final flush of
+    an empty collection -- writes an empty line; the shard holding line 1 (resp. the
+    first shard) writes it."""
     lo, hi = (0, None) if doc_range is None else doc_range
     pending = None  # submitted, not yet written
 
@@ -78,15 +84,17 @@ def _index_file(indexer, collection_path, collection_type, output_file_path,
     with open(collection_path) as f, open(output_file_path, "w") as out:
         batch = []
         n = 0
+        any_line = False
         for i, passage in enumerate(f, start=1):
+            any_line = True
             if hi is not None and i - 1 >= hi:
                 break
             if i - 1 < lo:
                 continue
-            # index.py:35 (first batch one short); a shard never flushes an empty batch
-            # (its flush points need not fall inside it: an empty flush would write a
-            # stray empty line and shift every later doc id of the joined file)
-            if i % process_batch_size == 0 and (doc_range is None or batch):
+            # index.py:35 (first batch one short).  A shard flushes an empty batch only
+            # where the single process does (line 1, process_batch_size 1): its other
+            # flush points may fall on another shard's batch
+            if i % process_batch_size == 0 and (doc_range is None or batch or i == 1):
                 flush(batch)
                 logger.info(f"Indexed {i} passages [Rate: {i / (time.time() - start):.2f} "
                             f"passages/s]")
@@ -94,7 +102,7 @@ def _index_file(indexer, collection_path, collection_type, output_file_path,
             doc_id, passage = CollectionParser.parse(passage, collection_type)
             batch.append(passage)
             n += 1
-        if doc_range is None or batch:
+        if doc_range is None or batch or (first_shard and not any_line):
             flush(batch)
         if pending is not None:
             indexer.finish(pending, out)
@@ -132,7 +140,7 @@ def main(argv=None):
         out, device = parallel.part_path(a.output_file_path, rank), parallel.rank_device(local)
     run(a.collection_path, a.collection_type, out, a.model_checkpoint_path,
         a.num_processes, a.process_batch_size, a.model_batch_size, a.tokenizer_path,
-        a.max_length, a.precision, device, a.variant, dr, a.pairwise)
+        a.max_length, a.precision, device, a.variant, dr, a.pairwise, first_shard=rank == 0)
     if world > 1:
         dist.barrier()
         if rank == 0:

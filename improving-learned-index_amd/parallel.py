@@ -79,13 +79,69 @@ def part_path(path, rank: int) -> Path:
 
 
 def count_lines(path) -> int:
-    """Lines as Python's file iteration sees them (a last line without '\\n' counts)."""
-    n, last = 0, b"\n"
+    """Lines as Python's text-mode file iteration sees them -- universal newlines
+    (\\n, \\r\\n and a lone \\r end a line; index.py and the reference read the
+    collection with open(path), index.py:32) and a last line without a terminator."""
+    n, prev_cr, last = 0, False, b""
     with open(path, "rb") as f:
         for blk in iter(lambda: f.read(1 << 24), b""):
-            n += blk.count(b"\n")
+            # terminators = \n + \r - \r\n pairs (one split across blocks included)
+            n += blk.count(b"\n") + blk.count(b"\r") - blk.count(b"\r\n")
+            if prev_cr and blk[:1] == b"\n":
+                n -= 1
+            prev_cr = blk[-1:] == b"\r"
             last = blk[-1:]
-    return n + (last != b"\n")
+    return n + (last not in (b"", b"\n", b"\r"))
+
+
+def line_offsets(path, lines: Sequence[int], block: int = 1 << 24) -> List[int]:
+    """Byte offsets where the given 0-based lines start (ascending; a line index past
+    the end -> the file size), with the universal-newline line ends of count_lines.
+    Streams the file: whole blocks are skipped by counting their terminators."""
+    import re
+
+    want = list(lines)
+    assert want == sorted(want)
+    out: List[int] = []
+    term = re.compile(rb"\r\n|\r|\n")
+    line, pos, carry_cr = 0, 0, False  # line index at byte pos (the start of a block)
+    with open(path, "rb") as f:
+        k = 0
+        while k < len(want) and want[k] <= 0:
+            out.append(0)
+            k += 1
+        for blk in iter(lambda: f.read(block), b""):
+            if k == len(want) and not carry_cr:  # (a pending \r may take the next \n)
+                break
+            start = 0
+            if carry_cr and blk[:1] == b"\n":  # the \n of a \r\n split across blocks
+                start = 1
+                # the line began after the \n: fix the offsets recorded for that line
+                j = len(out) - 1
+                while j >= 0 and out[j] == pos and want[j] == line:
+                    out[j] = pos + 1
+                    j -= 1
+            n_here = (blk.count(b"\n") + blk.count(b"\r") - blk.count(b"\r\n")
+                      - (1 if start else 0))
+            if k == len(want):
+                break
+            if line + n_here < want[k]:  # no wanted line starts inside this block
+                line += n_here
+                carry_cr = blk[-1:] == b"\r"
+                pos += len(blk)
+                continue
+            for m in term.finditer(blk, start):
+                line += 1
+                while k < len(want) and want[k] == line:
+                    out.append(pos + m.end())
+                    k += 1
+                if k == len(want):
+                    break
+            carry_cr = blk[-1:] == b"\r"
+            pos += len(blk)
+        size = pos + sum(len(b) for b in iter(lambda: f.read(block), b""))
+    out += [size] * (len(want) - len(out))
+    return out
 
 
 def shard_range(n_items: int, world: int, rank: int) -> Tuple[int, int]:
@@ -128,13 +184,20 @@ def quantize_sharded(input_path, output_path, max_val, world: int, rank: int,
     kernels (the HIP di_quantize_file by default in quantize.py)."""
     import torch.distributed as dist
 
-    with open(input_path, "rb") as f:
-        lines = f.readlines()
-    lo, hi = shard_range(len(lines), world, rank)
+    # the shard's lines by byte offsets (universal newlines, as the reference's text-mode
+    # iteration): streamed, never the whole file in memory
+    lo, hi = shard_range(count_lines(input_path), world, rank)
+    b_lo, b_hi = line_offsets(input_path, [lo, hi])
     part_in = Path(f"{part_path(output_path, rank)}.in")
-    with open(part_in, "wb") as f:
-        f.writelines(lines[lo:hi])
-    del lines
+    with open(input_path, "rb") as src, open(part_in, "wb") as f:
+        src.seek(b_lo)
+        left = b_hi - b_lo
+        while left > 0:
+            blk = src.read(min(left, 1 << 24))
+            if not blk:
+                break
+            f.write(blk)
+            left -= len(blk)
     if max_val is None:
         m = global_max(shard_max(part_in) if hi > lo else 0.0)
         if not m > 0.0:

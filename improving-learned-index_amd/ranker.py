@@ -50,7 +50,12 @@ class Ranker:
             # cannot initialise the GPU after the library's (newer) runtime has
             torch.cuda.set_device(device)
             parallel.init_group(parallel.exchange_backend(self.world), device)
-            lo, hi = parallel.shard_range(reference_n_docs(index_path), self.world, self.rank)
+            # the collection size: one scan of inverted_index.dat on rank 0, broadcast
+            import torch.distributed as dist
+
+            n = [reference_n_docs(index_path) if self.rank == 0 else 0]
+            dist.broadcast_object_list(n, src=0)
+            lo, hi = parallel.shard_range(n[0], self.world, self.rank)
         self.device = device
         self.index = InvertedIndex(index_path=index_path, device=device, doc_lo=lo, doc_hi=hi,
                                    min_impact=min_impact)

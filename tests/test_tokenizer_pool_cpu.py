@@ -147,10 +147,19 @@ def test_merged_chunks_equal_one_packed_batch(restore_class):
 def test_worker_threads_follow_the_cpu_share(monkeypatch):
     """Each tokenizer worker's thread pool is sized from the process's CPU share
     (OMP_NUM_THREADS when set, as on the GPU box) over the worker count, 2..4."""
+    import os
+
     from improving_learned_index_amd import indexer
 
+    # a fixed CPU affinity (256 CPUs, like the GPU box): the share is then the
+    # OMP_NUM_THREADS value alone, whatever machine runs the test
+    monkeypatch.setattr(os, "sched_getaffinity", lambda pid: set(range(256)), raising=False)
     monkeypatch.setenv("OMP_NUM_THREADS", "16")
     assert indexer.worker_threads(16) == 2
     assert indexer.worker_threads(2) == 4
     monkeypatch.setenv("OMP_NUM_THREADS", "64")
-    assert indexer.worker_threads(16) == min(4, max(2, min(64, len(__import__("os").sched_getaffinity(0))) // 16))
+    assert indexer.worker_threads(16) == 4
+    monkeypatch.setenv("OMP_NUM_THREADS", "")
+    assert indexer.worker_threads(16) == 4  # 256 // 16 = 16, capped at 4
+    monkeypatch.setattr(os, "sched_getaffinity", lambda pid: set(range(8)), raising=False)
+    assert indexer.worker_threads(8) == 2  # 8 // 8 = 1, at least 2
