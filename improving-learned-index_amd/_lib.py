@@ -53,6 +53,7 @@ SIGNATURES = {
     "di_index_reserve": (ctypes.c_int, [P, I32, I32]),
     "di_index_info": (ctypes.c_int, [P, P, P, P, P]),
     "di_index_set_min_impact": (ctypes.c_int, [P, I32]),
+    "di_index_set_block_max": (ctypes.c_int, [P, ctypes.c_float]),
     "di_index_set_stream": (ctypes.c_int, [P, P]),
     "di_index_sync": (ctypes.c_int, [P]),
     "di_index_timing": (ctypes.c_int, [P, ctypes.c_char_p, P, ctypes.c_int]),
@@ -211,6 +212,10 @@ class DeviceIndex:
     def set_min_impact(self, min_impact=1):
         """Score only postings with value >= 2^floor(log2 min_impact) (1 = exact)."""
         check(lib().di_index_set_min_impact(self._h, int(min_impact)))
+
+    def set_block_max(self, factor=0.0):
+        """Block-max skipping: 0 off, 1 exact, > 1 approximate (di_index_set_block_max)."""
+        check(lib().di_index_set_block_max(self._h, float(factor)))
 
     def set_stream(self, stream_ptr):
         check(lib().di_index_set_stream(self._h, ctypes.c_void_p(stream_ptr)))

@@ -93,6 +93,7 @@ struct ScoreShared {
     uint32_t thr, above, ties, bin, bin_above;
     uint32_t tq;                   // the query's shared threshold as this item read it
     uint32_t lmask[WTERMS / 32];   // terms (j < WTERMS) with a per-wave layout in this block
+    uint32_t wub[WSEG];            // block-max: each wave segment's score upper bound
     uint32_t wtab[WTERMS][WSEG];   // their per-wave runs: start << 16 | end (in the sublist)
 };
 static_assert(offsetof(ScoreShared, acc) == 0, "accumulators at LDS address 0");
@@ -311,6 +312,8 @@ struct SubIndex {
     const uint16_t *seg;
     const uint32_t *lid;
     const uint16_t *wmeta;
+    const uint8_t *emax;  // block-max metadata: the sublist's largest value
+    const uint8_t *wmax;  // long sublists: the largest value of each wave segment's run
 };
 
 // entry of (term t, block b), or -1 when t has no posting in b
@@ -345,8 +348,10 @@ struct ItemRec {
     int64_t lo, hi;        // the term's sublist [lo, hi) in this block (min_cls prefix)
     uint32_t wtab[WSEG];   // per-wave layout: run of wave w = start << 16 | end
     uint32_t flags;        // IR_LONG: per-wave layout; IR_BAD: invalid term id
+    uint8_t wmx[WSEG];     // block-max bound of each wave segment (emax / wmax)
     uint32_t pad[3];
 };
+static_assert(sizeof(ItemRec) % 16 == 0, "records stay 16-byte aligned");
 constexpr uint32_t IR_LONG = 1, IR_BAD = 2;
 
 // Items (query q, block b) as the scorer numbers them (item = b * n_q + q); records
@@ -378,6 +383,7 @@ item_setup_kernel(SubIndex si, int min_cls, int nb, int64_t n_terms,
             r[j].hi = hi;
             r[j].flags = id != 0xFFFFFFFFu ? IR_LONG : 0u;
         }
+        r[j].wmx[w] = en < 0 ? 0 : id != 0xFFFFFFFFu ? si.wmax[(int64_t)id * WSEG + w] : si.emax[en];
         if (id != 0xFFFFFFFFu) {
             const uint16_t *m = si.wmeta + (int64_t)id * (WSEG * 8);
             const uint32_t s0 = w ? m[(w - 1) * 8 + 7] : 0u;
@@ -544,7 +550,7 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
                                            int32_t *__restrict__ cand_n,
                                            uint32_t *__restrict__ qhist, int ablate,
                                            const ItemRec *__restrict__ ir,
-                                           uint32_t *__restrict__ long_flag) {
+                                           uint32_t *__restrict__ long_flag, float bm_factor) {
     int64_t *lo = sh.v.bounds[0], *hi = sh.v.bounds[1];
 
     // opaque per item: keeps the per-thread index arithmetic of the sweeps from being
@@ -584,6 +590,7 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
         sh.emit = 0;
         sh.n_tie = 0;
         for (int i = 0; i < WTERMS / 32; ++i) sh.lmask[i] = 0;
+        for (int i = 0; i < WSEG; ++i) sh.wub[i] = 0;
     }
     __syncthreads();
 
@@ -591,6 +598,8 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
     // docs -- long terms over their per-wave runs, short ones read in full by every wave
     // -- so no term needs a barrier; longer queries: the all-wave form, a barrier per term
     const bool wl = nt <= WTERMS;
+    // block-max skipping (opt-in, configs[4]): per-wave segment upper bounds (wub)
+    const bool bm = bm_factor > 0.0f && wl && qhist != nullptr;
     // The query's shared threshold histogram (qhist, below) is copied by LDS-DMA into
     // the selection histogram (idle until the selection) here, so its round trip
     // overlaps the scatter and the selection reads it from LDS; the fast selection
@@ -617,12 +626,13 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
         const int e = tid;
         const bool act = e < nt * WSEG;
         const int j = act ? e / WSEG : 0, w = e % WSEG;
-        uint32_t f = 0, wt = 0;
+        uint32_t f = 0, wt = 0, ub = 0;
         int64_t rlo = 0, rhi = 0;
         if (act) {
             const ItemRec &R = ir[j];
             f = R.flags;
             wt = R.wtab[w];
+            if (bm) ub = R.wmx[w];
             if (w == 0) {
                 rlo = R.lo;
                 rhi = R.hi;
@@ -630,6 +640,7 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
         }
         zero();
         if (act) {
+            if (bm && ub) atomicAdd(&sh.wub[w], ub);
             if (w == 0) {
                 lo[j] = rlo;
                 hi[j] = rhi;
@@ -649,13 +660,16 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
         const uint32_t t = act ? q_terms[q0 + j] : 0u;
         const bool tok = act && t < n_terms;  // (device-pointer callers are not pre-checked)
         int64_t en = -1, blo = 0, bhi = 0;
-        uint32_t id = 0xFFFFFFFFu;
+        uint32_t id = 0xFFFFFFFFu, ub = 0;
         if (tok) {
             en = find_entry(si, nb, t, b);
             if (en >= 0) id = si.lid[en];
             if (w == 0) entry_bounds(si, en, min_cls, blo, bhi);
+            if (bm && en >= 0)
+                ub = id != 0xFFFFFFFFu ? si.wmax[(int64_t)id * WSEG + w] : si.emax[en];
         }
         zero();
+        if (bm && ub) atomicAdd(&sh.wub[w], ub);
         if (act && !tok) {  // invalid term id
             if (w == 0) {
                 sh.bad = 1;
@@ -735,6 +749,23 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
         __syncthreads();  // (wsum / tq are reused)
         return r;
     };
+    // Block-max skipping (bm, opt-in; configs[4]): a wave segment whose upper bound
+    // wub = sum over the query terms of the segment's largest value in their sublists
+    // stays below the query's shared threshold Tq cannot hold a top-k doc (every doc of
+    // it scores <= wub < Tq <= the final k-th score): its wave skips its scatter and its
+    // docs stay 0.  bm_factor 1 is exact; > 1 skips segments below factor x Tq -- an
+    // approximation (the QPS-vs-recall sweep).  Every segment below: the item ends.
+    bool skip_wave = false;
+    if (bm) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the threshold copy (read_tq)
+        const uint32_t tq0 = read_tq();
+        const float thr = bm_factor * (float)tq0;
+        skip_wave = tq0 > 0 && (float)sh.wub[wave] < thr;
+        if (__syncthreads_and(tq0 > 0 && (float)sh.wub[tid & (WSEG - 1)] < thr)) {
+            if (tid == 0) *cn = 0;
+            return;
+        }
+    }
     // ---- scatter: terms in query order, barrier between terms -------------
     // A term's sublist goes in rounds of 16 postings per lane while 16 k remain, then
     // 4 per lane while more than 1 k remain, then 1: a short tail does not pay for a
@@ -755,7 +786,7 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
     const uint32_t wdn = wave == WSEG - 1 ? 0x7FFFFFFFu - wdlo : wseg;  // last: the rest
     const uint32_t wdummy = (uint32_t)(MAX_BLOCK_DOCS + lane) << 2;
     const uint32_t vmin = 1u << (7 - min(min_cls, 7));  // all-wave form: pruning by value
-    for (int j = (ablate & 1) ? nt : 0; j < nt; ++j) {  // ablate bit 0: skip (profiling)
+    for (int j = (ablate & 1) || skip_wave ? nt : 0; j < nt; ++j) {  // ablate bit 0: skip (profiling)
         const uint32_t first_bits = (uint32_t)(255 - j) << 8;
         const bool lj = is_long(j);
         if (lj) {
@@ -1187,7 +1218,8 @@ score_blocks_kernel(const uint32_t *__restrict__ post, SubIndex si, int min_cls,
                     const uint32_t *__restrict__ q_terms, const int32_t *__restrict__ cu_q, int k,
                     uint64_t *__restrict__ cand_key, int32_t *__restrict__ cand_n, int n_items,
                     int n_q, uint32_t *__restrict__ qhist, int ablate,
-                    const ItemRec *__restrict__ rec, uint32_t *__restrict__ long_flag) {
+                    const ItemRec *__restrict__ rec, uint32_t *__restrict__ long_flag,
+                    float bm_factor) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     ScoreShared &sh = *reinterpret_cast<ScoreShared *>(smem);
     if ((uint32_t)(uintptr_t)((__attribute__((address_space(3))) unsigned char *)smem) != 0) {
@@ -1201,7 +1233,7 @@ score_blocks_kernel(const uint32_t *__restrict__ post, SubIndex si, int min_cls,
     for (int item = blockIdx.x; item < n_items; item += gridDim.x) {
         score_item(sh, item % n_q, item / n_q, post, si, min_cls, nb, block_docs, n_terms,
                    n_docs, doc_lo, q_terms, cu_q, k, cand_key, cand_n, qhist, ablate,
-                   rec ? rec + (int64_t)item * WTERMS : nullptr, long_flag);
+                   rec ? rec + (int64_t)item * WTERMS : nullptr, long_flag, bm_factor);
         __syncthreads();  // every wave is done with the LDS of this item
     }
 }
@@ -1513,8 +1545,9 @@ struct di_index {
     uint32_t n_docs = 0, doc_lo = 0;  // shard [doc_lo, doc_lo + n_docs)
     int nb = 0, block_docs = 0;
     int min_cls = 7;                 // impact-class prefix scored (7 = every posting: exact)
+    float bm_factor = 0.0f;          // block-max skipping: 0 off, 1 exact, > 1 approximate
     // postings and the sparse (term, block) entries (SubIndex)
-    DevBuf post, tb_start, eblk, epos, seg, lid, wmeta, emax;
+    DevBuf post, tb_start, eblk, epos, seg, lid, wmeta, emax, wmax;
     DevBuf ws_q, ws_cu, ws_ck, ws_cn, ws_doc, ws_score, ws_n, ws_key, ws_thr;
     DevBuf ws_rec;  // ItemRec per (item, term slot): item_setup_kernel -> score_blocks
     DevBuf ws_long;  // score_blocks -> score_long_kernel: the batch has long queries
@@ -1527,7 +1560,8 @@ struct di_index {
 
     SubIndex sub() const {
         return SubIndex{tb_start.as<uint32_t>(), eblk.as<uint16_t>(), epos.as<uint32_t>(),
-                        seg.as<uint16_t>(), lid.as<uint32_t>(), wmeta.as<uint16_t>()};
+                        seg.as<uint16_t>(), lid.as<uint32_t>(), wmeta.as<uint16_t>(),
+                        emax.as<uint8_t>(), wmax.as<uint8_t>()};
     }
 };
 
@@ -1694,6 +1728,7 @@ void build_index(di_index *ix, const int64_t *term_off, int64_t n_terms, const u
     std::vector<uint16_t> seg((size_t)std::max<uint64_t>(n_ent * 8, 8), 0);
     std::vector<uint16_t> wmeta((size_t)std::max<uint32_t>(n_long, 1) * WSEG * 8, 0);
     std::vector<uint8_t> emax((size_t)std::max<uint64_t>(n_ent, 1), 0);
+    std::vector<uint8_t> wmax((size_t)std::max<uint32_t>(n_long, 1) * WSEG, 0);
     auto cls_of = [](uint32_t w) { return 7 - (31 - __builtin_clz(w & 255u)); };
     auto bank_of = [](uint32_t w) { return (w >> 8) & 31u; };  // doc_in_block mod 32
     const uint32_t S = (bd + WSEG - 1) / WSEG;
@@ -1771,9 +1806,13 @@ void build_index(di_index *ix, const int64_t *term_off, int64_t n_terms, const u
                 }
                 for (int w = 0; w < WSEG; ++w) {
                     seg_in.clear();
+                    uint32_t wm = 0;
                     for (uint32_t x : grp)
-                        if (std::min<uint32_t>((x >> 8) / S, WSEG - 1) == (uint32_t)w)
+                        if (std::min<uint32_t>((x >> 8) / S, WSEG - 1) == (uint32_t)w) {
                             seg_in.push_back(x);
+                            wm = std::max(wm, x & 255u);
+                        }
+                    wmax[(size_t)id * WSEG + w] = (uint8_t)wm;
                     emit_group(seg_in.data(), seg_in.size(), o, s0,
                                &wmeta[(size_t)id * WSEG * 8 + w * 8]);
                 }
@@ -1789,6 +1828,7 @@ void build_index(di_index *ix, const int64_t *term_off, int64_t n_terms, const u
     upload(ix->lid, lid);
     upload(ix->wmeta, wmeta);
     upload(ix->emax, emax);
+    upload(ix->wmax, wmax);
 }
 
 }  // namespace
@@ -2078,7 +2118,7 @@ int di_index_search(di_index *ix, const uint32_t *q_terms, const int32_t *cu_q, 
                                    ix->ws_ck.as<uint64_t>(), ix->ws_cn.as<int32_t>(), n_items,
                                    nq, thr ? ix->ws_thr.as<uint32_t>() : nullptr, ix->ablate,
                                    use_rec ? ix->ws_rec.as<ItemRec>() : nullptr,
-                                   ix->ws_long.as<uint32_t>());
+                                   ix->ws_long.as<uint32_t>(), thr ? ix->bm_factor : 0.0f);
                 check_launch("score_blocks");
                 hipLaunchKernelGGL(score_long_kernel, dim3(std::min(n_items, n_cu())),
                                    dim3(SC_THREADS), sizeof(ScoreShared), s,
@@ -2142,6 +2182,15 @@ int di_index_set_min_impact(di_index *ix, int32_t min_impact) {
                    "min_impact=%d outside [1, 255]", min_impact);
         // postings with value >= 2^floor(log2 min_impact): the class prefix
         ix->min_cls = 7 - (31 - __builtin_clz((unsigned)min_impact));
+    });
+}
+
+int di_index_set_block_max(di_index *ix, float factor) {
+    return guard([&] {
+        DI_REQUIRE(ix, DI_EINVAL, "null handle");
+        DI_REQUIRE(factor == 0.0f || (factor >= 1.0f && factor <= 16.0f), DI_ERANGE,
+                   "block-max factor %g: 0 (off) or in [1, 16]", (double)factor);
+        ix->bm_factor = factor;
     });
 }
 

@@ -122,6 +122,14 @@ int di_index_info(const di_index *ix, int64_t *n_terms, int64_t *n_postings, uin
  * anything larger is an approximation whose recall bench tools measure.  No reference
  * counterpart (the reference scores exhaustively).                                  */
 int di_index_set_min_impact(di_index *ix, int32_t min_impact);
+/* Block-max skipping (BASELINE configs[4]): per (term, block) and per (long sublist, wave
+ * segment of 2048 docs) the largest value is kept at build time; a segment whose bound
+ * (the sum over the query terms of those maxima) stays below the query's running top-k
+ * threshold is not scored.  factor 0: off (default); 1: exact -- the same ranking as
+ * InvertedIndex.score (inverted_index.py:55-62); in (1, 16]: skips segments below
+ * factor x threshold, an approximation (QPS vs recall@1000).  Queries of at most 64
+ * terms, with the shared threshold (>= 8 blocks). */
+int di_index_set_block_max(di_index *ix, float factor);
 int di_index_set_stream(di_index *ix, void *hip_stream);
 int di_index_sync(di_index *ix);
 int di_index_timing(di_index *ix, const char *name, di_timing *out, int reset);

@@ -369,3 +369,40 @@ def test_full_msmarco_scaled_vocab_on_one_gpu(L):
     ora.term_off, ora.pdoc, ora.pval, ora.n_docs = term_off, pdoc, pval, n
     qs = S.msmarco_like_queries(16, v, seed=3)
     assert dev.search(qs, 1000) == ora.score_ids(qs, 1000, n_threads=16)
+
+
+@pytest.mark.parametrize("k", [10, 1000])
+def test_block_max_exact_equals_oracle(L, synth, k, monkeypatch):
+    """configs[4] block-max skipping (di_index_set_block_max): factor 1 skips only wave
+    segments whose upper bound is below the query's running threshold -- the exact
+    ranking; a larger factor is approximate, but every doc it returns carries its full
+    score (a segment is scored for all terms or not at all) in key order."""
+    term_off, pdoc, pval, ora = synth
+    monkeypatch.setenv("DI_SCORE_THRESHOLD", "1")  # (3 blocks: force the shared threshold)
+    dev = L.DeviceIndex.from_postings(term_off, pdoc, pval)
+    qs = _queries(5000, 80, seed=k + 1) + _long_queries(5000, 2, seed=k, lo=65, hi=90)
+    want = ora.score_ids(qs, k, n_threads=8)
+    dev.set_block_max(1.0)
+    assert dev.search(qs, k) == want
+    dev.set_block_max(4.0)
+    got = dev.search(qs, k)
+    full = ora.score_ids(qs, ora.n_docs, n_threads=8)
+    for g, f in zip(got, full):
+        true = dict(f)
+        assert all(true[d] == s for d, s in g)
+        assert [s for _, s in g] == sorted((s for _, s in g), reverse=True)
+    dev.set_block_max(0.0)
+    assert dev.search(qs, k) == want
+    with pytest.raises(L.DIError):
+        dev.set_block_max(0.5)
+
+
+def test_million_block_max_exact(L, million):
+    """Block-max skipping, factor 1, at 34 blocks and the scaled vocabulary: exact."""
+    from improving_learned_index_amd import synthetic as S
+
+    term_off, pdoc, pval, ora = million
+    dev = L.DeviceIndex.from_postings(term_off, pdoc, pval, 0, ora.n_docs)
+    dev.set_block_max(1.0)
+    qs = S.msmarco_like_queries(24, 2_200_000, seed=5) + _queries(2_200_000, 8, seed=5)
+    assert dev.search(qs, 1000) == ora.score_ids(qs, 1000, n_threads=16)

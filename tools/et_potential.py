@@ -17,9 +17,10 @@ sys.path.insert(0, str(ROOT))
 from improving_learned_index_amd import synthetic as S  # noqa: E402
 
 
-def main(n_docs=1_100_000, n_q=40):
-    to, pd, pv, _ = S.synth_postings(n_docs, 200_000, seed=4321)
-    qs = S.msmarco_like_queries(n_q, 200_000, seed=1234)
+def main(n_docs=1_100_000, n_q=40, v_terms=None):
+    v_terms = v_terms or 2 * n_docs  # V scales with N
+    to, pd, pv, _ = S.synth_postings(n_docs, v_terms, seed=4321)
+    qs = S.msmarco_like_queries(n_q, v_terms, seed=1234)
     out = {}
     for R in (64, 256, 2048, 32768):
         alive, post_alive = [], []
@@ -42,9 +43,9 @@ def main(n_docs=1_100_000, n_q=40):
             post_alive.append(pa / max(tot, 1))
         out[str(R)] = {"alive_ranges": float(np.mean(alive)),
                        "alive_postings": float(np.mean(post_alive))}
-    print(json.dumps({"workload": f"{n_docs}-doc synthetic shard, {n_q} queries, top-1000",
-                      "by_range_docs": out}))
+    print(json.dumps({"workload": f"{n_docs}-doc synthetic shard, V = {v_terms}, {n_q} queries, "
+                                  "top-1000", "by_range_docs": out}))
 
 
 if __name__ == "__main__":
-    main()
+    main(v_terms=int(sys.argv[1]) if len(sys.argv) > 1 else None)

@@ -1,11 +1,12 @@
 """BASELINE configs[4] sweep: queries/s vs recall@1000 on a full-scale shard.
 
-Two knobs of the scorer, on one 8-way shard of configs[2] (1.1M docs, the bench's
-retrieve_shard generator) with 6980 dev.small-shaped queries at top-1000:
+Two knobs of the scorer, on a full-scale collection (default: full MS MARCO-sized,
+8.8M docs on one GPU; the bench's generator, V = 2 N) with 6980 dev.small-shaped
+queries at top-1000:
   * query-time impact pruning (di_index_set_min_impact): score only postings of value
     >= 2^floor(log2 m) -- approximate, the recall column measures it;
-  * safe early termination (DI_EARLY_TERMINATION=1, exact: recall 1.0 by construction,
-    checked here).
+  * block-max skipping (di_index_set_block_max): factor 1 exact (recall 1.0 by
+    construction, checked here), > 1 approximate.
 Recall@1000 = |pruned top-1000 ∩ exact top-1000| / |exact|, averaged over queries.
 Device time per batch = score_blocks + merge_topk over all the batch's launches.
     python tools/prune_sweep.py [n_docs] > profiles/r02_prune_sweep.json
@@ -37,34 +38,40 @@ def run(ix, flat, cuq, nq, k, reps=3):
 
 
 def main():
-    n_docs = int(sys.argv[1]) if len(sys.argv) > 1 else 1_100_000
-    v_terms, nq, k = 200_000, 6980, 1000
+    n_docs = int(sys.argv[1]) if len(sys.argv) > 1 else 8_800_000
+    v_terms, nq, k = 2 * n_docs, 6980, 1000
     term_off, pdoc, pval, _ = S.synth_postings(n_docs, v_terms, seed=4321)
     queries = S.msmarco_like_queries(nq, v_terms, seed=1234)
     flat, cuq = _lib.csr(queries)
     rows, exact = [], None
-    for et in ("0", "1"):
-        os.environ["DI_EARLY_TERMINATION"] = et
-        ix = _lib.DeviceIndex.from_postings(term_off, pdoc, pval, 0, n_docs)
-        ix.reserve(nq, k)
-        for mi in ((1, 2, 4, 8, 16, 32, 64, 128) if et == "0" else (1,)):
-            ix.set_min_impact(mi)
-            thr = 1 << (mi.bit_length() - 1)
-            posts = sum(int((pval[term_off[t]:term_off[t + 1]] >= thr).sum())
-                        for qq in queries for t in qq)
-            docs, n, dev_s, wall = run(ix, flat, cuq, nq, k)
-            res = [set(docs[i, :n[i]].tolist()) for i in range(nq)]
-            if exact is None:
-                exact = res
-            rec = float(np.mean([len(a & b) / max(len(b), 1) for a, b in zip(res, exact)]))
-            rows.append({"early_termination": et == "1", "min_impact": mi,
-                         "postings_per_query": posts / nq, "device_queries_per_s": nq / dev_s,
-                         "host_call_queries_per_s": nq / wall, "device_ms": dev_s * 1000,
-                         "recall_at_1000": rec})
-            print(json.dumps(rows[-1]), file=sys.stderr, flush=True)
-        del ix
-    print(json.dumps({"sweep": "configs[4]: query-time impact pruning and safe early "
-                               "termination of the quantized scorer",
+    ix = _lib.DeviceIndex.from_postings(term_off, pdoc, pval, 0, n_docs)
+    ix.reserve(nq, k)
+    lens = np.diff(term_off)
+    for mi, bm in [(m, 0.0) for m in (1, 2, 4, 8, 16, 32, 64, 128)] + \
+                  [(1, f) for f in (1.0, 1.25, 1.5, 2.0, 3.0, 4.0)]:
+        ix.set_min_impact(mi)
+        ix.set_block_max(bm)
+        thr = 1 << (mi.bit_length() - 1)
+        if thr == 1:
+            per_term = lens
+        else:  # postings of value >= thr per term (empty terms: reduceat's quirk masked)
+            per_term = np.add.reduceat((pval >= thr).astype(np.int64),
+                                       np.minimum(term_off[:-1], max(len(pval) - 1, 0)))
+            per_term[lens == 0] = 0
+        posts = int(per_term[flat.astype(np.int64)].sum())
+        docs, n, dev_s, wall = run(ix, flat, cuq, nq, k)
+        res = [set(docs[i, :n[i]].tolist()) for i in range(nq)]
+        if exact is None:
+            exact = res
+        rec = float(np.mean([len(a & b) / max(len(b), 1) for a, b in zip(res, exact)]))
+        rows.append({"min_impact": mi, "block_max_factor": bm,
+                     "postings_per_query": posts / nq, "device_queries_per_s": nq / dev_s,
+                     "host_call_queries_per_s": nq / wall, "device_ms": dev_s * 1000,
+                     "recall_at_1000": rec})
+        print(json.dumps(rows[-1]), file=sys.stderr, flush=True)
+    del ix
+    print(json.dumps({"sweep": "configs[4]: query-time impact pruning and block-max "
+                               "skipping of the quantized scorer",
                       "workload": f"{n_docs}-doc shard (synth_postings seed 4321), {nq} "
                                   f"dev.small-shaped queries, top-{k}",
                       "rows": rows}))
