@@ -591,6 +591,7 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
         sh.n_tie = 0;
         for (int i = 0; i < WTERMS / 32; ++i) sh.lmask[i] = 0;
         for (int i = 0; i < WSEG; ++i) sh.wub[i] = 0;
+        sh.tq = 0;
     }
     __syncthreads();
 
@@ -761,7 +762,12 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
         const uint32_t tq0 = read_tq();
         const float thr = bm_factor * (float)tq0;
         skip_wave = tq0 > 0 && (float)sh.wub[wave] < thr;
-        if (__syncthreads_and(tq0 > 0 && (float)sh.wub[tid & (WSEG - 1)] < thr)) {
+        // every segment below: lanes 0..15 of each wave check one each (no block
+        // reduction: __syncthreads_and would take static LDS, and the scatter needs the
+        // dynamic segment at address 0)
+        static_assert(WSEG <= 64, "one lane per segment");
+        const bool below = lane >= WSEG || (tq0 > 0 && (float)sh.wub[lane] < thr);
+        if (__ballot(below) == ~0ull) {
             if (tid == 0) *cn = 0;
             return;
         }
@@ -885,8 +891,19 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
         // term boundary: this term's LDS writes land before any wave reads the next
         if (j + 1 < nt) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     }
-    // the asm LDS writes; the threshold histogram's LDS-DMA copy
+    // the asm LDS writes; the threshold histogram's LDS-DMA copy.  The first half of the
+    // threshold read (read_tq) goes before the barrier: thread t's own 4 bins are the
+    // 16 B its own LDS-DMA wrote (no barrier needed to read them), their wave suffix
+    // sums go to wsum -- the barrier the scatter needs anyway publishes them.
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    uint32_t tq_hv[4] = {0, 0, 0, 0}, tq_c = 0, tq_sfx = 0;
+    if (qpre) {
+        const uint4 h = reinterpret_cast<const uint4 *>(sh.u.hist)[tid];
+        tq_hv[0] = h.x, tq_hv[1] = h.y, tq_hv[2] = h.z, tq_hv[3] = h.w;
+        tq_c = h.x + h.y + h.z + h.w;
+        tq_sfx = wave_suffix_sum(tq_c);
+        if (lane == 0) sh.wsum[wave] = tq_sfx;
+    }
     __syncthreads();
 
     stamp(1);  // scatter
@@ -941,13 +958,33 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
     // still gives a valid lower bound.
     uint32_t Tq = 0;
     if (qh) {
-        Tq = read_tq();
+        // second half of read_tq over the suffix sums published by the scatter barrier:
+        // the crossing thread writes tq (0 from the item's start when the histogram
+        // holds fewer than k candidates); one barrier
+        for (int w2 = wave + 1; w2 < SC_WAVES; ++w2) tq_sfx += sh.wsum[w2];
+        if (tq_sfx >= (uint32_t)k && tq_sfx - tq_c < (uint32_t)k) {
+            uint32_t above = tq_sfx - tq_c;
+            int e = 3;
+            for (; e > 0; --e) {
+                if (above + tq_hv[e] >= (uint32_t)k) break;
+                above += tq_hv[e];
+            }
+            sh.tq = (uint32_t)(4 * tid + e);
+        }
+        __syncthreads();
+        Tq = sh.tq;
+        // (wsum is written again only after a barrier of the selection below; tq only
+        // at the next item's start)
         if (Tq > 0) {
+            // one sweep: the docs reaching Tq (usually a few dozen) are appended by
+            // wave-aggregated LDS atomics in any order (the merge orders them by key)
             const uint32_t thr_w = Tq << 16;
-            const uint32_t n = compact_words(
-                sh, n_local, tid, [thr_w](uint32_t w, int) { return w >= thr_w ? 1u : 0u; },
-                [&](int, uint32_t pos, uint32_t w, int idx) { cand(pos, w, idx); });
-            const uint32_t na = n & 0xFFFFu;
+            sweep_words(sh.acc, n_local, tid, [&](uint32_t w, int idx) {
+                uint32_t pos;
+                if (wave_append(w >= thr_w, &sh.emit, pos)) cand(pos, w, idx);
+            });
+            __syncthreads();
+            const uint32_t na = sh.emit;
             if (na <= (uint32_t)k) {
                 flush(na);
                 if (tid == 0) *cn = (int32_t)na;
