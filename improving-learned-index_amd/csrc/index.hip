@@ -56,7 +56,7 @@ constexpr int MAX_TERMS = DI_SHORT_QUERY_TERMS;  // query terms of the compact w
 // run every term that way (short terms: every wave reads the sublist, applies its own
 // docs); longer ones run the all-wave form, a barrier per term.
 constexpr int WSEG = SC_WAVES;
-constexpr int WLONG_MIN = 1024;
+constexpr int WLONG_MIN = 512;  // (1024 / 512 / 256 / 64: within 1%, profiles/r03j)
 constexpr int WTERMS = 64;
 // Fast selection: with at most 16 query terms every score is below 255 * 16 < 4096,
 // so one pass of a 4096-bin score histogram finds the k-th score; the docs tied at
@@ -1739,11 +1739,14 @@ void build_index(di_index *ix, const int64_t *term_off, int64_t n_terms, const u
     });
     epos[n_ent] = (uint32_t)total;
 
-    // long sublists (>= WLONG_MIN postings) get ids in entry order
+    // long sublists (>= WLONG_MIN postings) get ids in entry order (DI_WLONG_MIN
+    // overrides the threshold: layout A/B only, any value is exact)
+    uint32_t wlong_min = WLONG_MIN;
+    if (const char *e = std::getenv("DI_WLONG_MIN")) wlong_min = (uint32_t)std::max(1, std::atoi(e));
     std::vector<uint32_t> lid((size_t)std::max<uint64_t>(n_ent, 1), NO);
     uint32_t n_long = 0;
     for (uint64_t e = 0; e < n_ent; ++e)
-        if (epos[e + 1] - epos[e] >= (uint32_t)WLONG_MIN) lid[e] = n_long++;
+        if (epos[e + 1] - epos[e] >= wlong_min) lid[e] = n_long++;
     ix->n_long = n_long;
 
     // pass 3: order inside every sublist, the impact-class offsets and the block max.
