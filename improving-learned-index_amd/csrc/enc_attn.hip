@@ -269,7 +269,7 @@ attention_kernel(const T *__restrict__ qk, const T *__restrict__ vt,
 // Fragment reads are inline-asm ds_reads with their lgkmcnt wait in the same statement
 // (the compiler would otherwise drain the in-flight prefetch with vmcnt(0) before an
 // LDS read it cannot tell apart from the DMA's destination).
-constexpr int AX_WAVES = 8, AX_QT = 2, AX_KC = 64;  // keys per staged chunk (2 x 32)
+constexpr int AX_WAVES = 8, AX_QT = 2;
 // Image swizzle: slot j of key row r at j ^ ax_swz(r), ax_swz(r) = r0 r1 r3 in bits 1-3.
 // A ds_read_b128 lane group (16 lanes: rows c&3 + 8 (c>>2) + 4 t, slot bit 0 = g) and a
 // ds_read_b64_tr_b16 lane group (32 lanes: rows q + 8 g + 4 h2, slot bit 0 = p>>1)
@@ -277,13 +277,23 @@ constexpr int AX_WAVES = 8, AX_QT = 2, AX_KC = 64;  // keys per staged chunk (2 
 // (r & 15 conflicts 2-way on both).  Row bit 5 (the 32-key sub-chunk) is not used, so
 // the sub-chunk stays an immediate offset.
 __device__ __forceinline__ int ax_swz(int r) { return ((r & 3) << 1) | (r & 8); }
-constexpr int AX_IMG = AX_KC * 256, AX_STAGE = 2 * AX_IMG;
-constexpr int AX_LDS = 2 * AX_STAGE;
+// LDS: [K image, buffer 0 | K, buffer 1 | V, buffer 0 | V, buffer 1], one image = KC
+// key rows of 256 B; every fragment read's (buffer, sub-chunk) offset is an immediate
+// (< 64 KiB for KC <= 128).
+template <int KC>
+constexpr int ax_lds() {
+    return 4 * KC * 256;
+}
 
+// KC: keys per staged chunk (a multiple of 64; one barrier per chunk); PRIO: raise the
+// wave's issue priority over its MFMA blocks.
+template <int KC, bool PRIO>
 __global__ void __launch_bounds__(64 * AX_WAVES)
 attention_x3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu_seqlens, int H,
                     int n_heads, int n_pairs, bf16 *__restrict__ ctx_split,
                     const int32_t *__restrict__ qsel, const int32_t *__restrict__ cu_qsel) {
+    static_assert(KC % 64 == 0 && KC <= 128, "chunk: 64 or 128 keys");
+    constexpr int AX_KC = KC, AX_IMG = KC * 256;
     // qsel (optional, the pruned last layer): only the query rows qsel[cu_qsel[d] ..)
     // (doc-local token indices) of document d are computed, into ctx rows cu_qsel[d] + i;
     // keys and values are every token of the document either way.
@@ -329,20 +339,21 @@ attention_x3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
     };
     // chunk ci of unit u -> stage buffer b: key rows 8 wave..+7 of K and of V (two
     // 1 KiB pieces each), 16 B per lane, source slots permuted by the swizzle
+    // (piece pc: key rows 64 (pc >> 1) + 8 wave + 4 (pc & 1) + lane >> 4)
     const int sr = 8 * wave + (lane >> 4);
     auto stage = [&](const Unit &u, int ci, int b) {
         const bf16 *kg = qkv + split_col(H + u.h * ATT_D);      // + key row * ld: 256 B
         const bf16 *vg = qkv + split_col(2 * H + u.h * ATT_D);
 #pragma unroll
-        for (int pc = 0; pc < 2; ++pc) {
-            const int row = u.tok0 + min(ci * AX_KC + sr + 4 * pc, u.n - 1);
-            const int j = (lane & 15) ^ ax_swz(sr + 4 * pc);
-            __builtin_amdgcn_global_load_lds(
-                (const void *)(kg + row * ld + j * 8),
-                (lds_void *)(lds + b * AX_STAGE + wave * 2048 + pc * 1024), 16, 0, 0);
-            __builtin_amdgcn_global_load_lds(
-                (const void *)(vg + row * ld + j * 8),
-                (lds_void *)(lds + b * AX_STAGE + AX_IMG + wave * 2048 + pc * 1024), 16, 0, 0);
+        for (int pc = 0; pc < AX_KC / 32; ++pc) {
+            const int rl = 64 * (pc >> 1) + sr + 4 * (pc & 1);
+            const int row = u.tok0 + min(ci * AX_KC + rl, u.n - 1);
+            const int j = (lane & 15) ^ ax_swz(rl);
+            const int dst = b * AX_IMG + (pc >> 1) * 16384 + wave * 2048 + (pc & 1) * 1024;
+            __builtin_amdgcn_global_load_lds((const void *)(kg + row * ld + j * 8),
+                                             (lds_void *)(lds + dst), 16, 0, 0);
+            __builtin_amdgcn_global_load_lds((const void *)(vg + row * ld + j * 8),
+                                             (lds_void *)(lds + 2 * AX_IMG + dst), 16, 0, 0);
         }
     };
     // B operands Q^T of unit u, lane (g, c): Q[q_base + 16 qt + c][32 ch + 8 g + e]
@@ -363,7 +374,7 @@ attention_x3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
             }
         }
     };
-    // fragment addresses (buffer 0; buffer 1 is the immediate offset AX_STAGE)
+    // fragment addresses (buffer 0; buffer 1 is the immediate offset AX_IMG)
     uint32_t ka[2][2][2];  // [t][ch][hi, lo]: key row 8 (c >> 2) + 4 t + (c & 3)
 #pragma unroll
     for (int t = 0; t < 2; ++t)
@@ -387,7 +398,7 @@ attention_x3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
                 const int q = c >> 2, pp = c & 3;
                 const int r = 8 * g + 4 * h2 + q;
                 const int j = (dt >> 1) * 8 + pt * 4 + 2 * (dt & 1) + (pp >> 1);
-                va[dt][pt][h2] = lds_base + AX_IMG + r * 256 + ((j ^ ax_swz(r)) << 4) + 8 * (pp & 1);
+                va[dt][pt][h2] = lds_base + 2 * AX_IMG + r * 256 + ((j ^ ax_swz(r)) << 4) + 8 * (pp & 1);
             }
 
     Unit cu;
@@ -472,17 +483,19 @@ attention_x3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
         : "memory")
 #define AX_SEL(M)                                                                                  \
     do {                                                                                           \
-        if (b == 0 && u == 0)                                                                      \
-            M(0);                                                                                  \
-        else if (b == 0)                                                                           \
-            M(8192);                                                                               \
-        else if (u == 0)                                                                           \
-            M(32768);                                                                              \
-        else                                                                                       \
-            M(40960);                                                                              \
+        switch (b * AX_IMG + u * 8192) {                                                           \
+        case 0: M(0); break;                                                                       \
+        case 8192: M(8192); break;                                                                 \
+        case 16384: M(16384); break;                                                               \
+        case 24576: M(24576); break;                                                               \
+        case 32768: M(32768); break;                                                               \
+        case 40960: M(40960); break;                                                               \
+        case 49152: M(49152); break;                                                               \
+        default: M(57344); break;                                                                  \
+        }                                                                                          \
     } while (0)
-            // (immediate offset: buffer b at b * AX_STAGE, sub-chunk u at u * 32 rows)
-            static_assert(AX_STAGE == 32768 && AX_KC == 64, "AX_READ offsets");
+            // (immediate offset: buffer b at b * AX_IMG, sub-chunk u at u * 32 rows; u is
+            // a constant of the unrolled loop, so each site keeps two cases)
             AX_SEL(AX_READ_K);
             __builtin_amdgcn_sched_barrier(0);
             bf16x8 kfr[2][2][2];  // [t][ch][hi, lo]
@@ -499,6 +512,7 @@ attention_x3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
             for (int qt = 0; qt < AX_QT; ++qt)
 #pragma unroll
                 for (int t = 0; t < 2; ++t) s[qt][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+            if (PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
             for (int ch = 0; ch < 2; ++ch)
 #pragma unroll
@@ -510,6 +524,7 @@ attention_x3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
                             s[qt][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
                                 kfr[t][ch][p == 1], p == 2 ? ql[qt][ch] : qh[qt][ch], s[qt][t], 0,
                                 0, 0);
+            if (PRIO) __builtin_amdgcn_s_setprio(0);
             __builtin_amdgcn_sched_barrier(0);
             AX_SEL(AX_READ_V);
             __builtin_amdgcn_sched_barrier(0);
@@ -575,6 +590,7 @@ attention_x3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
                                                 vt2[dt][pt][1].x, vt2[dt][pt][1].y);
                     __builtin_memcpy(&vfr[dt][pt], &v4, 16);
                 }
+            if (PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
             for (int p = 0; p < 3; ++p)
 #pragma unroll
@@ -583,6 +599,7 @@ attention_x3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
                     for (int dt = 0; dt < 4; ++dt)
                         o[qt][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
                             vfr[dt][p == 1], p == 2 ? pl[qt] : ph[qt], o[qt][dt], 0, 0, 0);
+            if (PRIO) __builtin_amdgcn_s_setprio(0);
             }
         }
         if (has_q) {
@@ -635,8 +652,30 @@ void launch_attention_x3(const bf16 *qkv, const int32_t *cu_seqlens, int n_docs,
     const int64_t n_pairs = (int64_t)n_docs * n_heads;
     DI_REQUIRE(n_pairs < (1ll << 31), DI_ERANGE, "attention grid too large");
     const int grid = (int)std::min<int64_t>(n_pairs, n_cu());  // persistent, one per CU
-    hipLaunchKernelGGL(attention_x3_kernel, dim3(grid), dim3(64 * AX_WAVES), AX_LDS, s, qkv,
-                       cu_seqlens, H, n_heads, (int)n_pairs, ctx_split, qsel, cu_qsel);
+    // DI_ATTN_X3 (developer A/B): bit 0 = 128-key chunks, bit 1 = MFMA priority
+    static const int variant = [] {
+        const char *e = getenv("DI_ATTN_X3");
+        return e ? atoi(e) & 3 : 0;
+    }();
+#define AX_LAUNCH(KC, PR)                                                                      \
+    do {                                                                                       \
+        static bool attr_ = false;                                                             \
+        if (!attr_) {                                                                          \
+            DI_HIP(hipFuncSetAttribute((const void *)attention_x3_kernel<KC, PR>,              \
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, ax_lds<KC>())); \
+            attr_ = true;                                                                      \
+        }                                                                                      \
+        hipLaunchKernelGGL((attention_x3_kernel<KC, PR>), dim3(grid), dim3(64 * AX_WAVES),     \
+                           ax_lds<KC>(), s, qkv, cu_seqlens, H, n_heads, (int)n_pairs,         \
+                           ctx_split, qsel, cu_qsel);                                          \
+    } while (0)
+    switch (variant) {
+    case 1: AX_LAUNCH(128, false); break;
+    case 2: AX_LAUNCH(64, true); break;
+    case 3: AX_LAUNCH(128, true); break;
+    default: AX_LAUNCH(64, false); break;
+    }
+#undef AX_LAUNCH
     check_launch("attention_x3");
 }
 

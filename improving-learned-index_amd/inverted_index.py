@@ -36,13 +36,14 @@ class InvertedIndex:
     """
 
     def __init__(self, index_path: Union[str, Path], device: int = 0, doc_lo: int = 0,
-                 doc_hi: int = 0, min_impact: int = 1):
+                 doc_hi: int = 0, min_impact: int = 1, block_max: float = 0.0):
         self.index_path = Path(index_path)
         self.vocab = self._load_vocab()
         self.device = device
         self.doc_lo, self.doc_hi = doc_lo, doc_hi
         self._dev = DeviceIndex.from_reference_dir(self.index_path, doc_lo, doc_hi, device)
         self.set_min_impact(min_impact)
+        self.set_block_max(block_max)
 
     def set_min_impact(self, min_impact: int) -> None:
         """Query-time impact pruning (config 5): score only postings of value >= the
@@ -50,6 +51,13 @@ class InvertedIndex:
         ranking).  Recall trade-off: DESIGN.md §4."""
         self.min_impact = int(min_impact)
         self._dev.set_min_impact(self.min_impact)
+
+    def set_block_max(self, factor: float) -> None:
+        """Block-max skipping (configs[4]): 0 off; 1 skips only wave segments of a block
+        whose impact upper bound is below the query's running k-th score (the exact
+        ranking); f > 1 skips those below f times it (approximate)."""
+        self.block_max = float(factor)
+        self._dev.set_block_max(self.block_max)
 
     def _load_vocab(self):
         vocab = dict()

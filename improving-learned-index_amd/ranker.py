@@ -31,7 +31,7 @@ class Ranker:
                  qrels_path: Optional[Union[str, Path]] = None, pairwise: bool = False,
                  dataset_type: Optional[str] = COLLECTION_TYPES[0], tokenizer_path=None,
                  device: int = 0, top_k: int = 1000, batch_queries: int = 8192,
-                 min_impact: int = 1):
+                 min_impact: int = 1, block_max: float = 0.0):
         if pairwise:
             raise NotImplementedError("pairwise terms are outside this build (SURVEY §8f F4)")
         if tokenizer_path is not None:
@@ -58,7 +58,7 @@ class Ranker:
             lo, hi = parallel.shard_range(n[0], self.world, self.rank)
         self.device = device
         self.index = InvertedIndex(index_path=index_path, device=device, doc_lo=lo, doc_hi=hi,
-                                   min_impact=min_impact)
+                                   min_impact=min_impact, block_max=block_max)
         self.run_file = RunFile(run_file_path=output_path) if self.rank == 0 else None
         self.top_k = top_k
         self.batch_queries = batch_queries
@@ -106,10 +106,13 @@ def main(argv=None):
     p.add_argument("--min_impact", type=int, default=1,
                    help="query-time pruning: score postings with value >= this (rounded down "
                         "to a power of two); 1 = exact")
+    p.add_argument("--block_max", type=float, default=0.0,
+                   help="block-max skipping: 0 off, 1 exact, > 1 approximate (skip block "
+                        "segments whose bound is below this factor x the running k-th score)")
     a = p.parse_args(argv)
     Ranker(a.index_path, a.queries_path, a.output_path, a.num_workers, a.qrels_path, a.pairwise,
            a.dataset_type, a.tokenizer_path, a.device, top_k=a.top_k,
-           min_impact=a.min_impact).run()
+           min_impact=a.min_impact, block_max=a.block_max).run()
 
 
 if __name__ == "__main__":

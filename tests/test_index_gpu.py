@@ -294,6 +294,9 @@ def test_inverted_index_min_impact_matches_pruned_oracle(L):
     assert [[list(x) for x in g] for g in ix.score_batch(fx["queries"], 1000)] == fx["top1000"]
     with pytest.raises(Exception):
         ix.set_min_impact(0)
+    # configs[4] knob of the drop-in (rank --block_max): factor 1 is the exact ranking
+    ex = InvertedIndex(GOLDEN / "index", block_max=1.0)
+    assert [[list(x) for x in g] for g in ex.score_batch(fx["queries"], 1000)] == fx["top1000"]
 
 
 def test_shared_threshold_off_equals_oracle(L, synth, monkeypatch):
