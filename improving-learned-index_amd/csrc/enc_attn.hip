@@ -286,12 +286,17 @@ constexpr int ax_lds() {
 }
 
 // KC: keys per staged chunk (a multiple of 64; one barrier per chunk); PRIO: raise the
-// wave's issue priority over its MFMA blocks.
-template <int KC, bool PRIO>
+// wave's issue priority over its MFMA blocks; BAL: wave w owns the 16-query tiles w and
+// w + 8 of a pass (instead of 2w, 2w + 1), so the tiles of a short pass spread over the
+// four SIMDs (wave w runs on SIMD w % 4), and a tile with no query is skipped.
+template <int KC, bool PRIO, bool BAL>
 __global__ void __launch_bounds__(64 * AX_WAVES)
 attention_x3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu_seqlens, int H,
                     int n_heads, int n_pairs, bf16 *__restrict__ ctx_split,
-                    const int32_t *__restrict__ qsel, const int32_t *__restrict__ cu_qsel) {
+                    const int32_t *__restrict__ qsel, const int32_t *__restrict__ cu_qsel,
+                    int abl) {
+    // abl (developer timing ablations, wrong results): 1 no softmax arithmetic, 2 no S^T
+    // products, 4 no O^T products
     static_assert(KC % 64 == 0 && KC <= 128, "chunk: 64 or 128 keys");
     constexpr int AX_KC = KC, AX_IMG = KC * 256;
     // qsel (optional, the pruned last layer): only the query rows qsel[cu_qsel[d] ..)
@@ -358,12 +363,13 @@ attention_x3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
     };
     // B operands Q^T of unit u, lane (g, c): Q[q_base + 16 qt + c][32 ch + 8 g + e]
     // (hi; lo 32 later)
+    // first query (within its pass) of this wave's tile qt
+    auto qtile = [&](int qt) { return BAL ? 16 * (wave + 8 * qt) : wave * (AX_QT * 16) + 16 * qt; };
     auto load_q = [&](const Unit &u, bf16x8 (&qh)[AX_QT][2], bf16x8 (&ql)[AX_QT][2]) {
-        const int q_base = u.pass * PASS_Q + wave * (AX_QT * 16);
         const bf16 *qbase = qkv + split_col(u.h * ATT_D) + 8 * g;
 #pragma unroll
         for (int qt = 0; qt < AX_QT; ++qt) {
-            const int qi = min(q_base + 16 * qt + c, u.nq - 1);
+            const int qi = min(u.pass * PASS_Q + qtile(qt) + c, u.nq - 1);
             const int qloc = qsel ? min(max(qsel[u.q0 + qi], 0), u.n - 1) : qi;
             const int qrow = u.tok0 + qloc;
 #pragma unroll
@@ -416,8 +422,9 @@ attention_x3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
     int b = 0;  // stage buffer of the next chunk to compute
     for (;;) {
         const int n = cu.n, h = cu.h, q0 = cu.q0, nq = cu.nq;
-        const int q_base = cu.pass * PASS_Q + wave * (AX_QT * 16);
-        const bool has_q = q_base < nq;
+        const int q_pass = cu.pass * PASS_Q;
+        const bool has_q = q_pass + qtile(0) < nq;
+        const bool two = BAL ? q_pass + qtile(1) < nq : has_q;  // (uniform) tile 1 has queries
         const int n_chunks = (n + AX_KC - 1) / AX_KC;
         Unit nu;
         const bool more = next_unit(cu, nu);
@@ -440,6 +447,9 @@ attention_x3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
                 load_q(nu, qnh, qnl);
             }
             if (!has_q) continue;
+            // the chunk's sub-chunks for the wave's NQT non-empty query tiles
+            auto chunk = [&](auto nqt_c) {
+            constexpr int NQT = decltype(nqt_c)::value;
 #pragma unroll
             for (int u = 0; u < AX_KC / 32; ++u) {  // 32-key sub-chunks
             const int key0 = ci * AX_KC + 32 * u;
@@ -509,16 +519,17 @@ attention_x3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
             // accumulators before the next (one accumulator's 3 products are a chain)
             f32x4 s[AX_QT][2];
 #pragma unroll
-            for (int qt = 0; qt < AX_QT; ++qt)
+            for (int qt = 0; qt < NQT; ++qt)
 #pragma unroll
                 for (int t = 0; t < 2; ++t) s[qt][t] = f32x4{0.f, 0.f, 0.f, 0.f};
             if (PRIO) __builtin_amdgcn_s_setprio(1);
+            if (!(abl & 2))
 #pragma unroll
             for (int ch = 0; ch < 2; ++ch)
 #pragma unroll
                 for (int p = 0; p < 3; ++p)
 #pragma unroll
-                    for (int qt = 0; qt < AX_QT; ++qt)
+                    for (int qt = 0; qt < NQT; ++qt)
 #pragma unroll
                         for (int t = 0; t < 2; ++t)
                             s[qt][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
@@ -530,8 +541,17 @@ attention_x3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
             __builtin_amdgcn_sched_barrier(0);
             const bool full = key0 + 32 <= n;  // (uniform) no masked key in this sub-chunk
             bf16x8 ph[AX_QT], pl[AX_QT];
+            if (abl & 1) {
 #pragma unroll
-            for (int qt = 0; qt < AX_QT; ++qt) {
+                for (int qt = 0; qt < NQT; ++qt)
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) {
+                        ph[qt][e] = (bf16)s[qt][e >> 2][e & 3];
+                        pl[qt][e] = ph[qt][e];
+                    }
+            } else
+#pragma unroll
+            for (int qt = 0; qt < NQT; ++qt) {
                 // lane holds S^T[key0 + 8 g + 4 t + r][q_base + 16 qt + c]
                 float cmax = -INFINITY;
 #pragma unroll
@@ -591,16 +611,22 @@ attention_x3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
                     __builtin_memcpy(&vfr[dt][pt], &v4, 16);
                 }
             if (PRIO) __builtin_amdgcn_s_setprio(1);
+            if (!(abl & 4))
 #pragma unroll
             for (int p = 0; p < 3; ++p)
 #pragma unroll
-                for (int qt = 0; qt < AX_QT; ++qt)
+                for (int qt = 0; qt < NQT; ++qt)
 #pragma unroll
                     for (int dt = 0; dt < 4; ++dt)
                         o[qt][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
                             vfr[dt][p == 1], p == 2 ? pl[qt] : ph[qt], o[qt][dt], 0, 0, 0);
             if (PRIO) __builtin_amdgcn_s_setprio(0);
             }
+            };
+            if (two)
+                chunk(std::integral_constant<int, 2>{});
+            else
+                chunk(std::integral_constant<int, 1>{});
         }
         if (has_q) {
 #pragma unroll
@@ -609,7 +635,7 @@ attention_x3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
                 l += __shfl_xor(l, 16, 64);
                 l += __shfl_xor(l, 32, 64);
                 const float inv = 1.0f / l;
-                const int q = q_base + 16 * qt + c;
+                const int q = q_pass + qtile(qt) + c;
                 if (q < nq) {
                     bf16 *out = ctx_split + (int64_t)(q0 + q) * 2 * H;
 #pragma unroll
@@ -652,28 +678,37 @@ void launch_attention_x3(const bf16 *qkv, const int32_t *cu_seqlens, int n_docs,
     const int64_t n_pairs = (int64_t)n_docs * n_heads;
     DI_REQUIRE(n_pairs < (1ll << 31), DI_ERANGE, "attention grid too large");
     const int grid = (int)std::min<int64_t>(n_pairs, n_cu());  // persistent, one per CU
-    // DI_ATTN_X3 (developer A/B): bit 0 = 128-key chunks, bit 1 = MFMA priority
+    // DI_ATTN_X3 (developer A/B): bit 0 = 128-key chunks, bit 1 = MFMA priority, bit 2 =
+    // balanced query tiles
     static const int variant = [] {
         const char *e = getenv("DI_ATTN_X3");
-        return e ? atoi(e) & 3 : 0;
+        return e ? atoi(e) & 7 : 0;
     }();
-#define AX_LAUNCH(KC, PR)                                                                      \
+    static const int abl = [] {
+        const char *e = getenv("DI_ATTN_X3_ABLATE");
+        return e ? atoi(e) : 0;
+    }();
+#define AX_LAUNCH(KC, PR, BL)                                                                  \
     do {                                                                                       \
         static bool attr_ = false;                                                             \
         if (!attr_) {                                                                          \
-            DI_HIP(hipFuncSetAttribute((const void *)attention_x3_kernel<KC, PR>,              \
+            DI_HIP(hipFuncSetAttribute((const void *)attention_x3_kernel<KC, PR, BL>,          \
                                        hipFuncAttributeMaxDynamicSharedMemorySize, ax_lds<KC>())); \
             attr_ = true;                                                                      \
         }                                                                                      \
-        hipLaunchKernelGGL((attention_x3_kernel<KC, PR>), dim3(grid), dim3(64 * AX_WAVES),     \
+        hipLaunchKernelGGL((attention_x3_kernel<KC, PR, BL>), dim3(grid), dim3(64 * AX_WAVES), \
                            ax_lds<KC>(), s, qkv, cu_seqlens, H, n_heads, (int)n_pairs,         \
-                           ctx_split, qsel, cu_qsel);                                          \
+                           ctx_split, qsel, cu_qsel, abl);                                     \
     } while (0)
     switch (variant) {
-    case 1: AX_LAUNCH(128, false); break;
-    case 2: AX_LAUNCH(64, true); break;
-    case 3: AX_LAUNCH(128, true); break;
-    default: AX_LAUNCH(64, false); break;
+    case 1: AX_LAUNCH(128, false, false); break;
+    case 2: AX_LAUNCH(64, true, false); break;
+    case 3: AX_LAUNCH(128, true, false); break;
+    case 4: AX_LAUNCH(64, false, true); break;
+    case 5: AX_LAUNCH(128, false, true); break;
+    case 6: AX_LAUNCH(64, true, true); break;
+    case 7: AX_LAUNCH(128, true, true); break;
+    default: AX_LAUNCH(64, false, false); break;
     }
 #undef AX_LAUNCH
     check_launch("attention_x3");

@@ -1,16 +1,18 @@
 #!/bin/bash
-# A/B of attention_x3 variants (DI_ATTN_X3 bits: 1 = 128-key chunks, 2 = MFMA priority)
-# on the bench's encode_x3 leg, one box, alternating; attention ms per step per run.
-# Usage: VARIANTS="0 1 2 3" REPS=2 bash tools/ab_attn.sh
+# A/B of attention_x3 variants (DI_ATTN_X3 bits: 1 = 128-key chunks, 2 = MFMA priority,
+# 4 = balanced query tiles; ":a" = DI_ATTN_X3_ABLATE a, timing only) on the bench's
+# encode_x3 leg, one box, alternating; attention ms per step per run.
+# Usage: VARIANTS="0 4 0:1 0:2 0:4" REPS=2 bash tools/ab_attn.sh
 set -o pipefail
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 OUT="$R/gpurun_out/ab_attn"
 mkdir -p "$OUT"
 for rep in $(seq 1 ${REPS:-2}); do
-  for v in ${VARIANTS:-0 1 2 3}; do
-    DI_ATTN_X3=$v timeout -k 10 ${RUN_TIMEOUT:-240} python3 "$R/bench.py" --steps 3 --warmup 1 \
-      --no-cpu --legs encode_x3 > "$OUT/v${v}_r${rep}.json" 2> "$OUT/v${v}_r${rep}.err" || exit $?
-    python3 - "$OUT/v${v}_r${rep}.json" "$v" <<'PY'
+  for va in ${VARIANTS:-0 4}; do
+    v=${va%%:*}; a=0; [ "$va" != "$v" ] && a=${va#*:}
+    DI_ATTN_X3=$v DI_ATTN_X3_ABLATE=$a timeout -k 10 ${RUN_TIMEOUT:-240} python3 "$R/bench.py" --steps 3 --warmup 1 \
+      --no-cpu --legs encode_x3 > "$OUT/v${v}a${a}_r${rep}.json" 2> "$OUT/v${v}a${a}_r${rep}.err" || exit $?
+    python3 - "$OUT/v${v}a${a}_r${rep}.json" "$va" <<'PY'
 import json, sys
 for l in open(sys.argv[1]):
     if l.startswith("{"):
