@@ -277,19 +277,18 @@ constexpr int AX_WAVES = 8, AX_QT = 2;
 // (r & 15 conflicts 2-way on both).  Row bit 5 (the 32-key sub-chunk) is not used, so
 // the sub-chunk stays an immediate offset.
 __device__ __forceinline__ int ax_swz(int r) { return ((r & 3) << 1) | (r & 8); }
-// LDS: [K image, buffer 0 | K, buffer 1 | V, buffer 0 | V, buffer 1], one image = KC
-// key rows of 256 B; every fragment read's (buffer, sub-chunk) offset is an immediate
-// (< 64 KiB for KC <= 128).
-template <int KC>
-constexpr int ax_lds() {
-    return 4 * KC * 256;
-}
+// LDS: [K image, buffer 0 | K, buffer 1 | V, buffer 0 | V, buffer 1], one image = AX_KC
+// key rows of 256 B; every fragment read's (buffer, sub-chunk) offset is an immediate.
+// (Measured: 128-key chunks -- half the barriers -- and raised MFMA issue priority
+// were both slower, r03 ab_attn.)
+constexpr int AX_KC = 64, AX_IMG = AX_KC * 256, AX_LDS = 4 * AX_IMG;
 
-// KC: keys per staged chunk (a multiple of 64; one barrier per chunk); PRIO: raise the
-// wave's issue priority over its MFMA blocks; BAL: wave w owns the 16-query tiles w and
-// w + 8 of a pass (instead of 2w, 2w + 1), so the tiles of a short pass spread over the
-// four SIMDs (wave w runs on SIMD w % 4), and a tile with no query is skipped.
-template <int KC, bool PRIO, bool BAL>
+// BAL: wave w owns the 16-query tiles w and w + 8 of a pass (instead of 2w, 2w + 1), so
+// the tiles of a short pass spread over the four SIMDs (wave w runs on SIMD w % 4), and
+// a tile with no query is skipped.  LAZY: the softmax's reference max moves only when a
+// score exceeds it by 8 / sc (p <= 2^8): one max per lane and one ballot in the common
+// case instead of the cross-lane max; the scale folds into the exponent's fma.
+template <bool BAL, bool LAZY>
 __global__ void __launch_bounds__(64 * AX_WAVES)
 attention_x3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu_seqlens, int H,
                     int n_heads, int n_pairs, bf16 *__restrict__ ctx_split,
@@ -297,8 +296,6 @@ attention_x3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
                     int abl) {
     // abl (developer timing ablations, wrong results): 1 no softmax arithmetic, 2 no S^T
     // products, 4 no O^T products
-    static_assert(KC % 64 == 0 && KC <= 128, "chunk: 64 or 128 keys");
-    constexpr int AX_KC = KC, AX_IMG = KC * 256;
     // qsel (optional, the pruned last layer): only the query rows qsel[cu_qsel[d] ..)
     // (doc-local token indices) of document d are computed, into ctx rows cu_qsel[d] + i;
     // keys and values are every token of the document either way.
@@ -428,11 +425,13 @@ attention_x3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
         const int n_chunks = (n + AX_KC - 1) / AX_KC;
         Unit nu;
         const bool more = next_unit(cu, nu);
-        float m[AX_QT], lsum[AX_QT];
+        float m[AX_QT], lsum[AX_QT], lim[AX_QT], mneg[AX_QT];
         f32x4 o[AX_QT][4];
 #pragma unroll
         for (int qt = 0; qt < AX_QT; ++qt) {
             m[qt] = -INFINITY;
+            lim[qt] = -INFINITY;
+            mneg[qt] = 0.f;
             lsum[qt] = 0.f;
 #pragma unroll
             for (int dt = 0; dt < 4; ++dt) o[qt][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -491,6 +490,26 @@ attention_x3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
           "v"(va[2][0][0]), "v"(va[2][0][1]), "v"(va[2][1][0]), "v"(va[2][1][1]),                 \
           "v"(va[3][0][0]), "v"(va[3][0][1]), "v"(va[3][1][0]), "v"(va[3][1][1])                  \
         : "memory")
+#define AX_READ_VW(OFF)                                                                             \
+    asm volatile(                                                                                  \
+        "ds_read_b64_tr_b16 %0, %16 offset:" #OFF "\n\tds_read_b64_tr_b16 %1, %17 offset:" #OFF    \
+        "\n\tds_read_b64_tr_b16 %2, %18 offset:" #OFF "\n\tds_read_b64_tr_b16 %3, %19 offset:" #OFF \
+        "\n\tds_read_b64_tr_b16 %4, %20 offset:" #OFF "\n\tds_read_b64_tr_b16 %5, %21 offset:" #OFF \
+        "\n\tds_read_b64_tr_b16 %6, %22 offset:" #OFF "\n\tds_read_b64_tr_b16 %7, %23 offset:" #OFF \
+        "\n\tds_read_b64_tr_b16 %8, %24 offset:" #OFF "\n\tds_read_b64_tr_b16 %9, %25 offset:" #OFF \
+        "\n\tds_read_b64_tr_b16 %10, %26 offset:" #OFF "\n\tds_read_b64_tr_b16 %11, %27 offset:" #OFF \
+        "\n\tds_read_b64_tr_b16 %12, %28 offset:" #OFF "\n\tds_read_b64_tr_b16 %13, %29 offset:" #OFF \
+        "\n\tds_read_b64_tr_b16 %14, %30 offset:" #OFF "\n\tds_read_b64_tr_b16 %15, %31 offset:" #OFF \
+        "\n\ts_waitcnt lgkmcnt(0)"                                                                 \
+        : "=&v"(vt2[0][0][0]), "=&v"(vt2[0][0][1]), "=&v"(vt2[0][1][0]), "=&v"(vt2[0][1][1]),     \
+          "=&v"(vt2[1][0][0]), "=&v"(vt2[1][0][1]), "=&v"(vt2[1][1][0]), "=&v"(vt2[1][1][1]),     \
+          "=&v"(vt2[2][0][0]), "=&v"(vt2[2][0][1]), "=&v"(vt2[2][1][0]), "=&v"(vt2[2][1][1]),     \
+          "=&v"(vt2[3][0][0]), "=&v"(vt2[3][0][1]), "=&v"(vt2[3][1][0]), "=&v"(vt2[3][1][1])      \
+        : "v"(va[0][0][0]), "v"(va[0][0][1]), "v"(va[0][1][0]), "v"(va[0][1][1]),                 \
+          "v"(va[1][0][0]), "v"(va[1][0][1]), "v"(va[1][1][0]), "v"(va[1][1][1]),                 \
+          "v"(va[2][0][0]), "v"(va[2][0][1]), "v"(va[2][1][0]), "v"(va[2][1][1]),                 \
+          "v"(va[3][0][0]), "v"(va[3][0][1]), "v"(va[3][1][0]), "v"(va[3][1][1])                  \
+        : "memory")
 #define AX_SEL(M)                                                                                  \
     do {                                                                                           \
         switch (b * AX_IMG + u * 8192) {                                                           \
@@ -522,7 +541,6 @@ attention_x3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
             for (int qt = 0; qt < NQT; ++qt)
 #pragma unroll
                 for (int t = 0; t < 2; ++t) s[qt][t] = f32x4{0.f, 0.f, 0.f, 0.f};
-            if (PRIO) __builtin_amdgcn_s_setprio(1);
             if (!(abl & 2))
 #pragma unroll
             for (int ch = 0; ch < 2; ++ch)
@@ -535,9 +553,13 @@ attention_x3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
                             s[qt][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
                                 kfr[t][ch][p == 1], p == 2 ? ql[qt][ch] : qh[qt][ch], s[qt][t], 0,
                                 0, 0);
-            if (PRIO) __builtin_amdgcn_s_setprio(0);
             __builtin_amdgcn_sched_barrier(0);
-            AX_SEL(AX_READ_V);
+            // (BAL: the V^T reads with their wait in one statement -- its higher register
+            // pressure made the compiler copy a V^T register before a separate wait)
+            if constexpr (BAL)
+                AX_SEL(AX_READ_VW);
+            else
+                AX_SEL(AX_READ_V);
             __builtin_amdgcn_sched_barrier(0);
             const bool full = key0 + 32 <= n;  // (uniform) no masked key in this sub-chunk
             bf16x8 ph[AX_QT], pl[AX_QT];
@@ -549,6 +571,46 @@ attention_x3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
                         ph[qt][e] = (bf16)s[qt][e >> 2][e & 3];
                         pl[qt][e] = ph[qt][e];
                     }
+            } else if (LAZY) {
+#pragma unroll
+                for (int qt = 0; qt < NQT; ++qt) {
+                    // raw scores (masked keys -inf); the reference max m is in raw units
+                    float v[8];
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) {
+                        const int key = key0 + 8 * g + e;  // (t = e >> 2, r = e & 3)
+                        v[e] = (full || key < n) ? s[qt][e >> 2][e & 3] : -INFINITY;
+                    }
+                    const float lmax = fmaxf(fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3])),
+                                             fmaxf(fmaxf(v[4], v[5]), fmaxf(v[6], v[7])));
+                    // (always at a unit's first sub-chunk: lim = -inf, key 0 is valid)
+                    if (__any(lmax > lim[qt])) {
+                        float cmax = lmax;  // over the 4 lane groups: permlane swaps
+                        const auto p16 = __builtin_amdgcn_permlane16_swap(
+                            __float_as_uint(cmax), __float_as_uint(cmax), false, false);
+                        cmax = fmaxf(__uint_as_float(p16[0]), __uint_as_float(p16[1]));
+                        const auto p32 = __builtin_amdgcn_permlane32_swap(
+                            __float_as_uint(cmax), __float_as_uint(cmax), false, false);
+                        cmax = fmaxf(__uint_as_float(p32[0]), __uint_as_float(p32[1]));
+                        const float m_new = fmaxf(m[qt], cmax);
+                        if (m_new != m[qt]) {  // (per lane; 0 at the first)
+                            const float alpha = __builtin_amdgcn_exp2f((m[qt] - m_new) * sc);
+                            lsum[qt] *= alpha;
+#pragma unroll
+                            for (int dt = 0; dt < 4; ++dt) o[qt][dt] *= alpha;
+                        }
+                        m[qt] = m_new;
+                        lim[qt] = m_new + 8.0f / sc;
+                        mneg[qt] = -m_new * sc;
+                    }
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) {
+                        const float pr = __builtin_amdgcn_exp2f(fmaf(v[e], sc, mneg[qt]));
+                        lsum[qt] += pr;
+                        ph[qt][e] = split_hi(pr);
+                        pl[qt][e] = split_lo(pr);
+                    }
+                }
             } else
 #pragma unroll
             for (int qt = 0; qt < NQT; ++qt) {
@@ -591,6 +653,7 @@ attention_x3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
                         pl[qt][4 * t + r] = split_lo(pr);
                     }
             }
+            if constexpr (!BAL)
             asm volatile("s_waitcnt lgkmcnt(0)"
                          : "+v"(vt2[0][0][0]), "+v"(vt2[0][0][1]), "+v"(vt2[0][1][0]),
                            "+v"(vt2[0][1][1]), "+v"(vt2[1][0][0]), "+v"(vt2[1][0][1]),
@@ -610,7 +673,6 @@ attention_x3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
                                                 vt2[dt][pt][1].x, vt2[dt][pt][1].y);
                     __builtin_memcpy(&vfr[dt][pt], &v4, 16);
                 }
-            if (PRIO) __builtin_amdgcn_s_setprio(1);
             if (!(abl & 4))
 #pragma unroll
             for (int p = 0; p < 3; ++p)
@@ -620,7 +682,6 @@ attention_x3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
                     for (int dt = 0; dt < 4; ++dt)
                         o[qt][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
                             vfr[dt][p == 1], p == 2 ? pl[qt] : ph[qt], o[qt][dt], 0, 0, 0);
-            if (PRIO) __builtin_amdgcn_s_setprio(0);
             }
             };
             if (two)
@@ -666,6 +727,7 @@ attention_x3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
     }
 #undef AX_READ_K
 #undef AX_READ_V
+#undef AX_READ_VW
 #undef AX_SEL
 }
 
@@ -678,37 +740,24 @@ void launch_attention_x3(const bf16 *qkv, const int32_t *cu_seqlens, int n_docs,
     const int64_t n_pairs = (int64_t)n_docs * n_heads;
     DI_REQUIRE(n_pairs < (1ll << 31), DI_ERANGE, "attention grid too large");
     const int grid = (int)std::min<int64_t>(n_pairs, n_cu());  // persistent, one per CU
-    // DI_ATTN_X3 (developer A/B): bit 0 = 128-key chunks, bit 1 = MFMA priority, bit 2 =
-    // balanced query tiles
+    // DI_ATTN_X3 (developer A/B): bit 2 = balanced query tiles, bit 3 = lazy softmax max
     static const int variant = [] {
         const char *e = getenv("DI_ATTN_X3");
-        return e ? atoi(e) & 7 : 0;
+        return e ? atoi(e) & 12 : 0;
     }();
     static const int abl = [] {
         const char *e = getenv("DI_ATTN_X3_ABLATE");
         return e ? atoi(e) : 0;
     }();
-#define AX_LAUNCH(KC, PR, BL)                                                                  \
-    do {                                                                                       \
-        static bool attr_ = false;                                                             \
-        if (!attr_) {                                                                          \
-            DI_HIP(hipFuncSetAttribute((const void *)attention_x3_kernel<KC, PR, BL>,          \
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, ax_lds<KC>())); \
-            attr_ = true;                                                                      \
-        }                                                                                      \
-        hipLaunchKernelGGL((attention_x3_kernel<KC, PR, BL>), dim3(grid), dim3(64 * AX_WAVES), \
-                           ax_lds<KC>(), s, qkv, cu_seqlens, H, n_heads, (int)n_pairs,         \
-                           ctx_split, qsel, cu_qsel, abl);                                     \
-    } while (0)
+#define AX_LAUNCH(BL, LZ)                                                                      \
+    hipLaunchKernelGGL((attention_x3_kernel<BL, LZ>), dim3(grid), dim3(64 * AX_WAVES), AX_LDS, s, \
+                       qkv, cu_seqlens, H, n_heads, (int)n_pairs, ctx_split, qsel, cu_qsel, abl)
+    // (BAL alone, r03 ab_attn: -3.5%; not instantiated -- its compiled form copies a
+    // V^T register before the read's wait, tests/test_asm_waits_cpu.py)
     switch (variant) {
-    case 1: AX_LAUNCH(128, false, false); break;
-    case 2: AX_LAUNCH(64, true, false); break;
-    case 3: AX_LAUNCH(128, true, false); break;
-    case 4: AX_LAUNCH(64, false, true); break;
-    case 5: AX_LAUNCH(128, false, true); break;
-    case 6: AX_LAUNCH(64, true, true); break;
-    case 7: AX_LAUNCH(128, true, true); break;
-    default: AX_LAUNCH(64, false, false); break;
+    case 8: AX_LAUNCH(false, true); break;
+    case 12: AX_LAUNCH(true, true); break;
+    default: AX_LAUNCH(false, false); break;
     }
 #undef AX_LAUNCH
     check_launch("attention_x3");

@@ -16,6 +16,7 @@ process (the keys totally order score, first touch and doc).
 from __future__ import annotations
 
 import argparse
+from itertools import product
 from pathlib import Path
 from typing import Optional, Union
 
@@ -32,8 +33,12 @@ class Ranker:
                  dataset_type: Optional[str] = COLLECTION_TYPES[0], tokenizer_path=None,
                  device: int = 0, top_k: int = 1000, batch_queries: int = 8192,
                  min_impact: int = 1, block_max: float = 0.0):
-        if pairwise:
-            raise NotImplementedError("pairwise terms are outside this build (SURVEY §8f F4)")
+        # pairwise (F4): every query also scores the ordered pair terms 't1|t2' of its
+        # distinct terms (ranker.py:53-58), the keys a pairwise impact collection holds
+        # (deep_impact_collection.py:36-45).  The reference takes the query terms from
+        # its PhoBERT / VnCoreNLP class for this mode (out of scope); here
+        # they come from the configured tokenizer, like the plain mode.
+        self.pairwise = pairwise
         if tokenizer_path is not None:
             DeepImpact.set_tokenizer(tokenizer_path)
         self.queries = Queries(queries_path=queries_path, dataset_type=dataset_type)
@@ -64,7 +69,12 @@ class Ranker:
         self.batch_queries = batch_queries
 
     def get_query_terms(self, qid):
-        return DeepImpact.process_query(query=self.queries[qid])
+        terms = DeepImpact.process_query(query=self.queries[qid])
+        if self.pairwise:  # (product materialises both operands before the adds)
+            for term1, term2 in product(terms, terms):
+                if term1 != term2:
+                    terms.add(f"{term1}|{term2}")
+        return terms
 
     def run(self):
         qids = self.query_iterator

@@ -147,6 +147,48 @@ def test_create_and_rank_cli_match_reference():
         assert (td / "run.tsv").read_text() == "".join(want)
 
 
+def test_rank_pairwise_scores_pair_terms():
+    """F4 pairwise mode (ranker.py:53-58): each query also scores the ordered pair terms
+    't1|t2' of its distinct terms, against a collection holding pair keys (the
+    DeepPairwiseImpactCollection format); run file equal to the oracle's scores over
+    the same expanded term set."""
+    from itertools import product
+
+    from improving_learned_index_amd.inverted_index import InvertedIndexCreator
+    from improving_learned_index_amd.models import DeepImpact
+    from improving_learned_index_amd.ranker import Ranker
+
+    fx = json.loads((GOLDEN / "score.json").read_text())
+    with tempfile.TemporaryDirectory() as td:
+        td = Path(td)
+        lines = []
+        for line in (GOLDEN / "collection.quantized").read_text().split("\n")[:-1]:
+            parts = [p.split(": ") for p in line.split(", ")] if line else []
+            extra = [f"{a}|{b}: {(int(x) * 7 + int(y)) % 255 + 1}"
+                     for (a, x), (b, y) in product(parts[:4], parts[:4]) if a != b]
+            lines.append(", ".join([line] + extra if line else extra))
+        coll = td / "pairs.quantized"
+        coll.write_text("\n".join(lines) + "\n")
+        InvertedIndexCreator(coll, td / "index").run()
+        qf = td / "queries.tsv"
+        texts = [" ".join(t.lstrip("▁") for t in q) for q in fx["queries"][:40]]
+        qf.write_text("".join(f"q{i}\t{t}\n" for i, t in enumerate(texts)))
+        Ranker(td / "index", qf, td / "run.tsv", pairwise=True,
+               tokenizer_path=GOLDEN / "tokenizer.json").run()
+        ora = oracle.Index(td / "index")
+        want, n_pair_hits = [], 0
+        for i, t in enumerate(texts):
+            terms = DeepImpact.process_query(t)
+            for a, b in product(terms, terms):
+                if a != b:
+                    terms.add(f"{a}|{b}")
+            n_pair_hits += sum("|" in x and x in ora.vocab for x in terms)
+            for r, (d, s) in enumerate(ora.score(terms, 1000), start=1):
+                want.append(f"q{i}\t{d}\t{r}\t{s}\n")
+        assert n_pair_hits > 0  # some pair terms exist in the index
+        assert (td / "run.tsv").read_text() == "".join(want)
+
+
 def test_reranker_cli_on_the_hip_encoder(small_ckpt):
     """F3 (reranker.py:13-91): the rerank CLI on the HIP encoder (fp32) scores every
     candidate as the sum of its query terms' impacts; those equal the fp32 torch
