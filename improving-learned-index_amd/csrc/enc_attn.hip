@@ -287,8 +287,11 @@ constexpr int AX_KC = 64, AX_IMG = AX_KC * 256, AX_LDS = 4 * AX_IMG;
 // the tiles of a short pass spread over the four SIMDs (wave w runs on SIMD w % 4), and
 // a tile with no query is skipped.  LAZY: the softmax's reference max moves only when a
 // score exceeds it by 8 / sc (p <= 2^8): one max per lane and one ballot in the common
-// case instead of the cross-lane max; the scale folds into the exponent's fma.
-template <bool BAL, bool LAZY>
+// case instead of the cross-lane max; the scale folds into the exponent's fma.  PIPE
+// (with both, two query tiles): tile 1's S^T products interleaved with tile 0's
+// exponentials, tile 0's O^T products with tile 1's (sched_group_barrier), so the
+// softmax issues in the MFMAs' shadow.
+template <bool BAL, bool LAZY, bool PIPE = false>
 __global__ void __launch_bounds__(64 * AX_WAVES)
 attention_x3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu_seqlens, int H,
                     int n_heads, int n_pairs, bf16 *__restrict__ ctx_split,
@@ -534,6 +537,109 @@ attention_x3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
                 for (int ch = 0; ch < 2; ++ch)
 #pragma unroll
                     for (int pt = 0; pt < 2; ++pt) __builtin_memcpy(&kfr[t][ch][pt], &kf[t][ch][pt], 16);
+            if constexpr (PIPE && NQT == 2) {
+            static_assert(BAL && LAZY, "PIPE builds on the balanced lazy form");
+            const bool full = key0 + 32 <= n;  // (uniform) no masked key in this sub-chunk
+            f32x4 s[AX_QT][2];
+            float v[AX_QT][8];
+            bf16x8 ph[AX_QT], pl[AX_QT];
+            // S^T of tile qt (12 MFMAs; the two accumulators' chains interleaved)
+            auto s_mfma = [&](int qt) {
+                s[qt][0] = s[qt][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int ch = 0; ch < 2; ++ch)
+#pragma unroll
+                    for (int p = 0; p < 3; ++p)
+#pragma unroll
+                        for (int t = 0; t < 2; ++t)
+                            s[qt][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                                kfr[t][ch][p == 1], p == 2 ? ql[qt][ch] : qh[qt][ch], s[qt][t],
+                                0, 0, 0);
+            };
+            // softmax part A of tile qt: masked raw scores, the lazy max test and the rare
+            // rescale (a branch: outside the interleaved regions)
+            auto soft_a = [&](int qt) {
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    const int key = key0 + 8 * g + e;
+                    v[qt][e] = (full || key < n) ? s[qt][e >> 2][e & 3] : -INFINITY;
+                }
+                const float lmax = fmaxf(fmaxf(fmaxf(v[qt][0], v[qt][1]), fmaxf(v[qt][2], v[qt][3])),
+                                         fmaxf(fmaxf(v[qt][4], v[qt][5]), fmaxf(v[qt][6], v[qt][7])));
+                if (__any(lmax > lim[qt])) {
+                    float cmax = lmax;
+                    const auto p16 = __builtin_amdgcn_permlane16_swap(
+                        __float_as_uint(cmax), __float_as_uint(cmax), false, false);
+                    cmax = fmaxf(__uint_as_float(p16[0]), __uint_as_float(p16[1]));
+                    const auto p32 = __builtin_amdgcn_permlane32_swap(
+                        __float_as_uint(cmax), __float_as_uint(cmax), false, false);
+                    cmax = fmaxf(__uint_as_float(p32[0]), __uint_as_float(p32[1]));
+                    const float m_new = fmaxf(m[qt], cmax);
+                    if (m_new != m[qt]) {
+                        const float alpha = __builtin_amdgcn_exp2f((m[qt] - m_new) * sc);
+                        lsum[qt] *= alpha;
+#pragma unroll
+                        for (int dt = 0; dt < 4; ++dt) o[qt][dt] *= alpha;
+                    }
+                    m[qt] = m_new;
+                    lim[qt] = m_new + 8.0f / sc;
+                    mneg[qt] = -m_new * sc;
+                }
+            };
+            // softmax part B: the exponentials, row sums and split probabilities
+            auto soft_b = [&](int qt) {
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    const float pr = __builtin_amdgcn_exp2f(fmaf(v[qt][e], sc, mneg[qt]));
+                    lsum[qt] += pr;
+                    ph[qt][e] = split_hi(pr);
+                    pl[qt][e] = split_lo(pr);
+                }
+            };
+            bf16x8 vfr[4][2];
+            auto o_mfma = [&](int qt) {
+#pragma unroll
+                for (int p = 0; p < 3; ++p)
+#pragma unroll
+                    for (int dt = 0; dt < 4; ++dt)
+                        o[qt][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                            vfr[dt][p == 1], p == 2 ? pl[qt] : ph[qt], o[qt][dt], 0, 0, 0);
+            };
+            // 1 MFMA : 4 VALU (incl. transcendental) groups over a 12-MFMA region
+#define AX_INTERLEAVE()                                                                            \
+    do {                                                                                           \
+        _Pragma("unroll") for (int i_ = 0; i_ < 12; ++i_) {                                        \
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                                     \
+            __builtin_amdgcn_sched_group_barrier(0x402, 4, 0);                                     \
+        }                                                                                          \
+    } while (0)
+            s_mfma(0);
+            __builtin_amdgcn_sched_barrier(0);
+            AX_SEL(AX_READ_VW);  // (their wait overlaps tile 0's products)
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+                for (int pt = 0; pt < 2; ++pt) {
+                    const uint4 v4 = make_uint4(vt2[dt][pt][0].x, vt2[dt][pt][0].y,
+                                                vt2[dt][pt][1].x, vt2[dt][pt][1].y);
+                    __builtin_memcpy(&vfr[dt][pt], &v4, 16);
+                }
+            soft_a(0);
+            __builtin_amdgcn_sched_barrier(0);
+            s_mfma(1);
+            soft_b(0);
+            AX_INTERLEAVE();
+            __builtin_amdgcn_sched_barrier(0);
+            soft_a(1);
+            __builtin_amdgcn_sched_barrier(0);
+            o_mfma(0);
+            soft_b(1);
+            AX_INTERLEAVE();
+            __builtin_amdgcn_sched_barrier(0);
+            o_mfma(1);
+#undef AX_INTERLEAVE
+            } else {
             // S^T for both query tiles, each product stage over the 4 independent
             // accumulators before the next (one accumulator's 3 products are a chain)
             f32x4 s[AX_QT][2];
@@ -682,6 +788,7 @@ attention_x3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
                     for (int dt = 0; dt < 4; ++dt)
                         o[qt][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
                             vfr[dt][p == 1], p == 2 ? pl[qt] : ph[qt], o[qt][dt], 0, 0, 0);
+            }  // (PIPE)
             }
             };
             if (two)
@@ -740,24 +847,25 @@ void launch_attention_x3(const bf16 *qkv, const int32_t *cu_seqlens, int n_docs,
     const int64_t n_pairs = (int64_t)n_docs * n_heads;
     DI_REQUIRE(n_pairs < (1ll << 31), DI_ERANGE, "attention grid too large");
     const int grid = (int)std::min<int64_t>(n_pairs, n_cu());  // persistent, one per CU
-    // DI_ATTN_X3 (developer A/B): bit 2 = balanced query tiles, bit 3 = lazy softmax max
+    // balanced tiles + lazy max + interleaved softmax (r03 ab_attn: attention -8.5%,
+    // then -3% per step); DI_ATTN_X3 (developer A/B): 0 = the round-2 form, 12 = no
+    // interleave
     static const int variant = [] {
         const char *e = getenv("DI_ATTN_X3");
-        return e ? atoi(e) & 12 : 0;
+        return e ? atoi(e) & 28 : 28;
     }();
     static const int abl = [] {
         const char *e = getenv("DI_ATTN_X3_ABLATE");
         return e ? atoi(e) : 0;
     }();
-#define AX_LAUNCH(BL, LZ)                                                                      \
-    hipLaunchKernelGGL((attention_x3_kernel<BL, LZ>), dim3(grid), dim3(64 * AX_WAVES), AX_LDS, s, \
-                       qkv, cu_seqlens, H, n_heads, (int)n_pairs, ctx_split, qsel, cu_qsel, abl)
-    // (BAL alone, r03 ab_attn: -3.5%; not instantiated -- its compiled form copies a
-    // V^T register before the read's wait, tests/test_asm_waits_cpu.py)
+#define AX_LAUNCH(BL, LZ, PP)                                                                  \
+    hipLaunchKernelGGL((attention_x3_kernel<BL, LZ, PP>), dim3(grid), dim3(64 * AX_WAVES), AX_LDS, \
+                       s, qkv, cu_seqlens, H, n_heads, (int)n_pairs, ctx_split, qsel, cu_qsel, abl)
+    // (r03 ab_attn, attention ms per step: BAL alone -3.5%, LAZY alone -5.6%, both -8.5%)
     switch (variant) {
-    case 8: AX_LAUNCH(false, true); break;
-    case 12: AX_LAUNCH(true, true); break;
-    default: AX_LAUNCH(false, false); break;
+    case 12: AX_LAUNCH(true, true, false); break;
+    case 28: AX_LAUNCH(true, true, true); break;
+    default: AX_LAUNCH(false, false, false); break;
     }
 #undef AX_LAUNCH
     check_launch("attention_x3");

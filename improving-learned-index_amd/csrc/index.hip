@@ -205,11 +205,12 @@ __device__ __forceinline__ bool wave_append(bool take, uint32_t *cursor, uint32_
     return take;
 }
 
-// Device posting words are ((doc_in_block << 8) | value) XOR POST_X, never 0 (values
-// are >= 1).  A buffer load past the descriptor's range returns 0: a padding lane of a
-// round, whose update goes to its own dummy word past the block (MAX_BLOCK_DOCS +
-// lane: one word per lane, so the padding lanes of an instruction hit 32 distinct
-// banks instead of all writing one word).
+// Device posting words are ((doc_in_block << 8) | value) XOR POST_X.  A buffer load
+// past the descriptor's range returns 0, which decodes to doc MAX_BLOCK_DOCS -- the
+// dummy accumulator word after the block -- with value 0: the padding lanes of a
+// round need no clamp, no select and no branch (their update lands in the dummy).
+// (Per-lane dummy words for the padding, with a quad-wise threshold sweep, measured
+// 4.5% slower, r03pad; the quad sweep alone neutral, r03quad.)
 constexpr uint32_t POST_X = (uint32_t)MAX_BLOCK_DOCS << 8;
 
 // One scatter round over postings p[0 .. min(avail, UU * SC_THREADS)) (lane-
@@ -254,11 +255,8 @@ __device__ __forceinline__ void scatter_apply(uint32_t *acc, const uint32_t (&cu
 #pragma unroll
     for (int u = 0; u < UU; ++u) {
         a[u] = ((cur[u] ^ POST_X) >> 8) << 2;
-        // (FILT: padding has value 0 < vmin)
         if constexpr (FILT)
             a[u] = (cur[u] & 255u) >= vmin ? a[u] : (uint32_t)(MAX_BLOCK_DOCS + lane_id()) << 2;
-        else
-            a[u] = cur[u] ? a[u] : (uint32_t)(MAX_BLOCK_DOCS + lane_id()) << 2;
         asm volatile("ds_read_b32 %0, %1" : "=v"(w[u]) : "v"(a[u]) : "memory");
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -793,9 +791,7 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
     auto is_long = [&](int j) { return wl && ((sh.lmask[j >> 5] >> (j & 31)) & 1u); };
     const uint32_t wseg = ((uint32_t)block_docs + WSEG - 1) / WSEG;
     const uint32_t wdlo = (uint32_t)wave * wseg;
-    // (16 wseg >= block_docs: the segments cover the block; padding decodes to doc
-    // MAX_BLOCK_DOCS, outside every segment -> the lane's dummy)
-    const uint32_t wdn = wseg;
+    const uint32_t wdn = wave == WSEG - 1 ? 0x7FFFFFFFu - wdlo : wseg;  // last: the rest
     const uint32_t wdummy = (uint32_t)(MAX_BLOCK_DOCS + lane) << 2;
     const uint32_t vmin = 1u << (7 - min(min_cls, 7));  // all-wave form: pruning by value
     for (int j = (ablate & 1) || skip_wave ? nt : 0; j < nt; ++j) {  // ablate bit 0: skip (profiling)
