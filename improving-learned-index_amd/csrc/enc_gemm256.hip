@@ -27,6 +27,7 @@
 // fragment reads, lgkmcnt(0), before the phase's first barrier).  Per iteration of
 // 8 phases (K tiles 2i in buffer 0, 2i+1 in buffer 1):
 //   ph1 buf1<-B1(2i+1)  ph2 buf0<-A0(2i+2)  ph3 buf0<-B0(2i+2)  ph4 buf0<-A1(2i+2)
+//   (i = 0: B1(1) comes with the tile's prologue instead)
 //   ph5 buf0<-B1(2i+2)  ph6 buf1<-A0(2i+3)  ph7 buf1<-B0(2i+3)  ph8 buf1<-A1(2i+3)
 // Counted waits (never 0 in steady state): phase 4 waits vmcnt(6) -- everything
 // but the last three half tiles, i.e. all of K tile 2i+1 -- which phase 5 reads
@@ -250,7 +251,11 @@ __global__ void __launch_bounds__(G2_T) gemm256_kernel(GemmArgs g) {
             par1k(g.row_ln + m0r + 128, G2_PAR_ROW + 1024);
         }
     };
-    // prologue of a tile: K tile 0 whole, K tile 1 minus its B1 half
+    // prologue of a tile: K tiles 0 and 1 whole (8 loads each).  Issued before the
+    // previous tile's stores, so the first iteration's phase-4 wait (K tile 1) can leave
+    // those stores in flight: they must land only by phase 8 (K tile 2, issued after
+    // them) instead of phase 4 -- the stores are ~12-20% of a split GEMM when exposed
+    // (profiles/r03_gemm_check_ablations.txt, ablate 4).
     auto prologue = [&]() {
         G2_STAGE_A(0, 0, 0);
         G2_STAGE_B(0, 0, 0);
@@ -259,13 +264,16 @@ __global__ void __launch_bounds__(G2_T) gemm256_kernel(GemmArgs g) {
         G2_STAGE_A(1, 0, 1);
         G2_STAGE_B(1, 0, 1);
         G2_STAGE_A(1, 1, 1);
+        G2_STAGE_B(1, 1, 1);
     };
+    constexpr int NST = g2_stores<EPI, SPLIT>();
+    bool pend = false;  // (uniform) the previous tile's NST stores are in flight
 
     int pb = 0;  // parameter slot of the current tile
     setup(tix);
     stage_params(pb);
     prologue();
-    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    G2_WAITV(8);  // K tile 0 (and the parameters); K tile 1 in flight
     for (;;) {
         G2_BAR();
         if (wr == 1) G2_BAR();  // group 1 runs one barrier behind group 0
@@ -276,10 +284,10 @@ __global__ void __launch_bounds__(G2_T) gemm256_kernel(GemmArgs g) {
 
         for (int t = 0; t < nk; t += 2) {
             const bool more = t + 2 < nk;  // K tiles t+2, t+3 exist (nk is even)
-            // phase 1: buffer 0, A0 + B0
+            // phase 1: buffer 0, A0 + B0 (K tile 1's B1 half came with the prologue)
             G2_READ_B(0, 0);
             G2_READ_A(0, 0);
-            G2_STAGE_B(1, 1, t + 1);
+            if (t > 0) G2_STAGE_B(1, 1, t + 1);
             G2_SYNC_READS();
             G2_BAR();
             G2_MFMA(0, 0);
@@ -298,12 +306,16 @@ __global__ void __launch_bounds__(G2_T) gemm256_kernel(GemmArgs g) {
             G2_BAR();
             G2_MFMA(4, 2);
             G2_BAR();
-            // phase 4: registers only; retire K tile t+1 for phase 5
+            // phase 4: registers only; retire K tile t+1 for phase 5 (first iteration:
+            // the previous tile's stores, younger than K tile 1, may stay in flight)
             if (more) {
                 G2_STAGE_A(0, 1, t + 2);
-                asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+                if (t == 0 && pend)
+                    G2_WAITV((6 + NST));
+                else
+                    G2_WAITV(6);
             } else {
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                G2_WAITV(0);
             }
             G2_BAR();
             G2_MFMA(0, 2);
@@ -691,11 +703,12 @@ __global__ void __launch_bounds__(G2_T) gemm256_kernel(GemmArgs g) {
             stores(std::false_type{});
         if (!has_next) break;
         // (4) retire the next tile's K tile 0 (the parameters are older still), leaving
-        // this tile's stores in flight when their count is known
-        if (full && !vtile && !(g.ablate & 4))
-            G2_WAITV((6 + g2_stores<EPI, SPLIT>()));
+        // K tile 1 and this tile's stores in flight when their count is known
+        pend = full && !vtile && !(g.ablate & 4) && NST > 0;
+        if (pend)
+            G2_WAITV((8 + NST));
         else
-            G2_WAITV(6);
+            G2_WAITV(8);
         tix = nxt;
         pb ^= 1;
     }
