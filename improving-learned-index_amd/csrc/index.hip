@@ -86,7 +86,7 @@ struct ScoreShared {
         int64_t bounds[2][MAX_TERMS];  // scatter: sublist [lo, hi) of every query term
         uint32_t h256[256];            // fast path: digit histogram over the tie list
     } v;
-    alignas(16) uint32_t wsum[SC_WAVES];
+    uint32_t wsum[SC_WAVES];
     uint32_t emit;   // output cursor
     uint32_t n_tie;  // tie-list cursor
     uint32_t bad;
@@ -275,35 +275,11 @@ __device__ __forceinline__ void scatter_apply(uint32_t *acc, const uint32_t (&cu
 
 // scatter_apply restricted to the docs [dlo, dlo + dn) of one wave (a short term, whose
 // sublist every wave reads in full): the other postings (and the padding) update a
-// per-lane dummy word past the block instead -- or, MASK, are masked off (their lanes
-// then take no LDS bank: no conflict with the owned postings' banks).
-template <int UU, bool MASK = false>
+// per-lane dummy word past the block instead.  (Exec-masking them off instead measured
+// no faster, r03sc.)
+template <int UU>
 __device__ __forceinline__ void scatter_apply_own(const uint32_t (&cur)[UU], uint32_t first_bits,
                                                   uint32_t dlo, uint32_t dn, uint32_t dummy) {
-    if constexpr (MASK) {
-        uint32_t w[UU], a[UU];
-        bool own[UU];
-#pragma unroll
-        for (int u = 0; u < UU; ++u) {
-            const uint32_t d = (cur[u] ^ POST_X) >> 8;
-            own[u] = d - dlo < dn;
-            a[u] = d << 2;
-            w[u] = 0;
-            if (own[u]) asm volatile("ds_read_b32 %0, %1" : "=v"(w[u]) : "v"(a[u]) : "memory");
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-        for (int u = 0; u < UU; ++u) asm volatile("" : "+v"(w[u]));
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int u = 0; u < UU; ++u) {
-            const uint32_t v = cur[u] & 255u;
-            if (own[u])
-                asm volatile("ds_write_b32 %0, %1" ::"v"(a[u]), "v"(word_update(w[u], v, first_bits))
-                             : "memory");
-        }
-        return;
-    }
     uint32_t w[UU], a[UU];
 #pragma unroll
     for (int u = 0; u < UU; ++u) {
@@ -761,11 +737,7 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
         if (lane == 0) sh.wsum[wave] = sfx;
         if (tid == 0) sh.tq = 0;
         __syncthreads();
-#pragma unroll
-        for (int w2 = 0; w2 < SC_WAVES; ++w2) {  // (all 16: independent reads, no loop)
-            const uint32_t x = sh.wsum[w2];
-            if (w2 > wave) sfx += x;
-        }
+        for (int w2 = wave + 1; w2 < SC_WAVES; ++w2) sfx += sh.wsum[w2];
         // one thread holds the crossing: count(>= 4t + e) >= k > count(>= 4t + e + 1)
         if (sfx >= (uint32_t)k && sfx - c < (uint32_t)k) {
             uint32_t above = sfx - c;
@@ -822,7 +794,6 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
     const uint32_t wdlo = (uint32_t)wave * wseg;
     const uint32_t wdn = wave == WSEG - 1 ? 0x7FFFFFFFu - wdlo : wseg;  // last: the rest
     const uint32_t wdummy = (uint32_t)(MAX_BLOCK_DOCS + lane) << 2;
-    const bool own_mask = ablate & 128;  // (A/B: exec-masked short-term scatter)
     const uint32_t vmin = 1u << (7 - min(min_cls, 7));  // all-wave form: pruning by value
     for (int j = (ablate & 1) || skip_wave ? nt : 0; j < nt; ++j) {  // ablate bit 0: skip (profiling)
         const uint32_t first_bits = (uint32_t)(255 - j) << 8;
@@ -865,22 +836,22 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
                 if (rem > 8 * 64) {
                     uint32_t r[16];
                     scatter_load<16, 64>(post + pos, rem, lane, r);
-                    if (own_mask) scatter_apply_own<16, true>(r, first_bits, wdlo, wdn, wdummy); else scatter_apply_own<16>(r, first_bits, wdlo, wdn, wdummy);
+                    scatter_apply_own<16>(r, first_bits, wdlo, wdn, wdummy);
                     pos += 16 * 64;
                 } else if (rem > 4 * 64) {
                     uint32_t r[8];
                     scatter_load<8, 64>(post + pos, rem, lane, r);
-                    if (own_mask) scatter_apply_own<8, true>(r, first_bits, wdlo, wdn, wdummy); else scatter_apply_own<8>(r, first_bits, wdlo, wdn, wdummy);
+                    scatter_apply_own<8>(r, first_bits, wdlo, wdn, wdummy);
                     pos = end;
                 } else if (rem > 64) {
                     uint32_t r[4];
                     scatter_load<4, 64>(post + pos, rem, lane, r);
-                    if (own_mask) scatter_apply_own<4, true>(r, first_bits, wdlo, wdn, wdummy); else scatter_apply_own<4>(r, first_bits, wdlo, wdn, wdummy);
+                    scatter_apply_own<4>(r, first_bits, wdlo, wdn, wdummy);
                     pos = end;
                 } else {
                     uint32_t r[1];
                     scatter_load<1, 64>(post + pos, rem, lane, r);
-                    if (own_mask) scatter_apply_own<1, true>(r, first_bits, wdlo, wdn, wdummy); else scatter_apply_own<1>(r, first_bits, wdlo, wdn, wdummy);
+                    scatter_apply_own<1>(r, first_bits, wdlo, wdn, wdummy);
                     pos = end;
                 }
             }
@@ -996,11 +967,7 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
         // second half of read_tq over the suffix sums published by the scatter barrier:
         // the crossing thread writes tq (0 from the item's start when the histogram
         // holds fewer than k candidates); one barrier
-#pragma unroll
-        for (int w2 = 0; w2 < SC_WAVES; ++w2) {  // (all 16: independent reads, no loop)
-            const uint32_t x = sh.wsum[w2];
-            if (w2 > wave) tq_sfx += x;
-        }
+        for (int w2 = wave + 1; w2 < SC_WAVES; ++w2) tq_sfx += sh.wsum[w2];
         if (tq_sfx >= (uint32_t)k && tq_sfx - tq_c < (uint32_t)k) {
             uint32_t above = tq_sfx - tq_c;
             int e = 3;
@@ -1124,11 +1091,7 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
             if (lane == 63) sh.wsum[wave] = incl;
             __syncthreads();
             uint32_t base = incl - cnt;
-#pragma unroll
-            for (int w2 = 0; w2 < SC_WAVES; ++w2) {
-                const uint32_t x = sh.wsum[w2];
-                if (w2 < wave) base += x;
-            }
+            for (int w2 = 0; w2 < wave; ++w2) base += sh.wsum[w2];
             stamp(6);
             {
                 uint32_t pa = base & 0xFFFFu, pb = base >> 16;

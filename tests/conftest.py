@@ -12,3 +12,14 @@ GOLDEN = ROOT / "tests" / "golden"
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (HIP device)")
+
+
+def pytest_collection_modifyitems(config, items):
+    # torch's HIP runtime first when GPU tests run: torch cannot initialise the GPU after
+    # the library's own (newer) runtime has, and a module run alone (test_index_gpu.py)
+    # may reach a torch-using test only after library calls
+    if any(item.get_closest_marker("gpu") for item in items):
+        import torch
+
+        if torch.cuda.is_available():
+            torch.cuda.init()
