@@ -97,6 +97,85 @@ def _legacy_bert_map(tokens) -> Dict[int, int]:
     return out
 
 
+class _WordCache:
+    """Per-word token cache for the pre-tokenized document encode.  A pre-tokenized
+    input is normalized, pre-tokenized and modelled one word at a time, so a word's
+    tokens do not depend on its neighbours (except, for a Metaspace pre-tokenizer with
+    prepend_scheme "first", on whether it is the first word: two tables); a document's
+    encoding is then the template's prefix specials, its words' cached tokens cut to
+    max_length - #specials (the tokenizer's right truncation of a single sequence) and
+    the suffix specials.  Misses are encoded in one batched call per document batch.
+    Checked against encode_batch (tests/test_host_cpu.py) and self-checked on the first
+    batch of each process: any difference turns the cache off."""
+
+    MAX_ENTRIES = 1 << 20
+    ANCHOR = "a"
+
+    def __init__(self, tok):
+        self.tok = tok
+        self.first: Dict[str, List[int]] = {}
+        self.other: Dict[str, List[int]] = {}
+        e = tok.encode([self.ANCHOR], is_pretokenized=True, add_special_tokens=True)
+        wid = e.word_ids
+        lo = next(i for i, w in enumerate(wid) if w is not None)
+        hi = max(i for i, w in enumerate(wid) if w is not None) + 1
+        self.prefix, self.suffix = list(e.ids[:lo]), list(e.ids[hi:])
+        self.checked = False
+        self.ok = True
+
+    def _fill(self, terms_list: Sequence[Sequence[str]]) -> None:
+        mf = {t[0] for t in terms_list if t and t[0] not in self.first}
+        mo = {w for t in terms_list for w in t[1:] if w not in self.other}
+        if not mf and not mo:
+            return
+        tok = self.tok
+        trunc = tok.truncation
+        tok.no_truncation()  # (a cached word keeps all its tokens)
+        try:
+            if mf:
+                mf = list(mf)
+                for w, e in zip(mf, tok.encode_batch([[w] for w in mf], is_pretokenized=True,
+                                                     add_special_tokens=False)):
+                    self.first[w] = [i for i, x in zip(e.ids, e.word_ids) if x == 0]
+            if mo:
+                mo = list(mo)
+                for w, e in zip(mo, tok.encode_batch([[self.ANCHOR, w] for w in mo],
+                                                     is_pretokenized=True,
+                                                     add_special_tokens=False)):
+                    self.other[w] = [i for i, x in zip(e.ids, e.word_ids) if x == 1]
+        finally:
+            if trunc is not None:
+                tok.enable_truncation(**trunc)
+        if len(self.first) + len(self.other) > self.MAX_ENTRIES:
+            self.first.clear()
+            self.other.clear()
+
+    def encode(self, terms_list: Sequence[Sequence[str]], max_length: int):
+        """[(ids, word_ids)] of each document, as encode_batch(..., is_pretokenized=True,
+        add_special_tokens=True) under enable_truncation(max_length)."""
+        self._fill(terms_list)
+        budget = max(max_length - len(self.prefix) - len(self.suffix), 0)
+        out = []
+        first, other = self.first, self.other
+        for terms in terms_list:
+            ids = list(self.prefix)
+            wids: List[Optional[int]] = [None] * len(ids)
+            room = budget
+            for i, w in enumerate(terms):
+                if room <= 0:
+                    break
+                tk = first[w] if i == 0 else other[w]
+                if len(tk) > room:
+                    tk = tk[:room]
+                ids.extend(tk)
+                wids.extend([i] * len(tk))
+                room -= len(tk)
+            ids.extend(self.suffix)
+            wids.extend([None] * len(self.suffix))
+            out.append((ids, wids))
+        return out
+
+
 def _filter_terms(terms: Sequence[str], idx_map: Dict[int, int]) -> Dict[str, int]:
     """Unique, non-punctuation terms whose tokens survived truncation, in
     first-occurrence order (xlmr_original.py:181-187)."""
@@ -158,6 +237,19 @@ class DeepImpact:
         ml = max_length or cls.max_length
         tok = cls._tok(ml)
         terms = [_pre_tokenize(tok, _normalize(tok, d)) for d in documents]
+        wc = cls._word_cache(tok) if cls.term_mapping == "word_ids" else None
+        if wc is not None:
+            enc = wc.encode(terms, ml)
+            if not wc.checked:  # first batch of this process: the same as encode_batch?
+                wc.checked = True
+                ref = tok.encode_batch(terms, is_pretokenized=True, add_special_tokens=True)
+                wc.ok = all(list(e.ids) == ids and list(e.word_ids) == wids
+                            for e, (ids, wids) in zip(ref, enc))
+                if not wc.ok:
+                    cls._wcache = None
+                    enc = [(e.ids, e.word_ids) for e in ref]
+            return [(Encoding(ids, wids), _filter_terms(t, _first_token_map(wids)))
+                    for t, (ids, wids) in zip(terms, enc)]
         encs = tok.encode_batch(terms, is_pretokenized=True, add_special_tokens=True)
         out = []
         for t, e in zip(terms, encs):
@@ -167,6 +259,21 @@ class DeepImpact:
                 m = _first_token_map(e.word_ids)
             out.append((Encoding(e.ids, e.word_ids), _filter_terms(t, m)))
         return out
+
+    _wcache = None
+    _wcache_tok = None
+    word_cache = os.environ.get("DI_TOKEN_CACHE", "1") != "0"
+
+    @classmethod
+    def _word_cache(cls, tok):
+        """The process's per-word token cache for `tok` (None when disabled or found
+        unequal to encode_batch)."""
+        if not cls.word_cache:
+            return None
+        if cls._wcache_tok is not tok:
+            cls._wcache_tok = tok
+            cls._wcache = _WordCache(tok)
+        return cls._wcache if cls._wcache is not None and cls._wcache.ok else None
 
     @staticmethod
     def compute_term_impacts(documents_term_to_token_index_map: List[Dict[str, int]],
