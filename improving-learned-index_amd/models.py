@@ -128,6 +128,13 @@ class _WordCache:
         mo = {w for t in terms_list for w in t[1:] if w not in self.other}
         if not mf and not mo:
             return
+        if len(self.first) + len(self.other) + len(mf) + len(mo) > self.MAX_ENTRIES:
+            # bounded memory: start over before this batch's fill, which then holds
+            # every word the batch looks up
+            self.first.clear()
+            self.other.clear()
+            mf = {t[0] for t in terms_list if t}
+            mo = {w for t in terms_list for w in t[1:]}
         tok = self.tok
         trunc = tok.truncation
         tok.no_truncation()  # (a cached word keeps all its tokens)
@@ -146,9 +153,6 @@ class _WordCache:
         finally:
             if trunc is not None:
                 tok.enable_truncation(**trunc)
-        if len(self.first) + len(self.other) > self.MAX_ENTRIES:
-            self.first.clear()
-            self.other.clear()
 
     def encode(self, terms_list: Sequence[Sequence[str]], max_length: int):
         """[(ids, word_ids)] of each document, as encode_batch(..., is_pretokenized=True,

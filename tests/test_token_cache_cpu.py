@@ -54,3 +54,25 @@ def test_cache_equals_batched_encode(model_cls, max_length):
         assert ge.ids == we.ids
         assert ge.word_ids == we.word_ids
         assert gm == wm  # same terms, same first-token positions, same order
+
+
+def test_cache_bound_keeps_the_batch_words(model_cls, monkeypatch):
+    """Past MAX_ENTRIES the cache starts over before a batch's fill (not after it), so
+    every word the batch looks up is present: same encodings as without the cache."""
+    from improving_learned_index_amd import models
+
+    docs = _docs(200, 7)
+    model_cls.word_cache = False
+    model_cls._wcache_tok = None
+    want = model_cls.process_documents(docs, 64)
+    model_cls.word_cache = True
+    model_cls._wcache_tok = None
+    monkeypatch.setattr(models._WordCache, "MAX_ENTRIES", 150)
+    got = []
+    for i in range(0, len(docs), 9):  # every batch brings new words past the bound
+        got += model_cls.process_documents(docs[i:i + 9], 64)
+    wc = model_cls._wcache
+    assert wc is not None and wc.ok
+    assert len(wc.first) + len(wc.other) <= 150 + 9 * 120
+    for (ge, gm), (we, wm) in zip(got, want):
+        assert ge.ids == we.ids and ge.word_ids == we.word_ids and gm == wm
