@@ -89,10 +89,11 @@ void parse_collection(std::string_view buf, Parsed &P) {
                 hs.resize(n);
                 for (size_t i = 0; i < n; ++i) hs[i] = {fnv1a(P.term[first + i]), (uint32_t)i};
                 std::sort(hs.begin(), hs.end());
+                // any equal hash (a repeat, or a collision of two different terms) takes
+                // the exact path: with a collision, sorted neighbours need not be the
+                // repeat itself
                 bool dup = false;
-                for (size_t i = 1; i < n && !dup; ++i)
-                    dup = hs[i].first == hs[i - 1].first &&
-                          P.term[first + hs[i].second] == P.term[first + hs[i - 1].second];
+                for (size_t i = 1; i < n && !dup; ++i) dup = hs[i].first == hs[i - 1].first;
                 if (dup) {  // the dict: first slot, last value
                     std::unordered_map<std::string_view, size_t> seen;
                     size_t o = first;
