@@ -549,6 +549,7 @@ def text_legs(args):
 
     n = args.text_docs
     V = v_terms(n)
+    log(f"text legs: {n} docs (rank 0)")
     td = Path(tempfile.mkdtemp(dir="/tmp"))
     try:
         t0 = time.perf_counter()
@@ -556,7 +557,9 @@ def text_legs(args):
         t_gen = time.perf_counter() - t0
         in_bytes = (td / "collection.index").stat().st_size
         t0 = time.perf_counter()
-        quantize_file(td / "collection.index", td / "collection.quantized")
+        # (rank 0 alone runs these legs: the single-process quantizer, never the
+        # torchrun-sharded one, whose collectives the other ranks would never join)
+        quantize_file(td / "collection.index", td / "collection.quantized", sharded=False)
         t_q = time.perf_counter() - t0
         (td / "collection.index").unlink()
         q_bytes = (td / "collection.quantized").stat().st_size

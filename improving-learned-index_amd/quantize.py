@@ -54,16 +54,19 @@ def _quantize_one(input_file_path, output_file_path, max_val, device) -> "ctypes
 
 
 def quantize_file(input_file_path: Union[str, Path], output_file_path: Union[str, Path],
-                  max_val: Optional[float] = None, device: int = 0) -> float:
+                  max_val: Optional[float] = None, device: int = 0,
+                  sharded: Optional[bool] = None) -> float:
     """quantize.py:27-47.  max_val None: the file's max; an explicit 0 raises
-    ZeroDivisionError and a negative one writes empty lines, as the reference."""
+    ZeroDivisionError and a negative one writes empty lines, as the reference.
+    sharded: None = doc-sharded under torchrun (WORLD_SIZE > 1: every rank must call
+    it), False = this process alone quantizes the whole file."""
     if max_val is not None and max_val == 0:
         raise ZeroDivisionError("float division by zero")  # quantize.py:37
     if max_val is not None and max_val < 0:
         _negative_max(input_file_path, output_file_path)
         return float(max_val)
     world, rank, local = parallel.dist_env()
-    if world > 1:
+    if world > 1 and sharded is not False:
         parallel.init_group("gloo")
         dev = parallel.rank_device(local)
         return parallel.quantize_sharded(

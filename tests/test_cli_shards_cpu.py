@@ -123,3 +123,30 @@ def test_line_offsets_match_text_mode_lines(tmp_path):
         want = [starts[i] if i < len(starts) and i < n else len(data) for i in want_lines]
         for blk in (1, 2, 3, 7, 1 << 20):
             assert parallel.line_offsets(p, want_lines, block=blk) == want, (data, want_lines, blk)
+
+
+def test_quantize_file_sharded_false_stays_local(tmp_path, monkeypatch):
+    """Under a torchrun environment (WORLD_SIZE > 1) quantize_file shards by default, and
+    every rank must call it; sharded=False (bench.py's rank-0-only text legs) quantizes
+    the whole file in this process and starts no collective."""
+    from improving_learned_index_amd import parallel, quantize
+
+    calls = []
+    monkeypatch.setenv("WORLD_SIZE", "2")
+    monkeypatch.setenv("RANK", "0")
+    monkeypatch.setenv("LOCAL_RANK", "0")
+    monkeypatch.setattr(quantize, "_quantize_one",
+                        lambda i, o, m, d: calls.append(("local", m)) or _Used(3.0))
+    monkeypatch.setattr(parallel, "quantize_sharded",
+                        lambda *a, **k: calls.append(("sharded",)) or 3.0)
+    monkeypatch.setattr(parallel, "init_group", lambda *a, **k: calls.append(("group",)))
+    assert quantize.quantize_file(tmp_path / "in", tmp_path / "out", sharded=False) == 3.0
+    assert calls == [("local", None)]
+    calls.clear()
+    quantize.quantize_file(tmp_path / "in", tmp_path / "out")
+    assert calls[0] == ("group",) and ("sharded",) in calls
+
+
+class _Used:
+    def __init__(self, v):
+        self.value = v
