@@ -212,9 +212,10 @@ def retrieve_leg(args, rank, world, dev, n_docs=DOCS_PER_SHARD, check_queries=0)
     res["roofline"] = {
         "kernel": "score_blocks_kernel",
         # priced against HBM by the algorithmic bytes, but the counters show the popular
-        # lists served from L2 / MALL (PMC traffic below) and the LDS scatter's latency
-        # and bank conflicts as the limit
-        "bound": "lds",
+        # lists served from L2 / MALL (PMC traffic below); the limit is the scatter's
+        # posting-load instructions (a duplicated 4-byte load costs +56%, a duplicated
+        # 16-byte load per 4 postings +21%) and its LDS read-modify-write
+        "bound": "vmem_issue+lds",
         "priced_against": "hbm",
         "achieved": round(achieved, 1),
         "peak": HBM_PEAK_GBS,
