@@ -291,8 +291,11 @@ constexpr int AX_KC = 64, AX_IMG = AX_KC * 256, AX_LDS = 4 * AX_IMG;
 // (with both, two query tiles): tile 1's S^T products interleaved with tile 0's
 // exponentials, tile 0's O^T products with tile 1's (sched_group_barrier), so the
 // softmax issues in the MFMAs' shadow.
-template <bool BAL, bool LAZY, bool PIPE = false>
-__global__ void __launch_bounds__(64 * AX_WAVES)
+// NW: waves per workgroup.  8: one workgroup per CU, 256-query passes.  4: two
+// workgroups per CU (64 KiB of LDS and <= 256 VGPRs each), 128-query passes -- a SIMD
+// idle at one workgroup's short last pass runs the other workgroup's wave.
+template <bool BAL, bool LAZY, bool PIPE = false, int NW = AX_WAVES>
+__global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2)))
 attention_x3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu_seqlens, int H,
                     int n_heads, int n_pairs, bf16 *__restrict__ ctx_split,
                     const int32_t *__restrict__ qsel, const int32_t *__restrict__ cu_qsel,
@@ -311,7 +314,7 @@ attention_x3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
     const uint32_t lds_base =
         (uint32_t)(uintptr_t)((__attribute__((address_space(3))) unsigned char *)lds);
     const float sc = 0.125f * 1.4426950408889634f;  // 1/sqrt(64) * log2(e)
-    constexpr int PASS_Q = AX_WAVES * AX_QT * 16;   // queries per pass (256)
+    constexpr int PASS_Q = NW * AX_QT * 16;         // queries per pass (256 or 128)
 
     // Work units: (pair, pass), pairs blockIdx.x, + gridDim.x, ... (persistent); the
     // next unit's Q and first K / V chunk load while the current unit's last chunk
@@ -342,19 +345,20 @@ attention_x3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
         }
         return false;
     };
-    // chunk ci of unit u -> stage buffer b: key rows 8 wave..+7 of K and of V (two
-    // 1 KiB pieces each), 16 B per lane, source slots permuted by the swizzle
-    // (piece pc: key rows 64 (pc >> 1) + 8 wave + 4 (pc & 1) + lane >> 4)
-    const int sr = 8 * wave + (lane >> 4);
+    // chunk ci of unit u -> stage buffer b: key rows RPW wave..+RPW-1 of K and of V
+    // (RPW / 4 pieces of 1 KiB each), 16 B per lane, source slots permuted by the
+    // swizzle (piece pc: key rows RPW wave + 4 pc + lane >> 4)
+    constexpr int RPW = AX_KC / NW;  // key rows per wave and image (8 or 16)
+    const int sr = RPW * wave + (lane >> 4);
     auto stage = [&](const Unit &u, int ci, int b) {
         const bf16 *kg = qkv + split_col(H + u.h * ATT_D);      // + key row * ld: 256 B
         const bf16 *vg = qkv + split_col(2 * H + u.h * ATT_D);
 #pragma unroll
-        for (int pc = 0; pc < AX_KC / 32; ++pc) {
-            const int rl = 64 * (pc >> 1) + sr + 4 * (pc & 1);
+        for (int pc = 0; pc < RPW / 4; ++pc) {
+            const int rl = sr + 4 * pc;
             const int row = u.tok0 + min(ci * AX_KC + rl, u.n - 1);
             const int j = (lane & 15) ^ ax_swz(rl);
-            const int dst = b * AX_IMG + (pc >> 1) * 16384 + wave * 2048 + (pc & 1) * 1024;
+            const int dst = b * AX_IMG + (RPW * wave + 4 * pc) * 256;
             __builtin_amdgcn_global_load_lds((const void *)(kg + row * ld + j * 8),
                                              (lds_void *)(lds + dst), 16, 0, 0);
             __builtin_amdgcn_global_load_lds((const void *)(vg + row * ld + j * 8),
@@ -364,7 +368,7 @@ attention_x3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
     // B operands Q^T of unit u, lane (g, c): Q[q_base + 16 qt + c][32 ch + 8 g + e]
     // (hi; lo 32 later)
     // first query (within its pass) of this wave's tile qt
-    auto qtile = [&](int qt) { return BAL ? 16 * (wave + 8 * qt) : wave * (AX_QT * 16) + 16 * qt; };
+    auto qtile = [&](int qt) { return BAL ? 16 * (wave + NW * qt) : wave * (AX_QT * 16) + 16 * qt; };
     auto load_q = [&](const Unit &u, bf16x8 (&qh)[AX_QT][2], bf16x8 (&ql)[AX_QT][2]) {
         const bf16 *qbase = qkv + split_col(u.h * ATT_D) + 8 * g;
 #pragma unroll
@@ -846,26 +850,29 @@ void launch_attention_x3(const bf16 *qkv, const int32_t *cu_seqlens, int n_docs,
     const int n_heads = H / ATT_D;
     const int64_t n_pairs = (int64_t)n_docs * n_heads;
     DI_REQUIRE(n_pairs < (1ll << 31), DI_ERANGE, "attention grid too large");
-    const int grid = (int)std::min<int64_t>(n_pairs, n_cu());  // persistent, one per CU
+    // persistent: one 8-wave or two 4-wave workgroups per CU
     // balanced tiles + lazy max + interleaved softmax (r03 ab_attn: attention -8.5%,
     // then -3% per step); DI_ATTN_X3 (developer A/B): 0 = the round-2 form, 12 = no
     // interleave
     static const int variant = [] {
         const char *e = getenv("DI_ATTN_X3");
-        return e ? atoi(e) & 28 : 28;
+        return e ? atoi(e) & 60 : 28;
     }();
     static const int abl = [] {
         const char *e = getenv("DI_ATTN_X3_ABLATE");
         return e ? atoi(e) : 0;
     }();
-#define AX_LAUNCH(BL, LZ, PP)                                                                  \
-    hipLaunchKernelGGL((attention_x3_kernel<BL, LZ, PP>), dim3(grid), dim3(64 * AX_WAVES), AX_LDS, \
-                       s, qkv, cu_seqlens, H, n_heads, (int)n_pairs, ctx_split, qsel, cu_qsel, abl)
+#define AX_LAUNCH(BL, LZ, PP, NW)                                                              \
+    hipLaunchKernelGGL((attention_x3_kernel<BL, LZ, PP, NW>),                                  \
+                       dim3((int)std::min<int64_t>(n_pairs, (int64_t)n_cu() * (AX_WAVES / NW))), \
+                       dim3(64 * NW), AX_LDS, s, qkv, cu_seqlens, H, n_heads, (int)n_pairs,   \
+                       ctx_split, qsel, cu_qsel, abl)
     // (r03 ab_attn, attention ms per step: BAL alone -3.5%, LAZY alone -5.6%, both -8.5%)
     switch (variant) {
-    case 12: AX_LAUNCH(true, true, false); break;
-    case 28: AX_LAUNCH(true, true, true); break;
-    default: AX_LAUNCH(false, false, false); break;
+    case 12: AX_LAUNCH(true, true, false, AX_WAVES); break;
+    case 28: AX_LAUNCH(true, true, true, AX_WAVES); break;
+    case 60: AX_LAUNCH(true, true, true, 4); break;
+    default: AX_LAUNCH(false, false, false, AX_WAVES); break;
     }
 #undef AX_LAUNCH
     check_launch("attention_x3");
