@@ -1,0 +1,28 @@
+"""Scorer phase stamps (DI_PROFILE_ABLATE=64, workgroup 0) and device ms per batch at one
+impact-pruning level, to see where a pruned (query, block) item's time goes.
+Profiling only (the stamps change nothing but timing).
+    DI_PROFILE_ABLATE=64 python tools/phase_prune.py <n_docs> <min_impact>
+"""
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT))
+from improving_learned_index_amd import _lib  # noqa: E402
+from improving_learned_index_amd import synthetic as S  # noqa: E402
+
+n_docs, mi = int(sys.argv[1]), int(sys.argv[2])
+nq, k = 6980, 1000
+term_off, pdoc, pval, _ = S.synth_postings(n_docs, 2 * n_docs, seed=4321)
+flat, cuq = _lib.csr(S.msmarco_like_queries(nq, 2 * n_docs, seed=1234))
+ix = _lib.DeviceIndex.from_postings(term_off, pdoc, pval, 0, n_docs)
+ix.reserve(nq, k)
+ix.set_min_impact(mi)
+ix.search_csr(flat, cuq, k)
+print("---- timed", file=sys.stderr, flush=True)
+ix.timing("score_blocks", reset=True)
+ix.search_csr(flat, cuq, k, timing=True)
+nb = (n_docs + 32767) // 32768
+ms = ix.timing("score_blocks")[0]
+print(f"n_docs {n_docs} min_impact {mi} items {nq * nb} score_blocks {ms:.3f} ms "
+      f"({ms * 1e3 * 256 / (nq * nb):.2f} us per item per CU)", flush=True)
