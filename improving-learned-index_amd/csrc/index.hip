@@ -301,7 +301,7 @@ __device__ __forceinline__ void scatter_apply_own(const uint32_t (&cur)[UU], uin
 
 // Profiling (DI_PROFILE_ABLATE bit 64): per-phase shader cycles of workgroup 0's items
 // accumulated here and printed by di_index_search.
-__device__ unsigned long long g_sb_phase[8];
+__device__ unsigned long long g_sb_phase[10];
 
 // The (term, block) sublists: sparse per term -- the entries of term t are
 // [tb_start[t], tb_start[t+1]), one per block holding postings of t, in block order
@@ -979,6 +979,7 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
         }
         __syncthreads();
         Tq = sh.tq;
+        stamp(8);  // threshold read (the part of tq-select before the sweep)
         // (wsum is written again only after a barrier of the selection below; tq only
         // at the next item's start)
         if (Tq > 0) {
@@ -2193,13 +2194,13 @@ int di_index_search(di_index *ix, const uint32_t *q_terms, const int32_t *cu_q, 
                                       s));
         }
         if (ix->ablate & 64) {
-            unsigned long long ph[8];
+            unsigned long long ph[10];
             DI_HIP(hipStreamSynchronize(s));
             DI_HIP(hipMemcpyFromSymbol(ph, HIP_SYMBOL(g_sb_phase), sizeof ph));
             fprintf(stderr, "score_blocks phase cycles (workgroup 0, cumulative): setup %llu "
                             "scatter %llu hist %llu [count %llu] write %llu ties %llu copy %llu "
-                            "tq-select %llu\n",
-                    ph[0], ph[1], ph[2], ph[6], ph[3], ph[4], ph[5], ph[7]);
+                            "tq-select %llu [tq-read %llu]\n",
+                    ph[0], ph[1], ph[2], ph[6], ph[3], ph[4], ph[5], ph[7], ph[8]);
         }
         if (!(flags & DI_F_ASYNC) || !dev) {
             DI_HIP(hipStreamSynchronize(s));
