@@ -218,9 +218,15 @@ constexpr uint32_t POST_X = (uint32_t)MAX_BLOCK_DOCS << 8;
 // bounds-checked by the hardware, a 32-bit lane offset and no per-posting address
 // arithmetic -- then the LDS reads, then the writes.  A doc occurs once per term, so
 // the read-modify-write needs no atomics.
+//
+// wide (UU a multiple of 4): 16-byte loads, lane tid taking the postings 4 tid ..
+// 4 tid + 3 of each group of 4 NT -- a quarter of the load instructions (the scatter
+// is bound by them).  Any posting -> lane mapping is exact (a doc occurs
+// once per term), and a multi-dword buffer load is range-checked per dword, so the
+// padding past avail still reads 0.
 template <int UU, int NT = SC_THREADS>
 __device__ __forceinline__ void scatter_load(const uint32_t *p, int64_t avail, int tid,
-                                             uint32_t (&cur)[UU]) {
+                                             uint32_t (&cur)[UU], bool wide = false) {
     const uint64_t pa = reinterpret_cast<uint64_t>(p);
     const uint32_t lo32 = __builtin_amdgcn_readfirstlane((uint32_t)pa);
     const uint32_t hi32 = __builtin_amdgcn_readfirstlane((uint32_t)(pa >> 32));
@@ -228,6 +234,18 @@ __device__ __forceinline__ void scatter_load(const uint32_t *p, int64_t avail, i
         (int)(min(avail, (int64_t)UU * NT) * 4));
     void *base = reinterpret_cast<void *>(((uint64_t)hi32 << 32) | lo32);
     const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(base, (short)0, bytes, 0x00020000);
+    if constexpr (UU % 4 == 0) {
+        if (wide) {
+#pragma unroll
+            for (int g = 0; g < UU / 4; ++g) {
+                const auto v =
+                    __builtin_amdgcn_raw_buffer_load_b128(rsrc, (4 * tid + g * 4 * NT) * 4, 0, 0);
+#pragma unroll
+                for (int k = 0; k < 4; ++k) cur[4 * g + k] = v[k];
+            }
+            return;
+        }
+    }
 #pragma unroll
     for (int u = 0; u < UU; ++u)
         cur[u] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, (tid + u * NT) * 4, 0, 0);
@@ -795,6 +813,7 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
     const uint32_t wdn = wave == WSEG - 1 ? 0x7FFFFFFFu - wdlo : wseg;  // last: the rest
     const uint32_t wdummy = (uint32_t)(MAX_BLOCK_DOCS + lane) << 2;
     const uint32_t vmin = 1u << (7 - min(min_cls, 7));  // all-wave form: pruning by value
+    const bool x4 = !(ablate & 4096);  // rounds of 4k postings per lane by 16-byte loads (bit 4096: 4-byte, A/B)
     for (int j = (ablate & 1) || skip_wave ? nt : 0; j < nt; ++j) {  // ablate bit 0: skip (profiling)
         const uint32_t first_bits = (uint32_t)(255 - j) << 8;
         const bool lj = is_long(j);
@@ -806,17 +825,17 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
                 const int64_t rem = end - pos;
                 if (rem > 8 * 64) {
                     uint32_t r[16];
-                    scatter_load<16, 64>(post + pos, rem, lane, r);
+                    scatter_load<16, 64>(post + pos, rem, lane, r, x4);
                     scatter_apply<16>(sh.acc, r, first_bits);
                     pos += 16 * 64;
                 } else if (rem > 4 * 64) {
                     uint32_t r[8];
-                    scatter_load<8, 64>(post + pos, rem, lane, r);
+                    scatter_load<8, 64>(post + pos, rem, lane, r, x4);
                     scatter_apply<8>(sh.acc, r, first_bits);
                     pos = end;
                 } else if (rem > 64) {
                     uint32_t r[4];
-                    scatter_load<4, 64>(post + pos, rem, lane, r);
+                    scatter_load<4, 64>(post + pos, rem, lane, r, x4);
                     scatter_apply<4>(sh.acc, r, first_bits);
                     pos = end;
                 } else {
@@ -835,17 +854,17 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
                 const int64_t rem = end - pos;
                 if (rem > 8 * 64) {
                     uint32_t r[16];
-                    scatter_load<16, 64>(post + pos, rem, lane, r);
+                    scatter_load<16, 64>(post + pos, rem, lane, r, x4);
                     scatter_apply_own<16>(r, first_bits, wdlo, wdn, wdummy);
                     pos += 16 * 64;
                 } else if (rem > 4 * 64) {
                     uint32_t r[8];
-                    scatter_load<8, 64>(post + pos, rem, lane, r);
+                    scatter_load<8, 64>(post + pos, rem, lane, r, x4);
                     scatter_apply_own<8>(r, first_bits, wdlo, wdn, wdummy);
                     pos = end;
                 } else if (rem > 64) {
                     uint32_t r[4];
-                    scatter_load<4, 64>(post + pos, rem, lane, r);
+                    scatter_load<4, 64>(post + pos, rem, lane, r, x4);
                     scatter_apply_own<4>(r, first_bits, wdlo, wdn, wdummy);
                     pos = end;
                 } else {
@@ -866,20 +885,20 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
         }
         const bool next = j + 1 < nt && hi[j + 1] > lo[j + 1] && !is_long(j + 1);
         auto prefetch_next = [&]() {
-            scatter_load<4>(post + lo[j + 1], hi[j + 1] - lo[j + 1], tid, pre);
+            scatter_load<4>(post + lo[j + 1], hi[j + 1] - lo[j + 1], tid, pre, x4);
             have_pre = true;
         };
         while (pos < end) {
             const int64_t rem = end - pos;
             if (rem >= 16 * SC_THREADS) {
                 uint32_t r[16];
-                scatter_load<16>(post + pos, rem, tid, r);
+                scatter_load<16>(post + pos, rem, tid, r, x4);
                 if (rem == 16 * SC_THREADS && next) prefetch_next();
                 scatter_apply<16, true>(sh.acc, r, first_bits, vmin);
                 pos += 16 * SC_THREADS;
             } else if (rem > SC_THREADS) {
                 uint32_t r[4];
-                scatter_load<4>(post + pos, rem, tid, r);
+                scatter_load<4>(post + pos, rem, tid, r, x4);
                 if (rem <= 4 * SC_THREADS && next) prefetch_next();
                 scatter_apply<4, true>(sh.acc, r, first_bits, vmin);
                 pos += 4 * SC_THREADS;
@@ -1780,6 +1799,11 @@ void build_index(di_index *ix, const int64_t *term_off, int64_t n_terms, const u
     auto cls_of = [](uint32_t w) { return 7 - (31 - __builtin_clz(w & 255u)); };
     auto bank_of = [](uint32_t w) { return (w >> 8) & 31u; };  // doc_in_block mod 32
     const uint32_t S = (bd + WSEG - 1) / WSEG;
+    // The scorer's 16-byte loads (scatter_load wide) give a 32-lane group of one LDS
+    // update the positions 4 L + k (L < 32) of an aligned 128-position block; DI_DEAL_X4=0
+    // deals for the 4-byte loads' lane-consecutive groups instead (A/B).
+    bool deal_x4 = true;
+    if (const char *e = std::getenv("DI_DEAL_X4")) deal_x4 = std::atoi(e) != 0;
     parallel_for(n_terms, [&](int64_t t0, int64_t t1, int) {
         std::vector<uint32_t> grp, tmp, bk, seg_in, cls_cnt(8), cls_pos(8), bucket_cnt(32),
             head(32), fill(32);
@@ -1798,11 +1822,12 @@ void build_index(di_index *ix, const int64_t *term_off, int64_t n_terms, const u
             tmp.resize(n);
             for (size_t i = 0; i < n; ++i) tmp[cls_pos[cls_of(in[i])]++] = in[i];
             // The scorer's lanes take the group's postings in rounds from its start,
-            // and a 32-lane group of its LDS updates is one aligned block of 32
-            // positions: each position takes, from its class, a posting whose bank is
-            // not yet used in the current block (bank cursor carried on across sweeps
-            // and class boundaries), else any.
-            uint32_t c0 = 0, used = 0;
+            // and a 32-lane group of its LDS updates is one set of 32 positions (by
+            // 16-byte loads: p = 4 L + k of an aligned 128-block, one set per k; by
+            // 4-byte loads: an aligned 32-block): each position takes, from its class,
+            // a posting whose bank is not yet used in its set (bank cursor carried on
+            // across sweeps and class boundaries), else any.
+            uint32_t c0 = 0, usedq[4] = {0, 0, 0, 0};
             int cursor = 0;
             const int64_t o_start = o;
             for (int c = 0; c < 8; ++c) {
@@ -1819,7 +1844,9 @@ void build_index(di_index *ix, const int64_t *term_off, int64_t n_terms, const u
                 fill = head;
                 for (uint32_t i = c0; i < c1; ++i) bk[fill[bank_of(tmp[i])]++] = tmp[i];
                 for (uint32_t i = c0; i < c1; ++i) {
-                    if (((o - o_start) & 31) == 0) used = 0;
+                    const int64_t rp = o - o_start;
+                    if ((rp & (deal_x4 ? 127 : 31)) == 0) usedq[0] = usedq[1] = usedq[2] = usedq[3] = 0;
+                    uint32_t &used = usedq[deal_x4 ? (rp & 3) : 0];
                     uint32_t cand = avail & ~used;
                     if (!cand) cand = avail;  // every bank left is taken in this block
                     const uint32_t rot = cursor ? (cand >> cursor) | (cand << (32 - cursor)) : cand;

@@ -23,5 +23,7 @@ for v in ${VARIANTS:-old new}; do
         new) run new X=0 || exit 1 ;;
         ablate*) run $v DI_PROFILE_ABLATE=${v#ablate} || exit 1 ;;
         wlong*) run $v DI_WLONG_MIN=${v#wlong} || exit 1 ;;
+        b32) run $v DI_PROFILE_ABLATE=4096 DI_DEAL_X4=0 || exit 1 ;;  # 4-byte loads, 32-block dealing
+        x4deal32) run $v DI_DEAL_X4=0 || exit 1 ;;                    # 16-byte loads, 32-block dealing
     esac
 done
