@@ -205,13 +205,14 @@ __device__ __forceinline__ bool wave_append(bool take, uint32_t *cursor, uint32_
     return take;
 }
 
-// Device posting words are ((doc_in_block << 8) | value) XOR POST_X.  A buffer load
+// Device posting words are ((doc_in_block << 10) | value) XOR POST_X: bits 8-9 stay 0,
+// so (word ^ POST_X) >> 8 is the doc's LDS byte address.  A buffer load
 // past the descriptor's range returns 0, which decodes to doc MAX_BLOCK_DOCS -- the
 // dummy accumulator word after the block -- with value 0: the padding lanes of a
 // round need no clamp, no select and no branch (their update lands in the dummy).
 // (Per-lane dummy words for the padding, with a quad-wise threshold sweep, measured
 // 4.5% slower, r03pad; the quad sweep alone neutral, r03quad.)
-constexpr uint32_t POST_X = (uint32_t)MAX_BLOCK_DOCS << 8;
+constexpr uint32_t POST_X = (uint32_t)MAX_BLOCK_DOCS << 10;
 
 // One scatter round over postings p[0 .. min(avail, UU * SC_THREADS)) (lane-
 // consecutive, UU per lane; p and avail wave-uniform): all loads first -- buffer loads
@@ -272,7 +273,7 @@ __device__ __forceinline__ void scatter_apply(uint32_t *acc, const uint32_t (&cu
     uint32_t w[UU], a[UU];
 #pragma unroll
     for (int u = 0; u < UU; ++u) {
-        a[u] = ((cur[u] ^ POST_X) >> 8) << 2;
+        a[u] = (cur[u] ^ POST_X) >> 8;
         if constexpr (FILT)
             a[u] = (cur[u] & 255u) >= vmin ? a[u] : (uint32_t)(MAX_BLOCK_DOCS + lane_id()) << 2;
         asm volatile("ds_read_b32 %0, %1" : "=v"(w[u]) : "v"(a[u]) : "memory");
@@ -301,7 +302,7 @@ __device__ __forceinline__ void scatter_apply_own(const uint32_t (&cur)[UU], uin
     uint32_t w[UU], a[UU];
 #pragma unroll
     for (int u = 0; u < UU; ++u) {
-        const uint32_t d = (cur[u] ^ POST_X) >> 8;
+        const uint32_t d = (cur[u] ^ POST_X) >> 10;
         a[u] = (d - dlo < dn) ? d << 2 : dummy;
         asm volatile("ds_read_b32 %0, %1" : "=v"(w[u]) : "v"(a[u]) : "memory");
     }
@@ -485,7 +486,7 @@ __device__ __forceinline__ void score_long_item(
                     scatter_load<4>(post + p0, H - p0, tid, r);  // past the end: doc 32768, v 0
 #pragma unroll
                     for (int u = 0; u < 4; ++u) {
-                        const uint32_t d = ((r[u] ^ POST_X) >> 8) - (uint32_t)hb;
+                        const uint32_t d = ((r[u] ^ POST_X) >> 10) - (uint32_t)hb;
                         const uint64_t v = r[u] & 255u;
                         if (d < (uint32_t)hn && v >= vmin) {  // a doc occurs once per term
                             const uint64_t w = acc[d];
@@ -1894,7 +1895,7 @@ void build_index(di_index *ix, const int64_t *term_off, int64_t n_terms, const u
             }
         }
     });
-    for (auto &w : packed) w ^= POST_X;  // device encoding (see POST_X)
+    for (auto &w : packed) w = (((w >> 8) << 10) | (w & 255u)) ^ POST_X;  // device encoding (see POST_X)
     upload(ix->post, packed);
     upload(ix->tb_start, tb_start);
     upload(ix->eblk, eblk);
