@@ -87,7 +87,24 @@ def load_pmc_traffic(name, leg=None):
     return None, None
 
 
-def retrieve_leg(args, rank, world, dev, n_docs=DOCS_PER_SHARD, check_queries=0):
+def load_pmc_counters(name, leg):
+    """(counter dict, file name) of kernel `name` in the leg's newest PMC summary."""
+    for p in sorted((ROOT / "profiles").glob(f"*pmc_{leg}.json"), reverse=True):
+        try:
+            k = json.loads(p.read_text()).get("kernels", {}).get(name)
+        except Exception:
+            continue
+        if k:
+            return k, p.name
+    return None
+
+
+LDS_CUS = 256
+LDS_CLOCK_HZ = 2.4e9
+LDS_CYCLES_PER_64_POSTINGS = 6.0
+
+
+def retrieve_leg(args, rank, world, dev, n_docs=DOCS_PER_SHARD, check_queries=20):
     """One doc-id shard of n_docs per rank.  100k docs: the numpy generator
     (synthetic.msmarco_like_docs, one doc at a time); larger shards: the same
     distribution from the library's threaded generator (synthetic.synth_postings).
@@ -227,6 +244,25 @@ def retrieve_leg(args, rank, world, dev, n_docs=DOCS_PER_SHARD, check_queries=0)
         "launches": n_sb,
         "traffic_source": src,
     }
+    # the scatter's own ceiling: one conflict-free ds_read_b32 (2 LDS cycles per wave) +
+    # ds_write_b32 (4) per 64 postings on each CU (MI355X_MICROARCH.md "LDS" table)
+    lds_peak = LDS_CUS * LDS_CLOCK_HZ / LDS_CYCLES_PER_64_POSTINGS * 64.0
+    posts_per_s = post_per_launch / avg_s if avg_s > 0 else 0.0
+    lds = {"kernel": "score_blocks_kernel", "bound": "lds_rmw",
+           "achieved": round(posts_per_s / 1e12, 4), "peak": round(lds_peak / 1e12, 4),
+           "unit": "Tpostings/s", "frac": round(posts_per_s / lds_peak, 4),
+           "model": f"{LDS_CYCLES_PER_64_POSTINGS:g} LDS cycles per 64 postings (ds_read_b32 2 + "
+                    f"ds_write_b32 4) x {LDS_CUS} CUs x {LDS_CLOCK_HZ / 1e9:g} GHz"}
+    pmc = load_pmc_counters("score_blocks_kernel", leg) if leg else None
+    if pmc:
+        for c in ("SQ_LDS_BANK_CONFLICT", "SQ_LDS_IDX_ACTIVE", "GRBM_GUI_ACTIVE"):
+            if c in pmc[0]:
+                lds[c.lower() + "_per_launch"] = pmc[0][c]
+        if "SQ_LDS_BANK_CONFLICT" in pmc[0] and "SQ_LDS_IDX_ACTIVE" in pmc[0]:
+            lds["bank_conflict_share"] = round(pmc[0]["SQ_LDS_BANK_CONFLICT"] /
+                                               max(pmc[0]["SQ_LDS_IDX_ACTIVE"], 1.0), 4)
+        lds["counters_source"] = pmc[1]
+    res["lds_roofline"] = lds
     return res, (term_off, pdoc - np.uint32(doc_lo), pval, queries,
                  out_doc, out_score, out_n)
 
@@ -593,6 +629,41 @@ def text_legs(args):
     }
 
 
+def _free_port():
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n, argv):
+    """`bench.py --gpus N` without a launcher (WORLD_SIZE unset): start N ranks as a
+    child torchrun, one process per GPU, and forward its JSON line.  The reference's
+    multi-GPU encode needs no launcher either (`Indexer` wraps the model in
+    DataParallel whenever device_count() > 1, indexer.py:25-26).  Runs before any GPU
+    call in this process and never execs: the parent only waits on the child."""
+    import subprocess
+
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={n}", "--master-addr", "127.0.0.1",
+           f"--master-port={_free_port()}", str(ROOT / "bench.py")] + argv
+    log(f"bench: launching {n} ranks: {' '.join(cmd[1:])}")
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get(
+        "HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    p = subprocess.Popen(cmd, cwd=str(ROOT), env=env, stdout=subprocess.PIPE, text=True)
+    n_lines = 0
+    for line in p.stdout:
+        if line.startswith("{"):
+            n_lines += 1
+        print(line, end="", flush=True)
+    rc = p.wait()
+    if rc == 0 and n_lines != 1:
+        log(f"bench: the {n}-rank run printed {n_lines} JSON lines, expected 1")
+        return 3
+    return rc
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -620,9 +691,20 @@ def main():
                          "index_e2e (index.py's path end to end, tokenizer workers included)")
     args = ap.parse_args()
 
+    if args.gpus < 1:
+        raise SystemExit(f"--gpus must be >= 1 (got {args.gpus})")
+    if "WORLD_SIZE" not in os.environ:
+        if args.gpus > 1:
+            raise SystemExit(launch_ranks(args.gpus, sys.argv[1:]))
+    elif int(os.environ["WORLD_SIZE"]) != args.gpus:
+        raise SystemExit(f"bench: WORLD_SIZE={os.environ['WORLD_SIZE']} but --gpus {args.gpus}: "
+                         f"launch one rank per GPU (--nproc-per-node {args.gpus}) or drop the "
+                         f"launcher and let bench.py start the ranks")
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    backend = None
+    ranks_seen = 1
     if world > 1:
         # one rank per GPU over RCCL; more ranks than GPUs (a 1-GPU rehearsal of the
         # multi-rank path) share the devices over gloo with host-staged collectives
@@ -632,6 +714,14 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group("gloo")
+        backend = dist.get_backend()
+        # every rank contributes a 1: the count the collective actually saw
+        one = torch.ones(1, dtype=torch.int64, device="cpu" if _gloo() else "cuda")
+        seen = torch.zeros(world, dtype=torch.int64, device=one.device)
+        dist.all_gather_into_tensor(seen, one)
+        ranks_seen = int(seen.sum().item())
+        if ranks_seen != world:
+            raise SystemExit(f"bench: all_gather saw {ranks_seen} ranks of {world}")
     else:
         torch.cuda.set_device(0)
     dev = torch.cuda.current_device()
@@ -648,16 +738,16 @@ def main():
         x3_res, x3_ctx = encode_leg(args, rank, world, dev, precision="bf16x3")
     if "encode" in legs:
         enc_res, enc_ctx = encode_leg(args, rank, world, dev)
+    # (profiling ablations of the scorer, DI_PROFILE_ABLATE, change its results)
+    n_check = 0 if os.environ.get("DI_PROFILE_ABLATE") else 20
     if "retrieve" in legs:
-        ret_res, ret_ctx = retrieve_leg(args, rank, world, dev)
+        ret_res, ret_ctx = retrieve_leg(args, rank, world, dev, check_queries=n_check)
     e2e_res = index_e2e_leg(args, dev) if "index_e2e" in legs and world == 1 else None
     text_res = text_legs(args) if "text" in legs and rank == 0 else None
     big = {}
     for leg, nd in (("retrieve_shard", 1_100_000), ("retrieve_full", 8_800_000)):
         if leg in legs:
-            # (profiling ablations of the scorer, DI_PROFILE_ABLATE, change its results)
-            big[leg], _ = retrieve_leg(args, rank, world, dev, n_docs=nd,
-                                       check_queries=0 if os.environ.get("DI_PROFILE_ABLATE") else 20)
+            big[leg], _ = retrieve_leg(args, rank, world, dev, n_docs=nd, check_queries=n_check)
             torch.cuda.empty_cache()
     # the headline is the fp32-faithful encode (bf16x3: the reference computes in fp32,
     # indexer.py:46); the bf16 throughput mode is a side line (it flips a third of the
@@ -671,6 +761,8 @@ def main():
         "value": round(primary["value"], 2),
         "unit": "docs/s" if primary in (enc_res, x3_res, e2e_res) else "queries/s",
         "n_gpus": world,
+        "backend": backend,
+        "ranks_seen": ranks_seen,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(primary.get("ms_per_step") or 1e3 * primary.get("seconds", 0), 4),
@@ -720,7 +812,7 @@ def main():
                            "ms_per_step": round(ret_res["ms_per_step"], 4),
                            "postings_per_query": round(ret_res["postings_per_query"], 1),
                            "kernel_ms": ret_res["kernel_ms"], "roofline": ret_res["roofline"],
-                           "cpu_baseline": None}
+                           "lds_roofline": ret_res["lds_roofline"], "cpu_baseline": None}
     if e2e_res is not None:
         out["index_e2e"] = e2e_res
     if text_res is not None:
@@ -731,7 +823,8 @@ def main():
                     "ms_per_step": round(r["ms_per_step"], 4),
                     "postings_per_query": round(r["postings_per_query"], 1),
                     "kernel_ms": r["kernel_ms"], "kernel_ms_per_step": r["kernel_ms_per_step"],
-                    "launches_per_step": r["launches_per_step"], "roofline": r["roofline"]}
+                    "launches_per_step": r["launches_per_step"], "roofline": r["roofline"],
+                    "lds_roofline": r["lds_roofline"]}
     if rank == 0 and world == 1 and not args.no_cpu:
         if x3_res is not None or enc_res is not None:
             cb = cpu_baseline_encode(args, *(x3_ctx if x3_res is not None else enc_ctx))

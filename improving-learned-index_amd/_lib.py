@@ -85,6 +85,56 @@ SIGNATURES = {
 _LIB = None
 
 
+def hip_runtimes_mapped():
+    """Real paths of every libamdhip64 mapped into this process (/proc/self/maps)."""
+    found = set()
+    try:
+        with open("/proc/self/maps") as f:
+            for line in f:
+                p = line.split(maxsplit=5)
+                if len(p) == 6 and "libamdhip64.so" in p[5]:
+                    found.add(os.path.realpath(p[5].strip()))
+    except OSError:
+        pass
+    return found
+
+
+def _torch_lib_dir():
+    import importlib.util
+
+    spec = importlib.util.find_spec("torch")
+    if spec is None or not spec.origin:
+        return None
+    return os.path.realpath(os.path.join(os.path.dirname(spec.origin), "lib"))
+
+
+def _guard_hip_runtime():
+    """torch bundles its own libamdhip64.so (SONAME libamdhip64.so.7, like
+    /opt/rocm's this library links), and whichever loads first serves both.  So
+    when torch is importable, torch's runtime must be the one mapped: import torch
+    before loading the library, and refuse if a different HIP runtime is already in
+    the process (an embedder that loaded /opt/rocm's first would break torch)."""
+    import sys
+
+    tdir = _torch_lib_dir()
+    if tdir is None:
+        return  # no torch: the library's own runtime (RUNPATH /opt/rocm) serves alone
+    if "torch" not in sys.modules:
+        foreign = [p for p in hip_runtimes_mapped() if not p.startswith(tdir + os.sep)]
+        if foreign:
+            raise RuntimeError(
+                f"a HIP runtime other than torch's is already loaded ({', '.join(foreign)}); "
+                f"torch ({tdir}) would bind to it. Import torch before loading any HIP "
+                f"library, or before importing improving_learned_index_amd")
+        import torch  # noqa: F401  (maps torch's libamdhip64 first)
+
+
+def _check_one_runtime():
+    rts = hip_runtimes_mapped()
+    if len(rts) > 1:
+        raise RuntimeError(f"two HIP runtimes are mapped into this process: {sorted(rts)}")
+
+
 def lib():
     """Load the HIP library (raises if it is missing -- no fallback)."""
     global _LIB
@@ -93,7 +143,9 @@ def lib():
             raise RuntimeError(
                 f"{LIB_PATH} is missing: the HIP extension must be built "
                 f"(python -c 'import __graft_entry__; __graft_entry__.build()')")
+        _guard_hip_runtime()
         L = ctypes.CDLL(str(LIB_PATH))
+        _check_one_runtime()
         # (DI_LIB_ALLOW_MISSING=1: an older build for an A/B run, tools/ab_scorer.sh)
         allow_missing = os.environ.get("DI_LIB_ALLOW_MISSING") == "1"
         for name, (res, args) in SIGNATURES.items():

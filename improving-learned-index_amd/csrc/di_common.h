@@ -10,6 +10,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
+#include <exception>
 #include <map>
 #include <string>
 #include <thread>
@@ -39,19 +40,50 @@ inline int host_threads() {
     return std::max(1, std::min(t > 0 ? t : 1, 64));
 }
 
-// f(lo, hi, thread) over [0, n) split in host_threads() contiguous ranges.  f must not
-// throw (a worker has no one to report to): collect failures and check them after.
+// f(lo, hi, thread) over [0, n) split in `threads` contiguous ranges (thread t always
+// gets the same range for the same n and threads).  A worker's exception -- a
+// di::Error with its thread-local message, std::bad_alloc, anything -- is carried to
+// the calling thread and rethrown there after every worker has joined (the lowest
+// thread's), so the C-ABI guard turns it into a status code instead of
+// std::terminate.
 template <class F>
-void parallel_for(int64_t n, F &&f) {
-    const int T = (int)std::min<int64_t>(host_threads(), std::max<int64_t>(n, 1));
+void parallel_for_threads(int64_t n, int threads, F &&f) {
+    const int T = (int)std::min<int64_t>(std::max(threads, 1), std::max<int64_t>(n, 1));
     if (T == 1) {
         f((int64_t)0, n, 0);
         return;
     }
+    std::vector<std::exception_ptr> err((size_t)T);
+    std::vector<int> code((size_t)T, 0);
+    std::vector<std::string> msg((size_t)T);
     std::vector<std::thread> th;
     th.reserve((size_t)T);
-    for (int t = 0; t < T; ++t) th.emplace_back([&, t] { f(n * t / T, n * (t + 1) / T, t); });
+    for (int t = 0; t < T; ++t)
+        th.emplace_back([&, t] {
+            try {
+                f(n * t / T, n * (t + 1) / T, t);
+            } catch (const Error &e) {
+                code[(size_t)t] = e.code;
+                msg[(size_t)t] = last_error();
+                err[(size_t)t] = std::current_exception();
+            } catch (...) {
+                err[(size_t)t] = std::current_exception();
+            }
+        });
     for (auto &x : th) x.join();
+    for (int t = 0; t < T; ++t)
+        if (err[(size_t)t]) {
+            if (code[(size_t)t]) {
+                set_error("%s", msg[(size_t)t].c_str());
+                throw Error{code[(size_t)t]};
+            }
+            std::rethrow_exception(err[(size_t)t]);
+        }
+}
+
+template <class F>
+void parallel_for(int64_t n, F &&f) {
+    parallel_for_threads(n, host_threads(), std::forward<F>(f));
 }
 
 // parallel_for over n chunks whose bodies may throw di::Error: f(chunk, thread).  The
@@ -81,6 +113,19 @@ void parallel_chunks(int64_t n, F &&f) {
             set_error("%s", msg[(size_t)c].c_str());
             throw Error{code[(size_t)c]};
         }
+}
+
+// body(); a di::Error it throws gets "line N: " in front of its message, N = line_of()
+// (1-based; evaluated on the error path only, so it may rescan the input).
+template <class Body, class LineOf>
+void with_line_context(Body &&body, LineOf &&line_of) {
+    try {
+        body();
+    } catch (const Error &) {
+        const std::string m = last_error();
+        set_error("line %lld: %s", (long long)line_of(), m.c_str());
+        throw;
+    }
 }
 
 [[noreturn]] inline void fail(int code, const char *msg) {

@@ -90,6 +90,14 @@ inline void for_each_line(std::string_view buf, F &&f) {
     }
 }
 
+// Lines for_each_line yields over buf (for a prefix that ends at a line boundary: the
+// number of lines before it).  Used on error paths to place a line in the whole file.
+inline int64_t count_lines(std::string_view buf) {
+    int64_t n = 0;
+    for_each_line(buf, [&](std::string_view) { ++n; });
+    return n;
+}
+
 // Cut buf into at most `parts` ranges of whole lines: boundaries right after a line
 // terminator (\n, a \r\n pair, a lone \r), so for_each_line over the ranges in order
 // yields exactly the lines of the whole buffer.  Returns the cut positions (first 0,

@@ -86,8 +86,11 @@ extern "C" int di_quantize_file(const char *input_path, const char *output_path,
         parallel_chunks(C, [&](int64_t c, int) {
             Part &pc = P[(size_t)c];
             std::vector<std::string_view> pieces, tv;
+            int64_t ln = 0;  // lines of this range seen so far
+            with_line_context([&] {
             py::for_each_line(std::string_view(buf).substr(cut[c], cut[c + 1] - cut[c]),
                               [&](std::string_view line) {
+                ++ln;
                 py::split(py::strip(line), ", ", pieces);
                 for (auto t : pieces) {
                     py::split(py::strip(t), ": ", tv);
@@ -103,6 +106,7 @@ extern "C" int di_quantize_file(const char *input_path, const char *output_path,
                 }
                 pc.cu.push_back((uint32_t)pc.terms.size());
             });
+            }, [&] { return py::count_lines(std::string_view(buf).substr(0, cut[c])) + ln; });
         });
         std::vector<int64_t> off((size_t)C + 1, 0);
         for (int c = 0; c < C; ++c) off[(size_t)c + 1] = off[(size_t)c] + (int64_t)P[(size_t)c].vals.size();

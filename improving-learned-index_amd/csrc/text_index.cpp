@@ -5,7 +5,8 @@
 // (src/deep_impact/indexing/deep_impact_collection.py:6-33); output is
 // byte-identical: vocab.txt, inverted_index.idx, inverted_index.dat.
 //
-// Every pass runs on host_threads() threads: the collection is cut into ranges of
+// Every pass runs on host_threads() threads (the per-term counting passes on as many
+// as fit a memory budget): the collection is cut into ranges of
 // whole lines (parsed in parallel, doc ids = global line numbers), the vocabulary is
 // the union of per-thread term sets merged by hash partition and sorted, the postings
 // are bucketed by term with per-thread write offsets (doc order inside a term), then
@@ -57,11 +58,12 @@ inline uint64_t fnv1a(std::string_view x) {
     return h;
 }
 
-void parse_collection(std::string_view buf, Parsed &P) {
+void parse_collection(std::string_view buf, Parsed &P, int64_t *ln) {
     P.cu.push_back(0);
     std::vector<std::string_view> pairs, tv;
     std::vector<std::pair<uint64_t, uint32_t>> hs;
     py::for_each_line(buf, [&](std::string_view line) {
+        ++*ln;
         std::string_view s = py::strip(line);
         if (!py::strip(s).empty()) {
             py::split(s, ", ", pairs);
@@ -115,10 +117,23 @@ void parse_collection(std::string_view buf, Parsed &P) {
         }
         P.cu.push_back((uint32_t)P.term.size());
     });
-    for (uint16_t v : P.val)
-        DI_REQUIRE(v <= 255, DI_EFORMAT,
-                   "a value does not fit the 1-byte impact record (struct.error in the "
-                   "reference)");
+    for (size_t d = 0; d + 1 < P.cu.size(); ++d)
+        for (uint32_t i = P.cu[d]; i < P.cu[d + 1]; ++i)
+            if (P.val[i] > 255) {
+                *ln = (int64_t)d + 1;  // (the line of the offending value)
+                DI_REQUIRE(false, DI_EFORMAT,
+                           "a value does not fit the 1-byte impact record (struct.error in "
+                           "the reference)");
+            }
+}
+
+// Threads for the per-term count arrays (V u32 counters per thread): at most
+// host_threads(), and no more than fit kCountBudget bytes together (V = 17.6 M terms
+// is 70 MB per thread).
+constexpr size_t kCountBudget = size_t(1) << 30;
+int count_threads(size_t V, int T) {
+    const size_t per = std::max<size_t>(V, 1) * sizeof(uint32_t);
+    return (int)std::max<size_t>(1, std::min<size_t>((size_t)T, kCountBudget / per));
 }
 
 void write_all(const std::string &path, const void *data, size_t n) {
@@ -141,8 +156,13 @@ extern "C" int di_build_reference_index(const char *collection_path, const char 
         const int C = (int)cut.size() - 1;
         std::vector<Parsed> P((size_t)std::max(C, 1));
         parallel_chunks(C, [&](int64_t c, int) {
-            parse_collection(std::string_view(buf).substr(cut[c], cut[c + 1] - cut[c]),
-                             P[(size_t)c]);
+            int64_t ln = 0;
+            with_line_context(
+                [&] {
+                    parse_collection(std::string_view(buf).substr(cut[c], cut[c + 1] - cut[c]),
+                                     P[(size_t)c], &ln);
+                },
+                [&] { return py::count_lines(std::string_view(buf).substr(0, cut[c])) + ln; });
         });
         std::vector<int64_t> doc0((size_t)C + 1, 0), occ0((size_t)C + 1, 0);
         for (int c = 0; c < C; ++c) {
@@ -152,25 +172,34 @@ extern "C" int di_build_reference_index(const char *collection_path, const char 
         const int64_t n_docs = doc0[(size_t)C], n_occ = occ0[(size_t)C];
         DI_REQUIRE(n_docs <= 0xFFFFFFFFll, DI_ERANGE, "more than 2^32 documents");
         // 2. vocabulary: sorted(set(terms)) -- code-point order == UTF-8 byte order.
-        // Per-thread sets over contiguous chunk ranges, merged by hash partition.
+        // Per-thread sets over contiguous chunk ranges, each dealt once into T hash
+        // partitions; partition p then merges its T buckets (total work ~ the sets'
+        // sizes, not T times them).
         const std::hash<std::string_view> H;
-        std::vector<std::unordered_set<std::string_view>> tset((size_t)T);
-        parallel_for(C, [&](int64_t lo, int64_t hi, int t) {
-            auto &st = tset[(size_t)t];
+        std::vector<std::vector<std::vector<std::string_view>>> bucket(
+            (size_t)T, std::vector<std::vector<std::string_view>>((size_t)T));
+        parallel_for_threads(C, T, [&](int64_t lo, int64_t hi, int t) {
+            std::unordered_set<std::string_view> st;
             for (int64_t c = lo; c < hi; ++c)
                 for (auto x : P[(size_t)c].term) st.insert(x);
+            auto &b = bucket[(size_t)t];
+            for (auto x : st) b[H(x) % (size_t)T].push_back(x);
         });
         std::vector<std::vector<std::string_view>> part((size_t)T);
-        parallel_for(T, [&](int64_t lo, int64_t hi, int) {
+        parallel_for_threads(T, T, [&](int64_t lo, int64_t hi, int) {
             for (int64_t p = lo; p < hi; ++p) {
+                size_t m = 0;
+                for (auto &b : bucket) m += b[(size_t)p].size();
                 std::unordered_set<std::string_view> u;
-                for (auto &st : tset)
-                    for (auto x : st)
-                        if (H(x) % (size_t)T == (size_t)p) u.insert(x);
+                u.reserve(m);
+                for (auto &b : bucket) {
+                    for (auto x : b[(size_t)p]) u.insert(x);
+                    std::vector<std::string_view>().swap(b[(size_t)p]);
+                }
                 part[(size_t)p].assign(u.begin(), u.end());
             }
         });
-        std::vector<std::unordered_set<std::string_view>>().swap(tset);
+        decltype(bucket)().swap(bucket);
         std::vector<std::string_view> vocab;
         for (auto &pp : part) vocab.insert(vocab.end(), pp.begin(), pp.end());
         std::sort(vocab.begin(), vocab.end());
@@ -178,10 +207,10 @@ extern "C" int di_build_reference_index(const char *collection_path, const char 
         DI_REQUIRE(V < 0xFFFFFFFFull, DI_ERANGE, "more than 2^32 terms");
         // id lookup: per-partition maps (built in parallel, read-only after)
         std::vector<std::unordered_map<std::string_view, uint32_t>> idmap((size_t)T);
-        parallel_for(T, [&](int64_t lo, int64_t hi, int) {
+        parallel_for_threads(T, T, [&](int64_t lo, int64_t hi, int) {
             for (int64_t p = lo; p < hi; ++p) idmap[(size_t)p].reserve(part[(size_t)p].size());
         });
-        parallel_for(T, [&](int64_t lo, int64_t hi, int) {
+        parallel_for_threads(T, T, [&](int64_t lo, int64_t hi, int) {
             for (int64_t p = lo; p < hi; ++p)
                 for (auto x : part[(size_t)p]) idmap[(size_t)p].emplace(x, 0u);
         });
@@ -191,10 +220,12 @@ extern "C" int di_build_reference_index(const char *collection_path, const char 
                 idmap[H(x) % (size_t)T].find(x)->second = (uint32_t)i;  // (own slot: no race)
             }
         });
-        // 3. term id of every occurrence; per-thread counts per term
+        // 3. term id of every occurrence; per-thread counts per term (TC threads: the
+        // count arrays are V words each, kept within kCountBudget together)
+        const int TC = count_threads(V, T);
         std::vector<uint32_t> tid((size_t)std::max<int64_t>(n_occ, 1));
-        std::vector<std::vector<uint32_t>> tcnt((size_t)T);
-        parallel_for(C, [&](int64_t lo, int64_t hi, int t) {
+        std::vector<std::vector<uint32_t>> tcnt((size_t)TC);
+        parallel_for_threads(C, TC, [&](int64_t lo, int64_t hi, int t) {
             auto &cnt = tcnt[(size_t)t];
             cnt.assign(V, 0);
             for (int64_t c = lo; c < hi; ++c) {
@@ -214,7 +245,7 @@ extern "C" int di_build_reference_index(const char *collection_path, const char 
         std::vector<std::vector<uint32_t>> &tpos = tcnt;  // counts -> offsets in place
         for (size_t t = 0; t < V; ++t) {
             int64_t run = toff[t];
-            for (int th = 0; th < T; ++th) {
+            for (int th = 0; th < TC; ++th) {
                 auto &v = tpos[(size_t)th];
                 if (v.empty()) continue;
                 const uint32_t c = v[t];
@@ -225,7 +256,8 @@ extern "C" int di_build_reference_index(const char *collection_path, const char 
         }
         std::vector<uint32_t> bdoc((size_t)std::max<int64_t>(n_occ, 1));
         std::vector<uint8_t> bval((size_t)std::max<int64_t>(n_occ, 1));
-        parallel_for(C, [&](int64_t lo, int64_t hi, int t) {
+        // (same TC threads and chunk ranges as the counting pass: thread t's offsets)
+        parallel_for_threads(C, TC, [&](int64_t lo, int64_t hi, int t) {
             auto &off = tpos[(size_t)t];
             for (int64_t c = lo; c < hi; ++c) {
                 const auto &pc = P[(size_t)c];

@@ -18,6 +18,7 @@ from __future__ import annotations
 
 import argparse
 import logging
+import sys
 import time
 from pathlib import Path
 
@@ -124,14 +125,27 @@ def main(argv=None):
     p.add_argument("--precision", choices=["bf16x3", "fp32", "bf16"], default="bf16x3",
                    help="bf16x3 (default): fp32-faithful split-bf16; fp32: f32 MFMA; "
                         "bf16: throughput mode, NOT fp32-faithful (different round3 text)")
-    p.add_argument("--device", type=int, default=0)
+    p.add_argument("--device", type=int, default=None,
+                   help="encode on this GPU only (default: every visible GPU, see --gpus)")
+    p.add_argument("--gpus", type=int, default=None,
+                   help="without torchrun: encode on this many GPUs, one child rank each, "
+                        "doc-id shards joined in order (default: every visible GPU, as the "
+                        "reference's DataParallel, indexer.py:25-26; 1 = this process only)")
     p.add_argument("--variant", choices=["xlmr", "bert"], default="xlmr")
     p.add_argument("--doc_range", type=str, default=None, help="start:end line range (shard)")
+    argv = list(sys.argv[1:] if argv is None else argv)
     a = p.parse_args(argv)
+    if a.doc_range is None and a.device is None:
+        n = parallel.ranks_to_spawn(a.gpus)
+        if n > 1:
+            rc = parallel.spawn_ranks("index", argv, n)
+            if rc:
+                raise SystemExit(rc)
+            return
     dr = tuple(int(x) for x in a.doc_range.split(":")) if a.doc_range else None
     logging.basicConfig(level=logging.INFO)
     world, rank, local = parallel.dist_env()
-    out, device = a.output_file_path, a.device
+    out, device = a.output_file_path, (a.device or 0)
     if world > 1:
         import torch.distributed as dist
 

@@ -28,6 +28,52 @@ def dist_env() -> Tuple[int, int, int]:
             int(os.environ.get("LOCAL_RANK", "0")))
 
 
+def visible_gpus() -> int:
+    """GPUs this process sees, counted without initialising HIP (torch's count reads
+    the device list only; HIP must not come up in a parent that spawns ranks)."""
+    import torch
+
+    return torch.cuda.device_count()
+
+
+def ranks_to_spawn(requested: Optional[int]) -> int:
+    """How many per-GPU ranks a CLI started without a launcher should fan out to: the
+    reference's Indexer wraps the model in DataParallel whenever
+    torch.cuda.device_count() > 1 (indexer.py:25-26), so by default every visible
+    GPU; `requested` (--gpus) overrides, and 1 keeps one process.  Under torchrun
+    (WORLD_SIZE set) the launcher already decided: 1."""
+    if "WORLD_SIZE" in os.environ:
+        return 1
+    n = max(1, visible_gpus()) if requested is None else int(requested)
+    if n < 1:
+        raise ValueError(f"--gpus must be >= 1 (got {n})")
+    return n
+
+
+def spawn_ranks(module: str, argv: Sequence[str], n: int) -> int:
+    """Run `python -m improving_learned_index_amd.<module> argv` as n ranks of a child
+    torchrun (one process per GPU, doc-id shards, rank 0 joins the outputs) and
+    return its exit status.  The parent has made no HIP call and never execs."""
+    import socket
+    import subprocess
+    import sys
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    root = str(Path(__file__).resolve().parent.parent)
+    env = dict(os.environ)
+    env["PYTHONPATH"] = root + (os.pathsep + env["PYTHONPATH"] if env.get("PYTHONPATH") else "")
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    # one hash seed for every rank: rank 0's query-term order is broadcast anyway, but
+    # the children then also agree with one another on everything set-ordered
+    env.setdefault("PYTHONHASHSEED", str(int.from_bytes(os.urandom(2), "little")))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={n}", "--master-addr", "127.0.0.1", f"--master-port={port}",
+           "-m", f"improving_learned_index_amd.{module}"] + list(argv)
+    return subprocess.call(cmd, env=env)
+
+
 def init_group(backend: str, local_rank: int = 0):
     """Process group of a torchrun-launched CLI: "nccl" (RCCL over xGMI; every rank
     owns GPU local_rank) for the retrieval exchange, "gloo" for the host-only
@@ -234,10 +280,18 @@ class ShardedRetriever:
                                np.ascontiguousarray(counts.T), k)
 
     def search_keys(self, queries) -> Tuple[np.ndarray, np.ndarray]:
+        mk, mn, _ = self._search_keys(queries)
+        return mk, mn
+
+    def _search_keys(self, queries):
         import torch
         import torch.distributed as dist
 
-        keys, counts = self.local_search(queries)
+        res = self.local_search(queries)
+        # local_search may drop terms (unknown words): it then returns the term counts it
+        # actually submitted, which decide the key layout (wide above 256 terms)
+        keys, counts = res[0], res[1]
+        n_terms = res[2] if len(res) > 2 else [len(q) for q in queries]
         world = dist.get_world_size(self.group)
         kt = torch.from_numpy(np.ascontiguousarray(keys).view(np.int64)).to(self.device)
         ct = torch.from_numpy(np.ascontiguousarray(counts, np.int32)).to(self.device)
@@ -249,11 +303,12 @@ class ShardedRetriever:
         dist.all_gather_into_tensor(gc, ct, group=self.group)
         gk = gk.cpu().numpy().view(np.uint64).reshape((world,) + tuple(kt.shape))
         gc = gc.cpu().numpy().reshape(world, -1)
-        return self.merge(gk, gc, self.k)
+        mk, mn = self.merge(gk, gc, self.k)
+        return mk, mn, n_terms
 
     def search(self, queries) -> List[List[Tuple[int, int]]]:
-        mk, mn = self.search_keys(queries)
-        return [decode_quant_keys(mk[i], int(mn[i]), len(queries[i])) for i in range(len(mn))]
+        mk, mn, n_terms = self._search_keys(queries)
+        return [decode_quant_keys(mk[i], int(mn[i]), int(n_terms[i])) for i in range(len(mn))]
 
 
 def exchange_merge_device(index, queries, k: int, device: int, flags: int = 0):
@@ -316,12 +371,13 @@ def _exchange_merge(index, queries, k, device, dev, stream, flags):
 
 
 def device_shard_search(index, k: int):
-    """local_search for ShardedRetriever over a DeviceIndex shard (HIP)."""
+    """local_search for ShardedRetriever over a DeviceIndex shard (HIP): queries are
+    term-id lists, submitted whole (the counts returned are theirs)."""
     from . import _lib
 
     def run(queries):
         flat, cu = _lib.csr(queries)
         _, _, n, keys = index.search_csr(flat, cu, k, with_keys=True)
-        return keys, n
+        return keys, n, np.diff(cu)
 
     return run

@@ -16,6 +16,7 @@ process (the keys totally order score, first touch and doc).
 from __future__ import annotations
 
 import argparse
+import sys
 from itertools import product
 from pathlib import Path
 from typing import Optional, Union
@@ -111,7 +112,11 @@ def main(argv=None):
     p.add_argument("--dataset_type", type=str, default=COLLECTION_TYPES[0], choices=COLLECTION_TYPES)
     p.add_argument("--pairwise", action="store_true")
     p.add_argument("--tokenizer_path", type=str, required=True)
-    p.add_argument("--device", type=int, default=0)
+    p.add_argument("--device", type=int, default=None,
+                   help="score on this GPU only (default: every visible GPU, see --gpus)")
+    p.add_argument("--gpus", type=int, default=None,
+                   help="without torchrun: shard the index over this many GPUs, one child rank "
+                        "each (default: every visible GPU; 1 = this process only)")
     p.add_argument("--top_k", type=int, default=1000)
     p.add_argument("--min_impact", type=int, default=1,
                    help="query-time pruning: score postings with value >= this (rounded down "
@@ -119,9 +124,17 @@ def main(argv=None):
     p.add_argument("--block_max", type=float, default=0.0,
                    help="block-max skipping: 0 off, 1 exact, > 1 approximate (skip block "
                         "segments whose bound is below this factor x the running k-th score)")
+    argv = list(sys.argv[1:] if argv is None else argv)
     a = p.parse_args(argv)
+    if a.device is None:
+        n = parallel.ranks_to_spawn(a.gpus)
+        if n > 1:
+            rc = parallel.spawn_ranks("rank", argv, n)
+            if rc:
+                raise SystemExit(rc)
+            return
     Ranker(a.index_path, a.queries_path, a.output_path, a.num_workers, a.qrels_path, a.pairwise,
-           a.dataset_type, a.tokenizer_path, a.device, top_k=a.top_k,
+           a.dataset_type, a.tokenizer_path, a.device or 0, top_k=a.top_k,
            min_impact=a.min_impact, block_max=a.block_max).run()
 
 

@@ -9,6 +9,11 @@ for p in (ROOT, ROOT / "oracle", ROOT / "tests" / "golden"):
 
 GOLDEN = ROOT / "tests" / "golden"
 
+# torch's bundled HIP runtime is mapped before anything loads libdeepimpact_hip.so
+# directly (ctypes.CDLL in test_boundary): _lib.lib() refuses a process where another
+# libamdhip64 came first (_lib._guard_hip_runtime)
+import torch  # noqa: E402,F401
+
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (HIP device)")

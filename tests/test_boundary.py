@@ -97,3 +97,37 @@ def test_native_index_builder_at_scale_equals_oracle(tmp_path):
         for name in ("vocab.txt", "inverted_index.idx", "inverted_index.dat"):
             assert (tmp_path / f"got{threads}" / name).read_bytes() == \
                 (tmp_path / "want" / name).read_bytes(), (threads, name)
+
+
+def test_parallel_parse_errors_name_the_global_line(tmp_path):
+    """The threaded parsers (index create, quantize) cut the file into line ranges; a
+    malformed 'term: score' still reports its line in the whole file (1-based), as the
+    serial parse did, whatever range it falls in.  (Both fail in the host parse, before
+    any GPU call.)"""
+    import os
+
+    from improving_learned_index_amd import _lib
+    from improving_learned_index_amd.inverted_index import create_index
+    from improving_learned_index_amd.quantize import quantize_file
+
+    lines = [", ".join(f"▁t{(i * 7 + j) % 97}: {1 + (i + j) % 9}.5" for j in range(20))
+             for i in range(3000)]
+    bad = 2345
+    lines[bad - 1] = "▁ok: 1.0, ▁broken 2.0"
+    src = tmp_path / "c.tsv"
+    src.write_text("\n".join(lines) + "\n", encoding="utf-8")
+    os.environ["DI_HOST_THREADS"] = "8"
+    try:
+        with pytest.raises(_lib.DIError) as e:
+            create_index(src, tmp_path / "out")
+        assert e.value.code == -7 and f"line {bad}:" in str(e.value), str(e.value)
+        with pytest.raises(_lib.DIError) as e:
+            quantize_file(src, tmp_path / "q", sharded=False)
+        assert e.value.code == -7 and f"line {bad}:" in str(e.value), str(e.value)
+        lines[bad - 1] = "▁ok: 300.0"  # past the 1-byte record
+        src.write_text("\n".join(lines) + "\n", encoding="utf-8")
+        with pytest.raises(_lib.DIError) as e:
+            create_index(src, tmp_path / "out")
+        assert f"line {bad}:" in str(e.value), str(e.value)
+    finally:
+        del os.environ["DI_HOST_THREADS"]

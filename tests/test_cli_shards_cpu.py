@@ -150,3 +150,42 @@ def test_quantize_file_sharded_false_stays_local(tmp_path, monkeypatch):
 class _Used:
     def __init__(self, v):
         self.value = v
+
+
+def test_plain_cli_fans_out_to_every_visible_gpu(monkeypatch, tmp_path):
+    """index / rank started without torchrun on a multi-GPU box start one child rank per
+    visible GPU (the reference's DataParallel whenever device_count() > 1,
+    indexer.py:25-26); --gpus overrides; --device or --doc_range keep one process; under
+    torchrun (WORLD_SIZE) nothing is spawned."""
+    from improving_learned_index_amd import parallel, ranker
+
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    monkeypatch.setattr(parallel, "visible_gpus", lambda: 8)
+    spawned = []
+    monkeypatch.setattr(parallel, "spawn_ranks",
+                        lambda mod, argv, n: spawned.append((mod, list(argv), n)) or 0)
+    common = ["--collection_path", "c.tsv", "--output_file_path", "o", "--model_checkpoint_path",
+              "m.pt"]
+    index_cli.main(common)
+    assert spawned == [("index", common, 8)]
+    index_cli.main(common + ["--gpus", "2"])
+    assert spawned[-1] == ("index", common + ["--gpus", "2"], 2)
+    rargs = ["--index_path", "i", "--queries_path", "q", "--output_path", "o",
+             "--tokenizer_path", "t"]
+    ranker.main(rargs)
+    assert spawned[-1] == ("rank", rargs, 8)
+    n = len(spawned)
+    # one process: --device, --doc_range, --gpus 1, or a launcher already running
+    monkeypatch.setattr(index_cli, "run", lambda *a, **k: spawned.append("run"))
+    index_cli.main(common + ["--device", "3"])
+    index_cli.main(common + ["--doc_range", "0:5"])
+    index_cli.main(common + ["--gpus", "1"])
+    monkeypatch.setenv("WORLD_SIZE", "1")
+    index_cli.main(common)
+    assert spawned[n:] == ["run"] * 4
+    assert parallel.ranks_to_spawn(None) == 1
+    monkeypatch.delenv("WORLD_SIZE")
+    monkeypatch.setattr(parallel, "visible_gpus", lambda: 0)
+    assert parallel.ranks_to_spawn(None) == 1  # (no GPU: one process, which fails loudly)
+    with pytest.raises(ValueError):
+        parallel.ranks_to_spawn(0)

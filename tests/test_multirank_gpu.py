@@ -72,6 +72,12 @@ def test_index_cli_two_ranks_equals_one(ckpt):
         _torchrun("index", common + ["--output_file_path", str(td / "two.index")])
         assert (td / "two.index").read_bytes() == (td / "one.index").read_bytes()
         assert not list(td.glob("*.part*"))
+        # no launcher: the plain CLI fans out to child ranks itself (--gpus 2 on this
+        # 1-GPU box; on an 8-GPU node the default is every visible GPU)
+        _torchrun("index", common + ["--output_file_path", str(td / "self.index"), "--gpus",
+                                     "2"], world=0)
+        assert (td / "self.index").read_bytes() == (td / "one.index").read_bytes()
+        assert not list(td.glob("*.part*"))
 
 
 def test_quantize_cli_two_ranks_equals_one():
@@ -112,6 +118,8 @@ def test_rank_cli_two_ranks_equals_one():
         _torchrun("rank", args + ["--output_path", str(td / "one.tsv")], world=0)
         _torchrun("rank", args + ["--output_path", str(td / "two.tsv")])
         _same_run((td / "two.tsv").read_text(), (td / "one.tsv").read_text())
+        _torchrun("rank", args + ["--output_path", str(td / "self.tsv"), "--gpus", "2"], world=0)
+        _same_run((td / "self.tsv").read_text(), (td / "one.tsv").read_text())
         _torchrun("rank", args + ["--output_path", str(td / "three.tsv"), "--top_k", "7"],
                   world=3)
         _torchrun("rank", args + ["--output_path", str(td / "one7.tsv"), "--top_k", "7"],
@@ -177,3 +185,21 @@ def test_bench_two_ranks_completes(tmp_path):
     d = json.loads(line[0])
     assert d["n_gpus"] == 2 and d["unit"] == "queries/s" and d["value"] > 0
     assert d["quantize"]["docs"] == 20000 and d["index_create"]["value"] > 0
+    assert d["ranks_seen"] == 2 and d["backend"] == "gloo"
+
+
+def test_bench_gpus_flag_launches_ranks_itself():
+    """Plain `python3 bench.py --gpus 2` (no launcher, as the driver may run it) starts
+    its two ranks as a child torchrun and reports the ranks its all_gather saw; on this
+    1-GPU box they share the GPU over gloo (an 8-GPU node takes RCCL)."""
+    env = dict(os.environ, PYTHONPATH=str(ROOT), OMP_NUM_THREADS="4")
+    env.pop("WORLD_SIZE", None)
+    cmd = [sys.executable, "bench.py", "--gpus", "2", "--legs", "retrieve,text", "--steps", "1",
+           "--warmup", "1", "--text-docs", "20000", "--queries", "512", "--no-cpu"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-4000:]
+    line = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(line) == 1, r.stdout[-2000:]
+    d = json.loads(line[0])
+    assert d["n_gpus"] == 2 and d["ranks_seen"] == 2 and d["backend"] == "gloo"
+    assert d["value"] > 0
