@@ -38,6 +38,12 @@ class di_timing(ctypes.Structure):
     _fields_ = [("ms", ctypes.c_double), ("launches", ctypes.c_int64)]
 
 
+class di_synth_skew(ctypes.Structure):
+    _fields_ = [("term_rank0", ctypes.c_double), ("term_exp", ctypes.c_double),
+                ("cluster_docs", ctypes.c_int32), ("cluster_sigma", ctypes.c_double),
+                ("doc_sigma", ctypes.c_double), ("mass_max", ctypes.c_double)]
+
+
 P = ctypes.c_void_p
 I32, I64, U32, U64 = ctypes.c_int32, ctypes.c_int64, ctypes.c_uint32, ctypes.c_uint64
 
@@ -78,6 +84,8 @@ SIGNATURES = {
     "di_sparse_destroy": (ctypes.c_int, [P]),
     "di_synth_postings": (ctypes.c_int, [I64, I32, U64, I32, I32, ctypes.c_double, P, P, P, I64,
                                          P, P]),
+    "di_synth_postings_skewed": (ctypes.c_int, [I64, I32, U64, I32, I32, ctypes.c_double, P, P,
+                                                P, P, I64, P, P]),
     "di_synth_impact_tsv": (ctypes.c_int, [ctypes.c_char_p, I64, I32, U64, I32, I32,
                                            ctypes.c_double, P]),
 }

@@ -104,11 +104,37 @@ inline float round3(float x) {
     return (float)(std::nearbyint(t)) / 1000.0f;
 }
 
+// Skew of the impacts (di_synth_skew, include/deepimpact.h; all off = SURVEY §8d's
+// i.i.d. impacts): impact = softplus(N(-0.5, 1.5)) x term factor x doc mass.
+struct Skew {
+    double term_rank0 = 0.0, term_exp = 0.0;
+    int32_t cluster_docs = 0;
+    double cluster_sigma = 0.0, doc_sigma = 0.0, mass_max = 0.0;
+    bool on() const { return term_rank0 > 0.0 || cluster_docs > 0 || doc_sigma > 0.0; }
+    // the term of 0-based zipf rank t: frequent terms carry small impacts (the IDF-like
+    // shape a learned impact model gives its common terms)
+    double term_factor(uint32_t t) const {
+        if (term_rank0 <= 0.0) return 1.0;
+        return std::min(1.0, std::pow(((double)t + 1.0) / term_rank0, term_exp));
+    }
+    // doc d's mass: a lognormal factor shared by its cluster of consecutive doc ids
+    // (passages of one source document sit together) times its own, clipped
+    double mass(uint64_t seed, int64_t d, Rng &r) const {
+        double z = doc_sigma > 0.0 ? doc_sigma * r.normal() : 0.0;
+        if (cluster_docs > 0) {
+            Rng rc(seed ^ 0x5BD1E9955BD1E995ull, (uint64_t)(d / cluster_docs));
+            z += cluster_sigma * rc.normal();
+        }
+        const double m = std::exp(z);
+        return mass_max > 0.0 ? std::min(m, mass_max) : m;
+    }
+};
+
 // Doc d of the collection: its sorted unique 0-based term ids and float32 impacts
 // (the stream depends on (seed, d) only).
 inline void synth_doc(const Alias &zipf, uint64_t seed, int64_t d, int32_t max_terms,
                       int32_t draws, std::vector<uint32_t> &buf, std::vector<uint32_t> &terms,
-                      std::vector<float> &imps) {
+                      std::vector<float> &imps, const Skew &sk = Skew()) {
     Rng r(seed, (uint64_t)d);
     buf.resize((size_t)draws);
     for (int i = 0; i < draws; ++i) buf[(size_t)i] = zipf.sample(r);
@@ -121,6 +147,11 @@ inline void synth_doc(const Alias &zipf, uint64_t seed, int64_t d, int32_t max_t
         const double x = r.normal() * 1.5 - 0.5;
         terms.push_back(buf[i] - 1);
         imps.push_back((float)std::log1p(std::exp(x)));
+    }
+    if (sk.on()) {  // (after the i.i.d. draws: the skew-free stream is unchanged)
+        const double md = sk.mass(seed, d, r);
+        for (size_t i = 0; i < m; ++i)
+            imps[i] = (float)((double)imps[i] * sk.term_factor(terms[i]) * md);
     }
 }
 
@@ -189,11 +220,33 @@ extern "C" int di_synth_postings(int64_t n_docs, int32_t v_terms, uint64_t seed,
                                  int32_t max_terms, int32_t draws, double zipf_a,
                                  int64_t *term_off, uint32_t *pdoc, uint8_t *pval, int64_t cap,
                                  int64_t *n_post, double *max_impact) {
+    return di_synth_postings_skewed(n_docs, v_terms, seed, max_terms, draws, zipf_a, nullptr,
+                                    term_off, pdoc, pval, cap, n_post, max_impact);
+}
+
+extern "C" int di_synth_postings_skewed(int64_t n_docs, int32_t v_terms, uint64_t seed,
+                                        int32_t max_terms, int32_t draws, double zipf_a,
+                                        const di_synth_skew *skew, int64_t *term_off,
+                                        uint32_t *pdoc, uint8_t *pval, int64_t cap,
+                                        int64_t *n_post, double *max_impact) {
     using namespace di;
     return guard([&] {
         DI_REQUIRE(n_docs >= 0 && n_docs <= 0xFFFFFFFFll && v_terms > 0 && max_terms > 0 &&
                        draws > 0 && zipf_a > 1.0 && term_off && n_post,
                    DI_EINVAL, "bad argument");
+        Skew sk;
+        if (skew) {
+            DI_REQUIRE(skew->term_rank0 >= 0.0 && skew->term_exp >= 0.0 &&
+                           skew->cluster_docs >= 0 && skew->cluster_sigma >= 0.0 &&
+                           skew->doc_sigma >= 0.0 && skew->mass_max >= 0.0,
+                       DI_EINVAL, "bad skew parameters");
+            sk.term_rank0 = skew->term_rank0;
+            sk.term_exp = skew->term_exp;
+            sk.cluster_docs = skew->cluster_docs;
+            sk.cluster_sigma = skew->cluster_sigma;
+            sk.doc_sigma = skew->doc_sigma;
+            sk.mass_max = skew->mass_max;
+        }
         const Alias zipf(v_terms, zipf_a);
         // 1. per doc: sorted unique term ids (0-based) and float32 impacts, chunked
         const int T = host_threads();
@@ -216,7 +269,7 @@ extern "C" int di_synth_postings(int64_t n_docs, int32_t v_terms, uint64_t seed,
                 std::vector<uint32_t> terms;
                 std::vector<float> imps;
                 for (int64_t d = d0; d < d1; ++d) {
-                    synth_doc(zipf, seed, d, max_terms, draws, buf, terms, imps);
+                    synth_doc(zipf, seed, d, max_terms, draws, buf, terms, imps, sk);
                     for (size_t i = 0; i < terms.size(); ++i) {
                         vt.push_back(terms[i]);
                         vi.push_back(imps[i]);

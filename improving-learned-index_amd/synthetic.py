@@ -72,15 +72,28 @@ def msmarco_like_queries(n_q, v_terms=200_000, seed=1234, draws=6):
     return out
 
 
-def synth_postings(n_docs, v_terms=200_000, seed=1234, max_terms=100, draws=200, zipf_a=1.2):
+# The skewed collection of the block-max measurements (BASELINE configs[4]; a stated
+# deviation from SURVEY §8d, whose impacts are i.i.d. -- on those every 2 K-doc segment
+# holds a high value of every frequent query term, so exact block-max can skip nothing,
+# DESIGN.md §3).  Impacts: frequent terms small (term factor ((t + 1) / 2000)^0.5 up to
+# rank 2000: the IDF-like shape of a learned impact model), and a heavy-tailed doc mass
+# shared by clusters of 512 consecutive doc ids (passages of one source document)
+# times a per-doc factor, clipped at 6.
+SKEW_CONFIG4 = {"term_rank0": 2000.0, "term_exp": 0.5, "cluster_docs": 512,
+                "cluster_sigma": 1.0, "doc_sigma": 0.5, "mass_max": 6.0}
+
+
+def synth_postings(n_docs, v_terms=200_000, seed=1234, max_terms=100, draws=200, zipf_a=1.2,
+                   skew=None):
     """The same generator at full scale, in the HIP library's host code (threads over
     doc chunks, a counter-based stream per doc): reference-order postings
     (term_off, pdoc u32, pval u8) of the quantized collection and the fp64 max impact.
     Same distribution as msmarco_like_docs -> quantize_like_reference ->
-    postings_reference_order; a different random stream (seconds at 8.8 M docs)."""
+    postings_reference_order; a different random stream (seconds at 8.8 M docs).
+    skew: a dict of di_synth_skew fields (e.g. SKEW_CONFIG4), None = i.i.d. impacts."""
     import ctypes
 
-    from ._lib import check, lib, ptr
+    from ._lib import check, di_synth_skew, lib, ptr
 
     term_off = np.zeros(v_terms + 1, np.int64)
     cap = int(n_docs) * int(max_terms)
@@ -88,9 +101,10 @@ def synth_postings(n_docs, v_terms=200_000, seed=1234, max_terms=100, draws=200,
     pval = np.empty(max(cap, 1), np.uint8)
     n = ctypes.c_int64(0)
     m = ctypes.c_double(0.0)
-    check(lib().di_synth_postings(int(n_docs), int(v_terms), int(seed), int(max_terms),
-                                  int(draws), float(zipf_a), ptr(term_off), ptr(pdoc), ptr(pval),
-                                  cap, ctypes.byref(n), ctypes.byref(m)))
+    sk = ctypes.byref(di_synth_skew(**skew)) if skew else None
+    check(lib().di_synth_postings_skewed(int(n_docs), int(v_terms), int(seed), int(max_terms),
+                                         int(draws), float(zipf_a), sk, ptr(term_off), ptr(pdoc),
+                                         ptr(pval), cap, ctypes.byref(n), ctypes.byref(m)))
     return term_off, pdoc[:n.value], pval[:n.value], m.value
 
 

@@ -282,6 +282,27 @@ int di_synth_postings(int64_t n_docs, int32_t v_terms, uint64_t seed, int32_t ma
                       int32_t draws, double zipf_a, int64_t *term_off, uint32_t *pdoc,
                       uint8_t *pval, int64_t cap, int64_t *n_post, double *max_impact);
 
+/* Skew of a synthetic collection's impacts -- a documented deviation from SURVEY §8d's
+ * i.i.d. impacts, for block-max skipping (BASELINE configs[4]): impact =
+ * softplus(N(-0.5, 1.5)) x min(1, ((t + 1) / term_rank0)^term_exp) (t = the term's
+ * 0-based zipf rank: frequent terms carry small impacts; term_rank0 0 = off) x the doc's
+ * mass min(mass_max, exp(cluster_sigma z_c + doc_sigma z_d)) (z_c shared by the
+ * cluster_docs consecutive doc ids of a cluster, z_d per doc; mass_max 0 = no clip). */
+typedef struct di_synth_skew {
+    double term_rank0;
+    double term_exp;
+    int32_t cluster_docs;
+    double cluster_sigma;
+    double doc_sigma;
+    double mass_max;
+} di_synth_skew;
+
+/* di_synth_postings with skewed impacts (skew null: exactly di_synth_postings). */
+int di_synth_postings_skewed(int64_t n_docs, int32_t v_terms, uint64_t seed, int32_t max_terms,
+                             int32_t draws, double zipf_a, const di_synth_skew *skew,
+                             int64_t *term_off, uint32_t *pdoc, uint8_t *pval, int64_t cap,
+                             int64_t *n_post, double *max_impact);
+
 /* The same seeded collection as the impact TSV of the index CLI (indexer.py:62-68),
  * term id t spelled "\u2581t<t>": bench input of the quantize / index-create legs.
  * *n_terms receives the (doc, term) pairs written. */
