@@ -572,7 +572,8 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
                                            int32_t *__restrict__ cand_n,
                                            uint32_t *__restrict__ qhist, int ablate,
                                            const ItemRec *__restrict__ ir,
-                                           uint32_t *__restrict__ long_flag, float bm_factor) {
+                                           uint32_t *__restrict__ long_flag, float bm_factor,
+                                           unsigned long long *__restrict__ bm_stat) {
     int64_t *lo = sh.v.bounds[0], *hi = sh.v.bounds[1];
 
     // opaque per item: keeps the per-thread index arithmetic of the sweeps from being
@@ -789,7 +790,17 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
         // dynamic segment at address 0)
         static_assert(WSEG <= 64, "one lane per segment");
         const bool below = lane >= WSEG || (tq0 > 0 && (float)sh.wub[lane] < thr);
-        if (__ballot(below) == ~0ull) {
+        const bool all_below = __ballot(below) == ~0ull;
+        // skip statistics (di_index_timing "bm_segments" / "bm_segments_skipped"): every
+        // evaluated item counts its WSEG segments, every skipped segment one
+        if (bm_stat) {
+            if (tid == 0) {
+                atomicAdd(&bm_stat[0], (unsigned long long)WSEG);
+                if (all_below) atomicAdd(&bm_stat[1], (unsigned long long)WSEG);
+            }
+            if (!all_below && skip_wave && lane == 0) atomicAdd(&bm_stat[1], 1ull);
+        }
+        if (all_below) {
             if (tid == 0) *cn = 0;
             return;
         }
@@ -1284,7 +1295,7 @@ score_blocks_kernel(const uint32_t *__restrict__ post, SubIndex si, int min_cls,
                     uint64_t *__restrict__ cand_key, int32_t *__restrict__ cand_n, int n_items,
                     int n_q, uint32_t *__restrict__ qhist, int ablate,
                     const ItemRec *__restrict__ rec, uint32_t *__restrict__ long_flag,
-                    float bm_factor) {
+                    float bm_factor, unsigned long long *__restrict__ bm_stat) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     ScoreShared &sh = *reinterpret_cast<ScoreShared *>(smem);
     if ((uint32_t)(uintptr_t)((__attribute__((address_space(3))) unsigned char *)smem) != 0) {
@@ -1298,7 +1309,7 @@ score_blocks_kernel(const uint32_t *__restrict__ post, SubIndex si, int min_cls,
     for (int item = blockIdx.x; item < n_items; item += gridDim.x) {
         score_item(sh, item % n_q, item / n_q, post, si, min_cls, nb, block_docs, n_terms,
                    n_docs, doc_lo, q_terms, cu_q, k, cand_key, cand_n, qhist, ablate,
-                   rec ? rec + (int64_t)item * WTERMS : nullptr, long_flag, bm_factor);
+                   rec ? rec + (int64_t)item * WTERMS : nullptr, long_flag, bm_factor, bm_stat);
         __syncthreads();  // every wave is done with the LDS of this item
     }
 }
@@ -1616,6 +1627,7 @@ struct di_index {
     DevBuf ws_q, ws_cu, ws_ck, ws_cn, ws_doc, ws_score, ws_n, ws_key, ws_thr;
     DevBuf ws_rec;  // ItemRec per (item, term slot): item_setup_kernel -> score_blocks
     DevBuf ws_long;  // score_blocks -> score_long_kernel: the batch has long queries
+    DevBuf bm_stat;  // block-max statistics: u64 {segments evaluated, segments skipped}
     // per-query threshold shared across blocks: -1 = auto (on from 8 blocks: at 4 blocks it
     // measured 2.31 vs 2.14 ms per 6980-query batch, at 34 / 269 blocks 16.9 vs 19.5 and
     // 130 vs 161 ms, merge 0.5 vs 7.1 and 1.4 vs 74 ms); DI_SCORE_THRESHOLD=0 / 1 forces
@@ -2145,6 +2157,10 @@ int di_index_search(di_index *ix, const uint32_t *q_terms, const int32_t *cu_q, 
         ix->ws_cn.reserve((size_t)chunk * nb * 4);
         ix->ws_thr.reserve((size_t)chunk * QH_BINS * 4);
         ix->ws_long.reserve(4);
+        if (!ix->bm_stat.p) {
+            ix->bm_stat.reserve(16);
+            DI_HIP(hipMemsetAsync(ix->bm_stat.p, 0, 16, s));
+        }
         // (only the records of real terms are written / read: ~6 per query)
         // (bounded: WTERMS slots per item; a search whose records would pass 2 GiB -- a
         // small k leaves chunks of many queries -- walks the chain in the scorer instead)
@@ -2194,7 +2210,8 @@ int di_index_search(di_index *ix, const uint32_t *q_terms, const int32_t *cu_q, 
                                    ix->ws_ck.as<uint64_t>(), ix->ws_cn.as<int32_t>(), n_items,
                                    nq, thr ? ix->ws_thr.as<uint32_t>() : nullptr, ix->ablate,
                                    use_rec ? ix->ws_rec.as<ItemRec>() : nullptr,
-                                   ix->ws_long.as<uint32_t>(), thr ? ix->bm_factor : 0.0f);
+                                   ix->ws_long.as<uint32_t>(), thr ? ix->bm_factor : 0.0f,
+                                   ix->bm_stat.as<unsigned long long>());
                 check_launch("score_blocks");
                 hipLaunchKernelGGL(score_long_kernel, dim3(std::min(n_items, n_cu())),
                                    dim3(SC_THREADS), sizeof(ScoreShared), s,
@@ -2295,6 +2312,21 @@ int di_index_sync(di_index *ix) {
 int di_index_timing(di_index *ix, const char *name, di_timing *out, int reset) {
     return guard([&] {
         DI_REQUIRE(ix && name && out, DI_EINVAL, "null argument");
+        const std::string n(name);
+        if (n == "bm_segments" || n == "bm_segments_skipped") {
+            // block-max counters (launches = the count; ms = 0), accumulated on the device
+            // since the last reset: reading them synchronises the index's stream
+            DeviceScope ds(ix->device);
+            unsigned long long st[2] = {0, 0};
+            if (ix->bm_stat.p) {
+                DI_HIP(hipStreamSynchronize(ix->stream));
+                DI_HIP(hipMemcpy(st, ix->bm_stat.p, 16, hipMemcpyDeviceToHost));
+                if (reset) DI_HIP(hipMemset(ix->bm_stat.p, 0, 16));
+            }
+            out->ms = 0.0;
+            out->launches = (int64_t)st[n == "bm_segments" ? 0 : 1];
+            return;
+        }
         ix->timer.get(name, out, reset != 0);
     });
 }

@@ -79,8 +79,8 @@ def msmarco_like_queries(n_q, v_terms=200_000, seed=1234, draws=6):
 # rank 2000: the IDF-like shape of a learned impact model), and a heavy-tailed doc mass
 # shared by clusters of 512 consecutive doc ids (passages of one source document)
 # times a per-doc factor, clipped at 6.
-SKEW_CONFIG4 = {"term_rank0": 2000.0, "term_exp": 0.5, "cluster_docs": 512,
-                "cluster_sigma": 1.0, "doc_sigma": 0.5, "mass_max": 6.0}
+SKEW_CONFIG4 = {"term_rank0": 2000.0, "term_exp": 0.5, "cluster_docs": 4096,
+                "cluster_sigma": 1.2, "doc_sigma": 0.5, "mass_max": 6.0}
 
 
 def synth_postings(n_docs, v_terms=200_000, seed=1234, max_terms=100, draws=200, zipf_a=1.2,

@@ -132,6 +132,10 @@ int di_index_set_min_impact(di_index *ix, int32_t min_impact);
 int di_index_set_block_max(di_index *ix, float factor);
 int di_index_set_stream(di_index *ix, void *hip_stream);
 int di_index_sync(di_index *ix);
+/* Per-kernel HIP-event time ("score_blocks", "merge_topk") accumulated over DI_F_TIMING
+ * searches; also the block-max counters "bm_segments" (wave segments evaluated) and
+ * "bm_segments_skipped" (segments not scored), returned in out->launches (ms = 0),
+ * accumulated since the last reset (reading them synchronises the stream). */
 int di_index_timing(di_index *ix, const char *name, di_timing *out, int reset);
 int di_index_destroy(di_index *ix);
 

@@ -409,3 +409,33 @@ def test_million_block_max_exact(L, million):
     dev.set_block_max(1.0)
     qs = S.msmarco_like_queries(24, 2_200_000, seed=5) + _queries(2_200_000, 8, seed=5)
     assert dev.search(qs, 1000) == ora.score_ids(qs, 1000, n_threads=16)
+
+
+@pytest.mark.parametrize("k", [10, 1000])
+def test_block_max_exact_skips_on_skewed_collection(L, k):
+    """configs[4] where skipping fires: a 1.1 M-doc shard of the skewed collection
+    (synthetic.SKEW_CONFIG4: frequent terms carry small impacts, doc mass shared by
+    clusters of consecutive ids -- a stated deviation from SURVEY §8d, on whose i.i.d.
+    impacts exact block-max finds nothing to skip).  Factor 1 skips wave segments (the
+    scorer's own counter says how many) and the ranking still equals the oracle's."""
+    from improving_learned_index_amd import synthetic as S
+
+    n = 1_100_000
+    term_off, pdoc, pval, _ = S.synth_postings(n, 2 * n, seed=4321, skew=S.SKEW_CONFIG4)
+    ora = oracle.Index.__new__(oracle.Index)
+    ora.term_off, ora.pdoc, ora.pval, ora.n_docs = term_off, pdoc, pval, n
+    dev = L.DeviceIndex.from_postings(term_off, pdoc, pval, 0, n)
+    qs = S.msmarco_like_queries(1000, 2 * n, seed=k)
+    want = ora.score_ids(qs, k, n_threads=16)
+    dev.set_block_max(1.0)
+    dev.timing("bm_segments", reset=True)
+    dev.timing("bm_segments_skipped", reset=True)
+    assert dev.search(qs, k) == want
+    seg = dev.timing("bm_segments")[1]
+    skipped = dev.timing("bm_segments_skipped")[1]
+    print(f"k={k}: {skipped} of {seg} wave segments skipped ({skipped / max(seg, 1):.3f})")
+    assert seg > 0 and skipped > 0.2 * seg
+    dev.set_block_max(0.0)
+    dev.timing("bm_segments", reset=True)
+    assert dev.search(qs, k) == want
+    assert dev.timing("bm_segments")[1] == 0  # (off: nothing evaluated)

@@ -9,7 +9,10 @@ queries at top-1000:
     construction, checked here), > 1 approximate.
 Recall@1000 = |pruned top-1000 ∩ exact top-1000| / |exact|, averaged over queries.
 Device time per batch = score_blocks + merge_topk over all the batch's launches.
-    python tools/prune_sweep.py [n_docs] > profiles/r02_prune_sweep.json
+Block-max rows also carry the scorer's skip counters (segments evaluated / skipped).
+    python tools/prune_sweep.py [n_docs] [iid|skew] > profiles/<round>_prune_sweep.json
+skew: synthetic.SKEW_CONFIG4 (frequent terms carry small impacts, doc mass shared by
+clusters of consecutive ids -- a stated deviation from SURVEY §8d's i.i.d. impacts).
 """
 import json
 import os
@@ -39,8 +42,10 @@ def run(ix, flat, cuq, nq, k, reps=3):
 
 def main():
     n_docs = int(sys.argv[1]) if len(sys.argv) > 1 else 8_800_000
+    skew = len(sys.argv) > 2 and sys.argv[2] == "skew"
     v_terms, nq, k = 2 * n_docs, 6980, 1000
-    term_off, pdoc, pval, _ = S.synth_postings(n_docs, v_terms, seed=4321)
+    term_off, pdoc, pval, _ = S.synth_postings(n_docs, v_terms, seed=4321,
+                                               skew=S.SKEW_CONFIG4 if skew else None)
     queries = S.msmarco_like_queries(nq, v_terms, seed=1234)
     flat, cuq = _lib.csr(queries)
     rows, exact = [], None
@@ -59,7 +64,11 @@ def main():
                                        np.minimum(term_off[:-1], max(len(pval) - 1, 0)))
             per_term[lens == 0] = 0
         posts = int(per_term[flat.astype(np.int64)].sum())
+        ix.timing("bm_segments", reset=True)
+        ix.timing("bm_segments_skipped", reset=True)
         docs, n, dev_s, wall = run(ix, flat, cuq, nq, k)
+        seg_n = ix.timing("bm_segments")[1]
+        seg_s = ix.timing("bm_segments_skipped")[1]
         res = [set(docs[i, :n[i]].tolist()) for i in range(nq)]
         if exact is None:
             exact = res
@@ -67,13 +76,16 @@ def main():
         rows.append({"min_impact": mi, "block_max_factor": bm,
                      "postings_per_query": posts / nq, "device_queries_per_s": nq / dev_s,
                      "host_call_queries_per_s": nq / wall, "device_ms": dev_s * 1000,
-                     "recall_at_1000": rec})
+                     "recall_at_1000": rec,
+                     "bm_segments_skipped_frac": seg_s / seg_n if seg_n else None})
         print(json.dumps(rows[-1]), file=sys.stderr, flush=True)
     del ix
     print(json.dumps({"sweep": "configs[4]: query-time impact pruning and block-max "
                                "skipping of the quantized scorer",
-                      "workload": f"{n_docs}-doc shard (synth_postings seed 4321), {nq} "
+                      "workload": f"{n_docs}-doc shard (synth_postings seed 4321"
+                                  f"{', skew SKEW_CONFIG4' if skew else ''}), {nq} "
                                   f"dev.small-shaped queries, top-{k}",
+                      "skew": S.SKEW_CONFIG4 if skew else None,
                       "rows": rows}))
 
 

@@ -26,8 +26,10 @@ def main():
     skew = (sys.argv[3] if len(sys.argv) > 3 else "skew") == "skew"
     k = 1000
     V = 2 * n_docs
-    term_off, pdoc, pval, m = S.synth_postings(n_docs, V, seed=4321,
-                                               skew=S.SKEW_CONFIG4 if skew else None)
+    import os
+
+    sk = dict(S.SKEW_CONFIG4, **json.loads(os.environ.get("SKEW", "{}"))) if skew else None
+    term_off, pdoc, pval, m = S.synth_postings(n_docs, V, seed=4321, skew=sk)
     queries = S.msmarco_like_queries(nq, V, seed=1234)
     import oracle
 
@@ -57,7 +59,7 @@ def main():
         touched_frac.append(float(np.mean(bound > 0)))
     post = float(np.mean([sum(int(term_off[t + 1] - term_off[t]) for t in q) for q in queries]))
     print(json.dumps({"n_docs": n_docs, "collection": "skewed (SKEW_CONFIG4)" if skew else "iid (§8d)",
-                      "skew": S.SKEW_CONFIG4 if skew else None, "queries": nq, "k": k,
+                      "skew": sk, "queries": nq, "k": k,
                       "postings": int(len(pdoc)), "postings_per_query": post,
                       "segment_docs": seg, "segments": n_seg,
                       "skippable_segment_fraction": skip / max(tot, 1),
