@@ -60,6 +60,7 @@ SIGNATURES = {
     "di_index_info": (ctypes.c_int, [P, P, P, P, P]),
     "di_index_set_min_impact": (ctypes.c_int, [P, I32]),
     "di_index_set_block_max": (ctypes.c_int, [P, ctypes.c_float]),
+    "di_index_set_packed": (ctypes.c_int, [P, I32, P]),
     "di_index_set_stream": (ctypes.c_int, [P, P]),
     "di_index_sync": (ctypes.c_int, [P]),
     "di_index_timing": (ctypes.c_int, [P, ctypes.c_char_p, P, ctypes.c_int]),
@@ -276,6 +277,13 @@ class DeviceIndex:
     def set_block_max(self, factor=0.0):
         """Block-max skipping: 0 off, 1 exact, > 1 approximate (di_index_set_block_max)."""
         check(lib().di_index_set_block_max(self._h, float(factor)))
+
+    def set_packed(self, on=True):
+        """Block-compressed postings (di_index_set_packed, configs[4]); returns the packed
+        size in bytes."""
+        b = I64(0)
+        check(lib().di_index_set_packed(self._h, int(bool(on)), ctypes.byref(b)))
+        return b.value
 
     def set_stream(self, stream_ptr):
         check(lib().di_index_set_stream(self._h, ctypes.c_void_p(stream_ptr)))

@@ -318,6 +318,144 @@ __device__ __forceinline__ void scatter_apply_own(const uint32_t (&cur)[UU], uin
     }
 }
 
+// scatter_apply for the block-max cooperative form: postings of a skipped wave segment
+// (bit seg of live16 clear; seg = doc / wseg by the multiply-high `magic`, exact for
+// docs < 2^16) update the lane's dummy word instead.  The padding (doc MAX_BLOCK_DOCS)
+// lands in segment 15 or a dummy, both never read.
+template <int UU>
+__device__ __forceinline__ void scatter_apply_live(const uint32_t (&cur)[UU], uint32_t first_bits,
+                                                   uint32_t live16, uint32_t magic,
+                                                   uint32_t dummy) {
+    uint32_t w[UU], a[UU];
+#pragma unroll
+    for (int u = 0; u < UU; ++u) {
+        const uint32_t d = (cur[u] ^ POST_X) >> 10;
+        const uint32_t sg = min(__umulhi(d, magic), 15u);
+        a[u] = ((live16 >> sg) & 1u) ? d << 2 : dummy;
+        asm volatile("ds_read_b32 %0, %1" : "=v"(w[u]) : "v"(a[u]) : "memory");
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int u = 0; u < UU; ++u) asm volatile("" : "+v"(w[u]));
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int u = 0; u < UU; ++u) {
+        const uint32_t v = cur[u] & 255u;
+        asm volatile("ds_write_b32 %0, %1" ::"v"(a[u]), "v"(word_update(w[u], v, first_bits))
+                     : "memory");
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Packed (block-compressed) postings -- BASELINE configs[4], di_index_set_packed.
+// Every run (a short sublist, or one wave segment's run of a long sublist) is sorted
+// by doc and cut into frames of up to 512 postings.  Lane L of a frame holds postings
+// 8 L .. 8 L + 7 as eight W-bit fields, W = bd + bv rounded up to a multiple of 4
+// (<= 24): field = delta | (value - vmin) << bd, delta = doc - the previous posting's
+// doc in the frame (0 for the first), W / 4 dwords per lane, lanes back to back (a
+// frame of n postings stores ceil(n / 8) lanes).
+// Header (uint4): x = data offset (dwords), y = doc_base (the first doc, 16 bits) |
+// count << 16 (10 bits) | bd << 26 (5 bits), z = vmin | bv << 8 (4 bits) | W << 12.
+// Decoding happens in registers: the eight fields by static shifts, the lane's
+// running delta sums, a DPP wave scan for the lanes before it (no LDS crossbar).
+constexpr int PK_FRAME = 512, PK_PER_LANE = 8;
+
+template <int W>
+__device__ __forceinline__ void packed_fields(const uint32_t *data, uint32_t cnt, int lane,
+                                              uint32_t (&f)[8]) {
+    constexpr int ND = W / 4;  // dwords per lane
+    static_assert(W % 4 == 0 && W >= 4 && W <= 24, "field width");
+    const uint64_t pa = reinterpret_cast<uint64_t>(data);
+    const uint32_t lo32 = __builtin_amdgcn_readfirstlane((uint32_t)pa);
+    const uint32_t hi32 = __builtin_amdgcn_readfirstlane((uint32_t)(pa >> 32));
+    void *base = reinterpret_cast<void *>(((uint64_t)hi32 << 32) | lo32);
+    // the frame's ceil(cnt / 8) lanes of data (lanes past them read 0)
+    const int bytes = __builtin_amdgcn_readfirstlane((int)((cnt + PK_PER_LANE - 1) / PK_PER_LANE) * ND * 4);
+    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(base, (short)0, bytes, 0x00020000);
+    const int off = lane * ND * 4;
+    uint32_t d[ND + 1];
+    if constexpr (ND == 1) {
+        d[0] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, off, 0, 0);
+    } else if constexpr (ND == 2) {
+        const auto v = __builtin_amdgcn_raw_buffer_load_b64(rsrc, off, 0, 0);
+        d[0] = v[0], d[1] = v[1];
+    } else if constexpr (ND == 3) {
+        const auto v = __builtin_amdgcn_raw_buffer_load_b96(rsrc, off, 0, 0);
+        d[0] = v[0], d[1] = v[1], d[2] = v[2];
+    } else {
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, off, 0, 0);
+        d[0] = v[0], d[1] = v[1], d[2] = v[2], d[3] = v[3];
+        if constexpr (ND == 5) {
+            d[4] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, off + 16, 0, 0);
+        } else if constexpr (ND == 6) {
+            const auto u = __builtin_amdgcn_raw_buffer_load_b64(rsrc, off + 16, 0, 0);
+            d[4] = u[0], d[5] = u[1];
+        }
+    }
+    d[ND] = 0;
+    constexpr uint32_t mask = (1u << W) - 1u;
+#pragma unroll
+    for (int i = 0; i < PK_PER_LANE; ++i) {
+        const int bit = i * W, k = bit >> 5, sft = bit & 31;
+        if (sft + W <= 32)
+            f[i] = (d[k] >> sft) & mask;
+        else
+            f[i] = __builtin_amdgcn_alignbit(d[k + 1], d[k], (uint32_t)sft) & mask;
+    }
+}
+
+// One frame applied to the block's words (the read-modify-write of scatter_apply);
+// LIVE: postings in skipped wave segments go to the lane's dummy word.
+template <int W, bool LIVE>
+__device__ __forceinline__ void packed_apply_w(const uint4 h, const uint32_t *__restrict__ pdata,
+                                               int lane, uint32_t first_bits, uint32_t live16,
+                                               uint32_t magic, uint32_t dummy) {
+    uint32_t f[PK_PER_LANE];
+    const uint32_t base = h.y & 0xFFFFu, cnt = (h.y >> 16) & 1023u, bd = (h.y >> 26) & 31u;
+    packed_fields<W>(pdata + h.x, cnt, lane, f);
+    const uint32_t vmin = h.z & 255u, bv = (h.z >> 8) & 15u;
+    uint32_t run = 0, ds[PK_PER_LANE];
+#pragma unroll
+    for (int i = 0; i < PK_PER_LANE; ++i) {
+        run += __builtin_amdgcn_ubfe(f[i], 0, bd);
+        ds[i] = run;
+    }
+    const uint32_t first = base + wave_incl_scan_dpp(run) - run;  // doc before this lane's
+    uint32_t w[PK_PER_LANE], a[PK_PER_LANE];
+#pragma unroll
+    for (int i = 0; i < PK_PER_LANE; ++i) {
+        const uint32_t d = first + ds[i];
+        bool ok = (uint32_t)(PK_PER_LANE * lane + i) < cnt;
+        if constexpr (LIVE) ok = ok && ((live16 >> min(__umulhi(d, magic), 15u)) & 1u);
+        a[i] = ok ? d << 2 : dummy;
+        asm volatile("ds_read_b32 %0, %1" : "=v"(w[i]) : "v"(a[i]) : "memory");
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int i = 0; i < PK_PER_LANE; ++i) asm volatile("" : "+v"(w[i]));
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < PK_PER_LANE; ++i) {
+        const uint32_t v = vmin + __builtin_amdgcn_ubfe(f[i], bd, bv);
+        asm volatile("ds_write_b32 %0, %1" ::"v"(a[i]), "v"(word_update(w[i], v, first_bits))
+                     : "memory");
+    }
+}
+
+template <bool LIVE>
+__device__ __forceinline__ void packed_apply(const uint4 h, const uint32_t *__restrict__ pdata,
+                                             int lane, uint32_t first_bits, uint32_t live16,
+                                             uint32_t magic, uint32_t dummy) {
+    switch ((h.z >> 12) & 63u) {  // (wave-uniform)
+    case 4: packed_apply_w<4, LIVE>(h, pdata, lane, first_bits, live16, magic, dummy); break;
+    case 8: packed_apply_w<8, LIVE>(h, pdata, lane, first_bits, live16, magic, dummy); break;
+    case 12: packed_apply_w<12, LIVE>(h, pdata, lane, first_bits, live16, magic, dummy); break;
+    case 16: packed_apply_w<16, LIVE>(h, pdata, lane, first_bits, live16, magic, dummy); break;
+    case 20: packed_apply_w<20, LIVE>(h, pdata, lane, first_bits, live16, magic, dummy); break;
+    default: packed_apply_w<24, LIVE>(h, pdata, lane, first_bits, live16, magic, dummy); break;
+    }
+}
+
 // Profiling (DI_PROFILE_ABLATE bit 64): per-phase shader cycles of workgroup 0's items
 // accumulated here and printed by di_index_search.
 __device__ unsigned long long g_sb_phase[10];
@@ -336,6 +474,13 @@ struct SubIndex {
     const uint16_t *wmeta;
     const uint8_t *emax;  // block-max metadata: the sublist's largest value
     const uint8_t *wmax;  // long sublists: the largest value of each wave segment's run
+    // packed (block-compressed) postings, di_index_set_packed (null: off): frames of
+    // entry e = [pk_fs[e], pk_fs[e + 1]); a long entry's run w = frames pk_fs[e] +
+    // [pk_fwt[17 lid + w], pk_fwt[17 lid + w + 1])
+    const uint32_t *pk_fs;
+    const uint16_t *pk_fwt;
+    const uint4 *pk_fh;      // frame headers (PackedFrame)
+    const uint32_t *pk_data;
 };
 
 // entry of (term t, block b), or -1 when t has no posting in b
@@ -400,16 +545,26 @@ item_setup_kernel(SubIndex si, int min_cls, int nb, int64_t n_terms,
         const uint32_t id = en >= 0 ? si.lid[en] : 0xFFFFFFFFu;
         if (w == 0) {
             int64_t lo, hi;
-            entry_bounds(si, en, min_cls, lo, hi);
+            if (si.pk_fs) {  // packed: frame ranges (exact scoring only, min_cls 7)
+                lo = en >= 0 ? si.pk_fs[en] : 0;
+                hi = en >= 0 ? si.pk_fs[en + 1] : 0;
+            } else {
+                entry_bounds(si, en, min_cls, lo, hi);
+            }
             r[j].lo = lo;
             r[j].hi = hi;
             r[j].flags = id != 0xFFFFFFFFu ? IR_LONG : 0u;
         }
         r[j].wmx[w] = en < 0 ? 0 : id != 0xFFFFFFFFu ? si.wmax[(int64_t)id * WSEG + w] : si.emax[en];
         if (id != 0xFFFFFFFFu) {
-            const uint16_t *m = si.wmeta + (int64_t)id * (WSEG * 8);
-            const uint32_t s0 = w ? m[(w - 1) * 8 + 7] : 0u;
-            r[j].wtab[w] = (s0 << 16) | m[w * 8 + min(min_cls, 7)];
+            if (si.pk_fs) {
+                const uint16_t *m = si.pk_fwt + (int64_t)id * (WSEG + 1);
+                r[j].wtab[w] = ((uint32_t)m[w] << 16) | m[w + 1];
+            } else {
+                const uint16_t *m = si.wmeta + (int64_t)id * (WSEG * 8);
+                const uint32_t s0 = w ? m[(w - 1) * 8 + 7] : 0u;
+                r[j].wtab[w] = (s0 << 16) | m[w * 8 + min(min_cls, 7)];
+            }
         }
     }
 }
@@ -780,6 +935,7 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
     // docs stay 0.  bm_factor 1 is exact; > 1 skips segments below factor x Tq -- an
     // approximation (the QPS-vs-recall sweep).  Every segment below: the item ends.
     bool skip_wave = false;
+    uint32_t live16 = 0xFFFFu;  // bm: the wave segments that are scored (bit w)
     if (bm) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the threshold copy (read_tq)
         const uint32_t tq0 = read_tq();
@@ -790,7 +946,9 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
         // dynamic segment at address 0)
         static_assert(WSEG <= 64, "one lane per segment");
         const bool below = lane >= WSEG || (tq0 > 0 && (float)sh.wub[lane] < thr);
-        const bool all_below = __ballot(below) == ~0ull;
+        const uint64_t below_m = __ballot(below);
+        const bool all_below = below_m == ~0ull;
+        live16 = (uint32_t)~below_m & 0xFFFFu;
         // skip statistics (di_index_timing "bm_segments" / "bm_segments_skipped"): every
         // evaluated item counts its WSEG segments, every skipped segment one
         if (bm_stat) {
@@ -821,6 +979,96 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
     bool have_pre = false;
     auto is_long = [&](int j) { return wl && ((sh.lmask[j >> 5] >> (j & 31)) & 1u); };
     const uint32_t wseg = ((uint32_t)block_docs + WSEG - 1) / WSEG;
+    // Block-max with some segments skipped (coop): every wave works on every scored
+    // segment instead of its own only -- a skipped segment's wave would otherwise idle
+    // while the rest of the item runs as long as without skipping.  Terms in query
+    // order, a barrier between terms (a doc occurs once per term: no race inside one);
+    // a long term's runs of the scored segments in pieces of 512 postings dealt over
+    // the waves; a short term's sublist in block-wide rounds, the postings of skipped
+    // segments sent to the lane's dummy word.  (DI_PROFILE_ABLATE bit 8192: off, A/B.)
+    if (si.pk_fs && wl) {
+        // packed postings (configs[4]): every wave on every scored segment, frames dealt
+        // over the waves, a barrier between terms (the coop form below, on frames)
+        const uint32_t magic = (uint32_t)((0x100000000ull + wseg - 1) / wseg);
+        const uint32_t ldummy = (uint32_t)(MAX_BLOCK_DOCS + lane) << 2;
+        for (int j = 0; j < nt; ++j) {
+            const uint32_t first_bits = (uint32_t)(255 - j) << 8;
+            uint32_t piece = 0;
+            if (is_long(j)) {
+                for (int w = 0; w < WSEG; ++w) {
+                    if (!((live16 >> w) & 1u)) continue;
+                    const uint32_t se = sh.wtab[j][w];
+                    const int64_t f1 = lo[j] + (se & 0xFFFFu);
+                    for (int64_t f = lo[j] + (se >> 16); f < f1; ++f, ++piece)
+                        if ((int)(piece % SC_WAVES) == wave)
+                            packed_apply<false>(si.pk_fh[f], si.pk_data, lane, first_bits, live16,
+                                                magic, ldummy);
+                }
+            } else {
+                for (int64_t f = lo[j]; f < hi[j]; ++f, ++piece)
+                    if ((int)(piece % SC_WAVES) == wave) {
+                        if (live16 == 0xFFFFu)
+                            packed_apply<false>(si.pk_fh[f], si.pk_data, lane, first_bits, live16,
+                                                magic, ldummy);
+                        else
+                            packed_apply<true>(si.pk_fh[f], si.pk_data, lane, first_bits, live16,
+                                               magic, ldummy);
+                    }
+            }
+            if (j + 1 < nt) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        }
+        skip_wave = true;  // (nothing left for the per-wave loop below)
+    } else if (bm && live16 != 0xFFFFu && !(ablate & 8192)) {
+        const uint32_t magic = (uint32_t)((0x100000000ull + wseg - 1) / wseg);  // d / wseg
+        const uint32_t ldummy = (uint32_t)(MAX_BLOCK_DOCS + lane) << 2;
+        const bool x4c = !(ablate & 4096);
+        for (int j = 0; j < nt; ++j) {
+            const uint32_t first_bits = (uint32_t)(255 - j) << 8;
+            if (is_long(j)) {
+                uint32_t piece = 0;
+                for (int w = 0; w < WSEG; ++w) {
+                    if (!((live16 >> w) & 1u)) continue;
+                    const uint32_t se = sh.wtab[j][w];
+                    const int64_t end = lo[j] + (se & 0xFFFFu);
+                    for (int64_t pos = lo[j] + (se >> 16); pos < end; pos += 8 * 64, ++piece) {
+                        if ((int)(piece % SC_WAVES) != wave) continue;
+                        const int64_t rem = end - pos;
+                        if (rem > 4 * 64) {
+                            uint32_t r[8];
+                            scatter_load<8, 64>(post + pos, rem, lane, r, x4c);
+                            scatter_apply<8>(sh.acc, r, first_bits);
+                        } else if (rem > 64) {
+                            uint32_t r[4];
+                            scatter_load<4, 64>(post + pos, rem, lane, r, x4c);
+                            scatter_apply<4>(sh.acc, r, first_bits);
+                        } else {
+                            uint32_t r[1];
+                            scatter_load<1, 64>(post + pos, rem, lane, r);
+                            scatter_apply<1>(sh.acc, r, first_bits);
+                        }
+                    }
+                }
+            } else {
+                for (int64_t pos = lo[j], end = hi[j]; pos < end;) {
+                    const int64_t rem = end - pos;
+                    if (rem > SC_THREADS) {
+                        uint32_t r[4];
+                        scatter_load<4>(post + pos, rem, tid, r, x4c);
+                        scatter_apply_live<4>(r, first_bits, live16, magic, ldummy);
+                        pos += 4 * SC_THREADS;
+                    } else {
+                        uint32_t r[1];
+                        scatter_load<1>(post + pos, rem, tid, r);
+                        scatter_apply_live<1>(r, first_bits, live16, magic, ldummy);
+                        pos = end;
+                    }
+                }
+            }
+            // term boundary: this term's LDS writes land before any wave reads the next
+            if (j + 1 < nt) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        }
+        skip_wave = true;  // (the per-wave loop below has nothing left to do)
+    }
     const uint32_t wdlo = (uint32_t)wave * wseg;
     const uint32_t wdn = wave == WSEG - 1 ? 0x7FFFFFFFu - wdlo : wseg;  // last: the rest
     const uint32_t wdummy = (uint32_t)(MAX_BLOCK_DOCS + lane) << 2;
@@ -1628,6 +1876,10 @@ struct di_index {
     DevBuf ws_rec;  // ItemRec per (item, term slot): item_setup_kernel -> score_blocks
     DevBuf ws_long;  // score_blocks -> score_long_kernel: the batch has long queries
     DevBuf bm_stat;  // block-max statistics: u64 {segments evaluated, segments skipped}
+    // packed (block-compressed) postings, built by di_index_set_packed (SubIndex pk_*)
+    DevBuf pk_fs, pk_fwt, pk_fh, pk_data;
+    bool pk_built = false, packed = false;
+    int64_t pk_frames = 0, pk_bytes = 0;
     // per-query threshold shared across blocks: -1 = auto (on from 8 blocks: at 4 blocks it
     // measured 2.31 vs 2.14 ms per 6980-query batch, at 34 / 269 blocks 16.9 vs 19.5 and
     // 130 vs 161 ms, merge 0.5 vs 7.1 and 1.4 vs 74 ms); DI_SCORE_THRESHOLD=0 / 1 forces
@@ -1635,10 +1887,13 @@ struct di_index {
     int ablate = 0;  // DI_PROFILE_ABLATE: profiling only (1 no scatter, 2 no selection, 4 stop at the k-th score)
     Timer timer;
 
-    SubIndex sub() const {
+    SubIndex sub(bool with_packed = false) const {
+        const bool pk = with_packed && packed && pk_built;
         return SubIndex{tb_start.as<uint32_t>(), eblk.as<uint16_t>(), epos.as<uint32_t>(),
                         seg.as<uint16_t>(), lid.as<uint32_t>(), wmeta.as<uint16_t>(),
-                        emax.as<uint8_t>(), wmax.as<uint8_t>()};
+                        emax.as<uint8_t>(), wmax.as<uint8_t>(),
+                        pk ? pk_fs.as<uint32_t>() : nullptr, pk ? pk_fwt.as<uint16_t>() : nullptr,
+                        pk ? pk_fh.as<uint4>() : nullptr, pk ? pk_data.as<uint32_t>() : nullptr};
     }
 };
 
@@ -2196,15 +2451,17 @@ int di_index_search(di_index *ix, const uint32_t *q_terms, const int32_t *cu_q, 
                 DI_HIP(hipMemsetAsync(ix->ws_long.p, 0, 4, s));
                 TimedLaunch tl(ix->timer, timing, "score_blocks", s);  // (both kernels)
                 const int n_items = nq * nb;
+                // packed postings (configs[4]): exact scoring from the item records only
+                const bool pk = ix->packed && ix->pk_built && ix->min_cls >= 7 && use_rec;
                 if (use_rec) {
                     hipLaunchKernelGGL(item_setup_kernel, dim3(n_items), dim3(128), 0, s,
-                                       ix->sub(), ix->min_cls, nb, ix->n_terms, dq, dcu + q0, nq,
+                                       ix->sub(pk), ix->min_cls, nb, ix->n_terms, dq, dcu + q0, nq,
                                        ix->ws_rec.as<ItemRec>());
                     check_launch("item_setup");
                 }
                 hipLaunchKernelGGL(score_blocks_kernel, dim3(std::min(n_items, n_cu())),
                                    dim3(SC_THREADS), sizeof(ScoreShared), s,
-                                   ix->post.as<uint32_t>(), ix->sub(),
+                                   ix->post.as<uint32_t>(), ix->sub(pk),
                                    ix->min_cls, nb, ix->block_docs, ix->n_terms,
                                    ix->n_docs, ix->doc_lo, dq, dcu + q0, k,
                                    ix->ws_ck.as<uint64_t>(), ix->ws_cn.as<int32_t>(), n_items,
@@ -2284,6 +2541,157 @@ int di_index_set_block_max(di_index *ix, float factor) {
         DI_REQUIRE(factor == 0.0f || (factor >= 1.0f && factor <= 16.0f), DI_ERANGE,
                    "block-max factor %g: 0 (off) or in [1, 16]", (double)factor);
         ix->bm_factor = factor;
+    });
+}
+
+// Packed (block-compressed) postings from the device layout: every run (short
+// sublist, or one wave segment's run of a long one) sorted by doc, cut into frames of
+// up to PK_FRAME postings, each frame bit-packed with its own widths (see
+// packed_fields).  Host threads over entry ranges; three passes (frame counts, widths,
+// encoding) so every entry writes its own ranges.
+static void build_packed(di_index *ix) {
+    const int64_t ne = ix->n_ent, np = ix->n_post, nl = ix->n_long;
+    std::vector<uint32_t> post((size_t)std::max<int64_t>(np, 1)), epos((size_t)ne + 1);
+    std::vector<uint32_t> lid((size_t)std::max<int64_t>(ne, 1));
+    std::vector<uint16_t> wmeta((size_t)std::max<int64_t>(nl, 1) * WSEG * 8);
+    if (np) DI_HIP(hipMemcpy(post.data(), ix->post.p, (size_t)np * 4, hipMemcpyDeviceToHost));
+    DI_HIP(hipMemcpy(epos.data(), ix->epos.p, ((size_t)ne + 1) * 4, hipMemcpyDeviceToHost));
+    if (ne) DI_HIP(hipMemcpy(lid.data(), ix->lid.p, (size_t)ne * 4, hipMemcpyDeviceToHost));
+    if (nl)
+        DI_HIP(hipMemcpy(wmeta.data(), ix->wmeta.p, (size_t)nl * WSEG * 8 * 2,
+                         hipMemcpyDeviceToHost));
+    const uint32_t NO = 0xFFFFFFFFu;
+    // run r of entry e: [a, b) of the postings (w: segment of a long entry)
+    auto run_of = [&](int64_t e, int w, uint32_t &a, uint32_t &b) {
+        const uint32_t id = lid[(size_t)e];
+        if (id == NO) {
+            a = epos[(size_t)e];
+            b = epos[(size_t)e + 1];
+            return;
+        }
+        const uint16_t *m = &wmeta[(size_t)id * WSEG * 8];
+        a = epos[(size_t)e] + (w ? m[(w - 1) * 8 + 7] : 0u);
+        b = epos[(size_t)e] + m[w * 8 + 7];
+    };
+    auto n_runs = [&](int64_t e) { return lid[(size_t)e] == NO ? 1 : WSEG; };
+    auto frames_of = [](uint32_t n) { return (n + PK_FRAME - 1) / PK_FRAME; };
+    // pass 1: frames per entry -> fs; per long entry the run starts (fwt)
+    std::vector<uint32_t> fs((size_t)ne + 1, 0);
+    std::vector<uint16_t> fwt((size_t)std::max<int64_t>(nl, 1) * (WSEG + 1), 0);
+    parallel_for(ne, [&](int64_t e0, int64_t e1, int) {
+        for (int64_t e = e0; e < e1; ++e) {
+            uint32_t nf = 0;
+            const uint32_t id = lid[(size_t)e];
+            for (int w = 0; w < n_runs(e); ++w) {
+                uint32_t a, b;
+                run_of(e, w, a, b);
+                if (id != NO) fwt[(size_t)id * (WSEG + 1) + w] = (uint16_t)nf;
+                nf += frames_of(b - a);
+            }
+            if (id != NO) fwt[(size_t)id * (WSEG + 1) + WSEG] = (uint16_t)nf;
+            fs[(size_t)e + 1] = nf;
+        }
+    });
+    for (int64_t e = 0; e < ne; ++e) fs[(size_t)e + 1] += fs[(size_t)e];
+    const int64_t nfr = fs[(size_t)ne];
+    // one run's frames: sorted (doc, value), per frame (bd, bv, vmin, W)
+    struct FrameInfo {
+        uint32_t base, cnt, bd, bv, vmin, W;
+    };
+    auto bits = [](uint32_t x) { return x ? 32 - __builtin_clz(x) : 0; };
+    auto frame_info = [&](const std::vector<std::pair<uint32_t, uint32_t>> &dv, size_t i0,
+                          size_t i1) {
+        FrameInfo fi{dv[i0].first, (uint32_t)(i1 - i0), 0, 0, 255, 0};
+        uint32_t dmax = 0, vmax = 0;
+        for (size_t i = i0; i < i1; ++i) {
+            if (i > i0) dmax = std::max(dmax, dv[i].first - dv[i - 1].first);
+            fi.vmin = std::min(fi.vmin, dv[i].second);
+            vmax = std::max(vmax, dv[i].second);
+        }
+        fi.bd = (uint32_t)bits(dmax);
+        fi.bv = (uint32_t)bits(vmax - fi.vmin);
+        fi.W = std::max<uint32_t>(4, (fi.bd + fi.bv + 3) / 4 * 4);
+        return fi;
+    };
+    auto sorted_run = [&](uint32_t a, uint32_t b, std::vector<std::pair<uint32_t, uint32_t>> &dv) {
+        dv.resize(b - a);
+        for (uint32_t p = a; p < b; ++p)
+            dv[p - a] = {(post[p] ^ POST_X) >> 10, post[p] & 255u};
+        std::sort(dv.begin(), dv.end());
+    };
+    // pass 2: data dwords per frame
+    std::vector<uint32_t> fdw((size_t)std::max<int64_t>(nfr, 1) + 1, 0);
+    parallel_for(ne, [&](int64_t e0, int64_t e1, int) {
+        std::vector<std::pair<uint32_t, uint32_t>> dv;
+        for (int64_t e = e0; e < e1; ++e) {
+            uint32_t f = fs[(size_t)e];
+            for (int w = 0; w < n_runs(e); ++w) {
+                uint32_t a, b;
+                run_of(e, w, a, b);
+                sorted_run(a, b, dv);
+                for (size_t i0 = 0; i0 < dv.size(); i0 += PK_FRAME, ++f) {
+                    const size_t i1 = std::min(dv.size(), i0 + PK_FRAME);
+                    const FrameInfo fi = frame_info(dv, i0, i1);
+                    fdw[(size_t)f + 1] = (uint32_t)((fi.cnt + PK_PER_LANE - 1) / PK_PER_LANE) * (fi.W / 4);
+                }
+            }
+        }
+    });
+    std::vector<uint64_t> doff((size_t)nfr + 1, 0);
+    for (int64_t f = 0; f < nfr; ++f) doff[(size_t)f + 1] = doff[(size_t)f] + fdw[(size_t)f + 1];
+    DI_REQUIRE(doff[(size_t)nfr] < 0xFFFFFFFFull, DI_ERANGE, "packed postings past 2^32 dwords");
+    // pass 3: headers and data
+    std::vector<uint4> fh((size_t)std::max<int64_t>(nfr, 1));
+    std::vector<uint32_t> data((size_t)std::max<uint64_t>(doff[(size_t)nfr], 1), 0);
+    parallel_for(ne, [&](int64_t e0, int64_t e1, int) {
+        std::vector<std::pair<uint32_t, uint32_t>> dv;
+        for (int64_t e = e0; e < e1; ++e) {
+            uint32_t f = fs[(size_t)e];
+            for (int w = 0; w < n_runs(e); ++w) {
+                uint32_t a, b;
+                run_of(e, w, a, b);
+                sorted_run(a, b, dv);
+                for (size_t i0 = 0; i0 < dv.size(); i0 += PK_FRAME, ++f) {
+                    const size_t i1 = std::min(dv.size(), i0 + PK_FRAME);
+                    const FrameInfo fi = frame_info(dv, i0, i1);
+                    uint32_t *out = &data[(size_t)doff[(size_t)f]];
+                    const uint32_t nd = fi.W / 4;
+                    for (size_t i = i0; i < i1; ++i) {
+                        const uint32_t k = (uint32_t)(i - i0);
+                        const uint32_t delta = i > i0 ? dv[i].first - dv[i - 1].first : 0u;
+                        const uint64_t field = (uint64_t)delta | ((uint64_t)(dv[i].second - fi.vmin) << fi.bd);
+                        const uint32_t lane = k / PK_PER_LANE, slot = k % PK_PER_LANE;
+                        const uint64_t bit = (uint64_t)lane * nd * 32 + (uint64_t)slot * fi.W;
+                        const uint64_t sh = field << (bit & 31);
+                        out[bit >> 5] |= (uint32_t)sh;
+                        if ((bit & 31) + fi.W > 32) out[(bit >> 5) + 1] |= (uint32_t)(sh >> 32);
+                    }
+                    fh[(size_t)f] = make_uint4((uint32_t)doff[(size_t)f],
+                                               fi.base | (fi.cnt << 16) | (fi.bd << 26),
+                                               fi.vmin | (fi.bv << 8) | (fi.W << 12), 0u);
+                }
+            }
+        }
+    });
+    upload(ix->pk_fs, fs);
+    upload(ix->pk_fwt, fwt);
+    upload(ix->pk_fh, fh);
+    upload(ix->pk_data, data);
+    ix->pk_frames = nfr;
+    ix->pk_bytes = (int64_t)doff[(size_t)nfr] * 4 + nfr * (int64_t)sizeof(uint4);
+    ix->pk_built = true;
+}
+
+int di_index_set_packed(di_index *ix, int32_t on, int64_t *packed_bytes) {
+    return guard([&] {
+        DI_REQUIRE(ix, DI_EINVAL, "null handle");
+        DeviceScope ds(ix->device);
+        if (on && !ix->pk_built) {
+            DI_HIP(hipStreamSynchronize(ix->stream));
+            build_packed(ix);
+        }
+        ix->packed = on != 0;
+        if (packed_bytes) *packed_bytes = ix->pk_built ? ix->pk_bytes : 0;
     });
 }
 

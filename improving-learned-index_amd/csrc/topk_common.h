@@ -31,6 +31,20 @@ __device__ __forceinline__ uint32_t wave_prefix_sum(uint32_t x) {
     return x;
 }
 
+// lane l receives sum over lanes <= l, by DPP only (no LDS crossbar): a Hillis-Steele
+// scan inside each 16-lane row (row_shr 1, 2, 4, 8), then row 0's total into row 1 and
+// row 2's into row 3 (row_bcast:15), then rows 0-1's total into rows 2-3 (row_bcast:31).
+// Lanes whose DPP source is out of the row read `old` = 0.
+__device__ __forceinline__ uint32_t wave_incl_scan_dpp(uint32_t x) {
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, false);  // row_shr:1
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, false);  // row_shr:2
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, false);  // row_shr:4
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, false);  // row_shr:8
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false);  // row_bcast:15
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false);  // row_bcast:31
+    return x;
+}
+
 __device__ __forceinline__ uint32_t wave_sum(uint32_t x) {
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d, 64);

@@ -130,6 +130,16 @@ int di_index_set_min_impact(di_index *ix, int32_t min_impact);
  * factor x threshold, an approximation (QPS vs recall@1000).  Queries of at most 64
  * terms, with the shared threshold (>= 8 blocks). */
 int di_index_set_block_max(di_index *ix, float factor);
+/* Packed (block-compressed) postings -- BASELINE configs[4]: on != 0 builds (once, from
+ * the device layout) a second copy of the postings in which every run (a short
+ * (term, block) sublist, or one scorer wave segment's run of a long one) is sorted by doc
+ * and cut into frames of up to 512 postings, each bit-packed with its own widths (doc
+ * deltas in bd bits, value - vmin in bv bits, decoded in registers by the scorer), and
+ * scores queries of at most 64 terms from it, alone or with block-max skipping; the
+ * ranking is unchanged (same keys).  Exact scoring only: with impact pruning
+ * (di_index_set_min_impact > 1) the plain layout is used.  *packed_bytes (optional)
+ * receives the packed size (headers + data).  on = 0: the plain layout again. */
+int di_index_set_packed(di_index *ix, int32_t on, int64_t *packed_bytes);
 int di_index_set_stream(di_index *ix, void *hip_stream);
 int di_index_sync(di_index *ix);
 /* Per-kernel HIP-event time ("score_blocks", "merge_topk") accumulated over DI_F_TIMING

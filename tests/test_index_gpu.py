@@ -439,3 +439,83 @@ def test_block_max_exact_skips_on_skewed_collection(L, k):
     dev.timing("bm_segments", reset=True)
     assert dev.search(qs, k) == want
     assert dev.timing("bm_segments")[1] == 0  # (off: nothing evaluated)
+
+
+@pytest.mark.parametrize("k", [1, 10, 1000])
+def test_packed_postings_equal_oracle(L, synth, k):
+    """configs[4] block-compressed postings (di_index_set_packed): every run sorted by
+    doc, bit-packed frames of <= 512 postings decoded in registers -- the same ranking
+    as the reference (oracle), alone and with exact block-max skipping; queries past 64
+    terms in the same batch fall back to the plain layout.  The packed copy is smaller
+    than the plain 4-byte postings, and switching it off gives the plain scorer back."""
+    term_off, pdoc, pval, ora = synth
+    dev = L.DeviceIndex.from_postings(term_off, pdoc, pval)
+    qs = _queries(5000, 120, seed=k + 7) + _long_queries(5000, 2, seed=k, lo=65, hi=90)
+    want = ora.score_ids(qs, k, n_threads=8)
+    plain_bytes = 4 * dev.info()["n_postings"]
+    packed = dev.set_packed(True)
+    assert 0 < packed < plain_bytes
+    assert dev.search(qs, k) == want
+    dev.set_block_max(1.0)
+    assert dev.search(qs, k) == want
+    dev.set_min_impact(8)  # (pruning: the plain layout serves; still every doc's full score)
+    dev.set_min_impact(1)
+    dev.set_packed(False)
+    dev.set_block_max(0.0)
+    assert dev.search(qs, k) == want
+
+
+def test_packed_postings_edge_runs(L):
+    """Frames at their limits: a term in every doc of a block (deltas of 1, one long
+    run per wave segment, full 512-posting frames), a term with one posting, equal
+    values (bv = 0), values 1 and 255 in one frame (bv = 8), a sparse term spread over
+    a 32 K-doc block (15-bit deltas, W = 24), docs 0 and the block's last."""
+    rng = np.random.default_rng(3)
+    n_docs = 70_000
+    lists = []
+    lists.append((np.arange(0, 40_000), rng.integers(1, 256, 40_000)))      # dense, all values
+    lists.append((np.array([69_999]), np.array([7])))                       # one posting
+    lists.append((np.arange(0, n_docs, 3), np.full(len(range(0, n_docs, 3)), 5)))  # bv = 0
+    lists.append((np.array([0, 1, 2, 32_000, 32_767]), np.array([1, 255, 1, 255, 128])))
+    lists.append((np.sort(rng.choice(n_docs, 300, replace=False)), rng.integers(1, 4, 300)))
+    lists.append((np.arange(5, n_docs, 2), rng.integers(200, 256, len(range(5, n_docs, 2)))))
+    term_off, pd, pv = [0], [], []
+    for d, v in lists:
+        order = np.lexsort((d, -v))  # reference order: value desc, doc asc
+        pd.append(d[order].astype(np.uint32))
+        pv.append(v[order].astype(np.uint8))
+        term_off.append(term_off[-1] + len(d))
+    term_off = np.array(term_off, np.int64)
+    pdoc, pval = np.concatenate(pd), np.concatenate(pv)
+    ora = oracle.Index.__new__(oracle.Index)
+    ora.term_off, ora.pdoc, ora.pval, ora.n_docs = term_off, pdoc, pval, n_docs
+    dev = L.DeviceIndex.from_postings(term_off, pdoc, pval, 0, n_docs)
+    qs = [[0], [1], [2], [3], [4], [5], [0, 1, 2, 3, 4, 5], [5, 4, 3, 2, 1, 0], [2, 0], [3, 1]]
+    for k in (1, 10, 1000, 4096):
+        want = ora.score_ids(qs, k, n_threads=8)
+        dev.set_packed(False)
+        assert dev.search(qs, k) == want
+        dev.set_packed(True)
+        assert dev.search(qs, k) == want, k
+
+
+def test_packed_block_max_on_skewed_collection(L):
+    """Packed postings with exact block-max skipping on the skewed 1.1 M-doc collection
+    (SKEW_CONFIG4): oracle-equal top-1000, segments skipped."""
+    from improving_learned_index_amd import synthetic as S
+
+    n = 1_100_000
+    term_off, pdoc, pval, _ = S.synth_postings(n, 2 * n, seed=4321, skew=S.SKEW_CONFIG4)
+    ora = oracle.Index.__new__(oracle.Index)
+    ora.term_off, ora.pdoc, ora.pval, ora.n_docs = term_off, pdoc, pval, n
+    dev = L.DeviceIndex.from_postings(term_off, pdoc, pval, 0, n)
+    qs = S.msmarco_like_queries(500, 2 * n, seed=77)
+    want = ora.score_ids(qs, 1000, n_threads=16)
+    nbytes = dev.set_packed(True)
+    print(f"packed {nbytes} B vs plain {4 * len(pdoc)} B ({nbytes / (4 * len(pdoc)):.3f})")
+    assert dev.search(qs, 1000) == want
+    dev.set_block_max(1.0)
+    dev.timing("bm_segments_skipped", reset=True)
+    dev.timing("bm_segments", reset=True)
+    assert dev.search(qs, 1000) == want
+    assert dev.timing("bm_segments_skipped")[1] > 0
