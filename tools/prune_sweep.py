@@ -52,13 +52,18 @@ def main():
     ix = _lib.DeviceIndex.from_postings(term_off, pdoc, pval, 0, n_docs)
     ix.reserve(nq, k)
     lens = np.diff(term_off)
-    rows_sel = [(m, 0.0) for m in (1, 2, 4, 8, 16, 32, 64, 128)] + \
-        [(1, f) for f in (1.0, 1.25, 1.5, 2.0, 3.0, 4.0)]
+    rows_sel = [(m, 0.0, False) for m in (1, 2, 4, 8, 16, 32, 64, 128)] + \
+        [(1, f, False) for f in (1.0, 1.25, 1.5, 2.0, 3.0, 4.0)] + \
+        [(1, f, True) for f in (0.0, 1.0, 1.5, 2.0)]
     if os.environ.get("SWEEP") == "bm":  # exhaustive + the block-max rows only
-        rows_sel = [(1, 0.0)] + [(1, f) for f in (1.0, 1.5, 2.0)]
-    for mi, bm in rows_sel:
+        rows_sel = [(1, 0.0, False)] + [(1, f, False) for f in (1.0, 1.5, 2.0)]
+    packed_bytes = None
+    for mi, bm, pk in rows_sel:
         ix.set_min_impact(mi)
         ix.set_block_max(bm)
+        nb = ix.set_packed(pk)
+        if pk:
+            packed_bytes = nb
         thr = 1 << (mi.bit_length() - 1)
         if thr == 1:
             per_term = lens
@@ -76,7 +81,11 @@ def main():
         if exact is None:
             exact = res
         rec = float(np.mean([len(a & b) / max(len(b), 1) for a, b in zip(res, exact)]))
-        rows.append({"min_impact": mi, "block_max_factor": bm,
+        ratio = packed_bytes / (4.0 * len(pval)) if pk else 1.0
+        rows.append({"min_impact": mi, "block_max_factor": bm, "packed": pk,
+                     # algorithmic bytes read per query: 4 B per plain posting; packed --
+                     # the index's packed bytes per posting (headers included) x postings
+                     "bytes_per_query": 4.0 * ratio * posts / nq,
                      "postings_per_query": posts / nq, "device_queries_per_s": nq / dev_s,
                      "host_call_queries_per_s": nq / wall, "device_ms": dev_s * 1000,
                      "recall_at_1000": rec,
@@ -89,6 +98,8 @@ def main():
                                   f"{', skew SKEW_CONFIG4' if skew else ''}), {nq} "
                                   f"dev.small-shaped queries, top-{k}",
                       "skew": S.SKEW_CONFIG4 if skew else None,
+                      "postings": int(len(pval)), "plain_bytes": 4 * int(len(pval)),
+                      "packed_bytes": packed_bytes,
                       "rows": rows}))
 
 
