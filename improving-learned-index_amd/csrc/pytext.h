@@ -5,6 +5,7 @@
 #pragma once
 
 #include <algorithm>
+#include <cfloat>
 #include <charconv>
 #include <cmath>
 #include <cstdint>
@@ -156,8 +157,10 @@ inline bool parse_float(std::string_view s, double *out) {
         // x87 extended division (64-bit mantissa, m and 10^k exact) rounded to double.
         // The double rounding is exact unless the extended quotient is itself a midpoint
         // between two doubles (its low 11 bits 0x400): then strtod decides.
-        // (host code: x86-64 long double; a target without it takes strtod)
-        if constexpr (sizeof(long double) >= 10) {
+        // (host code: the x87 80-bit format -- a 64-bit significand whose low 8 bytes the
+        // memcpy below reads; IEEE quad (aarch64) or double-double long doubles are not
+        // that format and take strtod)
+        if constexpr (LDBL_MANT_DIG == 64 && sizeof(long double) >= 10) {
             if (fast && nd > 0 && k <= 22) {
                 const long double q = (long double)m / (long double)p10[k];
                 uint64_t mant;  // the x87 format's explicit 64-bit significand (low 8 bytes)
