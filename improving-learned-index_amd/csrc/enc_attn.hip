@@ -842,6 +842,279 @@ attention_x3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
 #undef AX_SEL
 }
 
+// ---------------------------------------------------------------------------
+// attention_x3w_kernel: the fp32-faithful (split-bf16) attention with every wave on its
+// own.  A workgroup is AW_WAVES = 4 waves, one per SIMD, each with its own 32 KiB of
+// LDS; a wave takes whole (doc, head) pairs (pairs dealt round-robin over all the
+// chip's waves) and, per group of up to AW_QT = 4 query tiles of 16 (64 queries), streams
+// the pair's K and V split rows through its own double-buffered LDS images in 32-key
+// chunks by LDS-DMA (chunk i + 1 lands while chunk i computes).  No workgroup barrier,
+// no idle SIMD at a pair's last tiles (attention_x3_kernel's 8 waves share a pass of 16
+// tiles: a 200-token document's 13 tiles ran 4 / 3 / 3 / 3 on the SIMDs), no waiting
+// for other waves' copies.  Per chunk and tile: S^T = K Q^T (12 MFMAs, split products
+// as attention_x3_kernel), the lazy-max online softmax in f32, O^T = V^T P^T (12).
+// Images as attention_x3_kernel's (256-byte key rows [ch0 hi | ch0 lo | ch1 hi | ch1
+// lo], 16-byte slot j at j ^ ax_swz(r)); rows 0..31 only.
+constexpr int AW_WAVES = 4, AW_QT = 4, AW_KC = 32;
+constexpr int AW_IMG = AW_KC * 256;            // 8 KiB: one K or V image
+constexpr int AW_BUF = 2 * AW_IMG;             // K | V of one chunk
+constexpr int AW_WAVE_LDS = 2 * AW_BUF;        // double-buffered: 32 KiB per wave
+constexpr int AW_LDS = AW_WAVES * AW_WAVE_LDS;  // 128 KiB
+
+template <int NQT>
+__device__ __forceinline__ void aw_group(const bf16 *__restrict__ qkv, int64_t ld, int H, int h,
+                                         int tok0, int n, int q0, int nq, int g0,
+                                         const int32_t *__restrict__ qsel, bf16 *__restrict__ ctx,
+                                         unsigned char *lds_w, uint32_t wbase, int lane) {
+    typedef __attribute__((address_space(3))) void lds_void;
+    const int g = lane >> 4, c = lane & 15;
+    const float sc = 0.125f * 1.4426950408889634f;  // 1/sqrt(64) * log2(e)
+    const bf16 *kg = qkv + split_col(H + h * ATT_D);
+    const bf16 *vg = qkv + split_col(2 * H + h * ATT_D);
+    // chunk ci -> buffer b: 8 pieces of 1 KiB for K and 8 for V (piece pc: key rows
+    // 4 pc .. 4 pc + 3, lane -> row 4 pc + lane / 16, slot (lane & 15) ^ swizzle)
+    auto stage = [&](int ci, int b) {
+#pragma unroll
+        for (int pc = 0; pc < AW_KC / 4; ++pc) {
+            const int rl = 4 * pc + (lane >> 4);
+            const int row = tok0 + min(ci * AW_KC + rl, n - 1);
+            const int j = (lane & 15) ^ ax_swz(rl);
+            unsigned char *dst = lds_w + b * AW_BUF + (4 * pc) * 256;
+            __builtin_amdgcn_global_load_lds((const void *)(kg + row * ld + j * 8),
+                                             (lds_void *)dst, 16, 0, 0);
+            __builtin_amdgcn_global_load_lds((const void *)(vg + row * ld + j * 8),
+                                             (lds_void *)(dst + AW_IMG), 16, 0, 0);
+        }
+    };
+    // Q^T B operands (hi, lo) of the group's tiles
+    bf16x8 qh[NQT][2], ql[NQT][2];
+    {
+        const bf16 *qbase = qkv + split_col(h * ATT_D) + 8 * g;
+#pragma unroll
+        for (int qt = 0; qt < NQT; ++qt) {
+            const int qi = min(g0 + 16 * qt + c, nq - 1);
+            const int qloc = qsel ? min(max(qsel[q0 + qi], 0), n - 1) : qi;
+            const bf16 *src = qbase + (int64_t)(tok0 + qloc) * ld;
+#pragma unroll
+            for (int ch = 0; ch < 2; ++ch) {
+                qh[qt][ch] = *reinterpret_cast<const bf16x8 *>(src + ch * 64);
+                ql[qt][ch] = *reinterpret_cast<const bf16x8 *>(src + ch * 64 + 32);
+            }
+        }
+    }
+    // fragment addresses in buffer 0 (buffer 1: + AW_BUF)
+    uint32_t ka[2][2][2], va[4][2][2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int ch = 0; ch < 2; ++ch)
+#pragma unroll
+            for (int pt = 0; pt < 2; ++pt) {
+                const int r = 8 * (c >> 2) + 4 * t + (c & 3), j = ch * 8 + pt * 4 + g;
+                ka[t][ch][pt] = wbase + r * 256 + ((j ^ ax_swz(r)) << 4);
+            }
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+        for (int pt = 0; pt < 2; ++pt)
+#pragma unroll
+            for (int h2 = 0; h2 < 2; ++h2) {
+                const int qq = c >> 2, pp = c & 3;
+                const int r = 8 * g + 4 * h2 + qq;
+                const int j = (dt >> 1) * 8 + pt * 4 + 2 * (dt & 1) + (pp >> 1);
+                va[dt][pt][h2] = wbase + AW_IMG + r * 256 + ((j ^ ax_swz(r)) << 4) + 8 * (pp & 1);
+            }
+    float m[NQT], lsum[NQT], lim[NQT], mneg[NQT];
+    f32x4 o[NQT][4];
+#pragma unroll
+    for (int qt = 0; qt < NQT; ++qt) {
+        m[qt] = -INFINITY;
+        lim[qt] = -INFINITY;
+        mneg[qt] = 0.f;
+        lsum[qt] = 0.f;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) o[qt][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    const int n_chunks = (n + AW_KC - 1) / AW_KC;
+    stage(0, 0);
+    for (int ci = 0; ci < n_chunks; ++ci) {
+        const uint32_t boff = (uint32_t)(ci & 1) * AW_BUF;
+        // this wave's chunk ci has landed (the Q loads with it); its buffer's reads of
+        // chunk ci - 1's other buffer are long done (waited below): chunk ci + 1 may go there
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (ci + 1 < n_chunks) stage(ci + 1, (ci + 1) & 1);
+        uint4 kf[2][2][2];
+        asm volatile("ds_read_b128 %0, %8\n\tds_read_b128 %1, %9\n\tds_read_b128 %2, %10\n\t"
+                     "ds_read_b128 %3, %11\n\tds_read_b128 %4, %12\n\tds_read_b128 %5, %13\n\t"
+                     "ds_read_b128 %6, %14\n\tds_read_b128 %7, %15\n\ts_waitcnt lgkmcnt(0)"
+                     : "=&v"(kf[0][0][0]), "=&v"(kf[0][0][1]), "=&v"(kf[0][1][0]),
+                       "=&v"(kf[0][1][1]), "=&v"(kf[1][0][0]), "=&v"(kf[1][0][1]),
+                       "=&v"(kf[1][1][0]), "=&v"(kf[1][1][1])
+                     : "v"(ka[0][0][0] + boff), "v"(ka[0][0][1] + boff), "v"(ka[0][1][0] + boff),
+                       "v"(ka[0][1][1] + boff), "v"(ka[1][0][0] + boff), "v"(ka[1][0][1] + boff),
+                       "v"(ka[1][1][0] + boff), "v"(ka[1][1][1] + boff)
+                     : "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        bf16x8 kfr[2][2][2];
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+            for (int ch = 0; ch < 2; ++ch)
+#pragma unroll
+                for (int pt = 0; pt < 2; ++pt) __builtin_memcpy(&kfr[t][ch][pt], &kf[t][ch][pt], 16);
+        f32x4 s[NQT][2];
+#pragma unroll
+        for (int qt = 0; qt < NQT; ++qt) s[qt][0] = s[qt][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ch = 0; ch < 2; ++ch)
+#pragma unroll
+            for (int p = 0; p < 3; ++p)
+#pragma unroll
+                for (int qt = 0; qt < NQT; ++qt)
+#pragma unroll
+                    for (int t = 0; t < 2; ++t)
+                        s[qt][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                            kfr[t][ch][p == 1], p == 2 ? ql[qt][ch] : qh[qt][ch], s[qt][t], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        uint2 vt2[4][2][2];
+        asm volatile(
+            "ds_read_b64_tr_b16 %0, %16\n\tds_read_b64_tr_b16 %1, %17\n\t"
+            "ds_read_b64_tr_b16 %2, %18\n\tds_read_b64_tr_b16 %3, %19\n\t"
+            "ds_read_b64_tr_b16 %4, %20\n\tds_read_b64_tr_b16 %5, %21\n\t"
+            "ds_read_b64_tr_b16 %6, %22\n\tds_read_b64_tr_b16 %7, %23\n\t"
+            "ds_read_b64_tr_b16 %8, %24\n\tds_read_b64_tr_b16 %9, %25\n\t"
+            "ds_read_b64_tr_b16 %10, %26\n\tds_read_b64_tr_b16 %11, %27\n\t"
+            "ds_read_b64_tr_b16 %12, %28\n\tds_read_b64_tr_b16 %13, %29\n\t"
+            "ds_read_b64_tr_b16 %14, %30\n\tds_read_b64_tr_b16 %15, %31\n\ts_waitcnt lgkmcnt(0)"
+            : "=&v"(vt2[0][0][0]), "=&v"(vt2[0][0][1]), "=&v"(vt2[0][1][0]), "=&v"(vt2[0][1][1]),
+              "=&v"(vt2[1][0][0]), "=&v"(vt2[1][0][1]), "=&v"(vt2[1][1][0]), "=&v"(vt2[1][1][1]),
+              "=&v"(vt2[2][0][0]), "=&v"(vt2[2][0][1]), "=&v"(vt2[2][1][0]), "=&v"(vt2[2][1][1]),
+              "=&v"(vt2[3][0][0]), "=&v"(vt2[3][0][1]), "=&v"(vt2[3][1][0]), "=&v"(vt2[3][1][1])
+            : "v"(va[0][0][0] + boff), "v"(va[0][0][1] + boff), "v"(va[0][1][0] + boff),
+              "v"(va[0][1][1] + boff), "v"(va[1][0][0] + boff), "v"(va[1][0][1] + boff),
+              "v"(va[1][1][0] + boff), "v"(va[1][1][1] + boff), "v"(va[2][0][0] + boff),
+              "v"(va[2][0][1] + boff), "v"(va[2][1][0] + boff), "v"(va[2][1][1] + boff),
+              "v"(va[3][0][0] + boff), "v"(va[3][0][1] + boff), "v"(va[3][1][0] + boff),
+              "v"(va[3][1][1] + boff)
+            : "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        const int key0 = ci * AW_KC;
+        const bool full = key0 + AW_KC <= n;  // (uniform) no masked key in this chunk
+        bf16x8 ph[NQT], pl[NQT];
+#pragma unroll
+        for (int qt = 0; qt < NQT; ++qt) {
+            float v[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const int key = key0 + 8 * g + e;  // (t = e >> 2, r = e & 3)
+                v[e] = (full || key < n) ? s[qt][e >> 2][e & 3] : -INFINITY;
+            }
+            const float lmax = fmaxf(fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3])),
+                                     fmaxf(fmaxf(v[4], v[5]), fmaxf(v[6], v[7])));
+            // lazy max: the reference max moves only when a score passes it by 8 / sc
+            // (always at the first chunk: lim = -inf, key 0 is valid)
+            if (__any(lmax > lim[qt])) {
+                float cmax = lmax;
+                const auto p16 = __builtin_amdgcn_permlane16_swap(
+                    __float_as_uint(cmax), __float_as_uint(cmax), false, false);
+                cmax = fmaxf(__uint_as_float(p16[0]), __uint_as_float(p16[1]));
+                const auto p32 = __builtin_amdgcn_permlane32_swap(
+                    __float_as_uint(cmax), __float_as_uint(cmax), false, false);
+                cmax = fmaxf(__uint_as_float(p32[0]), __uint_as_float(p32[1]));
+                const float m_new = fmaxf(m[qt], cmax);
+                if (m_new != m[qt]) {
+                    const float alpha = __builtin_amdgcn_exp2f((m[qt] - m_new) * sc);
+                    lsum[qt] *= alpha;
+#pragma unroll
+                    for (int dt = 0; dt < 4; ++dt) o[qt][dt] *= alpha;
+                }
+                m[qt] = m_new;
+                lim[qt] = m_new + 8.0f / sc;
+                mneg[qt] = -m_new * sc;
+            }
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const float pr = __builtin_amdgcn_exp2f(fmaf(v[e], sc, mneg[qt]));
+                lsum[qt] += pr;
+                ph[qt][e] = split_hi(pr);
+                pl[qt][e] = split_lo(pr);
+            }
+        }
+        bf16x8 vfr[4][2];
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+            for (int pt = 0; pt < 2; ++pt) {
+                const uint4 v4 = make_uint4(vt2[dt][pt][0].x, vt2[dt][pt][0].y, vt2[dt][pt][1].x,
+                                            vt2[dt][pt][1].y);
+                __builtin_memcpy(&vfr[dt][pt], &v4, 16);
+            }
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
+#pragma unroll
+            for (int qt = 0; qt < NQT; ++qt)
+#pragma unroll
+                for (int dt = 0; dt < 4; ++dt)
+                    o[qt][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                        vfr[dt][p == 1], p == 2 ? pl[qt] : ph[qt], o[qt][dt], 0, 0, 0);
+    }
+    // context rows: O / row sum, split
+#pragma unroll
+    for (int qt = 0; qt < NQT; ++qt) {
+        float l = lsum[qt];
+        l += __shfl_xor(l, 16, 64);
+        l += __shfl_xor(l, 32, 64);
+        const float inv = 1.0f / l;
+        const int q = g0 + 16 * qt + c;
+        if (q < nq) {
+            bf16 *out = ctx + (int64_t)(q0 + q) * 2 * H;
+#pragma unroll
+            for (int dt = 0; dt < 4; ++dt) {
+                bf16x4 hv, lv;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const float y = o[qt][dt][r] * inv;
+                    hv[r] = split_hi(y);
+                    lv[r] = split_lo(y);
+                }
+                const int64_t sc0 = split_col(h * ATT_D + dt * 16 + 4 * g);
+                *reinterpret_cast<bf16x4 *>(out + sc0) = hv;
+                *reinterpret_cast<bf16x4 *>(out + sc0 + 32) = lv;
+            }
+        }
+    }
+}
+
+__global__ void __launch_bounds__(64 * AW_WAVES) __attribute__((amdgpu_waves_per_eu(1)))
+attention_x3w_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu_seqlens, int H,
+                     int n_heads, int n_pairs, bf16 *__restrict__ ctx_split,
+                     const int32_t *__restrict__ qsel, const int32_t *__restrict__ cu_qsel) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t ld = 6 * (int64_t)H;
+    unsigned char *lds_w = lds + wave * AW_WAVE_LDS;
+    const uint32_t wbase =
+        (uint32_t)(uintptr_t)((__attribute__((address_space(3))) unsigned char *)lds_w);
+    const int stride = (int)gridDim.x * AW_WAVES;
+    for (int pr = (int)blockIdx.x * AW_WAVES + wave; pr < n_pairs; pr += stride) {
+        const int doc = pr / n_heads, h = pr % n_heads;
+        const int tok0 = cu_seqlens[doc], n = cu_seqlens[doc + 1] - tok0;
+        const int q0 = qsel ? cu_qsel[doc] : tok0;
+        const int nq = qsel ? cu_qsel[doc + 1] - q0 : n;
+        if (n <= 0 || nq <= 0) continue;
+        for (int g0 = 0; g0 < nq; g0 += AW_QT * 16) {
+            const int tiles = min(AW_QT, (nq - g0 + 15) / 16);
+            switch (tiles) {
+            case 1: aw_group<1>(qkv, ld, H, h, tok0, n, q0, nq, g0, qsel, ctx_split, lds_w, wbase, lane); break;
+            case 2: aw_group<2>(qkv, ld, H, h, tok0, n, q0, nq, g0, qsel, ctx_split, lds_w, wbase, lane); break;
+            case 3: aw_group<3>(qkv, ld, H, h, tok0, n, q0, nq, g0, qsel, ctx_split, lds_w, wbase, lane); break;
+            default: aw_group<4>(qkv, ld, H, h, tok0, n, q0, nq, g0, qsel, ctx_split, lds_w, wbase, lane); break;
+            }
+        }
+    }
+}
+
 void launch_attention_x3(const bf16 *qkv, const int32_t *cu_seqlens, int n_docs, int H,
                          bf16 *ctx_split, hipStream_t s, const int32_t *qsel,
                          const int32_t *cu_qsel) {
@@ -856,8 +1129,22 @@ void launch_attention_x3(const bf16 *qkv, const int32_t *cu_seqlens, int n_docs,
     // interleave
     static const int variant = [] {
         const char *e = getenv("DI_ATTN_X3");
-        return e ? atoi(e) & 60 : 28;
+        return e ? atoi(e) & 124 : 28;
     }();
+    if (variant & 64) {  // the per-wave form (attention_x3w_kernel)
+        static bool attr = false;
+        if (!attr) {
+            DI_HIP(hipFuncSetAttribute((const void *)attention_x3w_kernel,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, AW_LDS));
+            attr = true;
+        }
+        hipLaunchKernelGGL(attention_x3w_kernel,
+                           dim3((int)std::min<int64_t>((n_pairs + AW_WAVES - 1) / AW_WAVES, n_cu())),
+                           dim3(64 * AW_WAVES), AW_LDS, s, qkv, cu_seqlens, H, n_heads,
+                           (int)n_pairs, ctx_split, qsel, cu_qsel);
+        check_launch("attention_x3w");
+        return;
+    }
     static const int abl = [] {
         const char *e = getenv("DI_ATTN_X3_ABLATE");
         return e ? atoi(e) : 0;
