@@ -962,20 +962,21 @@ __device__ __forceinline__ void aw_group(const bf16 *__restrict__ qkv, int64_t l
             for (int ch = 0; ch < 2; ++ch)
 #pragma unroll
                 for (int pt = 0; pt < 2; ++pt) __builtin_memcpy(&kfr[t][ch][pt], &kf[t][ch][pt], 16);
+        // S^T tile by tile (tile qt's scores complete first, so its softmax can issue
+        // beside the next tiles' products; no scheduling fence after them)
         f32x4 s[NQT][2];
 #pragma unroll
-        for (int qt = 0; qt < NQT; ++qt) s[qt][0] = s[qt][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int qt = 0; qt < NQT; ++qt) {
+            s[qt][0] = s[qt][1] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int ch = 0; ch < 2; ++ch)
+            for (int ch = 0; ch < 2; ++ch)
 #pragma unroll
-            for (int p = 0; p < 3; ++p)
-#pragma unroll
-                for (int qt = 0; qt < NQT; ++qt)
+                for (int p = 0; p < 3; ++p)
 #pragma unroll
                     for (int t = 0; t < 2; ++t)
                         s[qt][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
                             kfr[t][ch][p == 1], p == 2 ? ql[qt][ch] : qh[qt][ch], s[qt][t], 0, 0, 0);
-        __builtin_amdgcn_sched_barrier(0);
+        }
         uint2 vt2[4][2][2];
         asm volatile(
             "ds_read_b64_tr_b16 %0, %16\n\tds_read_b64_tr_b16 %1, %17\n\t"
@@ -997,7 +998,6 @@ __device__ __forceinline__ void aw_group(const bf16 *__restrict__ qkv, int64_t l
               "v"(va[3][0][0] + boff), "v"(va[3][0][1] + boff), "v"(va[3][1][0] + boff),
               "v"(va[3][1][1] + boff)
             : "memory");
-        __builtin_amdgcn_sched_barrier(0);
         const int key0 = ci * AW_KC;
         const bool full = key0 + AW_KC <= n;  // (uniform) no masked key in this chunk
         bf16x8 ph[NQT], pl[NQT];

@@ -1,7 +1,6 @@
 set -o pipefail
 O=gpurun_out/round4_d; mkdir -p $O
-TAG=round4_d STEPS=tests TESTS="tests/test_index_gpu.py -k "block_max or packed or skew" -m gpu -s" bash tools/measure_r4.sh || exit 1
-mv $O/pytest_gpu.log $O/pytest_index.log
+timeout -k 10 600 python -u -m pytest tests/test_index_gpu.py -k "block_max or packed or skew" -m gpu -x -v -s --timeout 300 --timeout-method thread > $O/pytest_index.log 2>&1; rc=$?; tail -5 $O/pytest_index.log; [ $rc -eq 0 ] || exit $rc
 DI_ATTN_X3=64 timeout -k 10 600 python -u -m pytest tests/test_encoder_bf16x3_gpu.py tests/test_encoder_bert_gpu.py tests/test_encoder_phobert_gpu.py -m gpu -x -v -s --timeout 300 --timeout-method thread > $O/pytest_attn_x3w.log 2>&1; rc=$?; tail -5 $O/pytest_attn_x3w.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python3 bench.py --legs encode_x3 --steps 5 --warmup 2 --no-cpu > $O/bench_x3_old.json 2> $O/bench_x3_old.err || exit 1
 DI_ATTN_X3=64 timeout -k 10 300 python3 bench.py --legs encode_x3 --steps 5 --warmup 2 --no-cpu > $O/bench_x3_new.json 2> $O/bench_x3_new.err || exit 1
