@@ -506,7 +506,7 @@ def cpu_baseline_retrieve(args, term_off, pdoc, pval, queries, out_doc, out_scor
                       f"(OpenMP over queries), {el:.1f}s"}
 
 
-def index_e2e_leg(args, dev):
+def index_e2e_leg(args, dev, rank=0, world=1):
     """A1-A9 end to end through the drop-in CLI's own code path (index.py: collection
     file -> CollectionParser -> TokenizerPool workers -> HIP encoder -> native TSV
     writer), bf16x3 (the CLI default, fp32-faithful).  The collection is synthetic
@@ -524,7 +524,7 @@ def index_e2e_leg(args, dev):
     tok_path = ROOT / "tests" / "golden" / "tokenizer.json"
     vocab = json.loads(tok_path.read_text())["model"]["vocab"]
     words = np.array([w[1:] for w, _ in vocab if w.startswith("\u2581") and len(w) > 2])
-    rng = np.random.default_rng(7)
+    rng = np.random.default_rng(7 + rank)
     n_docs = args.e2e_docs
     lens = np.clip(rng.normal(150, 45, n_docs), 6, 230).astype(int)
     procs = max(1, min(args.e2e_procs, os.cpu_count() or 1))
@@ -549,6 +549,8 @@ def index_e2e_leg(args, dev):
                 with open(coll) as f:
                     indexer.index([next(f).split("\t", 1)[1] for _ in range(4 * procs)], dn)
             t_setup = time.perf_counter() - t0
+            if world > 1:  # every rank's workers start together (host cores shared)
+                dist.barrier()
             t1 = time.perf_counter()
             n = index_cli._index_file(indexer, coll, "msmarco", td / "collection.index",
                                       args.e2e_process_batch, None, t1)
@@ -556,9 +558,12 @@ def index_e2e_leg(args, dev):
             out_bytes = (td / "collection.index").stat().st_size
         finally:
             pool.close()
-    log(f"index e2e: {n} docs in {el:.2f}s after {t_setup:.1f}s setup ({procs} tokenizer "
-        f"workers)")
-    return {"value": round(n / el, 1), "unit": "docs/s", "docs": int(n), "seconds": round(el, 3),
+    log(f"[rank {rank}] index e2e: {n} docs in {el:.2f}s after {t_setup:.1f}s setup ({procs} "
+        f"tokenizer workers)")
+    if world > 1:  # all ranks' documents over the slowest rank's time (host tokenization of
+        el = max_over_ranks(el)  # N ranks x their workers on the node's shared cores)
+    return {"value": round(world * n / el, 1), "unit": "docs/s", "docs": int(world * n),
+            "ranks": world, "seconds": round(el, 3),
             "setup_seconds": round(t_setup, 2), "tokenizer_workers": procs,
             "precision": "bf16x3", "output_bytes": int(out_bytes),
             "model_batch_size": args.e2e_model_batch, "process_batch_size": args.e2e_process_batch,
@@ -742,7 +747,7 @@ def main():
     n_check = 0 if os.environ.get("DI_PROFILE_ABLATE") else 20
     if "retrieve" in legs:
         ret_res, ret_ctx = retrieve_leg(args, rank, world, dev, check_queries=n_check)
-    e2e_res = index_e2e_leg(args, dev) if "index_e2e" in legs and world == 1 else None
+    e2e_res = index_e2e_leg(args, dev, rank, world) if "index_e2e" in legs else None
     text_res = text_legs(args) if "text" in legs and rank == 0 else None
     big = {}
     for leg, nd in (("retrieve_shard", 1_100_000), ("retrieve_full", 8_800_000)):
