@@ -861,47 +861,100 @@ constexpr int AW_BUF = 2 * AW_IMG;             // K | V of one chunk
 constexpr int AW_WAVE_LDS = 2 * AW_BUF;        // double-buffered: 32 KiB per wave
 constexpr int AW_LDS = AW_WAVES * AW_WAVE_LDS;  // 128 KiB
 
-template <int NQT>
-__device__ __forceinline__ void aw_group(const bf16 *__restrict__ qkv, int64_t ld, int H, int h,
-                                         int tok0, int n, int q0, int nq, int g0,
-                                         const int32_t *__restrict__ qsel, bf16 *__restrict__ ctx,
-                                         unsigned char *lds_w, uint32_t wbase, int lane) {
+// One group of a wave: up to AW_QT query tiles of one (doc, head) pair.
+struct AwGroup {
+    int pr, g0, h, tok0, n, q0, nq, tiles;
+};
+
+// The wave's group after `cur` (or the first one when cur.pr < 0): the pair's next 64
+// queries, else the next pair (pairs pr, pr + stride, ...) with a token and a query.
+__device__ __forceinline__ bool aw_next(const AwGroup &cur, int first_pr, int stride, int n_pairs,
+                                        int n_heads, const int32_t *__restrict__ cu_seqlens,
+                                        const int32_t *__restrict__ qsel,
+                                        const int32_t *__restrict__ cu_qsel, AwGroup &nx) {
+    if (cur.pr >= 0 && cur.g0 + AW_QT * 16 < cur.nq) {
+        nx = cur;
+        nx.g0 = cur.g0 + AW_QT * 16;
+        nx.tiles = min(AW_QT, (nx.nq - nx.g0 + 15) / 16);
+        return true;
+    }
+    for (int pr = cur.pr >= 0 ? cur.pr + stride : first_pr; pr < n_pairs; pr += stride) {
+        const int doc = pr / n_heads;
+        nx.pr = pr;
+        nx.h = pr % n_heads;
+        nx.tok0 = cu_seqlens[doc];
+        nx.n = cu_seqlens[doc + 1] - nx.tok0;
+        nx.q0 = qsel ? cu_qsel[doc] : nx.tok0;
+        nx.nq = qsel ? cu_qsel[doc + 1] - nx.q0 : nx.n;
+        nx.g0 = 0;
+        nx.tiles = min(AW_QT, (nx.nq + 15) / 16);
+        if (nx.n > 0 && nx.nq > 0) return true;
+    }
+    return false;
+}
+
+// K and V of chunk ci of group G -> buffer b of the wave's LDS: 8 pieces of 1 KiB each
+// (piece pc: key rows 4 pc .. 4 pc + 3, lane -> row 4 pc + lane / 16, slot (lane & 15)
+// ^ swizzle); 16 LDS-DMA instructions.
+__device__ __forceinline__ void aw_stage(const bf16 *__restrict__ qkv, int64_t ld, int H,
+                                         const AwGroup &G, int ci, int b, unsigned char *lds_w,
+                                         int lane) {
     typedef __attribute__((address_space(3))) void lds_void;
+    const bf16 *kg = qkv + split_col(H + G.h * ATT_D);
+    const bf16 *vg = qkv + split_col(2 * H + G.h * ATT_D);
+#pragma unroll
+    for (int pc = 0; pc < AW_KC / 4; ++pc) {
+        const int rl = 4 * pc + (lane >> 4);
+        const int row = G.tok0 + min(ci * AW_KC + rl, G.n - 1);
+        const int j = (lane & 15) ^ ax_swz(rl);
+        unsigned char *dst = lds_w + b * AW_BUF + (4 * pc) * 256;
+        __builtin_amdgcn_global_load_lds((const void *)(kg + row * ld + j * 8), (lds_void *)dst,
+                                         16, 0, 0);
+        __builtin_amdgcn_global_load_lds((const void *)(vg + row * ld + j * 8),
+                                         (lds_void *)(dst + AW_IMG), 16, 0, 0);
+    }
+}
+
+// Q^T B operands (hi, lo) of group G's AW_QT tiles (tiles past G.tiles read a clamped
+// row: loaded, never used) -- 4 AW_QT loads of 16 B per lane.
+__device__ __forceinline__ void aw_load_q(const bf16 *__restrict__ qkv, int64_t ld, const AwGroup &G,
+                                          const int32_t *__restrict__ qsel, int lane,
+                                          bf16x8 (&qh)[AW_QT][2], bf16x8 (&ql)[AW_QT][2]) {
     const int g = lane >> 4, c = lane & 15;
-    const float sc = 0.125f * 1.4426950408889634f;  // 1/sqrt(64) * log2(e)
-    const bf16 *kg = qkv + split_col(H + h * ATT_D);
-    const bf16 *vg = qkv + split_col(2 * H + h * ATT_D);
-    // chunk ci -> buffer b: 8 pieces of 1 KiB for K and 8 for V (piece pc: key rows
-    // 4 pc .. 4 pc + 3, lane -> row 4 pc + lane / 16, slot (lane & 15) ^ swizzle)
-    auto stage = [&](int ci, int b) {
+    const bf16 *qbase = qkv + split_col(G.h * ATT_D) + 8 * g;
 #pragma unroll
-        for (int pc = 0; pc < AW_KC / 4; ++pc) {
-            const int rl = 4 * pc + (lane >> 4);
-            const int row = tok0 + min(ci * AW_KC + rl, n - 1);
-            const int j = (lane & 15) ^ ax_swz(rl);
-            unsigned char *dst = lds_w + b * AW_BUF + (4 * pc) * 256;
-            __builtin_amdgcn_global_load_lds((const void *)(kg + row * ld + j * 8),
-                                             (lds_void *)dst, 16, 0, 0);
-            __builtin_amdgcn_global_load_lds((const void *)(vg + row * ld + j * 8),
-                                             (lds_void *)(dst + AW_IMG), 16, 0, 0);
-        }
-    };
-    // Q^T B operands (hi, lo) of the group's tiles
-    bf16x8 qh[NQT][2], ql[NQT][2];
-    {
-        const bf16 *qbase = qkv + split_col(h * ATT_D) + 8 * g;
+    for (int qt = 0; qt < AW_QT; ++qt) {
+        const int qi = min(G.g0 + 16 * qt + c, G.nq - 1);
+        const int qloc = qsel ? min(max(qsel[G.q0 + qi], 0), G.n - 1) : qi;
+        const bf16 *src = qbase + (int64_t)(G.tok0 + qloc) * ld;
 #pragma unroll
-        for (int qt = 0; qt < NQT; ++qt) {
-            const int qi = min(g0 + 16 * qt + c, nq - 1);
-            const int qloc = qsel ? min(max(qsel[q0 + qi], 0), n - 1) : qi;
-            const bf16 *src = qbase + (int64_t)(tok0 + qloc) * ld;
-#pragma unroll
-            for (int ch = 0; ch < 2; ++ch) {
-                qh[qt][ch] = *reinterpret_cast<const bf16x8 *>(src + ch * 64);
-                ql[qt][ch] = *reinterpret_cast<const bf16x8 *>(src + ch * 64 + 32);
-            }
+        for (int ch = 0; ch < 2; ++ch) {
+            qh[qt][ch] = *reinterpret_cast<const bf16x8 *>(src + ch * 64);
+            ql[qt][ch] = *reinterpret_cast<const bf16x8 *>(src + ch * 64 + 32);
         }
     }
+}
+
+// Stores of one group: AW_STORES buffer stores per tile (4 column groups x hi, lo),
+// every one issued (rows past the group's queries fall outside the buffer range and are
+// dropped), so a later counted vmcnt can leave exactly them in flight.
+constexpr int AW_STORES = 8;
+
+// Group G: chunk ci in buffer (b0 + ci) & 1 (chunk 0 staged and G's Q loaded by the
+// caller); during the last chunk, the next group's chunk 0 and Q are issued (into
+// buffer (b0 + n_chunks) & 1 and qnh / qnl).  prev_stores: the previous group's stores
+// still in flight (NQT of it x AW_STORES) -- the first wait leaves them outstanding.
+template <int NQT>
+__device__ __forceinline__ void aw_group(const bf16 *__restrict__ qkv, int64_t ld, int H,
+                                         const AwGroup &G, int b0, bool has_next, const AwGroup &NX,
+                                         const int32_t *__restrict__ qsel, bf16 *__restrict__ ctx,
+                                         unsigned char *lds_w, uint32_t wbase, int lane,
+                                         const bf16x8 (&qh)[AW_QT][2], const bf16x8 (&ql)[AW_QT][2],
+                                         bf16x8 (&qnh)[AW_QT][2], bf16x8 (&qnl)[AW_QT][2],
+                                         int prev_stores) {
+    const int g = lane >> 4, c = lane & 15;
+    const float sc = 0.125f * 1.4426950408889634f;  // 1/sqrt(64) * log2(e)
+    const int n = G.n;
     // fragment addresses in buffer 0 (buffer 1: + AW_BUF)
     uint32_t ka[2][2][2], va[4][2][2];
 #pragma unroll
@@ -936,13 +989,27 @@ __device__ __forceinline__ void aw_group(const bf16 *__restrict__ qkv, int64_t l
         for (int dt = 0; dt < 4; ++dt) o[qt][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
     const int n_chunks = (n + AW_KC - 1) / AW_KC;
-    stage(0, 0);
     for (int ci = 0; ci < n_chunks; ++ci) {
-        const uint32_t boff = (uint32_t)(ci & 1) * AW_BUF;
-        // this wave's chunk ci has landed (the Q loads with it); its buffer's reads of
-        // chunk ci - 1's other buffer are long done (waited below): chunk ci + 1 may go there
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (ci + 1 < n_chunks) stage(ci + 1, (ci + 1) & 1);
+        const int b = (b0 + ci) & 1;
+        const uint32_t boff = (uint32_t)b * AW_BUF;
+        // chunk ci (and, at ci 0, this group's Q) has landed: everything this wave issued
+        // before the previous group's stores -- those may stay in flight
+        if (ci == 0 && prev_stores > 0) {
+            switch (prev_stores) {  // (s_waitcnt takes an immediate)
+            case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+            case 16: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
+            case 24: asm volatile("s_waitcnt vmcnt(24)" ::: "memory"); break;
+            default: asm volatile("s_waitcnt vmcnt(32)" ::: "memory"); break;
+            }
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        if (ci + 1 < n_chunks) {
+            aw_stage(qkv, ld, H, G, ci + 1, b ^ 1, lds_w, lane);
+        } else if (has_next) {  // the next group's first chunk and Q, behind this chunk
+            aw_stage(qkv, ld, H, NX, 0, b ^ 1, lds_w, lane);
+            aw_load_q(qkv, ld, NX, qsel, lane, qnh, qnl);
+        }
         uint4 kf[2][2][2];
         asm volatile("ds_read_b128 %0, %8\n\tds_read_b128 %1, %9\n\tds_read_b128 %2, %10\n\t"
                      "ds_read_b128 %3, %11\n\tds_read_b128 %4, %12\n\tds_read_b128 %5, %13\n\t"
@@ -1058,29 +1125,37 @@ __device__ __forceinline__ void aw_group(const bf16 *__restrict__ qkv, int64_t l
                     o[qt][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
                         vfr[dt][p == 1], p == 2 ? pl[qt] : ph[qt], o[qt][dt], 0, 0, 0);
     }
-    // context rows: O / row sum, split
+    // context rows: O / row sum, split; buffer stores over the group's rows [q0 + g0,
+    // q0 + nq) -- a query past them falls outside the range and is dropped
+    const uint64_t pa = reinterpret_cast<uint64_t>(ctx + (int64_t)(G.q0 + G.g0) * 2 * H);
+    const uint32_t lo32 = __builtin_amdgcn_readfirstlane((uint32_t)pa);
+    const uint32_t hi32 = __builtin_amdgcn_readfirstlane((uint32_t)(pa >> 32));
+    void *sbase = reinterpret_cast<void *>(((uint64_t)hi32 << 32) | lo32);
+    const int rows = __builtin_amdgcn_readfirstlane(G.nq - G.g0);
+    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(sbase, (short)0, rows * 2 * H * 2, 0x00020000);
 #pragma unroll
     for (int qt = 0; qt < NQT; ++qt) {
         float l = lsum[qt];
         l += __shfl_xor(l, 16, 64);
         l += __shfl_xor(l, 32, 64);
         const float inv = 1.0f / l;
-        const int q = g0 + 16 * qt + c;
-        if (q < nq) {
-            bf16 *out = ctx + (int64_t)(q0 + q) * 2 * H;
+        const int qr = 16 * qt + c;  // row within the group
 #pragma unroll
-            for (int dt = 0; dt < 4; ++dt) {
-                bf16x4 hv, lv;
+        for (int dt = 0; dt < 4; ++dt) {
+            typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+            u32x2 hv, lv;
+            bf16x4 h4, l4;
 #pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const float y = o[qt][dt][r] * inv;
-                    hv[r] = split_hi(y);
-                    lv[r] = split_lo(y);
-                }
-                const int64_t sc0 = split_col(h * ATT_D + dt * 16 + 4 * g);
-                *reinterpret_cast<bf16x4 *>(out + sc0) = hv;
-                *reinterpret_cast<bf16x4 *>(out + sc0 + 32) = lv;
+            for (int r = 0; r < 4; ++r) {
+                const float y = o[qt][dt][r] * inv;
+                h4[r] = split_hi(y);
+                l4[r] = split_lo(y);
             }
+            __builtin_memcpy(&hv, &h4, 8);
+            __builtin_memcpy(&lv, &l4, 8);
+            const int off = (qr * 2 * H + (int)split_col(G.h * ATT_D + dt * 16 + 4 * g)) * 2;
+            __builtin_amdgcn_raw_buffer_store_b64(hv, rsrc, off, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b64(lv, rsrc, off + 64, 0, 0);
         }
     }
 }
@@ -1097,21 +1172,34 @@ attention_x3w_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ c
     const uint32_t wbase =
         (uint32_t)(uintptr_t)((__attribute__((address_space(3))) unsigned char *)lds_w);
     const int stride = (int)gridDim.x * AW_WAVES;
-    for (int pr = (int)blockIdx.x * AW_WAVES + wave; pr < n_pairs; pr += stride) {
-        const int doc = pr / n_heads, h = pr % n_heads;
-        const int tok0 = cu_seqlens[doc], n = cu_seqlens[doc + 1] - tok0;
-        const int q0 = qsel ? cu_qsel[doc] : tok0;
-        const int nq = qsel ? cu_qsel[doc + 1] - q0 : n;
-        if (n <= 0 || nq <= 0) continue;
-        for (int g0 = 0; g0 < nq; g0 += AW_QT * 16) {
-            const int tiles = min(AW_QT, (nq - g0 + 15) / 16);
-            switch (tiles) {
-            case 1: aw_group<1>(qkv, ld, H, h, tok0, n, q0, nq, g0, qsel, ctx_split, lds_w, wbase, lane); break;
-            case 2: aw_group<2>(qkv, ld, H, h, tok0, n, q0, nq, g0, qsel, ctx_split, lds_w, wbase, lane); break;
-            case 3: aw_group<3>(qkv, ld, H, h, tok0, n, q0, nq, g0, qsel, ctx_split, lds_w, wbase, lane); break;
-            default: aw_group<4>(qkv, ld, H, h, tok0, n, q0, nq, g0, qsel, ctx_split, lds_w, wbase, lane); break;
-            }
+    const int first_pr = (int)blockIdx.x * AW_WAVES + wave;
+    AwGroup G, NX;
+    G.pr = -1;
+    if (!aw_next(G, first_pr, stride, n_pairs, n_heads, cu_seqlens, qsel, cu_qsel, G)) return;
+    bf16x8 qa[AW_QT][2], qb[AW_QT][2], qna[AW_QT][2], qnb[AW_QT][2];
+    aw_load_q(qkv, ld, G, qsel, lane, qa, qb);
+    aw_stage(qkv, ld, H, G, 0, 0, lds_w, lane);
+    int b0 = 0, prev_stores = 0;
+    for (;;) {
+        const bool has_next = aw_next(G, first_pr, stride, n_pairs, n_heads, cu_seqlens, qsel,
+                                      cu_qsel, NX);
+        switch (G.tiles) {
+        case 1: aw_group<1>(qkv, ld, H, G, b0, has_next, NX, qsel, ctx_split, lds_w, wbase, lane, qa, qb, qna, qnb, prev_stores); break;
+        case 2: aw_group<2>(qkv, ld, H, G, b0, has_next, NX, qsel, ctx_split, lds_w, wbase, lane, qa, qb, qna, qnb, prev_stores); break;
+        case 3: aw_group<3>(qkv, ld, H, G, b0, has_next, NX, qsel, ctx_split, lds_w, wbase, lane, qa, qb, qna, qnb, prev_stores); break;
+        default: aw_group<4>(qkv, ld, H, G, b0, has_next, NX, qsel, ctx_split, lds_w, wbase, lane, qa, qb, qna, qnb, prev_stores); break;
         }
+        if (!has_next) break;
+        prev_stores = G.tiles * AW_STORES;
+        b0 = (b0 + (G.n + AW_KC - 1) / AW_KC) & 1;
+        G = NX;
+#pragma unroll
+        for (int qt = 0; qt < AW_QT; ++qt)
+#pragma unroll
+            for (int ch = 0; ch < 2; ++ch) {
+                qa[qt][ch] = qna[qt][ch];
+                qb[qt][ch] = qnb[qt][ch];
+            }
     }
 }
 
