@@ -526,8 +526,9 @@ constexpr uint32_t IR_LONG = 1, IR_BAD = 2;
 __global__ void __launch_bounds__(128)
 item_setup_kernel(SubIndex si, int min_cls, int nb, int64_t n_terms,
                   const uint32_t *__restrict__ q_terms, const int32_t *__restrict__ cu_q, int n_q,
-                  ItemRec *__restrict__ rec) {
-    const int item = blockIdx.x, q = item % n_q, b = item / n_q;
+                  ItemRec *__restrict__ rec, const uint16_t *__restrict__ border) {
+    const int item = blockIdx.x, q = item % n_q, r_ = item / n_q;
+    const int b = border ? (int)border[(int64_t)q * nb + r_] : r_;
     const int q0 = cu_q[q], nt = cu_q[q + 1] - q0;
     if (nt > WTERMS || nt <= 0) return;
     ItemRec *r = rec + (int64_t)item * WTERMS;
@@ -1534,6 +1535,42 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
     if (tid == 0) *cn = (n & 0xFFFFu) == (uint32_t)k ? k : -2;
 }
 
+// Block order of each query for block-max scoring (BASELINE configs[4]): blocks by
+// descending upper bound sum_j emax(t_j, b) (ties: block order), so the query's shared
+// threshold -- the k-th score among the candidates of its finished blocks -- rises to
+// near its final value within the first blocks and the later, weaker blocks skip more
+// of their wave segments.  Any order is exact (the threshold is a lower bound of the
+// final k-th score whatever blocks it has seen; the merge orders by key).  One
+// workgroup per query; rank by counting (nb <= BO_MAX_BLOCKS).
+constexpr int BO_MAX_BLOCKS = 1024;
+__global__ void __launch_bounds__(256)
+block_order_kernel(SubIndex si, int nb, int64_t n_terms, const uint32_t *__restrict__ q_terms,
+                   const int32_t *__restrict__ cu_q, uint16_t *__restrict__ border) {
+    __shared__ uint32_t bound[BO_MAX_BLOCKS];
+    const int q = blockIdx.x;
+    const int q0 = cu_q[q], nt = cu_q[q + 1] - q0;
+    for (int b = threadIdx.x; b < nb; b += blockDim.x) {
+        uint32_t u = 0;
+        for (int j = 0; j < nt && j < WTERMS; ++j) {
+            const uint32_t t = q_terms[q0 + j];
+            if (t >= n_terms) continue;
+            const int64_t e = find_entry(si, nb, t, b);
+            if (e >= 0) u += si.emax[e];
+        }
+        bound[b] = u;
+    }
+    __syncthreads();
+    for (int b = threadIdx.x; b < nb; b += blockDim.x) {
+        const uint32_t u = bound[b];
+        int r = 0;
+        for (int x = 0; x < nb; ++x) {
+            const uint32_t v = bound[x];
+            r += v > u || (v == u && x < b);
+        }
+        border[(int64_t)q * nb + r] = (uint16_t)b;
+    }
+}
+
 // Persistent: one workgroup per CU walks the (query, block) items, so the per-
 // workgroup launch cost (16 waves, 154 KiB of LDS) is paid once per CU, not per item.
 __global__ void __launch_bounds__(SC_THREADS)
@@ -1543,7 +1580,8 @@ score_blocks_kernel(const uint32_t *__restrict__ post, SubIndex si, int min_cls,
                     uint64_t *__restrict__ cand_key, int32_t *__restrict__ cand_n, int n_items,
                     int n_q, uint32_t *__restrict__ qhist, int ablate,
                     const ItemRec *__restrict__ rec, uint32_t *__restrict__ long_flag,
-                    float bm_factor, unsigned long long *__restrict__ bm_stat) {
+                    float bm_factor, unsigned long long *__restrict__ bm_stat,
+                    const uint16_t *__restrict__ border) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     ScoreShared &sh = *reinterpret_cast<ScoreShared *>(smem);
     if ((uint32_t)(uintptr_t)((__attribute__((address_space(3))) unsigned char *)smem) != 0) {
@@ -1555,7 +1593,9 @@ score_blocks_kernel(const uint32_t *__restrict__ post, SubIndex si, int min_cls,
     }
     // items block-major: item = b * n_q + q (the shared threshold, see score_item)
     for (int item = blockIdx.x; item < n_items; item += gridDim.x) {
-        score_item(sh, item % n_q, item / n_q, post, si, min_cls, nb, block_docs, n_terms,
+        const int q = item % n_q, r_ = item / n_q;
+        score_item(sh, q, border ? (int)border[(int64_t)q * nb + r_] : r_, post, si, min_cls, nb,
+                   block_docs, n_terms,
                    n_docs, doc_lo, q_terms, cu_q, k, cand_key, cand_n, qhist, ablate,
                    rec ? rec + (int64_t)item * WTERMS : nullptr, long_flag, bm_factor, bm_stat);
         __syncthreads();  // every wave is done with the LDS of this item
@@ -1876,6 +1916,7 @@ struct di_index {
     DevBuf ws_rec;  // ItemRec per (item, term slot): item_setup_kernel -> score_blocks
     DevBuf ws_long;  // score_blocks -> score_long_kernel: the batch has long queries
     DevBuf bm_stat;  // block-max statistics: u64 {segments evaluated, segments skipped}
+    DevBuf ws_border;  // block-max: each query's block order (block_order_kernel)
     // packed (block-compressed) postings, built by di_index_set_packed (SubIndex pk_*)
     DevBuf pk_fs, pk_fwt, pk_fh, pk_data;
     bool pk_built = false, packed = false;
@@ -2453,10 +2494,22 @@ int di_index_search(di_index *ix, const uint32_t *q_terms, const int32_t *cu_q, 
                 const int n_items = nq * nb;
                 // packed postings (configs[4]): exact scoring from the item records only
                 const bool pk = ix->packed && ix->pk_built && ix->min_cls >= 7 && use_rec;
+                // block-max: blocks in descending order of their bound per query
+                // (DI_PROFILE_ABLATE bit 16384: block order, A/B)
+                const bool order = thr && ix->bm_factor > 0.0f && nb > 1 &&
+                                   nb <= BO_MAX_BLOCKS && !(ix->ablate & 16384);
+                if (order) {
+                    ix->ws_border.reserve((size_t)nq * nb * 2);
+                    hipLaunchKernelGGL(block_order_kernel, dim3(nq), dim3(256), 0, s, ix->sub(),
+                                       nb, ix->n_terms, dq, dcu + q0,
+                                       ix->ws_border.as<uint16_t>());
+                    check_launch("block_order");
+                }
+                const uint16_t *border = order ? ix->ws_border.as<uint16_t>() : nullptr;
                 if (use_rec) {
                     hipLaunchKernelGGL(item_setup_kernel, dim3(n_items), dim3(128), 0, s,
                                        ix->sub(pk), ix->min_cls, nb, ix->n_terms, dq, dcu + q0, nq,
-                                       ix->ws_rec.as<ItemRec>());
+                                       ix->ws_rec.as<ItemRec>(), border);
                     check_launch("item_setup");
                 }
                 hipLaunchKernelGGL(score_blocks_kernel, dim3(std::min(n_items, n_cu())),
@@ -2468,7 +2521,7 @@ int di_index_search(di_index *ix, const uint32_t *q_terms, const int32_t *cu_q, 
                                    nq, thr ? ix->ws_thr.as<uint32_t>() : nullptr, ix->ablate,
                                    use_rec ? ix->ws_rec.as<ItemRec>() : nullptr,
                                    ix->ws_long.as<uint32_t>(), thr ? ix->bm_factor : 0.0f,
-                                   ix->bm_stat.as<unsigned long long>());
+                                   ix->bm_stat.as<unsigned long long>(), border);
                 check_launch("score_blocks");
                 hipLaunchKernelGGL(score_long_kernel, dim3(std::min(n_items, n_cu())),
                                    dim3(SC_THREADS), sizeof(ScoreShared), s,

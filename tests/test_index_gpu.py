@@ -434,7 +434,9 @@ def test_block_max_exact_skips_on_skewed_collection(L, k):
     seg = dev.timing("bm_segments")[1]
     skipped = dev.timing("bm_segments_skipped")[1]
     print(f"k={k}: {skipped} of {seg} wave segments skipped ({skipped / max(seg, 1):.3f})")
-    assert seg > 0 and skipped > 0.2 * seg
+    # (the exact skip potential with the final k-th score is ~0.4 of the segments,
+    # tools/skip_potential.py; the running threshold reaches less of it at k = 1000)
+    assert seg > 0 and skipped > (0.3 if k == 10 else 0.1) * seg
     dev.set_block_max(0.0)
     dev.timing("bm_segments", reset=True)
     assert dev.search(qs, k) == want
