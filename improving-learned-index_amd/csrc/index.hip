@@ -93,6 +93,7 @@ struct ScoreShared {
     uint32_t thr, above, ties, bin, bin_above;
     uint32_t tq;                   // the query's shared threshold as this item read it
     uint32_t lmask[WTERMS / 32];   // terms (j < WTERMS) with a per-wave layout in this block
+    uint32_t pmask[WTERMS / 32];   // packed mode: short terms read from the plain postings
     uint32_t wub[WSEG];            // block-max: each wave segment's score upper bound
     uint32_t wtab[WTERMS][WSEG];   // their per-wave runs: start << 16 | end (in the sublist)
 };
@@ -405,11 +406,12 @@ __device__ __forceinline__ void packed_fields(const uint32_t *data, uint32_t cnt
 }
 
 // One frame applied to the block's words (the read-modify-write of scatter_apply);
-// LIVE: postings in skipped wave segments go to the lane's dummy word.
-template <int W, bool LIVE>
+// OWN: only the docs [dlo, dlo + dn) (the wave's own segment), the rest to the lane's
+// dummy word.
+template <int W, bool OWN>
 __device__ __forceinline__ void packed_apply_w(const uint4 h, const uint32_t *__restrict__ pdata,
-                                               int lane, uint32_t first_bits, uint32_t live16,
-                                               uint32_t magic, uint32_t dummy) {
+                                               int lane, uint32_t first_bits, uint32_t dlo,
+                                               uint32_t dn, uint32_t dummy) {
     uint32_t f[PK_PER_LANE];
     const uint32_t base = h.y & 0xFFFFu, cnt = (h.y >> 16) & 1023u, bd = (h.y >> 26) & 31u;
     packed_fields<W>(pdata + h.x, cnt, lane, f);
@@ -426,7 +428,7 @@ __device__ __forceinline__ void packed_apply_w(const uint4 h, const uint32_t *__
     for (int i = 0; i < PK_PER_LANE; ++i) {
         const uint32_t d = first + ds[i];
         bool ok = (uint32_t)(PK_PER_LANE * lane + i) < cnt;
-        if constexpr (LIVE) ok = ok && ((live16 >> min(__umulhi(d, magic), 15u)) & 1u);
+        if constexpr (OWN) ok = ok && d - dlo < dn;  // (the wave's own docs only)
         a[i] = ok ? d << 2 : dummy;
         asm volatile("ds_read_b32 %0, %1" : "=v"(w[i]) : "v"(a[i]) : "memory");
     }
@@ -442,17 +444,17 @@ __device__ __forceinline__ void packed_apply_w(const uint4 h, const uint32_t *__
     }
 }
 
-template <bool LIVE>
+template <bool OWN>
 __device__ __forceinline__ void packed_apply(const uint4 h, const uint32_t *__restrict__ pdata,
-                                             int lane, uint32_t first_bits, uint32_t live16,
-                                             uint32_t magic, uint32_t dummy) {
+                                             int lane, uint32_t first_bits, uint32_t dlo,
+                                             uint32_t dn, uint32_t dummy) {
     switch ((h.z >> 12) & 63u) {  // (wave-uniform)
-    case 4: packed_apply_w<4, LIVE>(h, pdata, lane, first_bits, live16, magic, dummy); break;
-    case 8: packed_apply_w<8, LIVE>(h, pdata, lane, first_bits, live16, magic, dummy); break;
-    case 12: packed_apply_w<12, LIVE>(h, pdata, lane, first_bits, live16, magic, dummy); break;
-    case 16: packed_apply_w<16, LIVE>(h, pdata, lane, first_bits, live16, magic, dummy); break;
-    case 20: packed_apply_w<20, LIVE>(h, pdata, lane, first_bits, live16, magic, dummy); break;
-    default: packed_apply_w<24, LIVE>(h, pdata, lane, first_bits, live16, magic, dummy); break;
+    case 4: packed_apply_w<4, OWN>(h, pdata, lane, first_bits, dlo, dn, dummy); break;
+    case 8: packed_apply_w<8, OWN>(h, pdata, lane, first_bits, dlo, dn, dummy); break;
+    case 12: packed_apply_w<12, OWN>(h, pdata, lane, first_bits, dlo, dn, dummy); break;
+    case 16: packed_apply_w<16, OWN>(h, pdata, lane, first_bits, dlo, dn, dummy); break;
+    case 20: packed_apply_w<20, OWN>(h, pdata, lane, first_bits, dlo, dn, dummy); break;
+    default: packed_apply_w<24, OWN>(h, pdata, lane, first_bits, dlo, dn, dummy); break;
     }
 }
 
@@ -519,7 +521,10 @@ struct ItemRec {
     uint32_t pad[3];
 };
 static_assert(sizeof(ItemRec) % 16 == 0, "records stay 16-byte aligned");
-constexpr uint32_t IR_LONG = 1, IR_BAD = 2;
+constexpr uint32_t IR_LONG = 1, IR_BAD = 2, IR_PLAIN = 4;
+// packed mode: short sublists of fewer postings stay in the plain layout (a frame's
+// header and lane rounding would cost more than their 4-byte words)
+constexpr uint32_t PK_MIN = 32;
 
 // Items (query q, block b) as the scorer numbers them (item = b * n_q + q); records
 // only for queries of 1..WTERMS terms (the scorer's per-wave form), WTERMS per item.
@@ -546,15 +551,18 @@ item_setup_kernel(SubIndex si, int min_cls, int nb, int64_t n_terms,
         const uint32_t id = en >= 0 ? si.lid[en] : 0xFFFFFFFFu;
         if (w == 0) {
             int64_t lo, hi;
-            if (si.pk_fs) {  // packed: frame ranges (exact scoring only, min_cls 7)
-                lo = en >= 0 ? si.pk_fs[en] : 0;
-                hi = en >= 0 ? si.pk_fs[en + 1] : 0;
+            uint32_t fl = id != 0xFFFFFFFFu ? IR_LONG : 0u;
+            if (si.pk_fs && en >= 0 && (id != 0xFFFFFFFFu || si.epos[en + 1] - si.epos[en] >= PK_MIN)) {
+                // packed: frame ranges (exact scoring only, min_cls 7)
+                lo = si.pk_fs[en];
+                hi = si.pk_fs[en + 1];
             } else {
                 entry_bounds(si, en, min_cls, lo, hi);
+                if (si.pk_fs) fl |= IR_PLAIN;
             }
             r[j].lo = lo;
             r[j].hi = hi;
-            r[j].flags = id != 0xFFFFFFFFu ? IR_LONG : 0u;
+            r[j].flags = fl;
         }
         r[j].wmx[w] = en < 0 ? 0 : id != 0xFFFFFFFFu ? si.wmax[(int64_t)id * WSEG + w] : si.emax[en];
         if (id != 0xFFFFFFFFu) {
@@ -718,6 +726,10 @@ __device__ __forceinline__ void score_long_item(
 }
 
 // One work item = (query q, doc block b): accumulate, select the block's top-k.
+// EXT: the configs[4] extensions -- block-max skipping (bm_factor), packed postings
+// (si.pk_fs), per-query block order -- compiled into a kernel of their own, so the plain
+// scorer's code and registers stay exactly as without them.
+template <bool EXT>
 __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
                                            const uint32_t *__restrict__ post, const SubIndex &si,
                                            int min_cls, int nb,
@@ -729,7 +741,8 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
                                            uint32_t *__restrict__ qhist, int ablate,
                                            const ItemRec *__restrict__ ir,
                                            uint32_t *__restrict__ long_flag, float bm_factor,
-                                           unsigned long long *__restrict__ bm_stat) {
+                                           unsigned long long *__restrict__ bm_stat,
+                                           uint32_t *__restrict__ qtq) {
     int64_t *lo = sh.v.bounds[0], *hi = sh.v.bounds[1];
 
     // opaque per item: keeps the per-thread index arithmetic of the sweeps from being
@@ -768,7 +781,7 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
         sh.bad = 0;
         sh.emit = 0;
         sh.n_tie = 0;
-        for (int i = 0; i < WTERMS / 32; ++i) sh.lmask[i] = 0;
+        for (int i = 0; i < WTERMS / 32; ++i) sh.lmask[i] = sh.pmask[i] = 0;
         for (int i = 0; i < WSEG; ++i) sh.wub[i] = 0;
         sh.tq = 0;
     }
@@ -779,7 +792,13 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
     // -- so no term needs a barrier; longer queries: the all-wave form, a barrier per term
     const bool wl = nt <= WTERMS;
     // block-max skipping (opt-in, configs[4]): per-wave segment upper bounds (wub)
-    const bool bm = bm_factor > 0.0f && wl && qhist != nullptr;
+    const bool bm = EXT && bm_factor > 0.0f && wl && qhist != nullptr;
+    // block-max: the query's running threshold as one word (qtq, raised by every item's
+    // selection with a lower bound of the final k-th score), loaded with the setup's
+    // loads -- the skip decision needs no histogram copy, no extra barrier
+    uint32_t tq_early = 0;
+    if (bm && qtq)
+        tq_early = __hip_atomic_load(&qtq[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     // The query's shared threshold histogram (qhist, below) is copied by LDS-DMA into
     // the selection histogram (idle until the selection) here, so its round trip
     // overlaps the scatter and the selection reads it from LDS; the fast selection
@@ -826,6 +845,7 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
                 hi[j] = rhi;
                 if (f & IR_BAD) sh.bad = 1;
                 if (f & IR_LONG) atomicOr(&sh.lmask[j >> 5], 1u << (j & 31));
+                if (EXT && (f & IR_PLAIN)) atomicOr(&sh.pmask[j >> 5], 1u << (j & 31));
             }
             if (f & IR_LONG) sh.wtab[j][w] = wt;
         }
@@ -938,8 +958,13 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
     bool skip_wave = false;
     uint32_t live16 = 0xFFFFu;  // bm: the wave segments that are scored (bit w)
     if (bm) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the threshold copy (read_tq)
-        const uint32_t tq0 = read_tq();
+        uint32_t tq0;
+        if (qtq) {
+            tq0 = tq_early;
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the threshold copy (read_tq)
+            tq0 = read_tq();
+        }
         const float thr = bm_factor * (float)tq0;
         skip_wave = tq0 > 0 && (float)sh.wub[wave] < thr;
         // every segment below: lanes 0..15 of each wave check one each (no block
@@ -986,40 +1011,54 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
     // order, a barrier between terms (a doc occurs once per term: no race inside one);
     // a long term's runs of the scored segments in pieces of 512 postings dealt over
     // the waves; a short term's sublist in block-wide rounds, the postings of skipped
-    // segments sent to the lane's dummy word.  (DI_PROFILE_ABLATE bit 8192: off, A/B.)
-    if (si.pk_fs && wl) {
-        // packed postings (configs[4]): every wave on every scored segment, frames dealt
-        // over the waves, a barrier between terms (the coop form below, on frames)
-        const uint32_t magic = (uint32_t)((0x100000000ull + wseg - 1) / wseg);
-        const uint32_t ldummy = (uint32_t)(MAX_BLOCK_DOCS + lane) << 2;
-        for (int j = 0; j < nt; ++j) {
+    // segments sent to the lane's dummy word.  (Opt-in, DI_PROFILE_ABLATE bit 8192: at
+    // 8.8 M skewed docs it measured no faster than the skipping waves idling, 45.8 k vs
+    // 46.3 k q/s, profiles/round4_d_*.)
+    if (!EXT) {
+        // (the plain kernel: the per-wave / all-wave loops below)
+    } else if (si.pk_fs && wl) {
+        // packed postings (configs[4]), the per-wave form of the plain scorer: a long
+        // term's frames of the wave's own segment run; a short term read whole by every
+        // wave (its frame, or its plain words when short of PK_MIN), applied to the
+        // wave's own docs only -- no barrier between terms; a skipped segment's wave
+        // scores nothing (skip_wave)
+        const uint32_t wd = (uint32_t)(MAX_BLOCK_DOCS + lane) << 2;
+        const uint32_t dlo = (uint32_t)wave * wseg;
+        const uint32_t dn = wave == WSEG - 1 ? 0x7FFFFFFFu - dlo : wseg;
+        for (int j = skip_wave ? nt : 0; j < nt; ++j) {
             const uint32_t first_bits = (uint32_t)(255 - j) << 8;
-            uint32_t piece = 0;
             if (is_long(j)) {
-                for (int w = 0; w < WSEG; ++w) {
-                    if (!((live16 >> w) & 1u)) continue;
-                    const uint32_t se = sh.wtab[j][w];
-                    const int64_t f1 = lo[j] + (se & 0xFFFFu);
-                    for (int64_t f = lo[j] + (se >> 16); f < f1; ++f, ++piece)
-                        if ((int)(piece % SC_WAVES) == wave)
-                            packed_apply<false>(si.pk_fh[f], si.pk_data, lane, first_bits, live16,
-                                                magic, ldummy);
+                const uint32_t se = sh.wtab[j][wave];
+                const int64_t f1 = lo[j] + (se & 0xFFFFu);
+                for (int64_t f = lo[j] + (se >> 16); f < f1; ++f)
+                    packed_apply<false>(si.pk_fh[f], si.pk_data, lane, first_bits, 0u, 0x7FFFFFFFu, wd);
+            } else if ((sh.pmask[j >> 5] >> (j & 31)) & 1u) {
+                for (int64_t pos = lo[j], end = hi[j]; pos < end;) {
+                    const int64_t rem = end - pos;
+                    if (rem > 4 * 64) {
+                        uint32_t r[8];
+                        scatter_load<8, 64>(post + pos, rem, lane, r, true);
+                        scatter_apply_own<8>(r, first_bits, dlo, dn, wd);
+                        pos += 8 * 64;
+                    } else if (rem > 64) {
+                        uint32_t r[4];
+                        scatter_load<4, 64>(post + pos, rem, lane, r, true);
+                        scatter_apply_own<4>(r, first_bits, dlo, dn, wd);
+                        pos = end;
+                    } else {
+                        uint32_t r[1];
+                        scatter_load<1, 64>(post + pos, rem, lane, r);
+                        scatter_apply_own<1>(r, first_bits, dlo, dn, wd);
+                        pos = end;
+                    }
                 }
             } else {
-                for (int64_t f = lo[j]; f < hi[j]; ++f, ++piece)
-                    if ((int)(piece % SC_WAVES) == wave) {
-                        if (live16 == 0xFFFFu)
-                            packed_apply<false>(si.pk_fh[f], si.pk_data, lane, first_bits, live16,
-                                                magic, ldummy);
-                        else
-                            packed_apply<true>(si.pk_fh[f], si.pk_data, lane, first_bits, live16,
-                                               magic, ldummy);
-                    }
+                for (int64_t f = lo[j]; f < hi[j]; ++f)
+                    packed_apply<true>(si.pk_fh[f], si.pk_data, lane, first_bits, dlo, dn, wd);
             }
-            if (j + 1 < nt) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
         }
         skip_wave = true;  // (nothing left for the per-wave loop below)
-    } else if (bm && live16 != 0xFFFFu && !(ablate & 8192)) {
+    } else if (bm && live16 != 0xFFFFu && (ablate & 8192)) {
         const uint32_t magic = (uint32_t)((0x100000000ull + wseg - 1) / wseg);  // d / wseg
         const uint32_t ldummy = (uint32_t)(MAX_BLOCK_DOCS + lane) << 2;
         const bool x4c = !(ablate & 4096);
@@ -1259,6 +1298,7 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
         }
         __syncthreads();
         Tq = sh.tq;
+        if (EXT && qtq && tid == 0 && Tq > tq_early) atomicMax(&qtq[q], Tq);
         stamp(8);  // threshold read (the part of tq-select before the sweep)
         // (wsum is written again only after a barrier of the selection below; tq only
         // at the next item's start)
@@ -1332,6 +1372,9 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
             if (tid == 0) *cn = 0;
             return;
         }
+        // (this block alone has >= k docs scoring >= T: a lower bound of the query's final
+        // k-th score for block-max, qtq)
+        if (EXT && qtq && tid == 0 && sh.thr > tq_early) atomicMax(&qtq[q], sh.thr);
         const uint32_t T = sh.thr, ties = sh.ties;  // T >= 1: every touched score is
         const uint32_t above = sh.above;             // nonzero
 
@@ -1502,6 +1545,7 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
                          });
     }
     const uint32_t T = prefix;
+    if (EXT && qtq && tid == 0 && (T >> 16) > tq_early) atomicMax(&qtq[q], T >> 16);
     const uint32_t ties = sh.u.rs.tot[sh.u.rs.bin];
 
     // doc-order cut among the ties: the `need` smallest doc indices
@@ -1573,6 +1617,7 @@ block_order_kernel(SubIndex si, int nb, int64_t n_terms, const uint32_t *__restr
 
 // Persistent: one workgroup per CU walks the (query, block) items, so the per-
 // workgroup launch cost (16 waves, 154 KiB of LDS) is paid once per CU, not per item.
+template <bool EXT>
 __global__ void __launch_bounds__(SC_THREADS)
 score_blocks_kernel(const uint32_t *__restrict__ post, SubIndex si, int min_cls, int nb,
                     int block_docs, int64_t n_terms, uint32_t n_docs, uint32_t doc_lo,
@@ -1581,7 +1626,7 @@ score_blocks_kernel(const uint32_t *__restrict__ post, SubIndex si, int min_cls,
                     int n_q, uint32_t *__restrict__ qhist, int ablate,
                     const ItemRec *__restrict__ rec, uint32_t *__restrict__ long_flag,
                     float bm_factor, unsigned long long *__restrict__ bm_stat,
-                    const uint16_t *__restrict__ border) {
+                    const uint16_t *__restrict__ border, uint32_t *__restrict__ qtq) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     ScoreShared &sh = *reinterpret_cast<ScoreShared *>(smem);
     if ((uint32_t)(uintptr_t)((__attribute__((address_space(3))) unsigned char *)smem) != 0) {
@@ -1594,10 +1639,11 @@ score_blocks_kernel(const uint32_t *__restrict__ post, SubIndex si, int min_cls,
     // items block-major: item = b * n_q + q (the shared threshold, see score_item)
     for (int item = blockIdx.x; item < n_items; item += gridDim.x) {
         const int q = item % n_q, r_ = item / n_q;
-        score_item(sh, q, border ? (int)border[(int64_t)q * nb + r_] : r_, post, si, min_cls, nb,
+        score_item<EXT>(sh, q, EXT && border ? (int)border[(int64_t)q * nb + r_] : r_, post, si,
+                   min_cls, nb,
                    block_docs, n_terms,
                    n_docs, doc_lo, q_terms, cu_q, k, cand_key, cand_n, qhist, ablate,
-                   rec ? rec + (int64_t)item * WTERMS : nullptr, long_flag, bm_factor, bm_stat);
+                   rec ? rec + (int64_t)item * WTERMS : nullptr, long_flag, bm_factor, bm_stat, qtq);
         __syncthreads();  // every wave is done with the LDS of this item
     }
 }
@@ -1917,6 +1963,7 @@ struct di_index {
     DevBuf ws_long;  // score_blocks -> score_long_kernel: the batch has long queries
     DevBuf bm_stat;  // block-max statistics: u64 {segments evaluated, segments skipped}
     DevBuf ws_border;  // block-max: each query's block order (block_order_kernel)
+    DevBuf ws_tq;      // block-max: each query's running threshold (one word)
     // packed (block-compressed) postings, built by di_index_set_packed (SubIndex pk_*)
     DevBuf pk_fs, pk_fwt, pk_fh, pk_data;
     bool pk_built = false, packed = false;
@@ -2221,7 +2268,10 @@ namespace di {
 // Kernels using more than 64 KiB of dynamic LDS must opt in, once per device.
 void enable_big_lds() {
     static_assert(sizeof(ScoreShared) <= 160 * 1024, "ScoreShared exceeds LDS");
-    DI_HIP(hipFuncSetAttribute((const void *)score_blocks_kernel,
+    DI_HIP(hipFuncSetAttribute((const void *)score_blocks_kernel<false>,
+                               hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)sizeof(ScoreShared)));
+    DI_HIP(hipFuncSetAttribute((const void *)score_blocks_kernel<true>,
                                hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)sizeof(ScoreShared)));
     DI_HIP(hipFuncSetAttribute((const void *)score_long_kernel,
@@ -2506,13 +2556,21 @@ int di_index_search(di_index *ix, const uint32_t *q_terms, const int32_t *cu_q, 
                     check_launch("block_order");
                 }
                 const uint16_t *border = order ? ix->ws_border.as<uint16_t>() : nullptr;
+                // (DI_PROFILE_ABLATE bit 32768: the histogram-copy threshold instead, A/B)
+                const bool use_qtq = thr && ix->bm_factor > 0.0f && !(ix->ablate & 32768);
+                if (use_qtq) {
+                    ix->ws_tq.reserve((size_t)nq * 4);
+                    DI_HIP(hipMemsetAsync(ix->ws_tq.p, 0, (size_t)nq * 4, s));
+                }
                 if (use_rec) {
                     hipLaunchKernelGGL(item_setup_kernel, dim3(n_items), dim3(128), 0, s,
                                        ix->sub(pk), ix->min_cls, nb, ix->n_terms, dq, dcu + q0, nq,
                                        ix->ws_rec.as<ItemRec>(), border);
                     check_launch("item_setup");
                 }
-                hipLaunchKernelGGL(score_blocks_kernel, dim3(std::min(n_items, n_cu())),
+                const bool ext = pk || order || (thr && ix->bm_factor > 0.0f);
+                hipLaunchKernelGGL(ext ? score_blocks_kernel<true> : score_blocks_kernel<false>,
+                                   dim3(std::min(n_items, n_cu())),
                                    dim3(SC_THREADS), sizeof(ScoreShared), s,
                                    ix->post.as<uint32_t>(), ix->sub(pk),
                                    ix->min_cls, nb, ix->block_docs, ix->n_terms,
@@ -2521,7 +2579,8 @@ int di_index_search(di_index *ix, const uint32_t *q_terms, const int32_t *cu_q, 
                                    nq, thr ? ix->ws_thr.as<uint32_t>() : nullptr, ix->ablate,
                                    use_rec ? ix->ws_rec.as<ItemRec>() : nullptr,
                                    ix->ws_long.as<uint32_t>(), thr ? ix->bm_factor : 0.0f,
-                                   ix->bm_stat.as<unsigned long long>(), border);
+                                   ix->bm_stat.as<unsigned long long>(), border,
+                                   use_qtq ? ix->ws_tq.as<uint32_t>() : nullptr);
                 check_launch("score_blocks");
                 hipLaunchKernelGGL(score_long_kernel, dim3(std::min(n_items, n_cu())),
                                    dim3(SC_THREADS), sizeof(ScoreShared), s,
@@ -2626,7 +2685,10 @@ static void build_packed(di_index *ix) {
         a = epos[(size_t)e] + (w ? m[(w - 1) * 8 + 7] : 0u);
         b = epos[(size_t)e] + m[w * 8 + 7];
     };
-    auto n_runs = [&](int64_t e) { return lid[(size_t)e] == NO ? 1 : WSEG; };
+    // (a short sublist under PK_MIN postings stays plain: no run, no frame)
+    auto n_runs = [&](int64_t e) {
+        return lid[(size_t)e] != NO ? WSEG : epos[(size_t)e + 1] - epos[(size_t)e] >= PK_MIN ? 1 : 0;
+    };
     auto frames_of = [](uint32_t n) { return (n + PK_FRAME - 1) / PK_FRAME; };
     // pass 1: frames per entry -> fs; per long entry the run starts (fwt)
     std::vector<uint32_t> fs((size_t)ne + 1, 0);
@@ -2731,7 +2793,12 @@ static void build_packed(di_index *ix) {
     upload(ix->pk_fh, fh);
     upload(ix->pk_data, data);
     ix->pk_frames = nfr;
-    ix->pk_bytes = (int64_t)doff[(size_t)nfr] * 4 + nfr * (int64_t)sizeof(uint4);
+    // bytes the packed scorer reads: headers + packed data + the plain words of the short
+    // sublists it reads from the plain layout
+    int64_t plain_small = 0;
+    for (int64_t e = 0; e < ne; ++e)
+        if (n_runs(e) == 0) plain_small += epos[(size_t)e + 1] - epos[(size_t)e];
+    ix->pk_bytes = (int64_t)doff[(size_t)nfr] * 4 + nfr * (int64_t)sizeof(uint4) + 4 * plain_small;
     ix->pk_built = true;
 }
 
