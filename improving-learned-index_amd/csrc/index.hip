@@ -94,6 +94,7 @@ struct ScoreShared {
     uint32_t tq;                   // the query's shared threshold as this item read it
     uint32_t lmask[WTERMS / 32];   // terms (j < WTERMS) with a per-wave layout in this block
     uint32_t pmask[WTERMS / 32];   // packed mode: short terms read from the plain postings
+    unsigned long long bm_cnt[2];  // block-max statistics of the workgroup (thread 0)
     uint32_t wub[WSEG];            // block-max: each wave segment's score upper bound
     uint32_t wtab[WTERMS][WSEG];   // their per-wave runs: start << 16 | end (in the sublist)
 };
@@ -305,34 +306,6 @@ __device__ __forceinline__ void scatter_apply_own(const uint32_t (&cur)[UU], uin
     for (int u = 0; u < UU; ++u) {
         const uint32_t d = (cur[u] ^ POST_X) >> 10;
         a[u] = (d - dlo < dn) ? d << 2 : dummy;
-        asm volatile("ds_read_b32 %0, %1" : "=v"(w[u]) : "v"(a[u]) : "memory");
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-    for (int u = 0; u < UU; ++u) asm volatile("" : "+v"(w[u]));
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int u = 0; u < UU; ++u) {
-        const uint32_t v = cur[u] & 255u;
-        asm volatile("ds_write_b32 %0, %1" ::"v"(a[u]), "v"(word_update(w[u], v, first_bits))
-                     : "memory");
-    }
-}
-
-// scatter_apply for the block-max cooperative form: postings of a skipped wave segment
-// (bit seg of live16 clear; seg = doc / wseg by the multiply-high `magic`, exact for
-// docs < 2^16) update the lane's dummy word instead.  The padding (doc MAX_BLOCK_DOCS)
-// lands in segment 15 or a dummy, both never read.
-template <int UU>
-__device__ __forceinline__ void scatter_apply_live(const uint32_t (&cur)[UU], uint32_t first_bits,
-                                                   uint32_t live16, uint32_t magic,
-                                                   uint32_t dummy) {
-    uint32_t w[UU], a[UU];
-#pragma unroll
-    for (int u = 0; u < UU; ++u) {
-        const uint32_t d = (cur[u] ^ POST_X) >> 10;
-        const uint32_t sg = min(__umulhi(d, magic), 15u);
-        a[u] = ((live16 >> sg) & 1u) ? d << 2 : dummy;
         asm volatile("ds_read_b32 %0, %1" : "=v"(w[u]) : "v"(a[u]) : "memory");
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -726,10 +699,12 @@ __device__ __forceinline__ void score_long_item(
 }
 
 // One work item = (query q, doc block b): accumulate, select the block's top-k.
-// EXT: the configs[4] extensions -- block-max skipping (bm_factor), packed postings
-// (si.pk_fs), per-query block order -- compiled into a kernel of their own, so the plain
-// scorer's code and registers stay exactly as without them.
-template <bool EXT>
+// EXT: the configs[4] extensions -- 0 none (the plain scorer: its code and registers
+// stay exactly as without them), EXT_BM block-max skipping over the plain postings
+// (bm_factor, per-query block order, the cooperative form), EXT_PK the packed postings
+// (si.pk_fs; with or without block-max) -- one kernel each.
+constexpr int EXT_BM = 1, EXT_PK = 2;
+template <int EXT>
 __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
                                            const uint32_t *__restrict__ post, const SubIndex &si,
                                            int min_cls, int nb,
@@ -741,7 +716,6 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
                                            uint32_t *__restrict__ qhist, int ablate,
                                            const ItemRec *__restrict__ ir,
                                            uint32_t *__restrict__ long_flag, float bm_factor,
-                                           unsigned long long *__restrict__ bm_stat,
                                            uint32_t *__restrict__ qtq) {
     int64_t *lo = sh.v.bounds[0], *hi = sh.v.bounds[1];
 
@@ -792,7 +766,7 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
     // -- so no term needs a barrier; longer queries: the all-wave form, a barrier per term
     const bool wl = nt <= WTERMS;
     // block-max skipping (opt-in, configs[4]): per-wave segment upper bounds (wub)
-    const bool bm = EXT && bm_factor > 0.0f && wl && qhist != nullptr;
+    const bool bm = EXT != 0 && bm_factor > 0.0f && wl && qhist != nullptr;
     // block-max: the query's running threshold as one word (qtq, raised by every item's
     // selection with a lower bound of the final k-th score), loaded with the setup's
     // loads -- the skip decision needs no histogram copy, no extra barrier
@@ -845,7 +819,7 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
                 hi[j] = rhi;
                 if (f & IR_BAD) sh.bad = 1;
                 if (f & IR_LONG) atomicOr(&sh.lmask[j >> 5], 1u << (j & 31));
-                if (EXT && (f & IR_PLAIN)) atomicOr(&sh.pmask[j >> 5], 1u << (j & 31));
+                if (EXT == EXT_PK && (f & IR_PLAIN)) atomicOr(&sh.pmask[j >> 5], 1u << (j & 31));
             }
             if (f & IR_LONG) sh.wtab[j][w] = wt;
         }
@@ -976,15 +950,18 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
         const bool all_below = below_m == ~0ull;
         live16 = (uint32_t)~below_m & 0xFFFFu;
         // skip statistics (di_index_timing "bm_segments" / "bm_segments_skipped"): every
-        // evaluated item counts its WSEG segments, every skipped segment one
-        if (bm_stat) {
-            if (tid == 0) {
-                atomicAdd(&bm_stat[0], (unsigned long long)WSEG);
-                if (all_below) atomicAdd(&bm_stat[1], (unsigned long long)WSEG);
-            }
-            if (!all_below && skip_wave && lane == 0) atomicAdd(&bm_stat[1], 1ull);
+        // evaluated item counts its WSEG segments, every skipped segment one -- in the
+        // workgroup's LDS, added to the device counters once per workgroup at the kernel's
+        // end (an atomic per item and skipping wave on one address cost tens of ms per
+        // 8.8 M-doc batch)
+        if (tid == 0) {
+            sh.bm_cnt[0] += WSEG;
+            sh.bm_cnt[1] += (unsigned long long)__builtin_popcount(~live16 & 0xFFFFu);
         }
         if (all_below) {
+            // the item's threshold-histogram copy (LDS-DMA into sh.u.hist) lands before
+            // the next item uses that LDS (it would overwrite the next query's copy)
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             if (tid == 0) *cn = 0;
             return;
         }
@@ -1005,18 +982,12 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
     bool have_pre = false;
     auto is_long = [&](int j) { return wl && ((sh.lmask[j >> 5] >> (j & 31)) & 1u); };
     const uint32_t wseg = ((uint32_t)block_docs + WSEG - 1) / WSEG;
-    // Block-max with some segments skipped (coop): every wave works on every scored
-    // segment instead of its own only -- a skipped segment's wave would otherwise idle
-    // while the rest of the item runs as long as without skipping.  Terms in query
-    // order, a barrier between terms (a doc occurs once per term: no race inside one);
-    // a long term's runs of the scored segments in pieces of 512 postings dealt over
-    // the waves; a short term's sublist in block-wide rounds, the postings of skipped
-    // segments sent to the lane's dummy word.  (Opt-in, DI_PROFILE_ABLATE bit 8192: at
-    // 8.8 M skewed docs it measured no faster than the skipping waves idling, 45.8 k vs
-    // 46.3 k q/s, profiles/round4_d_*.)
-    if (!EXT) {
+    // (A cooperative form -- every wave on every scored segment, barriers between terms,
+    // so that a skipped segment's wave does not idle -- measured no faster at 8.8 M skewed
+    // docs, 45.8 k vs 46.3 k q/s, and was removed; round-4 DESIGN §3.)
+    if (EXT == 0) {
         // (the plain kernel: the per-wave / all-wave loops below)
-    } else if (si.pk_fs && wl) {
+    } else if (EXT == EXT_PK && si.pk_fs && wl) {
         // packed postings (configs[4]), the per-wave form of the plain scorer: a long
         // term's frames of the wave's own segment run; a short term read whole by every
         // wave (its frame, or its plain words when short of PK_MIN), applied to the
@@ -1058,56 +1029,6 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
             }
         }
         skip_wave = true;  // (nothing left for the per-wave loop below)
-    } else if (bm && live16 != 0xFFFFu && (ablate & 8192)) {
-        const uint32_t magic = (uint32_t)((0x100000000ull + wseg - 1) / wseg);  // d / wseg
-        const uint32_t ldummy = (uint32_t)(MAX_BLOCK_DOCS + lane) << 2;
-        const bool x4c = !(ablate & 4096);
-        for (int j = 0; j < nt; ++j) {
-            const uint32_t first_bits = (uint32_t)(255 - j) << 8;
-            if (is_long(j)) {
-                uint32_t piece = 0;
-                for (int w = 0; w < WSEG; ++w) {
-                    if (!((live16 >> w) & 1u)) continue;
-                    const uint32_t se = sh.wtab[j][w];
-                    const int64_t end = lo[j] + (se & 0xFFFFu);
-                    for (int64_t pos = lo[j] + (se >> 16); pos < end; pos += 8 * 64, ++piece) {
-                        if ((int)(piece % SC_WAVES) != wave) continue;
-                        const int64_t rem = end - pos;
-                        if (rem > 4 * 64) {
-                            uint32_t r[8];
-                            scatter_load<8, 64>(post + pos, rem, lane, r, x4c);
-                            scatter_apply<8>(sh.acc, r, first_bits);
-                        } else if (rem > 64) {
-                            uint32_t r[4];
-                            scatter_load<4, 64>(post + pos, rem, lane, r, x4c);
-                            scatter_apply<4>(sh.acc, r, first_bits);
-                        } else {
-                            uint32_t r[1];
-                            scatter_load<1, 64>(post + pos, rem, lane, r);
-                            scatter_apply<1>(sh.acc, r, first_bits);
-                        }
-                    }
-                }
-            } else {
-                for (int64_t pos = lo[j], end = hi[j]; pos < end;) {
-                    const int64_t rem = end - pos;
-                    if (rem > SC_THREADS) {
-                        uint32_t r[4];
-                        scatter_load<4>(post + pos, rem, tid, r, x4c);
-                        scatter_apply_live<4>(r, first_bits, live16, magic, ldummy);
-                        pos += 4 * SC_THREADS;
-                    } else {
-                        uint32_t r[1];
-                        scatter_load<1>(post + pos, rem, tid, r);
-                        scatter_apply_live<1>(r, first_bits, live16, magic, ldummy);
-                        pos = end;
-                    }
-                }
-            }
-            // term boundary: this term's LDS writes land before any wave reads the next
-            if (j + 1 < nt) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        }
-        skip_wave = true;  // (the per-wave loop below has nothing left to do)
     }
     const uint32_t wdlo = (uint32_t)wave * wseg;
     const uint32_t wdn = wave == WSEG - 1 ? 0x7FFFFFFFu - wdlo : wseg;  // last: the rest
@@ -1298,7 +1219,7 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
         }
         __syncthreads();
         Tq = sh.tq;
-        if (EXT && qtq && tid == 0 && Tq > tq_early) atomicMax(&qtq[q], Tq);
+        if (EXT != 0 && qtq && tid == 0 && Tq > tq_early) atomicMax(&qtq[q], Tq);
         stamp(8);  // threshold read (the part of tq-select before the sweep)
         // (wsum is written again only after a barrier of the selection below; tq only
         // at the next item's start)
@@ -1374,7 +1295,7 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
         }
         // (this block alone has >= k docs scoring >= T: a lower bound of the query's final
         // k-th score for block-max, qtq)
-        if (EXT && qtq && tid == 0 && sh.thr > tq_early) atomicMax(&qtq[q], sh.thr);
+        if (EXT != 0 && qtq && tid == 0 && sh.thr > tq_early) atomicMax(&qtq[q], sh.thr);
         const uint32_t T = sh.thr, ties = sh.ties;  // T >= 1: every touched score is
         const uint32_t above = sh.above;             // nonzero
 
@@ -1545,7 +1466,7 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
                          });
     }
     const uint32_t T = prefix;
-    if (EXT && qtq && tid == 0 && (T >> 16) > tq_early) atomicMax(&qtq[q], T >> 16);
+    if (EXT != 0 && qtq && tid == 0 && (T >> 16) > tq_early) atomicMax(&qtq[q], T >> 16);
     const uint32_t ties = sh.u.rs.tot[sh.u.rs.bin];
 
     // doc-order cut among the ties: the `need` smallest doc indices
@@ -1617,7 +1538,7 @@ block_order_kernel(SubIndex si, int nb, int64_t n_terms, const uint32_t *__restr
 
 // Persistent: one workgroup per CU walks the (query, block) items, so the per-
 // workgroup launch cost (16 waves, 154 KiB of LDS) is paid once per CU, not per item.
-template <bool EXT>
+template <int EXT>
 __global__ void __launch_bounds__(SC_THREADS)
 score_blocks_kernel(const uint32_t *__restrict__ post, SubIndex si, int min_cls, int nb,
                     int block_docs, int64_t n_terms, uint32_t n_docs, uint32_t doc_lo,
@@ -1636,15 +1557,20 @@ score_blocks_kernel(const uint32_t *__restrict__ post, SubIndex si, int min_cls,
             if (threadIdx.x == 0) cand_n[item] = -1;
         return;
     }
+    if (EXT != 0 && threadIdx.x == 0) sh.bm_cnt[0] = sh.bm_cnt[1] = 0ull;  // (the first item's barriers publish it)
     // items block-major: item = b * n_q + q (the shared threshold, see score_item)
     for (int item = blockIdx.x; item < n_items; item += gridDim.x) {
         const int q = item % n_q, r_ = item / n_q;
-        score_item<EXT>(sh, q, EXT && border ? (int)border[(int64_t)q * nb + r_] : r_, post, si,
+        score_item<EXT>(sh, q, EXT != 0 && border ? (int)border[(int64_t)q * nb + r_] : r_, post, si,
                    min_cls, nb,
                    block_docs, n_terms,
                    n_docs, doc_lo, q_terms, cu_q, k, cand_key, cand_n, qhist, ablate,
-                   rec ? rec + (int64_t)item * WTERMS : nullptr, long_flag, bm_factor, bm_stat, qtq);
+                   rec ? rec + (int64_t)item * WTERMS : nullptr, long_flag, bm_factor, qtq);
         __syncthreads();  // every wave is done with the LDS of this item
+    }
+    if (EXT != 0 && bm_stat && threadIdx.x == 0 && sh.bm_cnt[0]) {
+        atomicAdd(&bm_stat[0], sh.bm_cnt[0]);
+        atomicAdd(&bm_stat[1], sh.bm_cnt[1]);
     }
 }
 
@@ -2268,10 +2194,13 @@ namespace di {
 // Kernels using more than 64 KiB of dynamic LDS must opt in, once per device.
 void enable_big_lds() {
     static_assert(sizeof(ScoreShared) <= 160 * 1024, "ScoreShared exceeds LDS");
-    DI_HIP(hipFuncSetAttribute((const void *)score_blocks_kernel<false>,
+    DI_HIP(hipFuncSetAttribute((const void *)score_blocks_kernel<0>,
                                hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)sizeof(ScoreShared)));
-    DI_HIP(hipFuncSetAttribute((const void *)score_blocks_kernel<true>,
+    DI_HIP(hipFuncSetAttribute((const void *)score_blocks_kernel<EXT_BM>,
+                               hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)sizeof(ScoreShared)));
+    DI_HIP(hipFuncSetAttribute((const void *)score_blocks_kernel<EXT_PK>,
                                hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)sizeof(ScoreShared)));
     DI_HIP(hipFuncSetAttribute((const void *)score_long_kernel,
@@ -2569,7 +2498,9 @@ int di_index_search(di_index *ix, const uint32_t *q_terms, const int32_t *cu_q, 
                     check_launch("item_setup");
                 }
                 const bool ext = pk || order || (thr && ix->bm_factor > 0.0f);
-                hipLaunchKernelGGL(ext ? score_blocks_kernel<true> : score_blocks_kernel<false>,
+                hipLaunchKernelGGL(pk    ? score_blocks_kernel<EXT_PK>
+                                   : ext ? score_blocks_kernel<EXT_BM>
+                                         : score_blocks_kernel<0>,
                                    dim3(std::min(n_items, n_cu())),
                                    dim3(SC_THREADS), sizeof(ScoreShared), s,
                                    ix->post.as<uint32_t>(), ix->sub(pk),
