@@ -9,3 +9,6 @@ SWEEP=bm DI_PROFILE_ABLATE=32768 timeout -k 10 300 python3 tools/prune_sweep.py 
 timeout -k 10 400 python3 tools/prune_sweep.py 8800000 skew > $O/sweep_8m_skew.json 2> $O/sweep_8m_skew.err; fatal $? sweep
 timeout -k 10 400 python3 tools/prune_sweep.py 8800000 > $O/sweep_8m_iid.json 2> $O/sweep_8m_iid.err; fatal $? sweep_iid
 echo all-done
+DI_PROFILE_ABLATE=64 timeout -k 10 300 python3 tools/phase_prune.py 8800000 1 skew 0 > gpurun_out/round4_f/phase_skew_exh.txt 2>&1; fatal $? phase1
+DI_PROFILE_ABLATE=64 timeout -k 10 300 python3 tools/phase_prune.py 8800000 1 skew 1 > gpurun_out/round4_f/phase_skew_bm1.txt 2>&1; fatal $? phase2
+echo phases-done

@@ -1,7 +1,8 @@
 """Scorer phase stamps (DI_PROFILE_ABLATE=64, workgroup 0) and device ms per batch at one
 impact-pruning level, to see where a pruned (query, block) item's time goes.
 Profiling only (the stamps change nothing but timing).
-    DI_PROFILE_ABLATE=64 python tools/phase_prune.py <n_docs> <min_impact>
+    DI_PROFILE_ABLATE=64 python tools/phase_prune.py <n_docs> <min_impact> [skew] [bm]
+(skew: synthetic.SKEW_CONFIG4; bm: block-max factor, default 0 = off)
 """
 import sys
 from pathlib import Path
@@ -12,12 +13,16 @@ from improving_learned_index_amd import _lib  # noqa: E402
 from improving_learned_index_amd import synthetic as S  # noqa: E402
 
 n_docs, mi = int(sys.argv[1]), int(sys.argv[2])
+skew = len(sys.argv) > 3 and sys.argv[3] == "skew"
+bm = float(sys.argv[4]) if len(sys.argv) > 4 else 0.0
 nq, k = 6980, 1000
-term_off, pdoc, pval, _ = S.synth_postings(n_docs, 2 * n_docs, seed=4321)
+term_off, pdoc, pval, _ = S.synth_postings(n_docs, 2 * n_docs, seed=4321,
+                                           skew=S.SKEW_CONFIG4 if skew else None)
 flat, cuq = _lib.csr(S.msmarco_like_queries(nq, 2 * n_docs, seed=1234))
 ix = _lib.DeviceIndex.from_postings(term_off, pdoc, pval, 0, n_docs)
 ix.reserve(nq, k)
 ix.set_min_impact(mi)
+ix.set_block_max(bm)
 ix.search_csr(flat, cuq, k)
 print("---- timed", file=sys.stderr, flush=True)
 ix.timing("score_blocks", reset=True)
