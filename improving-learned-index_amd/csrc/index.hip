@@ -1035,54 +1035,6 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
     const uint32_t wdummy = (uint32_t)(MAX_BLOCK_DOCS + lane) << 2;
     const uint32_t vmin = 1u << (7 - min(min_cls, 7));  // all-wave form: pruning by value
     const bool x4 = !(ablate & 4096);  // rounds of 4k postings per lane by 16-byte loads (bit 4096: 4-byte, A/B)
-    // Sparse items (a big collection: a few hundred postings per wave and term): every
-    // term of the wave is one round of at most 4 postings per lane, and the per-term
-    // rounds' load round trips, one after another, are the item's time.  Then all the
-    // terms' loads go out at once and are applied in term order (the wave's own LDS
-    // operations stay in program order).  (DI_PROFILE_ABLATE bit 131072: off, A/B.)
-    constexpr int SP_TERMS = 6;  // (dev.small-shaped queries: <= 6 terms)
-    if (wl && nt <= SP_TERMS && !skip_wave && !(ablate & 1) && !(ablate & 131072)) {
-        bool small = true;
-        for (int j = 0; j < nt; ++j) {
-            int64_t n_j;
-            if (is_long(j)) {
-                const uint32_t se = sh.wtab[j][wave];
-                n_j = (int64_t)(se & 0xFFFFu) - (int64_t)(se >> 16);
-            } else {
-                n_j = hi[j] - lo[j];
-            }
-            small = small && n_j <= 4 * 64;
-        }
-        if (small) {
-            uint32_t r[SP_TERMS][4];
-#pragma unroll
-            for (int j = 0; j < SP_TERMS; ++j) {
-                if (j < nt) {
-                    int64_t a, b;
-                    if (is_long(j)) {
-                        const uint32_t se = sh.wtab[j][wave];
-                        a = lo[j] + (se >> 16);
-                        b = lo[j] + (se & 0xFFFFu);
-                    } else {
-                        a = lo[j];
-                        b = hi[j];
-                    }
-                    scatter_load<4, 64>(post + a, b - a, lane, r[j], x4);
-                }
-            }
-#pragma unroll
-            for (int j = 0; j < SP_TERMS; ++j) {
-                if (j < nt) {
-                    const uint32_t first_bits = (uint32_t)(255 - j) << 8;
-                    if (is_long(j))
-                        scatter_apply<4>(sh.acc, r[j], first_bits);
-                    else
-                        scatter_apply_own<4>(r[j], first_bits, wdlo, wdn, wdummy);
-                }
-            }
-            skip_wave = true;  // (done: the loop below has nothing left)
-        }
-    }
     for (int j = (ablate & 1) || skip_wave ? nt : 0; j < nt; ++j) {  // ablate bit 0: skip (profiling)
         const uint32_t first_bits = (uint32_t)(255 - j) << 8;
         const bool lj = is_long(j);
