@@ -95,6 +95,8 @@ struct ScoreShared {
     uint32_t lmask[WTERMS / 32];   // terms (j < WTERMS) with a per-wave layout in this block
     uint32_t pmask[WTERMS / 32];   // packed mode: short terms read from the plain postings
     unsigned long long bm_cnt[2];  // block-max statistics of the workgroup (thread 0)
+    uint32_t tqe;                  // block-max: the query's running threshold (qtq) as
+                                   // thread 0 read it -- one value for every wave
     uint32_t wub[WSEG];            // block-max: each wave segment's score upper bound
     uint32_t wtab[WTERMS][WSEG];   // their per-wave runs: start << 16 | end (in the sublist)
 };
@@ -770,8 +772,11 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
     // block-max: the query's running threshold as one word (qtq, raised by every item's
     // selection with a lower bound of the final k-th score), loaded with the setup's
     // loads -- the skip decision needs no histogram copy, no extra barrier
+    // (thread 0 alone loads it and publishes it through LDS at the setup barrier: waves
+    // that read the word themselves could see different values -- other CUs raise it --
+    // and disagree on skipping, i.e. on which barriers they reach)
     uint32_t tq_early = 0;
-    if (bm && qtq)
+    if (bm && qtq && threadIdx.x == 0)
         tq_early = __hip_atomic_load(&qtq[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     // The query's shared threshold histogram (qhist, below) is copied by LDS-DMA into
     // the selection histogram (idle until the selection) here, so its round trip
@@ -875,6 +880,7 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
         }
         zero();
     }
+    if (bm && qtq && tid == 0) sh.tqe = tq_early;
     __syncthreads();
     if (sh.bad) {
         // (the histogram copy lands before the next item touches the histogram)
@@ -934,7 +940,7 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
     if (bm) {
         uint32_t tq0;
         if (qtq) {
-            tq0 = tq_early;
+            tq0 = sh.tqe;  // (written before the setup barrier)
         } else {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the threshold copy (read_tq)
             tq0 = read_tq();

@@ -521,3 +521,27 @@ def test_packed_block_max_on_skewed_collection(L):
     dev.timing("bm_segments", reset=True)
     assert dev.search(qs, 1000) == want
     assert dev.timing("bm_segments_skipped")[1] > 0
+
+
+def test_block_max_approximate_factors_on_skewed_collection(L):
+    """Factors > 1 skip far more (approximate): every search still completes (every item
+    writes a valid candidate count) and returns docs with their full scores in key
+    order.  (The block-max skip decision is one workgroup-wide value: waves that read the
+    running threshold themselves could disagree on skipping -- and on the barriers they
+    reach; this ran into a selection-count error and an illegal address before.)"""
+    from improving_learned_index_amd import synthetic as S
+
+    n = 1_100_000
+    term_off, pdoc, pval, _ = S.synth_postings(n, 2 * n, seed=4321, skew=S.SKEW_CONFIG4)
+    ora = oracle.Index.__new__(oracle.Index)
+    ora.term_off, ora.pdoc, ora.pval, ora.n_docs = term_off, pdoc, pval, n
+    dev = L.DeviceIndex.from_postings(term_off, pdoc, pval, 0, n)
+    qs = S.msmarco_like_queries(3000, 2 * n, seed=13)
+    full = ora.score_ids(qs[:200], n, n_threads=16)
+    for f in (1.5, 2.0, 3.0, 1.5, 2.0):
+        dev.set_block_max(f)
+        got = dev.search(qs, 1000)
+        for g, w in zip(got[:200], full):
+            true = dict(w)
+            assert all(true[d] == s_ for d, s_ in g)
+            assert [s_ for _, s_ in g] == sorted((s_ for _, s_ in g), reverse=True)
