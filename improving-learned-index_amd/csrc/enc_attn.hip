@@ -842,367 +842,6 @@ attention_x3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
 #undef AX_SEL
 }
 
-// ---------------------------------------------------------------------------
-// attention_x3w_kernel: the fp32-faithful (split-bf16) attention with every wave on its
-// own.  A workgroup is AW_WAVES = 4 waves, one per SIMD, each with its own 32 KiB of
-// LDS; a wave takes whole (doc, head) pairs (pairs dealt round-robin over all the
-// chip's waves) and, per group of up to AW_QT = 4 query tiles of 16 (64 queries), streams
-// the pair's K and V split rows through its own double-buffered LDS images in 32-key
-// chunks by LDS-DMA (chunk i + 1 lands while chunk i computes).  No workgroup barrier,
-// no idle SIMD at a pair's last tiles (attention_x3_kernel's 8 waves share a pass of 16
-// tiles: a 200-token document's 13 tiles ran 4 / 3 / 3 / 3 on the SIMDs), no waiting
-// for other waves' copies.  Per chunk and tile: S^T = K Q^T (12 MFMAs, split products
-// as attention_x3_kernel), the lazy-max online softmax in f32, O^T = V^T P^T (12).
-// Images as attention_x3_kernel's (256-byte key rows [ch0 hi | ch0 lo | ch1 hi | ch1
-// lo], 16-byte slot j at j ^ ax_swz(r)); rows 0..31 only.
-constexpr int AW_WAVES = 4, AW_QT = 4, AW_KC = 32;
-constexpr int AW_IMG = AW_KC * 256;            // 8 KiB: one K or V image
-constexpr int AW_BUF = 2 * AW_IMG;             // K | V of one chunk
-constexpr int AW_WAVE_LDS = 2 * AW_BUF;        // double-buffered: 32 KiB per wave
-constexpr int AW_LDS = AW_WAVES * AW_WAVE_LDS;  // 128 KiB
-
-// One group of a wave: up to AW_QT query tiles of one (doc, head) pair.
-struct AwGroup {
-    int pr, g0, h, tok0, n, q0, nq, tiles;
-};
-
-// The wave's group after `cur` (or the first one when cur.pr < 0): the pair's next 64
-// queries, else the next pair (pairs pr, pr + stride, ...) with a token and a query.
-__device__ __forceinline__ bool aw_next(const AwGroup &cur, int first_pr, int stride, int n_pairs,
-                                        int n_heads, const int32_t *__restrict__ cu_seqlens,
-                                        const int32_t *__restrict__ qsel,
-                                        const int32_t *__restrict__ cu_qsel, AwGroup &nx) {
-    if (cur.pr >= 0 && cur.g0 + AW_QT * 16 < cur.nq) {
-        nx = cur;
-        nx.g0 = cur.g0 + AW_QT * 16;
-        nx.tiles = min(AW_QT, (nx.nq - nx.g0 + 15) / 16);
-        return true;
-    }
-    for (int pr = cur.pr >= 0 ? cur.pr + stride : first_pr; pr < n_pairs; pr += stride) {
-        const int doc = pr / n_heads;
-        nx.pr = pr;
-        nx.h = pr % n_heads;
-        nx.tok0 = cu_seqlens[doc];
-        nx.n = cu_seqlens[doc + 1] - nx.tok0;
-        nx.q0 = qsel ? cu_qsel[doc] : nx.tok0;
-        nx.nq = qsel ? cu_qsel[doc + 1] - nx.q0 : nx.n;
-        nx.g0 = 0;
-        nx.tiles = min(AW_QT, (nx.nq + 15) / 16);
-        if (nx.n > 0 && nx.nq > 0) return true;
-    }
-    return false;
-}
-
-// K and V of chunk ci of group G -> buffer b of the wave's LDS: 8 pieces of 1 KiB each
-// (piece pc: key rows 4 pc .. 4 pc + 3, lane -> row 4 pc + lane / 16, slot (lane & 15)
-// ^ swizzle); 16 LDS-DMA instructions.
-__device__ __forceinline__ void aw_stage(const bf16 *__restrict__ qkv, int64_t ld, int H,
-                                         const AwGroup &G, int ci, int b, unsigned char *lds_w,
-                                         int lane) {
-    typedef __attribute__((address_space(3))) void lds_void;
-    const bf16 *kg = qkv + split_col(H + G.h * ATT_D);
-    const bf16 *vg = qkv + split_col(2 * H + G.h * ATT_D);
-#pragma unroll
-    for (int pc = 0; pc < AW_KC / 4; ++pc) {
-        const int rl = 4 * pc + (lane >> 4);
-        const int row = G.tok0 + min(ci * AW_KC + rl, G.n - 1);
-        const int j = (lane & 15) ^ ax_swz(rl);
-        unsigned char *dst = lds_w + b * AW_BUF + (4 * pc) * 256;
-        __builtin_amdgcn_global_load_lds((const void *)(kg + row * ld + j * 8), (lds_void *)dst,
-                                         16, 0, 0);
-        __builtin_amdgcn_global_load_lds((const void *)(vg + row * ld + j * 8),
-                                         (lds_void *)(dst + AW_IMG), 16, 0, 0);
-    }
-}
-
-// Q^T B operands (hi, lo) of group G's AW_QT tiles (tiles past G.tiles read a clamped
-// row: loaded, never used) -- 4 AW_QT loads of 16 B per lane.
-__device__ __forceinline__ void aw_load_q(const bf16 *__restrict__ qkv, int64_t ld, const AwGroup &G,
-                                          const int32_t *__restrict__ qsel, int lane,
-                                          bf16x8 (&qh)[AW_QT][2], bf16x8 (&ql)[AW_QT][2]) {
-    const int g = lane >> 4, c = lane & 15;
-    const bf16 *qbase = qkv + split_col(G.h * ATT_D) + 8 * g;
-#pragma unroll
-    for (int qt = 0; qt < AW_QT; ++qt) {
-        const int qi = min(G.g0 + 16 * qt + c, G.nq - 1);
-        const int qloc = qsel ? min(max(qsel[G.q0 + qi], 0), G.n - 1) : qi;
-        const bf16 *src = qbase + (int64_t)(G.tok0 + qloc) * ld;
-#pragma unroll
-        for (int ch = 0; ch < 2; ++ch) {
-            qh[qt][ch] = *reinterpret_cast<const bf16x8 *>(src + ch * 64);
-            ql[qt][ch] = *reinterpret_cast<const bf16x8 *>(src + ch * 64 + 32);
-        }
-    }
-}
-
-// Stores of one group: AW_STORES buffer stores per tile (4 column groups x hi, lo),
-// every one issued (rows past the group's queries fall outside the buffer range and are
-// dropped), so a later counted vmcnt can leave exactly them in flight.
-constexpr int AW_STORES = 8;
-
-// Group G: chunk ci in buffer (b0 + ci) & 1 (chunk 0 staged and G's Q loaded by the
-// caller); during the last chunk, the next group's chunk 0 and Q are issued (into
-// buffer (b0 + n_chunks) & 1 and qnh / qnl).  prev_stores: the previous group's stores
-// still in flight (NQT of it x AW_STORES) -- the first wait leaves them outstanding.
-template <int NQT>
-__device__ __forceinline__ void aw_group(const bf16 *__restrict__ qkv, int64_t ld, int H,
-                                         const AwGroup &G, int b0, bool has_next, const AwGroup &NX,
-                                         const int32_t *__restrict__ qsel, bf16 *__restrict__ ctx,
-                                         unsigned char *lds_w, uint32_t wbase, int lane,
-                                         const bf16x8 (&qh)[AW_QT][2], const bf16x8 (&ql)[AW_QT][2],
-                                         bf16x8 (&qnh)[AW_QT][2], bf16x8 (&qnl)[AW_QT][2],
-                                         int prev_stores) {
-    const int g = lane >> 4, c = lane & 15;
-    const float sc = 0.125f * 1.4426950408889634f;  // 1/sqrt(64) * log2(e)
-    const int n = G.n;
-    // fragment addresses in buffer 0 (buffer 1: + AW_BUF)
-    uint32_t ka[2][2][2], va[4][2][2];
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int ch = 0; ch < 2; ++ch)
-#pragma unroll
-            for (int pt = 0; pt < 2; ++pt) {
-                const int r = 8 * (c >> 2) + 4 * t + (c & 3), j = ch * 8 + pt * 4 + g;
-                ka[t][ch][pt] = wbase + r * 256 + ((j ^ ax_swz(r)) << 4);
-            }
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-        for (int pt = 0; pt < 2; ++pt)
-#pragma unroll
-            for (int h2 = 0; h2 < 2; ++h2) {
-                const int qq = c >> 2, pp = c & 3;
-                const int r = 8 * g + 4 * h2 + qq;
-                const int j = (dt >> 1) * 8 + pt * 4 + 2 * (dt & 1) + (pp >> 1);
-                va[dt][pt][h2] = wbase + AW_IMG + r * 256 + ((j ^ ax_swz(r)) << 4) + 8 * (pp & 1);
-            }
-    float m[NQT], lsum[NQT], lim[NQT], mneg[NQT];
-    f32x4 o[NQT][4];
-#pragma unroll
-    for (int qt = 0; qt < NQT; ++qt) {
-        m[qt] = -INFINITY;
-        lim[qt] = -INFINITY;
-        mneg[qt] = 0.f;
-        lsum[qt] = 0.f;
-#pragma unroll
-        for (int dt = 0; dt < 4; ++dt) o[qt][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-    const int n_chunks = (n + AW_KC - 1) / AW_KC;
-    for (int ci = 0; ci < n_chunks; ++ci) {
-        const int b = (b0 + ci) & 1;
-        const uint32_t boff = (uint32_t)b * AW_BUF;
-        // chunk ci (and, at ci 0, this group's Q) has landed: everything this wave issued
-        // before the previous group's stores -- those may stay in flight
-        if (ci == 0 && prev_stores > 0) {
-            switch (prev_stores) {  // (s_waitcnt takes an immediate)
-            case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
-            case 16: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
-            case 24: asm volatile("s_waitcnt vmcnt(24)" ::: "memory"); break;
-            default: asm volatile("s_waitcnt vmcnt(32)" ::: "memory"); break;
-            }
-        } else {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        if (ci + 1 < n_chunks) {
-            aw_stage(qkv, ld, H, G, ci + 1, b ^ 1, lds_w, lane);
-        } else if (has_next) {  // the next group's first chunk and Q, behind this chunk
-            aw_stage(qkv, ld, H, NX, 0, b ^ 1, lds_w, lane);
-            aw_load_q(qkv, ld, NX, qsel, lane, qnh, qnl);
-        }
-        uint4 kf[2][2][2];
-        asm volatile("ds_read_b128 %0, %8\n\tds_read_b128 %1, %9\n\tds_read_b128 %2, %10\n\t"
-                     "ds_read_b128 %3, %11\n\tds_read_b128 %4, %12\n\tds_read_b128 %5, %13\n\t"
-                     "ds_read_b128 %6, %14\n\tds_read_b128 %7, %15\n\ts_waitcnt lgkmcnt(0)"
-                     : "=&v"(kf[0][0][0]), "=&v"(kf[0][0][1]), "=&v"(kf[0][1][0]),
-                       "=&v"(kf[0][1][1]), "=&v"(kf[1][0][0]), "=&v"(kf[1][0][1]),
-                       "=&v"(kf[1][1][0]), "=&v"(kf[1][1][1])
-                     : "v"(ka[0][0][0] + boff), "v"(ka[0][0][1] + boff), "v"(ka[0][1][0] + boff),
-                       "v"(ka[0][1][1] + boff), "v"(ka[1][0][0] + boff), "v"(ka[1][0][1] + boff),
-                       "v"(ka[1][1][0] + boff), "v"(ka[1][1][1] + boff)
-                     : "memory");
-        __builtin_amdgcn_sched_barrier(0);
-        bf16x8 kfr[2][2][2];
-#pragma unroll
-        for (int t = 0; t < 2; ++t)
-#pragma unroll
-            for (int ch = 0; ch < 2; ++ch)
-#pragma unroll
-                for (int pt = 0; pt < 2; ++pt) __builtin_memcpy(&kfr[t][ch][pt], &kf[t][ch][pt], 16);
-        // S^T tile by tile (tile qt's scores complete first, so its softmax can issue
-        // beside the next tiles' products; no scheduling fence after them)
-        f32x4 s[NQT][2];
-#pragma unroll
-        for (int qt = 0; qt < NQT; ++qt) {
-            s[qt][0] = s[qt][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int ch = 0; ch < 2; ++ch)
-#pragma unroll
-                for (int p = 0; p < 3; ++p)
-#pragma unroll
-                    for (int t = 0; t < 2; ++t)
-                        s[qt][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                            kfr[t][ch][p == 1], p == 2 ? ql[qt][ch] : qh[qt][ch], s[qt][t], 0, 0, 0);
-        }
-        uint2 vt2[4][2][2];
-        asm volatile(
-            "ds_read_b64_tr_b16 %0, %16\n\tds_read_b64_tr_b16 %1, %17\n\t"
-            "ds_read_b64_tr_b16 %2, %18\n\tds_read_b64_tr_b16 %3, %19\n\t"
-            "ds_read_b64_tr_b16 %4, %20\n\tds_read_b64_tr_b16 %5, %21\n\t"
-            "ds_read_b64_tr_b16 %6, %22\n\tds_read_b64_tr_b16 %7, %23\n\t"
-            "ds_read_b64_tr_b16 %8, %24\n\tds_read_b64_tr_b16 %9, %25\n\t"
-            "ds_read_b64_tr_b16 %10, %26\n\tds_read_b64_tr_b16 %11, %27\n\t"
-            "ds_read_b64_tr_b16 %12, %28\n\tds_read_b64_tr_b16 %13, %29\n\t"
-            "ds_read_b64_tr_b16 %14, %30\n\tds_read_b64_tr_b16 %15, %31\n\ts_waitcnt lgkmcnt(0)"
-            : "=&v"(vt2[0][0][0]), "=&v"(vt2[0][0][1]), "=&v"(vt2[0][1][0]), "=&v"(vt2[0][1][1]),
-              "=&v"(vt2[1][0][0]), "=&v"(vt2[1][0][1]), "=&v"(vt2[1][1][0]), "=&v"(vt2[1][1][1]),
-              "=&v"(vt2[2][0][0]), "=&v"(vt2[2][0][1]), "=&v"(vt2[2][1][0]), "=&v"(vt2[2][1][1]),
-              "=&v"(vt2[3][0][0]), "=&v"(vt2[3][0][1]), "=&v"(vt2[3][1][0]), "=&v"(vt2[3][1][1])
-            : "v"(va[0][0][0] + boff), "v"(va[0][0][1] + boff), "v"(va[0][1][0] + boff),
-              "v"(va[0][1][1] + boff), "v"(va[1][0][0] + boff), "v"(va[1][0][1] + boff),
-              "v"(va[1][1][0] + boff), "v"(va[1][1][1] + boff), "v"(va[2][0][0] + boff),
-              "v"(va[2][0][1] + boff), "v"(va[2][1][0] + boff), "v"(va[2][1][1] + boff),
-              "v"(va[3][0][0] + boff), "v"(va[3][0][1] + boff), "v"(va[3][1][0] + boff),
-              "v"(va[3][1][1] + boff)
-            : "memory");
-        const int key0 = ci * AW_KC;
-        const bool full = key0 + AW_KC <= n;  // (uniform) no masked key in this chunk
-        bf16x8 ph[NQT], pl[NQT];
-#pragma unroll
-        for (int qt = 0; qt < NQT; ++qt) {
-            float v[8];
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-                const int key = key0 + 8 * g + e;  // (t = e >> 2, r = e & 3)
-                v[e] = (full || key < n) ? s[qt][e >> 2][e & 3] : -INFINITY;
-            }
-            const float lmax = fmaxf(fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3])),
-                                     fmaxf(fmaxf(v[4], v[5]), fmaxf(v[6], v[7])));
-            // lazy max: the reference max moves only when a score passes it by 8 / sc
-            // (always at the first chunk: lim = -inf, key 0 is valid)
-            if (__any(lmax > lim[qt])) {
-                float cmax = lmax;
-                const auto p16 = __builtin_amdgcn_permlane16_swap(
-                    __float_as_uint(cmax), __float_as_uint(cmax), false, false);
-                cmax = fmaxf(__uint_as_float(p16[0]), __uint_as_float(p16[1]));
-                const auto p32 = __builtin_amdgcn_permlane32_swap(
-                    __float_as_uint(cmax), __float_as_uint(cmax), false, false);
-                cmax = fmaxf(__uint_as_float(p32[0]), __uint_as_float(p32[1]));
-                const float m_new = fmaxf(m[qt], cmax);
-                if (m_new != m[qt]) {
-                    const float alpha = __builtin_amdgcn_exp2f((m[qt] - m_new) * sc);
-                    lsum[qt] *= alpha;
-#pragma unroll
-                    for (int dt = 0; dt < 4; ++dt) o[qt][dt] *= alpha;
-                }
-                m[qt] = m_new;
-                lim[qt] = m_new + 8.0f / sc;
-                mneg[qt] = -m_new * sc;
-            }
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-                const float pr = __builtin_amdgcn_exp2f(fmaf(v[e], sc, mneg[qt]));
-                lsum[qt] += pr;
-                ph[qt][e] = split_hi(pr);
-                pl[qt][e] = split_lo(pr);
-            }
-        }
-        bf16x8 vfr[4][2];
-#pragma unroll
-        for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-            for (int pt = 0; pt < 2; ++pt) {
-                const uint4 v4 = make_uint4(vt2[dt][pt][0].x, vt2[dt][pt][0].y, vt2[dt][pt][1].x,
-                                            vt2[dt][pt][1].y);
-                __builtin_memcpy(&vfr[dt][pt], &v4, 16);
-            }
-#pragma unroll
-        for (int p = 0; p < 3; ++p)
-#pragma unroll
-            for (int qt = 0; qt < NQT; ++qt)
-#pragma unroll
-                for (int dt = 0; dt < 4; ++dt)
-                    o[qt][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                        vfr[dt][p == 1], p == 2 ? pl[qt] : ph[qt], o[qt][dt], 0, 0, 0);
-    }
-    // context rows: O / row sum, split; buffer stores over the group's rows [q0 + g0,
-    // q0 + nq) -- a query past them falls outside the range and is dropped
-    const uint64_t pa = reinterpret_cast<uint64_t>(ctx + (int64_t)(G.q0 + G.g0) * 2 * H);
-    const uint32_t lo32 = __builtin_amdgcn_readfirstlane((uint32_t)pa);
-    const uint32_t hi32 = __builtin_amdgcn_readfirstlane((uint32_t)(pa >> 32));
-    void *sbase = reinterpret_cast<void *>(((uint64_t)hi32 << 32) | lo32);
-    const int rows = __builtin_amdgcn_readfirstlane(G.nq - G.g0);
-    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(sbase, (short)0, rows * 2 * H * 2, 0x00020000);
-#pragma unroll
-    for (int qt = 0; qt < NQT; ++qt) {
-        float l = lsum[qt];
-        l += __shfl_xor(l, 16, 64);
-        l += __shfl_xor(l, 32, 64);
-        const float inv = 1.0f / l;
-        const int qr = 16 * qt + c;  // row within the group
-#pragma unroll
-        for (int dt = 0; dt < 4; ++dt) {
-            typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-            u32x2 hv, lv;
-            bf16x4 h4, l4;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const float y = o[qt][dt][r] * inv;
-                h4[r] = split_hi(y);
-                l4[r] = split_lo(y);
-            }
-            __builtin_memcpy(&hv, &h4, 8);
-            __builtin_memcpy(&lv, &l4, 8);
-            const int off = (qr * 2 * H + (int)split_col(G.h * ATT_D + dt * 16 + 4 * g)) * 2;
-            __builtin_amdgcn_raw_buffer_store_b64(hv, rsrc, off, 0, 0);
-            __builtin_amdgcn_raw_buffer_store_b64(lv, rsrc, off + 64, 0, 0);
-        }
-    }
-}
-
-__global__ void __launch_bounds__(64 * AW_WAVES) __attribute__((amdgpu_waves_per_eu(1)))
-attention_x3w_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu_seqlens, int H,
-                     int n_heads, int n_pairs, bf16 *__restrict__ ctx_split,
-                     const int32_t *__restrict__ qsel, const int32_t *__restrict__ cu_qsel) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int64_t ld = 6 * (int64_t)H;
-    unsigned char *lds_w = lds + wave * AW_WAVE_LDS;
-    const uint32_t wbase =
-        (uint32_t)(uintptr_t)((__attribute__((address_space(3))) unsigned char *)lds_w);
-    const int stride = (int)gridDim.x * AW_WAVES;
-    const int first_pr = (int)blockIdx.x * AW_WAVES + wave;
-    AwGroup G, NX;
-    G.pr = -1;
-    if (!aw_next(G, first_pr, stride, n_pairs, n_heads, cu_seqlens, qsel, cu_qsel, G)) return;
-    bf16x8 qa[AW_QT][2], qb[AW_QT][2], qna[AW_QT][2], qnb[AW_QT][2];
-    aw_load_q(qkv, ld, G, qsel, lane, qa, qb);
-    aw_stage(qkv, ld, H, G, 0, 0, lds_w, lane);
-    int b0 = 0, prev_stores = 0;
-    for (;;) {
-        const bool has_next = aw_next(G, first_pr, stride, n_pairs, n_heads, cu_seqlens, qsel,
-                                      cu_qsel, NX);
-        switch (G.tiles) {
-        case 1: aw_group<1>(qkv, ld, H, G, b0, has_next, NX, qsel, ctx_split, lds_w, wbase, lane, qa, qb, qna, qnb, prev_stores); break;
-        case 2: aw_group<2>(qkv, ld, H, G, b0, has_next, NX, qsel, ctx_split, lds_w, wbase, lane, qa, qb, qna, qnb, prev_stores); break;
-        case 3: aw_group<3>(qkv, ld, H, G, b0, has_next, NX, qsel, ctx_split, lds_w, wbase, lane, qa, qb, qna, qnb, prev_stores); break;
-        default: aw_group<4>(qkv, ld, H, G, b0, has_next, NX, qsel, ctx_split, lds_w, wbase, lane, qa, qb, qna, qnb, prev_stores); break;
-        }
-        if (!has_next) break;
-        prev_stores = G.tiles * AW_STORES;
-        b0 = (b0 + (G.n + AW_KC - 1) / AW_KC) & 1;
-        G = NX;
-#pragma unroll
-        for (int qt = 0; qt < AW_QT; ++qt)
-#pragma unroll
-            for (int ch = 0; ch < 2; ++ch) {
-                qa[qt][ch] = qna[qt][ch];
-                qb[qt][ch] = qnb[qt][ch];
-            }
-    }
-}
-
 void launch_attention_x3(const bf16 *qkv, const int32_t *cu_seqlens, int n_docs, int H,
                          bf16 *ctx_split, hipStream_t s, const int32_t *qsel,
                          const int32_t *cu_qsel) {
@@ -1217,22 +856,9 @@ void launch_attention_x3(const bf16 *qkv, const int32_t *cu_seqlens, int n_docs,
     // interleave
     static const int variant = [] {
         const char *e = getenv("DI_ATTN_X3");
-        return e ? atoi(e) & 124 : 28;
+        return e ? atoi(e) & 60 : 28;
     }();
-    if (variant & 64) {  // the per-wave form (attention_x3w_kernel)
-        static bool attr = false;
-        if (!attr) {
-            DI_HIP(hipFuncSetAttribute((const void *)attention_x3w_kernel,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, AW_LDS));
-            attr = true;
-        }
-        hipLaunchKernelGGL(attention_x3w_kernel,
-                           dim3((int)std::min<int64_t>((n_pairs + AW_WAVES - 1) / AW_WAVES, n_cu())),
-                           dim3(64 * AW_WAVES), AW_LDS, s, qkv, cu_seqlens, H, n_heads,
-                           (int)n_pairs, ctx_split, qsel, cu_qsel);
-        check_launch("attention_x3w");
-        return;
-    }
+
     static const int abl = [] {
         const char *e = getenv("DI_ATTN_X3_ABLATE");
         return e ? atoi(e) : 0;
