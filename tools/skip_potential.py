@@ -40,7 +40,7 @@ def main():
     bd = min(32768, ((n_docs + nb - 1) // nb + 63) // 64 * 64)
     seg = (bd + 15) // 16
     n_seg = nb * 16
-    skip = tot = 0
+    skip = tot = bskip = 0
     touched_frac = []
     for q, r in zip(queries, res):
         if len(r) < k:
@@ -56,6 +56,14 @@ def main():
             bound += mx
         skip += int((bound < T).sum())
         tot += n_seg
+        # whole blocks: sum over the terms of the term's largest value in the block
+        bb = np.zeros(nb, np.int64)
+        for t in q:
+            a, b = term_off[t], term_off[t + 1]
+            mx = np.zeros(nb, np.int64)
+            np.maximum.at(mx, pdoc[a:b].astype(np.int64) // bd, pval[a:b].astype(np.int64))
+            bb += mx
+        bskip += int((bb < T).sum())
         touched_frac.append(float(np.mean(bound > 0)))
     post = float(np.mean([sum(int(term_off[t + 1] - term_off[t]) for t in q) for q in queries]))
     print(json.dumps({"n_docs": n_docs, "collection": "skewed (SKEW_CONFIG4)" if skew else "iid (§8d)",
@@ -63,6 +71,7 @@ def main():
                       "postings": int(len(pdoc)), "postings_per_query": post,
                       "segment_docs": seg, "segments": n_seg,
                       "skippable_segment_fraction": skip / max(tot, 1),
+                      "skippable_block_fraction": bskip / max(tot // 16, 1),
                       "segments_with_any_posting": float(np.mean(touched_frac)),
                       "max_impact": m}))
 
