@@ -787,10 +787,8 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
     static_assert(QH_BINS == 4 * SC_THREADS && QH_BINS <= HIST_BINS, "qhist prefetch");
     if (qpre) {
         typedef __attribute__((address_space(3))) void lds_void;
-        // (sc1, agent scope: past this CU's L1, whose copy of the bins may predate the
-        // atomics that this workgroup's own previous item of the query made at L2)
         __builtin_amdgcn_global_load_lds((const void *)(qh + 4 * tid),
-                                         (lds_void *)(sh.u.hist + wave * 256), 16, 0, 16);
+                                         (lds_void *)(sh.u.hist + wave * 256), 16, 0, 0);
     }
     // zeroing of the accumulators (and the fast path's histogram): LDS stores only,
     // placed where the setup's global loads are in flight
@@ -1555,8 +1553,7 @@ score_blocks_kernel(const uint32_t *__restrict__ post, SubIndex si, int min_cls,
                     int n_q, uint32_t *__restrict__ qhist, int ablate,
                     const ItemRec *__restrict__ rec, uint32_t *__restrict__ long_flag,
                     float bm_factor, unsigned long long *__restrict__ bm_stat,
-                    const uint16_t *__restrict__ border, uint32_t *__restrict__ qtq,
-                    int qseq) {
+                    const uint16_t *__restrict__ border, uint32_t *__restrict__ qtq) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     ScoreShared &sh = *reinterpret_cast<ScoreShared *>(smem);
     if ((uint32_t)(uintptr_t)((__attribute__((address_space(3))) unsigned char *)smem) != 0) {
@@ -1567,24 +1564,9 @@ score_blocks_kernel(const uint32_t *__restrict__ post, SubIndex si, int min_cls,
         return;
     }
     if (EXT != 0 && threadIdx.x == 0) sh.bm_cnt[0] = sh.bm_cnt[1] = 0ull;  // (the first item's barriers publish it)
-    // items block-major: item = b * n_q + q (the shared threshold, see score_item).
-    // Query-sequential (qseq): a workgroup takes all nb blocks of a query in turn, so
-    // each later block reads the threshold its own earlier blocks left; the queries past
-    // the last whole round of gridDim.x go block-major (no tail of whole queries).
-    const int G = gridDim.x;
-    const int q_seq = qseq ? n_q / G * G : 0;
-    for (int it = 0;; ++it) {
-        int q, r_;
-        if (it < q_seq / G * nb) {
-            q = it / nb * G + (int)blockIdx.x;
-            r_ = it % nb;
-        } else {
-            const int rest = (int)blockIdx.x + (it - q_seq / G * nb) * G;
-            if (rest >= (n_q - q_seq) * nb) break;
-            q = q_seq + rest % (n_q - q_seq);
-            r_ = rest / (n_q - q_seq);
-        }
-        const int item = r_ * n_q + q;
+    // items block-major: item = b * n_q + q (the shared threshold, see score_item)
+    for (int item = blockIdx.x; item < n_items; item += gridDim.x) {
+        const int q = item % n_q, r_ = item / n_q;
         score_item<EXT>(sh, q, EXT != 0 && border ? (int)border[(int64_t)q * nb + r_] : r_, post, si,
                    min_cls, nb,
                    block_docs, n_terms,
@@ -1921,7 +1903,6 @@ struct di_index {
     // per-query threshold shared across blocks: -1 = auto (on from 8 blocks: at 4 blocks it
     // measured 2.31 vs 2.14 ms per 6980-query batch, at 34 / 269 blocks 16.9 vs 19.5 and
     // 130 vs 161 ms, merge 0.5 vs 7.1 and 1.4 vs 74 ms); DI_SCORE_THRESHOLD=0 / 1 forces
-    // it off / on (block-major items), 2 on with query-sequential items (score_blocks_kernel)
     int shared_thr = -1;
     int ablate = 0;  // DI_PROFILE_ABLATE: profiling only (1 no scatter, 2 no selection, 4 stop at the k-th score)
     Timer timer;
@@ -2309,7 +2290,7 @@ int di_index_create(const int64_t *term_off, int64_t n_terms, const uint32_t *pd
         enable_big_lds();
         if (const char *ab = std::getenv("DI_PROFILE_ABLATE")) ix->ablate = std::atoi(ab);
         if (const char *st = std::getenv("DI_SCORE_THRESHOLD"))  // (tested both ways)
-            ix->shared_thr = st[0] == '0' ? 0 : st[0] == '2' ? 2 : 1;
+            ix->shared_thr = st[0] != '0' ? 1 : 0;
         build_index(ix.get(), term_off, n_terms, pdoc, pval, doc_lo, doc_hi);
         *out = ix.release();
     });
@@ -2491,8 +2472,7 @@ int di_index_search(di_index *ix, const uint32_t *q_terms, const int32_t *cu_q, 
             if (ix->nb == 0) {
                 DI_HIP(hipMemsetAsync(ix->ws_cn.p, 0, (size_t)nq * nb * 4, s));
             } else {
-                const bool thr = nb > 1 && (ix->shared_thr < 0 ? nb >= 8 : ix->shared_thr >= 1);
-                const bool qseq = thr && ix->shared_thr == 2;
+                const bool thr = nb > 1 && (ix->shared_thr < 0 ? nb >= 8 : ix->shared_thr == 1);
                 if (thr) DI_HIP(hipMemsetAsync(ix->ws_thr.p, 0, (size_t)nq * QH_BINS * 4, s));
                 DI_HIP(hipMemsetAsync(ix->ws_long.p, 0, 4, s));
                 TimedLaunch tl(ix->timer, timing, "score_blocks", s);  // (both kernels)
@@ -2537,8 +2517,7 @@ int di_index_search(di_index *ix, const uint32_t *q_terms, const int32_t *cu_q, 
                                    use_rec ? ix->ws_rec.as<ItemRec>() : nullptr,
                                    ix->ws_long.as<uint32_t>(), thr ? ix->bm_factor : 0.0f,
                                    ix->bm_stat.as<unsigned long long>(), border,
-                                   use_qtq ? ix->ws_tq.as<uint32_t>() : nullptr,
-                                   (int)qseq);
+                                   use_qtq ? ix->ws_tq.as<uint32_t>() : nullptr);
                 check_launch("score_blocks");
                 hipLaunchKernelGGL(score_long_kernel, dim3(std::min(n_items, n_cu())),
                                    dim3(SC_THREADS), sizeof(ScoreShared), s,

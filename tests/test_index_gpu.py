@@ -313,13 +313,6 @@ def test_shared_threshold_off_equals_oracle(L, synth, monkeypatch):
     assert on.search(qs, 1000) == want
     assert on.search(qs, 7) == ora.score_ids(qs, 7, n_threads=8)
     assert on.search(qs, 1) == ora.score_ids(qs, 1, n_threads=8)
-    # query-sequential items (a workgroup takes a query's blocks in turn; 5000 queries:
-    # whole rounds of the grid plus a block-major rest)
-    monkeypatch.setenv("DI_SCORE_THRESHOLD", "2")
-    seq = L.DeviceIndex.from_postings(term_off, pdoc, pval)
-    assert seq.search(qs, 1000) == want
-    assert seq.search(qs, 7) == ora.score_ids(qs, 7, n_threads=8)
-    assert seq.search(qs[:300], 1000) == want[:300]
 
 
 def test_in_kernel_setup_fallback_equals_oracle(L, synth, monkeypatch):
