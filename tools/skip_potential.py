@@ -41,12 +41,14 @@ def main():
     seg = (bd + 15) // 16
     n_seg = nb * 16
     skip = tot = bskip = 0
+    p_skip = p_tot = 0
     touched_frac = []
     for q, r in zip(queries, res):
         if len(r) < k:
             continue
         T = r[-1][1]
         bound = np.zeros(n_seg, np.int64)
+        cnt = np.zeros(n_seg, np.int64)
         for t in q:
             a, b = term_off[t], term_off[t + 1]
             d = pdoc[a:b].astype(np.int64)
@@ -54,8 +56,11 @@ def main():
             mx = np.zeros(n_seg, np.int64)
             np.maximum.at(mx, s_id, pval[a:b].astype(np.int64))
             bound += mx
+            cnt += np.bincount(s_id, minlength=n_seg)
         skip += int((bound < T).sum())
         tot += n_seg
+        p_skip += int(cnt[bound < T].sum())
+        p_tot += int(cnt.sum())
         # whole blocks: sum over the terms of the term's largest value in the block
         bb = np.zeros(nb, np.int64)
         for t in q:
@@ -71,6 +76,7 @@ def main():
                       "postings": int(len(pdoc)), "postings_per_query": post,
                       "segment_docs": seg, "segments": n_seg,
                       "skippable_segment_fraction": skip / max(tot, 1),
+                      "skippable_posting_fraction": p_skip / max(p_tot, 1),
                       "skippable_block_fraction": bskip / max(tot // 16, 1),
                       "segments_with_any_posting": float(np.mean(touched_frac)),
                       "max_impact": m}))
