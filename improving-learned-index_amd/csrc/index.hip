@@ -2503,7 +2503,9 @@ int di_index_search(di_index *ix, const uint32_t *q_terms, const int32_t *cu_q, 
                                        ix->ws_rec.as<ItemRec>(), border);
                     check_launch("item_setup");
                 }
-                const bool ext = pk || order || (thr && ix->bm_factor > 0.0f);
+                // (DI_PROFILE_ABLATE bit 65536: the block-max instantiation with block-max
+                // off, A/B of its code alone)
+                const bool ext = pk || order || (thr && ix->bm_factor > 0.0f) || (ix->ablate & 65536);
                 hipLaunchKernelGGL(pk    ? score_blocks_kernel<EXT_PK>
                                    : ext ? score_blocks_kernel<EXT_BM>
                                          : score_blocks_kernel<0>,
