@@ -97,6 +97,8 @@ struct ScoreShared {
     unsigned long long bm_cnt[2];  // block-max statistics of the workgroup (thread 0)
     uint32_t tqe;                  // block-max: the query's running threshold (qtq) as
                                    // thread 0 read it -- one value for every wave
+    uint32_t tqn;                  // EXT: a lower bound of the query's k-th score this item
+                                   // found (thread 0), raised into qtq after the item
     uint32_t wub[WSEG];            // block-max: each wave segment's score upper bound
     uint32_t wtab[WTERMS][WSEG];   // their per-wave runs: start << 16 | end (in the sublist)
 };
@@ -204,8 +206,12 @@ __device__ __forceinline__ bool wave_append(bool take, uint32_t *cursor, uint32_
     const int leader = __builtin_ctzll(m);
     uint32_t base = 0;
     if (lane == leader) base = atomicAdd(cursor, (uint32_t)__builtin_popcountll(m));
-    base = __shfl(base, leader, 64);
-    pos = base + (uint32_t)__builtin_popcountll(m & ((1ull << lane) - 1ull));
+    // (v_readlane with the uniform leader, and the lanes below by v_mbcnt: no LDS
+    // permute and no lane mask held in registers -- a held 64-bit mask was spilled and
+    // reloaded per sweep step in the block-max instantiation)
+    base = (uint32_t)__builtin_amdgcn_readlane((int)base, leader);
+    pos = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                           __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
     return take;
 }
 
@@ -880,7 +886,7 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
         }
         zero();
     }
-    if (bm && qtq && tid == 0) sh.tqe = tq_early;
+    if (EXT != 0 && tid == 0) sh.tqe = tq_early;
     __syncthreads();
     if (sh.bad) {
         // (the histogram copy lands before the next item touches the histogram)
@@ -1225,7 +1231,7 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
         }
         __syncthreads();
         Tq = sh.tq;
-        if (EXT != 0 && qtq && tid == 0 && Tq > tq_early) atomicMax(&qtq[q], Tq);
+        if (EXT != 0 && tid == 0) sh.tqn = max(sh.tqn, Tq);
         stamp(8);  // threshold read (the part of tq-select before the sweep)
         // (wsum is written again only after a barrier of the selection below; tq only
         // at the next item's start)
@@ -1301,7 +1307,7 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
         }
         // (this block alone has >= k docs scoring >= T: a lower bound of the query's final
         // k-th score for block-max, qtq)
-        if (EXT != 0 && qtq && tid == 0 && sh.thr > tq_early) atomicMax(&qtq[q], sh.thr);
+        if (EXT != 0 && tid == 0) sh.tqn = max(sh.tqn, sh.thr);
         const uint32_t T = sh.thr, ties = sh.ties;  // T >= 1: every touched score is
         const uint32_t above = sh.above;             // nonzero
 
@@ -1472,7 +1478,7 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
                          });
     }
     const uint32_t T = prefix;
-    if (EXT != 0 && qtq && tid == 0 && (T >> 16) > tq_early) atomicMax(&qtq[q], T >> 16);
+    if (EXT != 0 && tid == 0) sh.tqn = max(sh.tqn, T >> 16);
     const uint32_t ties = sh.u.rs.tot[sh.u.rs.bin];
 
     // doc-order cut among the ties: the `need` smallest doc indices
@@ -1563,7 +1569,10 @@ score_blocks_kernel(const uint32_t *__restrict__ post, SubIndex si, int min_cls,
             if (threadIdx.x == 0) cand_n[item] = -1;
         return;
     }
-    if (EXT != 0 && threadIdx.x == 0) sh.bm_cnt[0] = sh.bm_cnt[1] = 0ull;  // (the first item's barriers publish it)
+    if (EXT != 0 && threadIdx.x == 0) {  // (the first item's barriers publish them)
+        sh.bm_cnt[0] = sh.bm_cnt[1] = 0ull;
+        sh.tqn = 0;
+    }
     // items block-major: item = b * n_q + q (the shared threshold, see score_item)
     for (int item = blockIdx.x; item < n_items; item += gridDim.x) {
         const int q = item % n_q, r_ = item / n_q;
@@ -1573,6 +1582,14 @@ score_blocks_kernel(const uint32_t *__restrict__ post, SubIndex si, int min_cls,
                    n_docs, doc_lo, q_terms, cu_q, k, cand_key, cand_n, qhist, ablate,
                    rec ? rec + (int64_t)item * WTERMS : nullptr, long_flag, bm_factor, qtq);
         __syncthreads();  // every wave is done with the LDS of this item
+        // the item's threshold into the query's running one, here rather than inside the
+        // selection: qtq and the value read at the item's start need no registers across
+        // the scatter (they cost the instantiation spills)
+        if (EXT != 0 && threadIdx.x == 0) {
+            const uint32_t t = sh.tqn;
+            if (qtq && t > sh.tqe) atomicMax(&qtq[q], t);
+            sh.tqn = 0;
+        }
     }
     if (EXT != 0 && bm_stat && threadIdx.x == 0 && sh.bm_cnt[0]) {
         atomicAdd(&bm_stat[0], sh.bm_cnt[0]);
