@@ -952,14 +952,14 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
             tq0 = read_tq();
         }
         const float thr = bm_factor * (float)tq0;
-        skip_wave = tq0 > 0 && (float)sh.wub[wave] < thr;
+        skip_wave = tq0 > 0 && (float)sh.wub[wave] < thr && !(ablate & 131072);  // (bit 131072: no skips, A/B)
         // every segment below: lanes 0..15 of each wave check one each (no block
         // reduction: __syncthreads_and would take static LDS, and the scatter needs the
         // dynamic segment at address 0)
         static_assert(WSEG <= 64, "one lane per segment");
         const bool below = lane >= WSEG || (tq0 > 0 && (float)sh.wub[lane] < thr);
         const uint64_t below_m = __ballot(below);
-        const bool all_below = below_m == ~0ull;
+        const bool all_below = below_m == ~0ull && !(ablate & 131072);
         live16 = (uint32_t)~below_m & 0xFFFFu;
         // skip statistics (di_index_timing "bm_segments" / "bm_segments_skipped"): every
         // evaluated item counts its WSEG segments, every skipped segment one -- in the

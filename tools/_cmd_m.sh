@@ -10,7 +10,8 @@ run() {  # name ablate args...
   echo "$n: $(tail -1 $O/$n.txt)"; grep "phase cycles" $O/$n.txt | tail -1
 }
 run skew_exh_ext 65600 skew 0
-run skew_bm0001_noorder 16448 skew 0.001
+run skew_exh 64 skew 0
+run skew_bm1_noskip_noorder 147520 skew 1
 run skew_bm1_noorder 16448 skew 1
-run skew_bm0001_order 64 skew 0.001
+run skew_bm1_noskip_order 131136 skew 1
 run skew_bm1_order 64 skew 1
