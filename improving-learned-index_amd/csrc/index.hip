@@ -97,10 +97,11 @@ struct ScoreShared {
     unsigned long long bm_cnt[2];  // block-max statistics of the workgroup (thread 0)
     uint32_t tqe;                  // block-max: the query's running threshold (qtq) as
                                    // thread 0 read it -- one value for every wave
-    uint32_t tqn;                  // EXT: a lower bound of the query's k-th score this item
-                                   // found (thread 0), raised into qtq after the item
     uint32_t wub[WSEG];            // block-max: each wave segment's score upper bound
     uint32_t wtab[WTERMS][WSEG];   // their per-wave runs: start << 16 | end (in the sublist)
+    uint32_t tqn;                  // EXT: a lower bound of the query's k-th score this item
+                                   // found (thread 0), raised into qtq after the item
+                                   // (last: the fields above keep their alignment)
 };
 static_assert(offsetof(ScoreShared, acc) == 0, "accumulators at LDS address 0");
 static_assert(sizeof(ScoreShared().acc) >= LH_DOCS * sizeof(uint64_t), "half-block words fit");
@@ -199,6 +200,11 @@ __device__ __forceinline__ uint32_t compact_words(ScoreShared &sh, int n_local, 
 
 // Wave-aggregated append: lanes with `take` get consecutive slots of *cursor (one
 // LDS atomic per wave and call).  Call from wave-uniform control flow.
+// MB: the leader's base by v_readlane and the lanes below by v_mbcnt -- no LDS permute
+// and no lane mask held in registers (the block-max instantiation spilled a held 64-bit
+// mask and reloaded it per sweep step: 74 -> 8 scratch loads, its sweep 2x faster); the
+// plain scorer keeps the permute form (measured 2.06 vs 2.09 ms per 100 k-doc launch).
+template <bool MB = false>
 __device__ __forceinline__ bool wave_append(bool take, uint32_t *cursor, uint32_t &pos) {
     const uint64_t m = __ballot(take);
     if (m == 0) return false;
@@ -206,12 +212,14 @@ __device__ __forceinline__ bool wave_append(bool take, uint32_t *cursor, uint32_
     const int leader = __builtin_ctzll(m);
     uint32_t base = 0;
     if (lane == leader) base = atomicAdd(cursor, (uint32_t)__builtin_popcountll(m));
-    // (v_readlane with the uniform leader, and the lanes below by v_mbcnt: no LDS
-    // permute and no lane mask held in registers -- a held 64-bit mask was spilled and
-    // reloaded per sweep step in the block-max instantiation)
-    base = (uint32_t)__builtin_amdgcn_readlane((int)base, leader);
-    pos = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                           __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    if constexpr (MB) {
+        base = (uint32_t)__builtin_amdgcn_readlane((int)base, leader);
+        pos = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                               __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    } else {
+        base = __shfl(base, leader, 64);
+        pos = base + (uint32_t)__builtin_popcountll(m & ((1ull << lane) - 1ull));
+    }
     return take;
 }
 
@@ -1241,7 +1249,7 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
             const uint32_t thr_w = Tq << 16;
             sweep_words(sh.acc, n_local, tid, [&](uint32_t w, int idx) {
                 uint32_t pos;
-                if (wave_append(w >= thr_w, &sh.emit, pos)) cand(pos, w, idx);
+                if (wave_append<EXT != 0>(w >= thr_w, &sh.emit, pos)) cand(pos, w, idx);
             });
             __syncthreads();
             const uint32_t na = sh.emit;
@@ -1430,7 +1438,7 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
                     const uint32_t i = i0 + tid;
                     const uint32_t x = i < ties ? tl[i] : 0u;
                     uint32_t pos;
-                    if (wave_append(i < ties && x >= tp, &sh.emit, pos))
+                    if (wave_append<EXT != 0>(i < ties && x >= tp, &sh.emit, pos))
                         cand(pos, (T << 16) | (x >> 16), (int)(0xFFFFu - (x & 0xFFFFu)));
                 }
                 __syncthreads();
