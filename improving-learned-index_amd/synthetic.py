@@ -77,7 +77,7 @@ def msmarco_like_queries(n_q, v_terms=200_000, seed=1234, draws=6):
 # holds a high value of every frequent query term, so exact block-max can skip nothing,
 # DESIGN.md §3).  Impacts: frequent terms small (term factor ((t + 1) / 2000)^0.5 up to
 # rank 2000: the IDF-like shape of a learned impact model), and a heavy-tailed doc mass
-# shared by clusters of 512 consecutive doc ids (passages of one source document)
+# shared by clusters of 4096 consecutive doc ids (passages of one source document)
 # times a per-doc factor, clipped at 6.
 SKEW_CONFIG4 = {"term_rank0": 2000.0, "term_exp": 0.5, "cluster_docs": 4096,
                 "cluster_sigma": 1.2, "doc_sigma": 0.5, "mass_max": 6.0}
