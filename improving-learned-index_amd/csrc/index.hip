@@ -1929,6 +1929,7 @@ struct di_index {
     // measured 2.31 vs 2.14 ms per 6980-query batch, at 34 / 269 blocks 16.9 vs 19.5 and
     // 130 vs 161 ms, merge 0.5 vs 7.1 and 1.4 vs 74 ms); DI_SCORE_THRESHOLD=0 / 1 forces
     int shared_thr = -1;
+    bool block_order = false;  // DI_BLOCK_ORDER=1: block-max items in per-query bound order
     int ablate = 0;  // DI_PROFILE_ABLATE: profiling only (1 no scatter, 2 no selection, 4 stop at the k-th score)
     Timer timer;
 
@@ -2314,6 +2315,7 @@ int di_index_create(const int64_t *term_off, int64_t n_terms, const uint32_t *pd
         ix->own_stream = true;
         enable_big_lds();
         if (const char *ab = std::getenv("DI_PROFILE_ABLATE")) ix->ablate = std::atoi(ab);
+        if (const char *bo = std::getenv("DI_BLOCK_ORDER")) ix->block_order = bo[0] == '1';
         if (const char *st = std::getenv("DI_SCORE_THRESHOLD"))  // (tested both ways)
             ix->shared_thr = st[0] != '0' ? 1 : 0;
         build_index(ix.get(), term_off, n_terms, pdoc, pval, doc_lo, doc_hi);
@@ -2504,10 +2506,12 @@ int di_index_search(di_index *ix, const uint32_t *q_terms, const int32_t *cu_q, 
                 const int n_items = nq * nb;
                 // packed postings (configs[4]): exact scoring from the item records only
                 const bool pk = ix->packed && ix->pk_built && ix->min_cls >= 7 && use_rec;
-                // block-max: blocks in descending order of their bound per query
-                // (DI_PROFILE_ABLATE bit 16384: block order, A/B)
+                // block-max: blocks in descending order of their bound per query, opt-in
+                // (DI_BLOCK_ORDER=1): it raises the running threshold sooner but gives up
+                // the block-major L2 sharing of the popular sublists -- at 8.8 M docs, f = 1:
+                // skewed 79.4 vs 76.7 ms per batch, i.i.d. 126.0 vs 114.2 (round-4 DESIGN §4)
                 const bool order = thr && ix->bm_factor > 0.0f && nb > 1 &&
-                                   nb <= BO_MAX_BLOCKS && !(ix->ablate & 16384);
+                                   nb <= BO_MAX_BLOCKS && ix->block_order;
                 if (order) {
                     ix->ws_border.reserve((size_t)nq * nb * 2);
                     hipLaunchKernelGGL(block_order_kernel, dim3(nq), dim3(256), 0, s, ix->sub(),
