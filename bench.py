@@ -81,7 +81,8 @@ def load_pmc_traffic(name, leg=None):
             d = json.loads(p.read_text())
         except Exception:
             continue
-        k = d.get("kernels", {}).get(name)
+        ks = d.get("kernels", {})
+        k = ks.get(name) or ks.get(name.split("<")[0])  # (summaries before the template split)
         if k and k.get("hbm_bytes_per_launch"):
             return k["hbm_bytes_per_launch"], p.name
     return None, None
@@ -91,7 +92,8 @@ def load_pmc_counters(name, leg):
     """(counter dict, file name) of kernel `name` in the leg's newest PMC summary."""
     for p in sorted((ROOT / "profiles").glob(f"*pmc_{leg}.json"), reverse=True):
         try:
-            k = json.loads(p.read_text()).get("kernels", {}).get(name)
+            ks = json.loads(p.read_text()).get("kernels", {})
+            k = ks.get(name) or ks.get(name.split("<")[0])
         except Exception:
             continue
         if k:
@@ -223,11 +225,11 @@ def retrieve_leg(args, rank, world, dev, n_docs=DOCS_PER_SHARD, check_queries=20
     # leg's own summary, per launch -> per step
     leg = {DOCS_PER_SHARD: "retrieve", 1_100_000: "retrieve_shard",
            8_800_000: "retrieve_full"}.get(n_docs)
-    traffic, src = load_pmc_traffic("score_blocks_kernel", leg) if leg else (None, None)
+    traffic, src = load_pmc_traffic("score_blocks_kernel<0>", leg) if leg else (None, None)
     if traffic is not None:
         traffic *= n_sb / max(args.steps, 1)
     res["roofline"] = {
-        "kernel": "score_blocks_kernel",
+        "kernel": "score_blocks_kernel<0>",
         # priced against HBM by the algorithmic bytes, but the counters show the popular
         # lists served from L2 / MALL (PMC traffic below); the limit is the scatter's
         # posting-load instructions (a duplicated 4-byte load costs +56%, a duplicated
@@ -248,12 +250,12 @@ def retrieve_leg(args, rank, world, dev, n_docs=DOCS_PER_SHARD, check_queries=20
     # ds_write_b32 (4) per 64 postings on each CU (MI355X_MICROARCH.md "LDS" table)
     lds_peak = LDS_CUS * LDS_CLOCK_HZ / LDS_CYCLES_PER_64_POSTINGS * 64.0
     posts_per_s = post_per_launch / avg_s if avg_s > 0 else 0.0
-    lds = {"kernel": "score_blocks_kernel", "bound": "lds_rmw",
+    lds = {"kernel": "score_blocks_kernel<0>", "bound": "lds_rmw",
            "achieved": round(posts_per_s / 1e12, 4), "peak": round(lds_peak / 1e12, 4),
            "unit": "Tpostings/s", "frac": round(posts_per_s / lds_peak, 4),
            "model": f"{LDS_CYCLES_PER_64_POSTINGS:g} LDS cycles per 64 postings (ds_read_b32 2 + "
                     f"ds_write_b32 4) x {LDS_CUS} CUs x {LDS_CLOCK_HZ / 1e9:g} GHz"}
-    pmc = load_pmc_counters("score_blocks_kernel", leg) if leg else None
+    pmc = load_pmc_counters("score_blocks_kernel<0>", leg) if leg else None
     if pmc:
         for c in ("SQ_LDS_BANK_CONFLICT", "SQ_LDS_IDX_ACTIVE", "GRBM_GUI_ACTIVE"):
             if c in pmc[0]:
