@@ -36,7 +36,8 @@ class InvertedIndex:
     """
 
     def __init__(self, index_path: Union[str, Path], device: int = 0, doc_lo: int = 0,
-                 doc_hi: int = 0, min_impact: int = 1, block_max: float = 0.0):
+                 doc_hi: int = 0, min_impact: int = 1, block_max: float = 0.0,
+                 packed: bool = False):
         self.index_path = Path(index_path)
         self.vocab = self._load_vocab()
         self.device = device
@@ -44,6 +45,7 @@ class InvertedIndex:
         self._dev = DeviceIndex.from_reference_dir(self.index_path, doc_lo, doc_hi, device)
         self.set_min_impact(min_impact)
         self.set_block_max(block_max)
+        self.packed_bytes = self.set_packed(packed) if packed else 0
 
     def set_min_impact(self, min_impact: int) -> None:
         """Query-time impact pruning (config 5): score only postings of value >= the
@@ -58,6 +60,12 @@ class InvertedIndex:
         ranking); f > 1 skips those below f times it (approximate)."""
         self.block_max = float(factor)
         self._dev.set_block_max(self.block_max)
+
+    def set_packed(self, on: bool) -> int:
+        """Score from the block-compressed postings (configs[4]; built on first use,
+        exact scoring only -- DESIGN.md §3 "Packed postings").  Returns their bytes."""
+        self.packed = bool(on)
+        return self._dev.set_packed(self.packed)
 
     def _load_vocab(self):
         vocab = dict()

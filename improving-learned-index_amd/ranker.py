@@ -33,7 +33,7 @@ class Ranker:
                  qrels_path: Optional[Union[str, Path]] = None, pairwise: bool = False,
                  dataset_type: Optional[str] = COLLECTION_TYPES[0], tokenizer_path=None,
                  device: int = 0, top_k: int = 1000, batch_queries: int = 8192,
-                 min_impact: int = 1, block_max: float = 0.0):
+                 min_impact: int = 1, block_max: float = 0.0, packed: bool = False):
         # pairwise (F4): every query also scores the ordered pair terms 't1|t2' of its
         # distinct terms (ranker.py:53-58), the keys a pairwise impact collection holds
         # (deep_impact_collection.py:36-45).  The reference takes the query terms from
@@ -64,7 +64,7 @@ class Ranker:
             lo, hi = parallel.shard_range(n[0], self.world, self.rank)
         self.device = device
         self.index = InvertedIndex(index_path=index_path, device=device, doc_lo=lo, doc_hi=hi,
-                                   min_impact=min_impact, block_max=block_max)
+                                   min_impact=min_impact, block_max=block_max, packed=packed)
         self.run_file = RunFile(run_file_path=output_path) if self.rank == 0 else None
         self.top_k = top_k
         self.batch_queries = batch_queries
@@ -124,6 +124,8 @@ def main(argv=None):
     p.add_argument("--block_max", type=float, default=0.0,
                    help="block-max skipping: 0 off, 1 exact, > 1 approximate (skip block "
                         "segments whose bound is below this factor x the running k-th score)")
+    p.add_argument("--packed", action="store_true",
+                   help="score from the block-compressed postings (configs[4]; exact)")
     argv = list(sys.argv[1:] if argv is None else argv)
     a = p.parse_args(argv)
     if a.device is None:
@@ -135,7 +137,7 @@ def main(argv=None):
             return
     Ranker(a.index_path, a.queries_path, a.output_path, a.num_workers, a.qrels_path, a.pairwise,
            a.dataset_type, a.tokenizer_path, a.device or 0, top_k=a.top_k,
-           min_impact=a.min_impact, block_max=a.block_max).run()
+           min_impact=a.min_impact, block_max=a.block_max, packed=a.packed).run()
 
 
 if __name__ == "__main__":

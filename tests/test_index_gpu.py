@@ -297,6 +297,11 @@ def test_inverted_index_min_impact_matches_pruned_oracle(L):
     # configs[4] knob of the drop-in (rank --block_max): factor 1 is the exact ranking
     ex = InvertedIndex(GOLDEN / "index", block_max=1.0)
     assert [[list(x) for x in g] for g in ex.score_batch(fx["queries"], 1000)] == fx["top1000"]
+    # rank --packed: the block-compressed postings, alone and with exact block-max
+    pk = InvertedIndex(GOLDEN / "index", packed=True)
+    assert [[list(x) for x in g] for g in pk.score_batch(fx["queries"], 1000)] == fx["top1000"]
+    pk.set_block_max(1.0)
+    assert [[list(x) for x in g] for g in pk.score_batch(fx["queries"], 10)] == fx["top10"]
 
 
 def test_shared_threshold_off_equals_oracle(L, synth, monkeypatch):
