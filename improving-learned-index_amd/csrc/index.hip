@@ -998,9 +998,6 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
     // A long term (per-wave layout) is scattered by each wave over its own doc segment,
     // rounds of up to 16 postings per lane: no other wave touches those docs, so a run
     // of long terms needs no barrier between its terms, only at its ends.
-    // (profiling: each wave's own scatter time, summed over the 16 waves, into phase 9)
-    const bool wstamps = (ablate & 64) && blockIdx.x == 0;
-    const uint64_t t_ws = wstamps ? __builtin_amdgcn_s_memtime() : 0;
     uint32_t pre[4];
     bool have_pre = false;
     auto is_long = [&](int j) { return wl && ((sh.lmask[j >> 5] >> (j & 31)) & 1u); };
@@ -1162,8 +1159,6 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
     // 16 B its own LDS-DMA wrote (no barrier needed to read them), their wave suffix
     // sums go to wsum -- the barrier the scatter needs anyway publishes them.
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    if (wstamps && lane == 0)
-        atomicAdd(&g_sb_phase[9], (unsigned long long)(__builtin_amdgcn_s_memtime() - t_ws));
     uint32_t tq_hv[4] = {0, 0, 0, 0}, tq_c = 0, tq_sfx = 0;
     if (qpre) {
         const uint4 h = reinterpret_cast<const uint4 *>(sh.u.hist)[tid];
@@ -2586,8 +2581,8 @@ int di_index_search(di_index *ix, const uint32_t *q_terms, const int32_t *cu_q, 
             DI_HIP(hipMemcpyFromSymbol(ph, HIP_SYMBOL(g_sb_phase), sizeof ph));
             fprintf(stderr, "score_blocks phase cycles (workgroup 0, cumulative): setup %llu "
                             "scatter %llu hist %llu [count %llu] write %llu ties %llu copy %llu "
-                            "tq-select %llu [tq-read %llu] wave-mean scatter %llu\n",
-                    ph[0], ph[1], ph[2], ph[6], ph[3], ph[4], ph[5], ph[7], ph[8], ph[9] / 16);
+                            "tq-select %llu [tq-read %llu]\n",
+                    ph[0], ph[1], ph[2], ph[6], ph[3], ph[4], ph[5], ph[7], ph[8]);
         }
         if (!(flags & DI_F_ASYNC) || !dev) {
             DI_HIP(hipStreamSynchronize(s));
