@@ -1064,17 +1064,11 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
             const int64_t end = lo[j] + (se & 0xFFFFu);
             while (pos < end) {
                 const int64_t rem = end - pos;
-                if (rem > 12 * 64) {
+                if (rem > 8 * 64) {
                     uint32_t r[16];
                     scatter_load<16, 64>(post + pos, rem, lane, r, x4);
                     scatter_apply<16>(sh.acc, r, first_bits);
                     pos += 16 * 64;
-                } else if (rem > 8 * 64) {
-                    // (a 12-per-lane round: 768 slots for 513..768 postings, not 1024)
-                    uint32_t r[12];
-                    scatter_load<12, 64>(post + pos, rem, lane, r, x4);
-                    scatter_apply<12>(sh.acc, r, first_bits);
-                    pos = end;
                 } else if (rem > 4 * 64) {
                     uint32_t r[8];
                     scatter_load<8, 64>(post + pos, rem, lane, r, x4);
@@ -1099,16 +1093,11 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
             // sublist and applies the postings of its own doc segment -- no barrier
             for (int64_t pos = lo[j], end = hi[j]; pos < end;) {
                 const int64_t rem = end - pos;
-                if (rem > 12 * 64) {
+                if (rem > 8 * 64) {
                     uint32_t r[16];
                     scatter_load<16, 64>(post + pos, rem, lane, r, x4);
                     scatter_apply_own<16>(r, first_bits, wdlo, wdn, wdummy);
                     pos += 16 * 64;
-                } else if (rem > 8 * 64) {
-                    uint32_t r[12];
-                    scatter_load<12, 64>(post + pos, rem, lane, r, x4);
-                    scatter_apply_own<12>(r, first_bits, wdlo, wdn, wdummy);
-                    pos = end;
                 } else if (rem > 4 * 64) {
                     uint32_t r[8];
                     scatter_load<8, 64>(post + pos, rem, lane, r, x4);
