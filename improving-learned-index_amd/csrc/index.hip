@@ -56,7 +56,10 @@ constexpr int MAX_TERMS = DI_SHORT_QUERY_TERMS;  // query terms of the compact w
 // run every term that way (short terms: every wave reads the sublist, applies its own
 // docs); longer ones run the all-wave form, a barrier per term.
 constexpr int WSEG = SC_WAVES;
-constexpr int WLONG_MIN = 512;  // (1024 / 512 / 256 / 64: within 1%, profiles/r03j)
+constexpr int WLONG_MIN = 128;  // (1024 / 512 / 256 / 64: within 1%, profiles/r03j; 128 vs
+                                // 512 in round 4: exhaustive equal, block-max segment bounds
+                                // for more terms -- f = 1 skips 0.44 vs 0.30 of the segments
+                                // at 8.8 M skewed docs, gpurun_out/round4_h)
 constexpr int WTERMS = 64;
 // Fast selection: with at most 16 query terms every score is below 255 * 16 < 4096,
 // so one pass of a 4096-bin score histogram finds the k-th score; the docs tied at
