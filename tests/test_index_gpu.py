@@ -469,8 +469,15 @@ def test_packed_postings_equal_oracle(L, synth, k):
     assert dev.search(qs, k) == want
     dev.set_block_max(1.0)
     assert dev.search(qs, k) == want
-    dev.set_min_impact(8)  # (pruning: the plain layout serves; still every doc's full score)
+    dev.set_min_impact(8)  # (pruning: the plain layout serves -- the pruned oracle's ranking)
+    keep = pval >= 8
+    cnt = np.array([int(keep[term_off[t]:term_off[t + 1]].sum()) for t in range(len(term_off) - 1)])
+    pr = oracle.Index.__new__(oracle.Index)
+    pr.term_off = np.concatenate([[0], np.cumsum(cnt)]).astype(np.int64)
+    pr.pdoc, pr.pval, pr.n_docs = pdoc[keep], pval[keep], ora.n_docs
+    assert dev.search(qs, k) == pr.score_ids(qs, k, n_threads=8)
     dev.set_min_impact(1)
+    assert dev.search(qs, k) == want
     dev.set_packed(False)
     dev.set_block_max(0.0)
     assert dev.search(qs, k) == want
