@@ -563,10 +563,17 @@ attention_x3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
             // softmax part A of tile qt: masked raw scores, the lazy max test and the rare
             // rescale (a branch: outside the interleaved regions)
             auto soft_a = [&](int qt) {
+                // (a uniform branch: the common full sub-chunk takes the scores as they are,
+                // without 8 compares and selects per tile)
+                if (full) {
 #pragma unroll
-                for (int e = 0; e < 8; ++e) {
-                    const int key = key0 + 8 * g + e;
-                    v[qt][e] = (full || key < n) ? s[qt][e >> 2][e & 3] : -INFINITY;
+                    for (int e = 0; e < 8; ++e) v[qt][e] = s[qt][e >> 2][e & 3];
+                } else {
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) {
+                        const int key = key0 + 8 * g + e;
+                        v[qt][e] = key < n ? s[qt][e >> 2][e & 3] : -INFINITY;
+                    }
                 }
                 const float lmax = fmaxf(fmaxf(fmaxf(v[qt][0], v[qt][1]), fmaxf(v[qt][2], v[qt][3])),
                                          fmaxf(fmaxf(v[qt][4], v[qt][5]), fmaxf(v[qt][6], v[qt][7])));
