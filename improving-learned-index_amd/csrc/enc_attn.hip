@@ -517,21 +517,6 @@ attention_x3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
           "v"(va[2][0][0]), "v"(va[2][0][1]), "v"(va[2][1][0]), "v"(va[2][1][1]),                 \
           "v"(va[3][0][0]), "v"(va[3][0][1]), "v"(va[3][1][0]), "v"(va[3][1][1])                  \
         : "memory")
-#define AX_READ_VB(OFF)                                                                            \
-    do {                                                                                           \
-        typedef short v4s_ __attribute__((ext_vector_type(4)));                                    \
-        typedef short v8s_ __attribute__((ext_vector_type(8)));                                    \
-        typedef __attribute__((address_space(3))) v4s_ lds_v4s_;                                   \
-        _Pragma("unroll") for (int dt_ = 0; dt_ < 4; ++dt_)                                        \
-        _Pragma("unroll") for (int pt_ = 0; pt_ < 2; ++pt_) {                                      \
-            const v4s_ a_ = __builtin_amdgcn_ds_read_tr16_b64_v4i16(                               \
-                (lds_v4s_ *)(uintptr_t)(va[dt_][pt_][0] + (OFF)));                                 \
-            const v4s_ b_ = __builtin_amdgcn_ds_read_tr16_b64_v4i16(                               \
-                (lds_v4s_ *)(uintptr_t)(va[dt_][pt_][1] + (OFF)));                                 \
-            const v8s_ c_ = __builtin_shufflevector(a_, b_, 0, 1, 2, 3, 4, 5, 6, 7);               \
-            __builtin_memcpy(&vfr[dt_][pt_], &c_, 16);                                             \
-        }                                                                                          \
-    } while (0)
 #define AX_SEL(M)                                                                                  \
     do {                                                                                           \
         switch (b * AX_IMG + u * 8192) {                                                           \
@@ -641,11 +626,16 @@ attention_x3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
     } while (0)
             s_mfma(0);
             __builtin_amdgcn_sched_barrier(0);
-            // V^T fragments by the ds_read_b64_tr_b16 builtin: the two halves of a fragment
-            // land in adjacent registers (no 64-bit moves to assemble them) and the
-            // compiler waits for them where the O^T products first read them
-            AX_SEL(AX_READ_VB);
+            AX_SEL(AX_READ_VW);  // (their wait overlaps tile 0's products)
             __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+                for (int pt = 0; pt < 2; ++pt) {
+                    const uint4 v4 = make_uint4(vt2[dt][pt][0].x, vt2[dt][pt][0].y,
+                                                vt2[dt][pt][1].x, vt2[dt][pt][1].y);
+                    __builtin_memcpy(&vfr[dt][pt], &v4, 16);
+                }
             soft_a(0);
             __builtin_amdgcn_sched_barrier(0);
             s_mfma(1);
@@ -854,7 +844,6 @@ attention_x3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
             }
     }
 #undef AX_READ_K
-#undef AX_READ_VB
 #undef AX_READ_V
 #undef AX_READ_VW
 #undef AX_SEL
