@@ -517,17 +517,16 @@ attention_x3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
           "v"(va[2][0][0]), "v"(va[2][0][1]), "v"(va[2][1][0]), "v"(va[2][1][1]),                 \
           "v"(va[3][0][0]), "v"(va[3][0][1]), "v"(va[3][1][0]), "v"(va[3][1][1])                  \
         : "memory")
+// (b, the stage buffer, is 0 or 1 at run time; u, the sub-chunk, a constant of the
+// unrolled loop: one branch per site -- a switch over the offsets' value range compiled
+// to a chain of compares)
+static_assert(AX_IMG == 16384 && AX_KC == 64, "AX_SEL's immediate offsets");
 #define AX_SEL(M)                                                                                  \
     do {                                                                                           \
-        switch (b * AX_IMG + u * 8192) {                                                           \
-        case 0: M(0); break;                                                                       \
-        case 8192: M(8192); break;                                                                 \
-        case 16384: M(16384); break;                                                               \
-        case 24576: M(24576); break;                                                               \
-        case 32768: M(32768); break;                                                               \
-        case 40960: M(40960); break;                                                               \
-        case 49152: M(49152); break;                                                               \
-        default: M(57344); break;                                                                  \
+        if (b) {                                                                                   \
+            if (u) M(24576); else M(16384);                                                        \
+        } else {                                                                                   \
+            if (u) M(8192); else M(0);                                                             \
         }                                                                                          \
     } while (0)
             // (immediate offset: buffer b at b * AX_IMG, sub-chunk u at u * 32 rows; u is
