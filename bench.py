@@ -142,7 +142,7 @@ def retrieve_leg(args, rank, world, dev, n_docs=DOCS_PER_SHARD, check_queries=20
     out_n = torch.empty(nq, dtype=torch.int32, device="cuda")
     out_key = torch.empty(nq * k, dtype=torch.int64, device="cuda")
     ix.reserve(nq, k)
-    if world > 1:
+    if dist.is_initialized():
         g_key = torch.empty(world * nq * k, dtype=torch.int64, device="cuda")
         g_n = torch.empty(world * nq, dtype=torch.int32, device="cuda")
         m_key = torch.empty(nq * k, dtype=torch.int64, device="cuda")
@@ -152,7 +152,7 @@ def retrieve_leg(args, rank, world, dev, n_docs=DOCS_PER_SHARD, check_queries=20
     def step(timing):
         ix.search_device(d_terms, d_cu, nq, k, out_doc, out_score, out_n, out_key,
                          flags | (_lib.DI_F_TIMING if timing else 0))
-        if world > 1:
+        if dist.is_initialized():
             all_gather_dev(g_key, out_key)
             all_gather_dev(g_n, out_n)
             _lib.topk_merge_device(g_key, g_n, nq, world, k, m_key, m_n, device=dev,
@@ -164,19 +164,19 @@ def retrieve_leg(args, rank, world, dev, n_docs=DOCS_PER_SHARD, check_queries=20
     torch.cuda.synchronize()
     ix.sync()
     ix.timing("score_blocks", reset=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step(True)
     torch.cuda.synchronize()
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
     el = time.perf_counter() - t0
     ix.sync()
     # a query the scorer rejected (out_n < 0: a kernel limit) invalidates the leg
-    n_min = int((m_n if world > 1 else out_n).min().item()) if nq else 0
+    n_min = int((m_n if dist.is_initialized() else out_n).min().item()) if nq else 0
     if n_min < 0:
         raise SystemExit(f"scorer rejected a query (out_n = {n_min}): the leg is invalid")
     ms_sb, n_sb = ix.timing("score_blocks")
@@ -196,7 +196,7 @@ def retrieve_leg(args, rank, world, dev, n_docs=DOCS_PER_SHARD, check_queries=20
             if got != want[i]:
                 raise SystemExit(f"bench parity check failed on query {i} ({n_docs} docs)")
         log(f"[rank 0] {n_docs}-doc shard: the first {check_queries} queries equal the oracle")
-    if world > 1:
+    if dist.is_initialized():
         el = max_over_ranks(el)
 
     # correctness spot check of the timed outputs against the oracle (rank 0, N=1)
@@ -380,18 +380,18 @@ def encode_leg(args, rank, world, dev, precision="bf16"):
     torch.cuda.synchronize()
     enc.sync()
     enc.timing("gemm_qkv", reset=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     for _ in range(args.steps):
         step(True)
     torch.cuda.synchronize()
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
     el = time.perf_counter() - t1
     enc.sync()
-    if world > 1:
+    if dist.is_initialized():
         el = max_over_ranks(el)
     kernels = {}
     for name in ("embed_ln", "gemm_qkv", "attention", "gemm_o", "ln", "gemm_ffn1", "gemm_ffn2",
@@ -551,7 +551,7 @@ def index_e2e_leg(args, dev, rank=0, world=1):
                 with open(coll) as f:
                     indexer.index([next(f).split("\t", 1)[1] for _ in range(4 * procs)], dn)
             t_setup = time.perf_counter() - t0
-            if world > 1:  # every rank's workers start together (host cores shared)
+            if dist.is_initialized():  # every rank's workers start together (host cores shared)
                 dist.barrier()
             t1 = time.perf_counter()
             n = index_cli._index_file(indexer, coll, "msmarco", td / "collection.index",
@@ -562,7 +562,7 @@ def index_e2e_leg(args, dev, rank=0, world=1):
             pool.close()
     log(f"[rank {rank}] index e2e: {n} docs in {el:.2f}s after {t_setup:.1f}s setup ({procs} "
         f"tokenizer workers)")
-    if world > 1:  # all ranks' documents over the slowest rank's time (host tokenization of
+    if dist.is_initialized():  # all ranks' documents over the slowest rank's time (host tokenization of
         el = max_over_ranks(el)  # N ranks x their workers on the node's shared cores)
     return {"value": round(world * n / el, 1), "unit": "docs/s", "docs": int(world * n),
             "ranks": world, "seconds": round(el, 3),
@@ -712,7 +712,9 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     backend = None
     ranks_seen = 1
-    if world > 1:
+    # DI_BENCH_DIST=1 under a launcher: the process group and every collective of the
+    # multi-rank path even at one rank (a 1-GPU box rehearses the RCCL path that way)
+    if world > 1 or (os.environ.get("DI_BENCH_DIST") == "1" and "MASTER_ADDR" in os.environ):
         # one rank per GPU over RCCL; more ranks than GPUs (a 1-GPU rehearsal of the
         # multi-rank path) share the devices over gloo with host-staged collectives
         n_dev = max(1, torch.cuda.device_count())
@@ -843,7 +845,7 @@ def main():
                 out["cpu_baseline"] = cb
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

@@ -203,3 +203,24 @@ def test_bench_gpus_flag_launches_ranks_itself():
     d = json.loads(line[0])
     assert d["n_gpus"] == 2 and d["ranks_seen"] == 2 and d["backend"] == "gloo"
     assert d["value"] > 0
+
+
+def test_bench_single_rank_rccl_path():
+    """The RCCL (nccl) branch of the multi-rank bench, rehearsed on the 1-GPU box: one
+    torchrun rank with DI_BENCH_DIST=1 initialises the nccl process group and runs every
+    collective of the N-rank path (barriers, the max-over-ranks time, the device
+    all_gather of the per-shard top-k keys and the GPU merge of the gathered lists) --
+    the path the 8-GPU scaling run takes, whose gloo rehearsals cover only host tensors."""
+    env = dict(os.environ, PYTHONPATH=str(ROOT), OMP_NUM_THREADS="4", DI_BENCH_DIST="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
+           "--master-addr", "127.0.0.1", f"--master-port={_port()}", "bench.py", "--gpus", "1",
+           "--legs", "retrieve,retrieve_shard", "--steps", "2", "--warmup", "1",
+           "--queries", "512", "--no-cpu"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-4000:]
+    line = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(line) == 1, r.stdout[-2000:]
+    d = json.loads(line[0])
+    assert d["backend"] == "nccl" and d["ranks_seen"] == 1 and d["n_gpus"] == 1
+    assert d["value"] > 0 and d["retrieve_shard"]["value"] > 0
+    assert "the first 20 queries equal the oracle" in r.stderr
