@@ -712,9 +712,9 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     backend = None
     ranks_seen = 1
-    # DI_BENCH_DIST=1 under a launcher: the process group and every collective of the
+    # DI_FORCE_DIST=1 under a launcher: the process group and every collective of the
     # multi-rank path even at one rank (a 1-GPU box rehearses the RCCL path that way)
-    if world > 1 or (os.environ.get("DI_BENCH_DIST") == "1" and "MASTER_ADDR" in os.environ):
+    if world > 1 or (os.environ.get("DI_FORCE_DIST") == "1" and "MASTER_ADDR" in os.environ):
         # one rank per GPU over RCCL; more ranks than GPUs (a 1-GPU rehearsal of the
         # multi-rank path) share the devices over gloo with host-staged collectives
         n_dev = max(1, torch.cuda.device_count())

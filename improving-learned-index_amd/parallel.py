@@ -28,6 +28,12 @@ def dist_env() -> Tuple[int, int, int]:
             int(os.environ.get("LOCAL_RANK", "0")))
 
 
+def force_dist() -> bool:
+    """DI_FORCE_DIST=1 under a launcher: the multi-rank path (process group, exchange,
+    merge) even at one rank -- how a 1-GPU box runs the RCCL branch."""
+    return os.environ.get("DI_FORCE_DIST") == "1" and "MASTER_ADDR" in os.environ
+
+
 def visible_gpus() -> int:
     """GPUs this process sees, counted without initialising HIP (torch's count reads
     the device list only; HIP must not come up in a parent that spawns ranks)."""

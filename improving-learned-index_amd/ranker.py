@@ -48,7 +48,8 @@ class Ranker:
             self.query_iterator = list(QueryRelevanceDataset(qrels_path=qrels_path).keys())
         self.world, self.rank, local = parallel.dist_env()
         lo = hi = 0
-        if self.world > 1:
+        self.dist = self.world > 1 or parallel.force_dist()
+        if self.dist:
             import torch
 
             device = parallel.rank_device(local)
@@ -82,7 +83,7 @@ class Ranker:
         for s in range(0, len(qids), self.batch_queries):
             chunk = qids[s:s + self.batch_queries]
             terms = [self.get_query_terms(q) for q in chunk]
-            if self.world > 1:
+            if self.dist:
                 # every shard must apply the terms in one order (the first-touch tie key):
                 # process_query returns a set whose iteration order follows the process's
                 # hash seed, so rank 0's order is broadcast to all ranks

@@ -27,11 +27,12 @@ def _port():
         return s.getsockname()[1]
 
 
-def _torchrun(module, args, world=2, timeout=240):
+def _torchrun(module, args, world=2, timeout=240, extra_env=None):
     """world > 0: torchrun with `world` ranks; 0: one plain process.  PYTHONHASHSEED is
     fixed: query terms are a set (process_query), whose iteration order -- the
     reference's first-touch tie order -- follows the hash seed."""
-    env = dict(os.environ, PYTHONPATH=str(ROOT), OMP_NUM_THREADS="4", PYTHONHASHSEED="0")
+    env = dict(os.environ, PYTHONPATH=str(ROOT), OMP_NUM_THREADS="4", PYTHONHASHSEED="0",
+               **(extra_env or {}))
     run = ([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
             f"--nproc-per-node={world}", "--master-addr", "127.0.0.1",
             f"--master-port={_port()}"] if world else [sys.executable])
@@ -120,6 +121,10 @@ def test_rank_cli_two_ranks_equals_one():
         _same_run((td / "two.tsv").read_text(), (td / "one.tsv").read_text())
         _torchrun("rank", args + ["--output_path", str(td / "self.tsv"), "--gpus", "2"], world=0)
         _same_run((td / "self.tsv").read_text(), (td / "one.tsv").read_text())
+        # the RCCL exchange itself (one rank owns the GPU: nccl), DI_FORCE_DIST=1
+        _torchrun("rank", args + ["--output_path", str(td / "rccl.tsv")], world=1,
+                  extra_env={"DI_FORCE_DIST": "1"})
+        _same_run((td / "rccl.tsv").read_text(), (td / "one.tsv").read_text())
         _torchrun("rank", args + ["--output_path", str(td / "three.tsv"), "--top_k", "7"],
                   world=3)
         _torchrun("rank", args + ["--output_path", str(td / "one7.tsv"), "--top_k", "7"],
@@ -207,11 +212,11 @@ def test_bench_gpus_flag_launches_ranks_itself():
 
 def test_bench_single_rank_rccl_path():
     """The RCCL (nccl) branch of the multi-rank bench, rehearsed on the 1-GPU box: one
-    torchrun rank with DI_BENCH_DIST=1 initialises the nccl process group and runs every
+    torchrun rank with DI_FORCE_DIST=1 initialises the nccl process group and runs every
     collective of the N-rank path (barriers, the max-over-ranks time, the device
     all_gather of the per-shard top-k keys and the GPU merge of the gathered lists) --
     the path the 8-GPU scaling run takes, whose gloo rehearsals cover only host tensors."""
-    env = dict(os.environ, PYTHONPATH=str(ROOT), OMP_NUM_THREADS="4", DI_BENCH_DIST="1")
+    env = dict(os.environ, PYTHONPATH=str(ROOT), OMP_NUM_THREADS="4", DI_FORCE_DIST="1")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
            "--master-addr", "127.0.0.1", f"--master-port={_port()}", "bench.py", "--gpus", "1",
            "--legs", "retrieve,retrieve_shard", "--steps", "2", "--warmup", "1",
