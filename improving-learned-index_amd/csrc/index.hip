@@ -930,10 +930,7 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
         if (lane == 0) sh.wsum[wave] = sfx;
         if (tid == 0) sh.tq = 0;
         __syncthreads();
-        // (a fixed trip with a select: the wave index is a VGPR to the compiler, and a
-        // loop from wave + 1 compiled to an exec-masked loop with a remainder loop)
-#pragma unroll
-        for (int w2 = 0; w2 < SC_WAVES; ++w2) sfx += w2 > wave ? sh.wsum[w2] : 0u;
+        for (int w2 = wave + 1; w2 < SC_WAVES; ++w2) sfx += sh.wsum[w2];
         // one thread holds the crossing: count(>= 4t + e) >= k > count(>= 4t + e + 1)
         if (sfx >= (uint32_t)k && sfx - c < (uint32_t)k) {
             uint32_t above = sfx - c;
@@ -1233,8 +1230,7 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
         // second half of read_tq over the suffix sums published by the scatter barrier:
         // the crossing thread writes tq (0 from the item's start when the histogram
         // holds fewer than k candidates); one barrier
-#pragma unroll
-        for (int w2 = 0; w2 < SC_WAVES; ++w2) tq_sfx += w2 > wave ? sh.wsum[w2] : 0u;
+        for (int w2 = wave + 1; w2 < SC_WAVES; ++w2) tq_sfx += sh.wsum[w2];
         if (tq_sfx >= (uint32_t)k && tq_sfx - tq_c < (uint32_t)k) {
             uint32_t above = tq_sfx - tq_c;
             int e = 3;
