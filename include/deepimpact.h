@@ -128,7 +128,10 @@ int di_index_set_min_impact(di_index *ix, int32_t min_impact);
  * threshold is not scored.  factor 0: off (default); 1: exact -- the same ranking as
  * InvertedIndex.score (inverted_index.py:55-62); in (1, 16]: skips segments below
  * factor x threshold, an approximation (QPS vs recall@1000).  Queries of at most 64
- * terms, with the shared threshold (>= 8 blocks). */
+ * terms, with the shared threshold (>= 8 blocks).  Long sublists: >= 128 postings in a
+ * block.  di_index_timing("bm_segments" / "bm_segments_skipped") counts the evaluated
+ * and skipped segments.  Items run block-major; DI_BLOCK_ORDER=1 (environment, at index
+ * creation) runs each query's blocks in descending bound order instead. */
 int di_index_set_block_max(di_index *ix, float factor);
 /* Packed (block-compressed) postings -- BASELINE configs[4]: on != 0 builds (once, from
  * the device layout) a second copy of the postings in which every run (a short
