@@ -1900,6 +1900,182 @@ merge_topk_kernel(const uint64_t *__restrict__ keys, const int32_t *__restrict__
     if (tid == 0) out_n[q] = take;
 }
 
+// Merge of few short lists (n_lists <= MS_LISTS, all candidates <= MS_U per thread,
+// k <= MG_SEL_KEYS; the 4-block x 1000-candidate retrieve merge): the candidates stay
+// in registers (MS_U per thread), the score histogram and the selected keys are the
+// only LDS -- 33 KiB instead of the general kernel's 77 KiB, so four workgroups share
+// a CU instead of two.  Same selection as merge_topk_kernel's counting path; keys at or
+// past score 4096 (wide keys), more than MG_SEL_KEYS selected keys or at most
+// MG_SEL_MIN candidates take a radix select over the registers and a sort of the take
+// winners in the same LDS.  Output identical to merge_topk_kernel (the keys are unique
+// and totally ordered).
+constexpr int MS_LISTS = 64, MS_U = 8;
+
+template <int THREADS>
+struct alignas(16) MergeSelHead {
+    union {
+        RadixScratch<THREADS / 64> rs;
+        uint32_t hist[MG_SEL_BINS];
+    } u;
+    int32_t off[MS_LISTS + 1];
+    uint32_t thr, above, cnt, pad;
+};
+
+template <int THREADS>
+__global__ void __launch_bounds__(THREADS)
+merge_sel_kernel(const uint64_t *__restrict__ keys, const int32_t *__restrict__ counts,
+                 int n_lists, int k_in, int k, int64_t list_stride, int64_t cnt_stride,
+                 int64_t q_stride, int64_t cq_stride, uint64_t *__restrict__ out_key,
+                 uint32_t *__restrict__ out_doc, uint32_t *__restrict__ out_score,
+                 int32_t *__restrict__ out_n, int mode, const int32_t *__restrict__ cu_q) {
+    constexpr int WAVES = THREADS / 64;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    MergeSelHead<THREADS> &sh = *reinterpret_cast<MergeSelHead<THREADS> *>(smem);
+    static_assert(sizeof(MergeSelHead<THREADS>) % 16 == 0, "key array must stay 16-byte aligned");
+    uint64_t *out = reinterpret_cast<uint64_t *>(smem + sizeof(MergeSelHead<THREADS>));
+    const int q = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
+    const int32_t *cnt0 = counts + (int64_t)q * cq_stride;
+    const uint64_t *src0 = keys + (int64_t)q * q_stride;
+
+    // list offsets (one wave; n_lists <= 64); a negative count marks a rejected query
+    if (tid < 64) {
+        int c = lane < n_lists ? cnt0[(int64_t)lane * cnt_stride] : 0;
+        const bool bad = __any(c < 0);
+        c = min(max(c, 0), k_in);
+        const uint32_t incl = wave_prefix_sum((uint32_t)c);
+        if (lane < n_lists) sh.off[lane + 1] = (int32_t)incl;
+        if (lane == 0) {
+            sh.off[0] = 0;
+            sh.cnt = bad ? 1u : 0u;
+        }
+    }
+    __syncthreads();
+    if (sh.cnt) {
+        if (tid == 0) out_n[q] = -1;
+        return;
+    }
+    const int total = sh.off[n_lists];
+    const int take = min(total, k);
+    // the candidates, MS_U per thread (i = j THREADS + tid), in registers
+    uint64_t v[MS_U];
+#pragma unroll
+    for (int j = 0; j < MS_U; ++j) {
+        const int i = min(j * THREADS + tid, max(total - 1, 0));
+        int lo = 0, hi = n_lists - 1;  // last list with off[l] <= i
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (sh.off[mid] <= i) lo = mid;
+            else hi = mid - 1;
+        }
+        v[j] = total > 0 ? src0[(int64_t)lo * list_stride + (i - sh.off[lo])] : 0;
+    }
+    auto valid = [&](int j) { return j * THREADS + tid < total; };
+    const bool wide = mode == DECODE_QUANT && cu_q && cu_q[q + 1] - cu_q[q] > MAX_TERMS;
+    uint64_t *ok = out_key ? out_key + (int64_t)q * k : nullptr;
+    auto emit = [&](int i, uint64_t x) {  // output rank i
+        if (ok) ok[i] = x;
+        if (mode == DECODE_QUANT) {
+            out_doc[(int64_t)q * k + i] =
+                wide ? 0xFFFFFFu - (uint32_t)(x & 0xFFFFFFu) : 0xFFFFFFFFu - (uint32_t)x;
+            out_score[(int64_t)q * k + i] = (uint32_t)(x >> (wide ? 44 : 48));
+        } else if (mode == DECODE_SPARSE) {
+            out_doc[(int64_t)q * k + i] = 0xFFFFFFu - (uint32_t)(x & 0xFFFFFFu);
+            out_score[(int64_t)q * k + i] = (uint32_t)(x >> 32);  // f32 bits
+        }
+    };
+    bool big = false;
+#pragma unroll
+    for (int j = 0; j < MS_U; ++j) big |= valid(j) && (v[j] >> 60) != 0;
+    const bool counting = !__syncthreads_or(big) && total > MG_SEL_MIN && take < total;
+    if (counting) {
+        // counting selection (merge_topk_kernel's): bin = key bits 48..59 (the score)
+        uint32_t *hist = sh.u.hist;
+        auto bin = [](uint64_t x) { return (uint32_t)(x >> 48) & (MG_SEL_BINS - 1); };
+        for (int i = tid; i < MG_SEL_BINS; i += THREADS) hist[i] = 0;
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < MS_U; ++j)
+            if (valid(j)) atomicAdd(&hist[bin(v[j])], 1u);
+        __syncthreads();
+        constexpr int BPT = MG_SEL_BINS / THREADS;
+        const int top = MG_SEL_BINS - 1 - tid * BPT;
+        uint32_t hc[BPT], c = 0;
+#pragma unroll
+        for (int j = 0; j < BPT; ++j) c += (hc[j] = hist[top - j]);
+        const uint32_t incl = wave_prefix_sum(c);
+        const int w = tid >> 6;
+        __syncthreads();  // (every thread read its bins; the wave totals go to off's tail)
+        uint32_t *wtot = reinterpret_cast<uint32_t *>(out);  // (out is idle until placing)
+        if (lane == 63) wtot[w] = incl;
+        __syncthreads();
+        uint32_t run = incl - c;
+        for (int u = 0; u < w; ++u) run += wtot[u];
+#pragma unroll
+        for (int j = 0; j < BPT; ++j) {
+            if (run < (uint32_t)take && run + hc[j] >= (uint32_t)take) {
+                sh.thr = (uint32_t)(top - j);
+                sh.above = run + hc[j];  // keys in bins >= T
+            }
+            hist[top - j] = run;
+            run += hc[j];
+        }
+        __syncthreads();
+        const uint32_t T = sh.thr, n_sel = sh.above;
+        if (n_sel <= (uint32_t)MG_SEL_KEYS) {
+#pragma unroll
+            for (int j = 0; j < MS_U; ++j)
+                if (valid(j) && bin(v[j]) >= T) out[atomicAdd(&hist[bin(v[j])], 1u)] = v[j];
+            __syncthreads();
+            for (int p = tid; p < (int)n_sel; p += THREADS) {
+                const uint64_t x = out[p];
+                const uint32_t b = bin(x);
+                const uint32_t lo = b == MG_SEL_BINS - 1 ? 0u : hist[b + 1], hi = hist[b];
+                uint32_t r = lo;
+                for (uint32_t j = lo; j < hi; ++j) r += out[j] > x;
+                if (r < (uint32_t)take) emit((int)r, x);
+            }
+            if (tid == 0) out_n[q] = take;
+            return;
+        }
+        __syncthreads();  // (the radix select below reuses the histogram's LDS)
+    }
+    // radix select of the take-th largest key over the registers, then the take winners
+    // (keys are unique: exactly `take` are >= the selected prefix) sorted in LDS
+    uint64_t prefix = 0, mask = 0;
+    uint32_t need = (uint32_t)take;
+    if (take < total) {
+        for (int shift = 56; shift >= 0; shift -= 8) {
+            radix_clear<THREADS, WAVES>(sh.u.rs);
+            __syncthreads();
+            RunLen rl;
+#pragma unroll
+            for (int j = 0; j < MS_U; ++j)
+                if (valid(j) && (v[j] & mask) == prefix)
+                    rl.add(sh.u.rs, (uint32_t)(v[j] >> shift) & 255u);
+            rl.flush(sh.u.rs);
+            __syncthreads();
+            radix_pick<THREADS, WAVES>(sh.u.rs, need);
+            prefix |= (uint64_t)sh.u.rs.bin << shift;
+            mask |= (uint64_t)255 << shift;
+            need -= sh.u.rs.above;
+            __syncthreads();
+        }
+    }
+    if (tid == 0) sh.cnt = 0;
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < MS_U; ++j)
+        if (valid(j) && v[j] >= prefix) out[atomicAdd(&sh.cnt, 1u)] = v[j];
+    int n2 = 64;
+    while (n2 < take) n2 <<= 1;
+    __syncthreads();
+    for (int i = take + tid; i < n2; i += THREADS) out[i] = 0;
+    __syncthreads();
+    bitonic_sort_desc<THREADS>(out, n2);
+    for (int i = tid; i < take; i += THREADS) emit(i, out[i]);
+    if (tid == 0) out_n[q] = take;
+}
+
 }  // namespace di
 
 // ===========================================================================
@@ -2250,6 +2426,9 @@ void enable_big_lds() {
     DI_HIP(hipFuncSetAttribute((const void *)merge_topk_kernel<512>,
                                hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)(sizeof(MergeHead<512>) + MG_LDS_KEYS * 8)));
+    DI_HIP(hipFuncSetAttribute((const void *)merge_sel_kernel<512>,
+                               hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)(sizeof(MergeSelHead<512>) + MG_SEL_KEYS * 8)));
 }
 
 void launch_merge(const uint64_t *keys, const int32_t *counts, int n_q, int n_lists, int k_in,
@@ -2263,6 +2442,20 @@ void launch_merge(const uint64_t *keys, const int32_t *counts, int n_q, int n_li
         cs = n_q;
         qs = k_in;
         cqs = 1;
+    }
+    // few short lists: the register-resident merge (DI_PROFILE_MERGE=0: the general one, A/B)
+    static const bool sel_ok = [] {
+        const char *e = std::getenv("DI_PROFILE_MERGE");
+        return !(e && e[0] == '0');
+    }();
+    if (sel_ok && n_lists <= MS_LISTS && (int64_t)n_lists * k_in <= (int64_t)MS_U * 512 &&
+        k <= MG_SEL_KEYS) {
+        hipLaunchKernelGGL(merge_sel_kernel<512>, dim3(n_q), dim3(512),
+                           sizeof(MergeSelHead<512>) + (size_t)MG_SEL_KEYS * 8, s, keys, counts,
+                           n_lists, k_in, k, ls, cs, qs, cqs, out_key, out_doc, out_score, out_n,
+                           mode, cu_q);
+        check_launch("merge_sel");
+        return;
     }
     // LDS key capacity: all candidates when they fit, else the k survivors of the
     // slow path's radix select
