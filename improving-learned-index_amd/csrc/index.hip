@@ -1663,10 +1663,6 @@ constexpr int MG_SEL_MIN = 1024;
 constexpr int MG_SEL_BINS = 4096;   // 16 KiB of LDS after the key array
 constexpr int MG_SEL_KEYS = 2048;   // + 16 KiB: up to 2048 selected keys
 constexpr int MG_SEL_CAP = 8192;    // key arrays up to 64 KiB (+32 KiB within the LDS max)
-// merge_sel_kernel (below): lists, candidates per thread; the out_n of a query it leaves
-// to merge_topk_kernel (more candidates than its registers hold)
-constexpr int MS_LISTS = 64, MS_U = 8;
-constexpr int32_t MS_FLAG = -3;
 
 template <int THREADS>
 struct alignas(16) MergeHead {  // 16-byte multiple: the u64 key array follows it
@@ -1688,10 +1684,8 @@ merge_topk_kernel(const uint64_t *__restrict__ keys, const int32_t *__restrict__
                   int64_t q_stride, int64_t cq_stride, int cap,
                   uint64_t *__restrict__ out_key, uint32_t *__restrict__ out_doc,
                   uint32_t *__restrict__ out_score, int32_t *__restrict__ out_n, int mode,
-                  int select, const int32_t *__restrict__ cu_q, int flagged_only) {
+                  int select, const int32_t *__restrict__ cu_q) {
     // key i of list l of query q: keys[q*q_stride + l*list_stride + i]
-    // flagged_only: only the queries merge_sel_kernel flagged (out_n == MS_FLAG)
-    if (flagged_only && out_n[blockIdx.x] != MS_FLAG) return;
     // its count:                  counts[q*cq_stride + l*cnt_stride]
     constexpr int WAVES = THREADS / 64;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -1915,7 +1909,7 @@ merge_topk_kernel(const uint64_t *__restrict__ keys, const int32_t *__restrict__
 // MG_SEL_MIN candidates take a radix select over the registers and a sort of the take
 // winners in the same LDS.  Output identical to merge_topk_kernel (the keys are unique
 // and totally ordered).
-
+constexpr int MS_LISTS = 64, MS_U = 8;
 
 template <int THREADS>
 struct alignas(16) MergeSelHead {
@@ -1961,10 +1955,6 @@ merge_sel_kernel(const uint64_t *__restrict__ keys, const int32_t *__restrict__ 
         return;
     }
     const int total = sh.off[n_lists];
-    if (total > MS_U * THREADS) {  // more candidates than registers: the general kernel's
-        if (tid == 0) out_n[q] = MS_FLAG;  // (launched after this one for flagged queries)
-        return;
-    }
     const int take = min(total, k);
     // the candidates, MS_U per thread (i = j THREADS + tid), in registers
     uint64_t v[MS_U];
@@ -2458,18 +2448,14 @@ void launch_merge(const uint64_t *keys, const int32_t *counts, int n_q, int n_li
         const char *e = std::getenv("DI_PROFILE_MERGE");
         return !(e && e[0] == '0');
     }();
-    // (candidates past MS_U x 512 -- possible only when n_lists x k_in exceeds it: the
-    // shared threshold usually leaves ~k + a few -- go to the general kernel, launched
-    // after it for the flagged queries only)
-    int flagged_only = 0;
-    if (sel_ok && n_lists <= MS_LISTS && k <= MG_SEL_KEYS) {
+    if (sel_ok && n_lists <= MS_LISTS && (int64_t)n_lists * k_in <= (int64_t)MS_U * 512 &&
+        k <= MG_SEL_KEYS) {
         hipLaunchKernelGGL(merge_sel_kernel<512>, dim3(n_q), dim3(512),
                            sizeof(MergeSelHead<512>) + (size_t)MG_SEL_KEYS * 8, s, keys, counts,
                            n_lists, k_in, k, ls, cs, qs, cqs, out_key, out_doc, out_score, out_n,
                            mode, cu_q);
         check_launch("merge_sel");
-        if ((int64_t)n_lists * k_in <= (int64_t)MS_U * 512) return;
-        flagged_only = 1;
+        return;
     }
     // LDS key capacity: all candidates when they fit, else the k survivors of the
     // slow path's radix select
@@ -2489,17 +2475,17 @@ void launch_merge(const uint64_t *keys, const int32_t *counts, int n_q, int n_li
         size_t lds = sizeof(MergeHead<256>) + (size_t)cap * 8 + sel_lds;
         hipLaunchKernelGGL(merge_topk_kernel<256>, dim3(n_q), dim3(256), lds, s, keys, counts,
                            n_lists, k_in, k, ls, cs, qs, cqs, cap, out_key, out_doc, out_score,
-                           out_n, mode, select, cu_q, flagged_only);
+                           out_n, mode, select, cu_q);
     } else if (mt == 512) {
         size_t lds = sizeof(MergeHead<512>) + (size_t)cap * 8 + sel_lds;
         hipLaunchKernelGGL(merge_topk_kernel<512>, dim3(n_q), dim3(512), lds, s, keys, counts,
                            n_lists, k_in, k, ls, cs, qs, cqs, cap, out_key, out_doc, out_score,
-                           out_n, mode, select, cu_q, flagged_only);
+                           out_n, mode, select, cu_q);
     } else {
         size_t lds = sizeof(MergeHead<1024>) + (size_t)cap * 8 + sel_lds;
         hipLaunchKernelGGL(merge_topk_kernel<1024>, dim3(n_q), dim3(1024), lds, s, keys,
                            counts, n_lists, k_in, k, ls, cs, qs, cqs, cap, out_key, out_doc,
-                           out_score, out_n, mode, select, cu_q, flagged_only);
+                           out_score, out_n, mode, select, cu_q);
     }
     check_launch("merge_topk");
 }
