@@ -81,8 +81,10 @@ def _queries(v_terms, n, seed, long_every=0):
     return qs
 
 
-@pytest.mark.parametrize("k", [1, 10, 1000, 4096])
+@pytest.mark.parametrize("k", [1, 10, 1000, 2000, 4096])
 def test_synthetic_matches_oracle(L, synth, k):
+    # (k 1000 over 3 blocks: the register merge; 2000 and 4096: past its 4096
+    # candidates, the general merge kernel)
     term_off, pdoc, pval, ora = synth
     dev = L.DeviceIndex.from_postings(term_off, pdoc, pval)
     info = dev.info()
