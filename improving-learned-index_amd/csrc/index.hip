@@ -1265,6 +1265,43 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
         }
     }
 
+    if (EXT == EXT_BM && fast) {
+        // A sparse item: at most k postings were scattered, so at most k docs are touched
+        // and every touched doc is a candidate.  One append sweep (any order: the merge
+        // orders by key) replaces the histogram sweep (an LDS atomic per word) and the two
+        // compaction sweeps.  Every wave sums the scattered postings itself from the LDS
+        // bounds (lane j: term j; a long term: its per-wave runs), so the branch is uniform
+        // with no barrier.  In the EXT_BM instantiation only, which impact-pruned searches
+        // use (di_index_search): in the plain kernel the same code cost the dense 100 k-doc
+        // items 4% (2.148 vs 2.062 ms per launch, profiles/round4_p5_sparse_items_ab.txt);
+        // here it takes 8.8 M skewed docs at min_impact 128 from 70.6 to 48.9 ms per batch.
+        uint32_t np = 0;
+        if (lane < nt) {
+            if (is_long(lane)) {
+#pragma unroll
+                for (int w = 0; w < WSEG; ++w) {
+                    const uint32_t se = sh.wtab[lane][w];
+                    const uint32_t s0 = se >> 16, s1 = se & 0xFFFFu;
+                    np += s1 > s0 ? s1 - s0 : 0u;
+                }
+            } else {
+                np = (uint32_t)min(hi[lane] - lo[lane], (int64_t)0xFFFFFF);
+            }
+        }
+        np = (uint32_t)__shfl(wave_prefix_sum(np), 63, 64);
+        if (np <= (uint32_t)k) {
+            sweep_words(sh.acc, n_local, tid, [&](uint32_t w, int idx) {
+                uint32_t pos;
+                if (wave_append<true>(w != 0, &sh.emit, pos)) cand(pos, w, idx);
+            });
+            __syncthreads();
+            const uint32_t na = sh.emit;
+            flush(na);
+            if (tid == 0) *cn = (int32_t)na;
+            return;
+        }
+    }
+
     uint32_t prefix = 0, mask = 0, need = (uint32_t)k;
     int shift = 24;  // next digit of the general radix path
     if (fast) {
@@ -2730,7 +2767,14 @@ int di_index_search(di_index *ix, const uint32_t *q_terms, const int32_t *cu_q, 
                 }
                 // (DI_PROFILE_ABLATE bit 65536: the block-max instantiation with block-max
                 // off, A/B of its code alone)
-                const bool ext = pk || order || (thr && ix->bm_factor > 0.0f) || (ix->ablate & 65536);
+                // Heavily pruned searches (min_impact >= 16: min_cls <= 3) run the EXT_BM
+                // instantiation too, block-max off, for its one-sweep selection of sparse
+                // items (score_item).  8.8 M docs, k q/s: skewed m 16 / 32 / 64 / 128
+                // 110.8 / 96.9 / 98.2 / 98.6 -> 121.4 / 124.9 / 131.2 / 133.1; i.i.d. 2.5-4%
+                // slower (the instantiation's own cost, items there rarely sparse); lighter
+                // pruning 1-4% slower, so it keeps the plain kernel (round-4 DESIGN §4).
+                const bool ext = pk || order || (thr && ix->bm_factor > 0.0f) ||
+                                 (thr && ix->min_cls <= 3) || (ix->ablate & 65536);
                 hipLaunchKernelGGL(pk    ? score_blocks_kernel<EXT_PK>
                                    : ext ? score_blocks_kernel<EXT_BM>
                                          : score_blocks_kernel<0>,

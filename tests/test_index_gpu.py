@@ -251,6 +251,42 @@ def test_zero_values_stop_term_lists(L):
     assert dev.search([[0]], 10) == [[(3, 9), (1, 5)]]
 
 
+def _pruned_oracle(term_off, pdoc, pval, n_docs, min_impact):
+    """The oracle over the postings a min_impact search scores (value >= 2^floor(log2 m))."""
+    keep = pval >= (1 << (int(min_impact).bit_length() - 1))
+    c = np.concatenate([[0], np.cumsum(keep, dtype=np.int64)])
+    cnt = c[term_off[1:]] - c[term_off[:-1]]
+    pr = oracle.Index.__new__(oracle.Index)
+    pr.term_off = np.concatenate([[0], np.cumsum(cnt)]).astype(np.int64)
+    pr.pdoc, pr.pval, pr.n_docs = pdoc[keep], pval[keep], n_docs
+    return pr
+
+
+@pytest.mark.parametrize("k", [10, 100, 1000])
+def test_sparse_items_equal_oracle(L, synth, k, monkeypatch):
+    """Items (query, block) that scatter at most k postings take the one-sweep selection
+    (every touched doc is a candidate) in the EXT_BM instantiation, which heavily pruned
+    searches on shards of >= 8 blocks run (here forced on the 3-block shard by
+    DI_PROFILE_ABLATE bit 65536): queries of rare terms, alone and next to a frequent
+    one (which puts some of their items over k), equal the oracle, exhaustive and pruned."""
+    term_off, pdoc, pval, ora = synth
+    df = np.diff(term_off)
+    rare = [int(t) for t in np.nonzero((df > 0) & (df <= 400))[0]]
+    rng = np.random.default_rng(k)
+    qs = [[int(t) for t in rng.choice(rare, int(rng.integers(1, 9)), replace=False)]
+          for _ in range(150)]
+    qs += [q + [0] for q in qs[:30]] + [[0] + q for q in qs[30:60]]
+    assert sum(int(df[q].sum()) <= k for q in qs) >= 10  # (more items are, per block)
+    want = ora.score_ids(qs, k, n_threads=8)
+    assert L.DeviceIndex.from_postings(term_off, pdoc, pval).search(qs, k) == want
+    monkeypatch.setenv("DI_PROFILE_ABLATE", "65536")
+    dev = L.DeviceIndex.from_postings(term_off, pdoc, pval)
+    assert dev.search(qs, k) == want
+    dev.set_min_impact(2)
+    assert dev.search(qs, k) == _pruned_oracle(term_off, pdoc, pval, ora.n_docs, 2).score_ids(
+        qs, k, n_threads=8)
+
+
 @pytest.mark.parametrize("min_impact", [2, 5, 64])
 def test_min_impact_pruning_equals_oracle_on_pruned_postings(L, synth, min_impact):
     """di_index_set_min_impact (BASELINE configs[4] sweep): scoring the postings with
@@ -361,6 +397,12 @@ def test_million_doc_shard_matches_oracle(L, million, k):
     qs = S.msmarco_like_queries(24, 2_200_000, seed=k) + _queries(2_200_000, 8, seed=k) + \
         _long_queries(3000, 3, seed=k, lo=65, hi=300)
     assert dev.search(qs, k) == ora.score_ids(qs, k, n_threads=16)
+    # min_impact 16 / 128 at 34 blocks: the EXT_BM instantiation and its one-sweep
+    # selection of sparse items
+    for m in (16, 128):
+        dev.set_min_impact(m)
+        assert dev.search(qs, k) == _pruned_oracle(term_off, pdoc, pval, ora.n_docs, m).score_ids(
+            qs, k, n_threads=16), m
 
 
 def test_full_msmarco_scaled_vocab_on_one_gpu(L):

@@ -20,6 +20,7 @@ PY
 for v in ${VARIANTS:-old new}; do
     case $v in
         old) run old DEEPIMPACT_HIP_LIB=$PWD/tools/_old/libdeepimpact_hip.so DI_LIB_ALLOW_MISSING=1 || exit 1 ;;
+        mid) run mid DEEPIMPACT_HIP_LIB=$PWD/tools/_mid/libdeepimpact_hip.so DI_LIB_ALLOW_MISSING=1 || exit 1 ;;
         new) run new X=0 || exit 1 ;;
         ablate*) run $v DI_PROFILE_ABLATE=${v#ablate} || exit 1 ;;
         wlong*) run $v DI_WLONG_MIN=${v#wlong} || exit 1 ;;
