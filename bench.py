@@ -217,7 +217,8 @@ def retrieve_leg(args, rank, world, dev, n_docs=DOCS_PER_SHARD, check_queries=20
     # algorithmic bytes of one step (every query's postings, 4 B each: the packed u32
     # posting (doc_in_block << 8) | value) over the score_blocks time of one step -- a
     # step is several launches when the candidate workspace splits the queries into
-    # chunks (nb * k * 8 bytes per query, <= 1 GiB per chunk)
+    # chunks (nb * k * 8 bytes per query, <= 4 GiB per chunk: one launch per step at
+    # 100 k and 1.1 M docs, 4 at 8.8 M)
     bytes_per_launch = 4.0 * post_per_launch
     avg_s = (ms_sb / max(args.steps, 1)) / 1000.0  # score_blocks time per step
     achieved = bytes_per_launch / avg_s / 1e9 if avg_s > 0 else 0.0

@@ -2691,9 +2691,14 @@ int di_index_search(di_index *ix, const uint32_t *q_terms, const int32_t *cu_q, 
                            "term id %u out of range", q_terms[i]);
         }
         const int nb = std::max(ix->nb, 1);
-        // query chunking keeps the candidate workspace bounded (<= 1 GiB)
+        // query chunking keeps the candidate workspace bounded: 4 GiB of the 288 GB HBM
+        // (DI_CAND_WS_MIB overrides, A/B).  A 1 GiB cap cut 8.8 M-doc batches into 14
+        // chunks of 499 queries, whose merge launches had ~2 workgroups per CU
+        // (round-4 DESIGN §4).
         const int64_t per_q = (int64_t)nb * k * 8;
-        const int chunk = (int)std::max<int64_t>(1, std::min<int64_t>(n_q, (1ll << 30) / per_q));
+        int64_t ws_cap = 4ll << 30;
+        if (const char *e = std::getenv("DI_CAND_WS_MIB")) ws_cap = std::max(1ll, std::atoll(e)) << 20;
+        const int chunk = (int)std::max<int64_t>(1, std::min<int64_t>(n_q, ws_cap / per_q));
         ix->ws_ck.reserve((size_t)chunk * per_q);
         ix->ws_cn.reserve((size_t)chunk * nb * 4);
         ix->ws_thr.reserve((size_t)chunk * QH_BINS * 4);
@@ -2703,10 +2708,10 @@ int di_index_search(di_index *ix, const uint32_t *q_terms, const int32_t *cu_q, 
             DI_HIP(hipMemsetAsync(ix->bm_stat.p, 0, 16, s));
         }
         // (only the records of real terms are written / read: ~6 per query)
-        // (bounded: WTERMS slots per item; a search whose records would pass 2 GiB -- a
+        // (bounded: WTERMS slots per item; a search whose records would pass 8 GiB -- a
         // small k leaves chunks of many queries -- walks the chain in the scorer instead)
         const size_t rec_bytes = (size_t)chunk * nb * WTERMS * sizeof(ItemRec);
-        const bool use_rec = !(ix->ablate & 1024) && rec_bytes <= (size_t(1) << 31);
+        const bool use_rec = !(ix->ablate & 1024) && rec_bytes <= (size_t(8) << 30);
         if (use_rec) ix->ws_rec.reserve(rec_bytes);
         const uint32_t *dq = (const uint32_t *)stage_in(
             q_terms, (size_t)nterms_total * 4, dev, ix->ws_q, s);

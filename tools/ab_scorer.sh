@@ -22,6 +22,7 @@ for v in ${VARIANTS:-old new}; do
         old) run old DEEPIMPACT_HIP_LIB=$PWD/tools/_old/libdeepimpact_hip.so DI_LIB_ALLOW_MISSING=1 || exit 1 ;;
         mid) run mid DEEPIMPACT_HIP_LIB=$PWD/tools/_mid/libdeepimpact_hip.so DI_LIB_ALLOW_MISSING=1 || exit 1 ;;
         new) run new X=0 || exit 1 ;;
+        ws1g) run ws1g DI_CAND_WS_MIB=1024 || exit 1 ;;
         ablate*) run $v DI_PROFILE_ABLATE=${v#ablate} || exit 1 ;;
         wlong*) run $v DI_WLONG_MIN=${v#wlong} || exit 1 ;;
         b32) run $v DI_PROFILE_ABLATE=4096 DI_DEAL_X4=0 || exit 1 ;;  # 4-byte loads, 32-block dealing
