@@ -9,4 +9,4 @@ PMC_TAG=round4_zzz LEGS="retrieve_shard" \
 cp gpurun_out/pmc_round4_zzz/retrieve_shard/summary.json profiles/round4_zzz_pmc_retrieve_shard.json || exit 1
 mkdir -p gpurun_out/round4_p9 && cp profiles/round4_zzz_pmc_retrieve_shard.json gpurun_out/round4_p9/
 TAG=round4_p9 STEPS="bench" bash tools/measure_r4.sh || exit 1
-TAG=round4_p9 bash tools/_cmd_z1.sh || exit 1
+# (the GPU suite: the round-end driver run)
