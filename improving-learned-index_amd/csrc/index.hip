@@ -102,6 +102,7 @@ struct ScoreShared {
                                    // thread 0 read it -- one value for every wave
     uint32_t wub[WSEG];            // block-max: each wave segment's score upper bound
     uint32_t wtab[WTERMS][WSEG];   // their per-wave runs: start << 16 | end (in the sublist)
+    uint32_t wstamp[SC_WAVES];     // profiling (DI_PROFILE_ABLATE bit 64): each wave's scatter loop
     uint32_t tqn;                  // EXT: a lower bound of the query's k-th score this item
                                    // found (thread 0), raised into qtq after the item
                                    // (last: the fields above keep their alignment)
@@ -452,7 +453,7 @@ __device__ __forceinline__ void packed_apply(const uint4 h, const uint32_t *__re
 
 // Profiling (DI_PROFILE_ABLATE bit 64): per-phase shader cycles of workgroup 0's items
 // accumulated here and printed by di_index_search.
-__device__ unsigned long long g_sb_phase[10];
+__device__ unsigned long long g_sb_phase[12];  // [9] slowest wave's scatter loop, [10] mean
 
 // The (term, block) sublists: sparse per term -- the entries of term t are
 // [tb_start[t], tb_start[t+1]), one per block holding postings of t, in block order
@@ -783,7 +784,7 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
     // per-wave form (at most WTERMS terms): every term applied by each wave to its own
     // docs -- long terms over their per-wave runs, short ones read in full by every wave
     // -- so no term needs a barrier; longer queries: the all-wave form, a barrier per term
-    const bool wl = nt <= WTERMS;
+    const bool wl = nt <= WTERMS && !(ablate & 524288);  // (bit 524288: the all-wave form, A/B)
     // block-max skipping (opt-in, configs[4]): per-wave segment upper bounds (wub)
     const bool bm = EXT != 0 && bm_factor > 0.0f && wl && qhist != nullptr;
     // block-max: the query's running threshold as one word (qtq, raised by every item's
@@ -907,6 +908,8 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
     }
 
     stamp(0);  // setup + zeroing
+    const bool wstamps = (ablate & 64) && blockIdx.x == 0;
+    const uint64_t t_w0 = wstamps ? __builtin_amdgcn_s_memtime() : 0;
     // The query's shared threshold (qhist, when given) counts the scores of every
     // candidate its finished blocks emitted (distinct docs, full scores; bin 4095 =
     // 4095 and above).  read_tq -> the largest s with >= k counted candidates scoring
@@ -1161,6 +1164,7 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
     // threshold read (read_tq) goes before the barrier: thread t's own 4 bins are the
     // 16 B its own LDS-DMA wrote (no barrier needed to read them), their wave suffix
     // sums go to wsum -- the barrier the scatter needs anyway publishes them.
+    if (wstamps && lane == 0) sh.wstamp[wave] = (uint32_t)(__builtin_amdgcn_s_memtime() - t_w0);
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     uint32_t tq_hv[4] = {0, 0, 0, 0}, tq_c = 0, tq_sfx = 0;
     if (qpre) {
@@ -1173,6 +1177,15 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
     __syncthreads();
 
     stamp(1);  // scatter
+    if (stamps) {
+        uint32_t mx = 0, sm = 0;
+        for (int w2 = 0; w2 < SC_WAVES; ++w2) {
+            mx = max(mx, sh.wstamp[w2]);
+            sm += sh.wstamp[w2];
+        }
+        atomicAdd(&g_sb_phase[9], (unsigned long long)mx);
+        atomicAdd(&g_sb_phase[10], (unsigned long long)(sm / SC_WAVES));
+    }
     if (ablate & 2) {  // profiling: skip the selection
         if (tid == 0) *cn = 0;
         return;
@@ -2821,13 +2834,13 @@ int di_index_search(di_index *ix, const uint32_t *q_terms, const int32_t *cu_q, 
                                       s));
         }
         if (ix->ablate & 64) {
-            unsigned long long ph[10];
+            unsigned long long ph[12];
             DI_HIP(hipStreamSynchronize(s));
             DI_HIP(hipMemcpyFromSymbol(ph, HIP_SYMBOL(g_sb_phase), sizeof ph));
             fprintf(stderr, "score_blocks phase cycles (workgroup 0, cumulative): setup %llu "
                             "scatter %llu hist %llu [count %llu] write %llu ties %llu copy %llu "
-                            "tq-select %llu [tq-read %llu]\n",
-                    ph[0], ph[1], ph[2], ph[6], ph[3], ph[4], ph[5], ph[7], ph[8]);
+                            "tq-select %llu [tq-read %llu] scatter-loop slowest wave %llu mean wave %llu\n",
+                    ph[0], ph[1], ph[2], ph[6], ph[3], ph[4], ph[5], ph[7], ph[8], ph[9], ph[10]);
         }
         if (!(flags & DI_F_ASYNC) || !dev) {
             DI_HIP(hipStreamSynchronize(s));

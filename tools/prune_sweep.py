@@ -57,6 +57,8 @@ def main():
         [(1, f, True) for f in (0.0, 1.0, 1.5, 2.0)]
     if os.environ.get("SWEEP") == "bm":  # exhaustive + the block-max rows only
         rows_sel = [(1, 0.0, False)] + [(1, f, False) for f in (1.0, 1.5, 2.0)]
+    elif os.environ.get("SWEEP") == "exh":  # the exhaustive row only
+        rows_sel = [(1, 0.0, False)]
     packed_bytes = None
     for mi, bm, pk in rows_sel:
         ix.set_min_impact(mi)
