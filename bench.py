@@ -31,6 +31,7 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
 from improving_learned_index_amd import _lib  # noqa: E402
+from improving_learned_index_amd import parallel  # noqa: E402
 from improving_learned_index_amd import synthetic as S  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md); 6.3 TB/s measured copy
@@ -114,13 +115,25 @@ def retrieve_leg(args, rank, world, dev, n_docs=DOCS_PER_SHARD, check_queries=20
     C scorer right after the timed loop."""
     t0 = time.time()
     V = v_terms(n_docs)
+    # Multi-rank: the shards of one collection, quantized with the collection's max (the
+    # all_reduce(MAX) of the shards' maxima, as the sharded quantize CLI does); per-shard
+    # maxima would give every shard its own scale, and one shard's scores would dominate
+    # the global top-k (and the exchange)
+    sharded = dist.is_initialized()
     if n_docs == DOCS_PER_SHARD:
         cu, term, imp = S.msmarco_like_docs(DOCS_PER_SHARD, V, seed=1234 + rank)
-        q, _ = S.quantize_like_reference(imp)
+        gmax = None
+        if sharded:
+            gmax = max_over_ranks(float(S.round3_f32(imp).astype(np.float64).max()))
+        q, _ = S.quantize_like_reference(imp, max_val=gmax)
         term_off, pdoc, pval = S.postings_reference_order(cu, term, q, V)
         del cu, term, imp, q
+    elif sharded:  # docs [rank n, (rank + 1) n) of the seed's collection
+        gmax = max_over_ranks(S.synth_max_impact(n_docs, V, seed=4321, doc0=rank * n_docs))
+        term_off, pdoc, pval, _ = S.synth_postings(n_docs, V, seed=4321, doc0=rank * n_docs,
+                                                   quant_max=gmax)
     else:
-        term_off, pdoc, pval, _ = S.synth_postings(n_docs, V, seed=4321 + rank)
+        term_off, pdoc, pval, _ = S.synth_postings(n_docs, V, seed=4321)
     t_gen = time.time() - t0
     doc_lo = rank * n_docs
     if doc_lo:
@@ -149,12 +162,32 @@ def retrieve_leg(args, rank, world, dev, n_docs=DOCS_PER_SHARD, check_queries=20
         m_n = torch.empty(nq, dtype=torch.int32, device="cuda")
     flags = _lib.DI_F_DEVICE_PTRS | _lib.DI_F_ASYNC
 
+    xch = {"ms": 0.0, "keys_per_query": 0.0, "bytes": 0, "n": 0}
+
     def step(timing):
         ix.search_device(d_terms, d_cu, nq, k, out_doc, out_score, out_n, out_key,
                          flags | (_lib.DI_F_TIMING if timing else 0))
         if dist.is_initialized():
-            all_gather_dev(g_key, out_key)
-            all_gather_dev(g_n, out_n)
+            # the pruned exact exchange (parallel.exchange_topk: two rounds, each rank
+            # sends its first ceil(k / world) keys, then its keys above the k-th of that
+            # union); its time is the scorer's wait included, the collective_ms line
+            torch.cuda.synchronize()
+            t_x = time.perf_counter()
+            st = {}
+            if _gloo():
+                gk, gn = parallel.exchange_topk(out_key.cpu(), out_n.cpu(), k, stats=st)
+                g_key.copy_(gk)
+                g_n.copy_(gn)
+            else:
+                gk, gn = parallel.exchange_topk(out_key, out_n, k, stats=st)
+                g_key.copy_(gk)
+                g_n.copy_(gn)
+            torch.cuda.synchronize()
+            if timing:
+                xch["ms"] += 1000.0 * (time.perf_counter() - t_x)
+                xch["keys_per_query"] += st["gathered_keys_per_query"]
+                xch["bytes"] += st["bytes_sent"]
+                xch["n"] += 1
             _lib.topk_merge_device(g_key, g_n, nq, world, k, m_key, m_n, device=dev,
                                    stream=stream.cuda_stream,
                                    flags=flags | _lib.DI_F_LISTS_MAJOR)
@@ -214,6 +247,18 @@ def retrieve_leg(args, rank, world, dev, n_docs=DOCS_PER_SHARD, check_queries=20
                                "merge_topk": ms_mg / max(args.steps, 1)},
         "launches_per_step": n_sb / max(args.steps, 1),
     }
+    if dist.is_initialized():
+        n_x = max(xch["n"], 1)
+        res["exchange"] = {
+            # device-synchronised host time of the two-round exchange per step (the
+            # scorer's tail included: the rounds need its counts), max over ranks
+            "collective_ms_per_step": max_over_ranks(xch["ms"] / n_x),
+            # keys this rank sent per query (a plain all_gather: k) and bytes per step
+            "gathered_keys_per_query": xch["keys_per_query"] / n_x,
+            "gathered_bytes_per_query": 8.0 * xch["keys_per_query"] / n_x,
+            "plain_all_gather_bytes_per_query": 8.0 * k,
+            "bytes_sent_per_step": xch["bytes"] / n_x,
+        }
     # algorithmic bytes of one step (every query's postings, 4 B each: the packed u32
     # posting (doc_in_block << 8) | value) over the score_blocks time of one step -- a
     # step is several launches when the candidate workspace splits the queries into
@@ -229,33 +274,39 @@ def retrieve_leg(args, rank, world, dev, n_docs=DOCS_PER_SHARD, check_queries=20
     traffic, src = load_pmc_traffic("score_blocks_kernel<0>", leg) if leg else (None, None)
     if traffic is not None:
         traffic *= n_sb / max(args.steps, 1)
-    res["roofline"] = {
+    # HBM pricing by the algorithmic bytes (a side figure: the counters show the popular
+    # lists served from L2 / MALL -- PMC traffic below -- so this ceiling does not bind):
+    # 4 B per posting (the device word (doc_in_block << 10 | value) ^ X) and the 5 B of
+    # the reference's on-disk record (inverted_index.py:18-29)
+    hbm = {
         "kernel": "score_blocks_kernel<0>",
-        # priced against HBM by the algorithmic bytes, but the counters show the popular
-        # lists served from L2 / MALL (PMC traffic below); the limit is the scatter's
-        # posting-load instructions (a duplicated 4-byte load costs +56%, a duplicated
-        # 16-byte load per 4 postings +21%) and its LDS read-modify-write
-        "bound": "vmem_issue+lds",
-        "priced_against": "hbm",
+        "bound": "hbm_priced_not_binding",
         "achieved": round(achieved, 1),
+        "achieved_at_5B_per_posting": round(achieved * 1.25, 1),
         "peak": HBM_PEAK_GBS,
         "unit": "GB/s",
         "frac": round(achieved / HBM_PEAK_GBS, 4),
+        "frac_at_5B_per_posting": round(1.25 * achieved / HBM_PEAK_GBS, 4),
         "traffic": traffic,
         "algorithmic_bytes_per_step": bytes_per_launch,
-        "score_blocks_ms_per_step": round(avg_s * 1000.0, 4),
-        "launches": n_sb,
+        "algorithmic_bytes_per_step_5B": 5.0 * post_per_launch,
         "traffic_source": src,
     }
-    # the scatter's own ceiling: one conflict-free ds_read_b32 (2 LDS cycles per wave) +
-    # ds_write_b32 (4) per 64 postings on each CU (MI355X_MICROARCH.md "LDS" table)
+    # the scatter's own ceiling (the headline roofline of the retrieve legs): one
+    # conflict-free ds_read_b32 (2 LDS cycles per wave) + ds_write_b32 (4) per 64
+    # postings on each CU (MI355X_MICROARCH.md "LDS" table)
     lds_peak = LDS_CUS * LDS_CLOCK_HZ / LDS_CYCLES_PER_64_POSTINGS * 64.0
     posts_per_s = post_per_launch / avg_s if avg_s > 0 else 0.0
-    lds = {"kernel": "score_blocks_kernel<0>", "bound": "lds_rmw",
+    lds = {"kernel": "score_blocks_kernel<0>", "bound": "lds",
            "achieved": round(posts_per_s / 1e12, 4), "peak": round(lds_peak / 1e12, 4),
            "unit": "Tpostings/s", "frac": round(posts_per_s / lds_peak, 4),
+           "traffic": traffic,
            "model": f"{LDS_CYCLES_PER_64_POSTINGS:g} LDS cycles per 64 postings (ds_read_b32 2 + "
-                    f"ds_write_b32 4) x {LDS_CUS} CUs x {LDS_CLOCK_HZ / 1e9:g} GHz"}
+                    f"ds_write_b32 4) x {LDS_CUS} CUs x {LDS_CLOCK_HZ / 1e9:g} GHz",
+           "postings_per_step": post_per_launch,
+           "score_blocks_ms_per_step": round(avg_s * 1000.0, 4),
+           "launches": n_sb,
+           "hbm_priced": hbm}
     pmc = load_pmc_counters("score_blocks_kernel<0>", leg) if leg else None
     if pmc:
         for c in ("SQ_LDS_BANK_CONFLICT", "SQ_LDS_IDX_ACTIVE", "GRBM_GUI_ACTIVE"):
@@ -265,12 +316,14 @@ def retrieve_leg(args, rank, world, dev, n_docs=DOCS_PER_SHARD, check_queries=20
             lds["bank_conflict_share"] = round(pmc[0]["SQ_LDS_BANK_CONFLICT"] /
                                                max(pmc[0]["SQ_LDS_IDX_ACTIVE"], 1.0), 4)
         lds["counters_source"] = pmc[1]
-    res["lds_roofline"] = lds
+    res["roofline"] = lds
     return res, (term_off, pdoc - np.uint32(doc_lo), pval, queries,
                  out_doc, out_score, out_n)
 
 
 MFMA_BF16_PEAK_TFLOPS = 2500.0  # MI355X dense bf16 (MI355X_MICROARCH.md; no sparsity)
+MFMA_F32_PEAK_TFLOPS = 157.3  # f32 MFMA (the fp32 leg)
+NOMINAL_CLOCK_GHZ = 2.4  # the clock the peaks are quoted at
 
 
 def synthetic_state_dict(cfg, seed=0):
@@ -348,10 +401,12 @@ def prune_last_layer():
     return True
 
 
-def encode_leg(args, rank, world, dev, precision="bf16"):
+def encode_leg(args, rank, world, dev, precision="bf16", steps=None):
     """precision "bf16": the throughput mode configs[1] names; "bf16x3": the
     fp32-faithful mode (split-bf16 GEMMs, f32 attention / LayerNorm; impacts within
-    1e-3 of the fp32 reference -- tests/test_encoder_bf16x3_gpu.py)."""
+    1e-3 of the fp32 reference -- tests/test_encoder_bf16x3_gpu.py); "fp32": f32 MFMA
+    throughout (the exactness side leg).  steps: timed steps (default: --steps)."""
+    n_steps = args.steps if steps is None else steps
     from improving_learned_index_amd.encoder import DeviceEncoder, EncoderConfig
 
     t0 = time.time()
@@ -385,7 +440,7 @@ def encode_leg(args, rank, world, dev, precision="bf16"):
         dist.barrier()
     torch.cuda.synchronize()
     t1 = time.perf_counter()
-    for _ in range(args.steps):
+    for _ in range(n_steps):
         step(True)
     torch.cuda.synchronize()
     if dist.is_initialized():
@@ -398,13 +453,14 @@ def encode_leg(args, rank, world, dev, precision="bf16"):
     for name in ("embed_ln", "gemm_qkv", "attention", "gemm_o", "ln", "gemm_ffn1", "gemm_ffn2",
                  "row_ln", "head", "gather_terms"):
         ms, n = enc.timing(name)
-        kernels[name] = {"ms_per_step": ms / max(args.steps, 1), "launches": n}
+        kernels[name] = {"ms_per_step": ms / max(n_steps, 1), "launches": n}
     M, H, F, L = float(cu[-1]), cfg.hidden, cfg.intermediate, cfg.layers
     # rows per launch, averaged over the L launches of a step: the pruned last layer runs
     # O / FFN1 / FFN2 on the T term rows (QKV on all M)
     T = float(ct[-1])
     split = precision == "bf16x3"
-    prune = prune_last_layer()
+    f32 = precision == "fp32"
+    prune = prune_last_layer() and not f32  # (the fp32 mode computes every row)
     Mp = ((L - 1) * M + T) / L if prune else M
     gemm_flops = {"gemm_qkv": 2 * M * H * 3 * H, "gemm_o": 2 * Mp * H * H,
                   "gemm_ffn1": 2 * Mp * H * F, "gemm_ffn2": 2 * Mp * F * H}
@@ -422,31 +478,74 @@ def encode_leg(args, rank, world, dev, precision="bf16"):
     pmc_name = {"gemm_qkv": "gemm256_kernel<5,%s>", "gemm_ffn1": "gemm256_kernel<6,%s>",
                 "gemm_o": "gemm256_kernel<7,%s>",
                 "gemm_ffn2": "gemm256_kernel<7,%s>"}[dom] % ("true" if split else "false")
+    if f32:
+        pmc_name = "gemm_nt_kernel<f32>"  # (the 128-tile f32 MFMA GEMM)
     traffic, src = load_pmc_traffic(pmc_name, "encode_x3" if split else "encode")
+    pmc = load_pmc_counters(pmc_name, "encode_x3" if split else "encode")
+    eff_ghz = None
+    if pmc and pmc[0].get("GRBM_GUI_ACTIVE") and avg > 0:
+        # GRBM_GUI_ACTIVE counts GPU-busy cycles summed over the 8 XCDs; over the
+        # launch's time (this run's) it is the clock the kernel held
+        eff_ghz = pmc[0]["GRBM_GUI_ACTIVE"] / 8.0 / avg / 1e9
     # bf16x3: algorithmic (fp32) FLOPs against the split scheme's own peak -- three
     # bf16 MFMA products per fp32 product, 2500 / 3 TF/s (the f32 MFMA peak is 157.3)
-    peak = MFMA_BF16_PEAK_TFLOPS / 3.0 if split else MFMA_BF16_PEAK_TFLOPS
+    peak = (MFMA_F32_PEAK_TFLOPS if f32 else
+            MFMA_BF16_PEAK_TFLOPS / 3.0 if split else MFMA_BF16_PEAK_TFLOPS)
     # executed FLOPs (the pruned last layer skips the rows no output reads)
     model_flops = float(flops_per_doc(lens, t=np.diff(ct) if prune else None).sum())
-    docs_per_s = world * args.docs * args.steps / el
+    docs_per_s = world * args.docs * n_steps / el
     res = {
         "value": docs_per_s,
-        "ms_per_step": 1000.0 * el / args.steps,
+        "ms_per_step": 1000.0 * el / n_steps,
+        "steps": n_steps,
         "tokens_per_step": int(cu[-1]),
         "kernels": kernels,
         "gemm_tflops": {k: round(v[2], 1) for k, v in per_launch.items()},
         # digest of the last step's impacts: kernel changes that claim bit-identical
         # outputs are checked by comparing it across builds (seeded weights and docs)
         "out_sha1": hashlib.sha1(out.cpu().numpy().tobytes()).hexdigest(),
-        "model_tflops": round(model_flops * args.steps / el / 1e12 * 1.0, 1),
-        "model_flops_frac": round(model_flops * args.steps / el / 1e12 / peak, 4),
+        "model_tflops": round(model_flops * n_steps / el / 1e12 * 1.0, 1),
+        "model_flops_frac": round(model_flops * n_steps / el / 1e12 / peak, 4),
         "roofline": {"kernel": f"{pmc_name} ({dom})", "bound": "mfma",
                      "achieved": round(tf, 1), "peak": round(peak, 1), "unit": "TFLOP/s",
                      "frac": round(tf / peak, 4), "traffic": traffic,
+                     "effective_clock_ghz": round(eff_ghz, 3) if eff_ghz else None,
+                     "peak_clock_ghz": NOMINAL_CLOCK_GHZ,
+                     "frac_at_effective_clock": (round(tf / (peak * eff_ghz / NOMINAL_CLOCK_GHZ), 4)
+                                                 if eff_ghz else None),
+                     "clock_source": (f"GRBM_GUI_ACTIVE / 8 of {pmc[1]} over this run's "
+                                      f"average launch time") if eff_ghz else None,
                      "traffic_source": src, "algorithmic_flops_per_launch": f, "avg_launch_ms": round(avg * 1000, 4),
                      "launches": enc.timing(dom)[1]},
     }
     return res, (sd, cfg, ids, cu, lens, tt, ct, out)
+
+
+# bf16x3 against the torch fp32 oracle (oracle/encoder_ref.py, CPU, padded batches):
+# tests/test_encoder_bf16x3_gpu.py::test_flip_rates_vs_torch_fp32_oracle, 512
+# bench-shaped docs (21 409 terms), GPUTEST_r04 / profiles/round4_z9_pytest_gpu.log
+ORACLE_FLIPS = {"text_flip_rate": 2.48e-3, "quantized_flip_rate": 2.80e-4, "max_rel": 2.5e-5,
+                "fp32_mode_text_flip_rate": 3.3e-4, "fp32_mode_quantized_flip_rate": 4.7e-5,
+                "source": "tests/test_encoder_bf16x3_gpu.py::test_flip_rates_vs_torch_fp32_oracle "
+                          "(512 bench-shaped docs vs oracle/encoder_ref.py fp32; DESIGN.md §0 row 8)"}
+
+
+def flip_rates(out_x3, out_f32):
+    """bf16x3 vs the fp32 mode over one bench step's impacts (same seeded docs and
+    weights): the 3-decimal texts (A9: the round3 f32 values print differently iff they
+    differ) and the 8-bit integers quantize.py writes (int(v * 255 / max), fp64, each
+    run quantized by its own max; indexing/quantize.py:31-44)."""
+    a = out_x3.cpu().numpy().astype(np.float64)
+    b = out_f32.cpu().numpy().astype(np.float64)
+    n = min(a.size, b.size)
+    a, b = a[:n], b[:n]
+    qa = np.trunc(a * (255.0 / a.max())) if n and a.max() > 0 else a
+    qb = np.trunc(b * (255.0 / b.max())) if n and b.max() > 0 else b
+    rel = np.abs(a - b) / np.maximum(np.abs(b), 1e-3)
+    return {"terms": int(n), "text_flip_rate": float((a != b).mean()) if n else 0.0,
+            "quantized_flip_rate": float((qa != qb).mean()) if n else 0.0,
+            "max_rel": float(rel.max()) if n else 0.0,
+            "vs_torch_fp32_oracle": ORACLE_FLIPS}
 
 
 def cpu_baseline_encode(args, sd, cfg, ids, cu, lens, tt, ct, out):
@@ -691,9 +790,12 @@ def main():
                     help="index_e2e leg: --process_batch_size (reference default 1600)")
     ap.add_argument("--text-docs", type=int, default=1_100_000,
                     help="text legs (quantize, index_create): docs of the impact TSV")
-    ap.add_argument("--legs", default="encode_x3,encode,retrieve,retrieve_shard,text,index_e2e",
+    ap.add_argument("--legs", default="encode_x3,encode,encode_fp32,retrieve,retrieve_shard,text,"
+                                      "index_e2e",
                     help="encode_x3 (fp32-faithful bf16x3: the headline), encode (bf16 throughput "
-                         "mode), retrieve (100k-doc shard, configs[1]), retrieve_shard (1.1M docs: "
+                         "mode), encode_fp32 (f32 MFMA: the exactness side leg, with the bf16x3 "
+                         "flip rates against it), retrieve (100k-doc shard, configs[1]), "
+                         "retrieve_shard (1.1M docs: "
                          "one 8-way shard of configs[2]), retrieve_full (8.8M docs on one GPU, "
                          "configs[2]), text (quantize + index_create of a 1.1M-doc impact TSV), "
                          "index_e2e (index.py's path end to end, tokenizer workers included)")
@@ -748,6 +850,14 @@ def main():
         x3_res, x3_ctx = encode_leg(args, rank, world, dev, precision="bf16x3")
     if "encode" in legs:
         enc_res, enc_ctx = encode_leg(args, rank, world, dev)
+    f32_res = None
+    if "encode_fp32" in legs:
+        # the exactness side leg: f32 MFMA throughout (fewer timed steps: ~5x the bf16x3
+        # step time), and the bf16x3 flips against it on the same docs
+        f32_res, f32_ctx = encode_leg(args, rank, world, dev, precision="fp32",
+                                      steps=max(1, args.steps // 4))
+        if x3_res is not None:
+            f32_res["exactness"] = flip_rates(x3_ctx[-1], f32_ctx[-1])
     # (profiling ablations of the scorer, DI_PROFILE_ABLATE, change its results)
     n_check = 0 if os.environ.get("DI_PROFILE_ABLATE") else 20
     if "retrieve" in legs:
@@ -789,7 +899,8 @@ def main():
                    "docs_per_step_per_gpu": args.docs, "max_length": args.max_len,
                    "docs_per_shard": DOCS_PER_SHARD, "queries": args.queries, "k": args.k,
                    "parallelism": f"doc-sharded x{world} (encode: no collective; retrieve: "
-                                  f"RCCL all-gather of per-shard top-k)",
+                                  f"pruned exact two-round RCCL all-gather of per-shard top-k, "
+                                  f"parallel.exchange_topk)",
                    "encode_output": "term impacts (A8/A9 gather + round3); the last layer "
                                     "computes only the rows the gather reads -- bit-identical "
                                     "impacts, DESIGN.md §3" if prune_last_layer() else
@@ -806,6 +917,17 @@ def main():
             "ms_per_step": round(enc_res["ms_per_step"], 4),
             **{k: enc_res[k] for k in ("tokens_per_step", "kernels", "gemm_tflops", "model_tflops",
                                        "model_flops_frac", "roofline", "out_sha1")}}
+    if f32_res is not None:
+        out["encode_fp32"] = {
+            "value": round(f32_res["value"], 2), "unit": "docs/s", "dtype": "f32",
+            "precision": "f32 MFMA GEMMs and attention, f32 LayerNorm, every row of the last "
+                         "layer: the library's fp32 mode (index --precision fp32), the price of "
+                         "exactness beside the bf16x3 default",
+            "steps": f32_res["steps"], "ms_per_step": round(f32_res["ms_per_step"], 4),
+            **{k: f32_res[k] for k in ("kernels", "gemm_tflops", "model_tflops",
+                                       "model_flops_frac", "roofline", "out_sha1")}}
+        if "exactness" in f32_res:
+            out["encode_fp32"]["bf16x3_vs_fp32"] = f32_res["exactness"]
     if x3_res is not None:
         out["encode_fp32_faithful"] = {
             "value": round(x3_res["value"], 2), "unit": "docs/s", "dtype": "bf16x3",
@@ -822,7 +944,9 @@ def main():
                            "ms_per_step": round(ret_res["ms_per_step"], 4),
                            "postings_per_query": round(ret_res["postings_per_query"], 1),
                            "kernel_ms": ret_res["kernel_ms"], "roofline": ret_res["roofline"],
-                           "lds_roofline": ret_res["lds_roofline"], "cpu_baseline": None}
+                           "cpu_baseline": None}
+        if "exchange" in ret_res:
+            out["retrieve"]["exchange"] = ret_res["exchange"]
     if e2e_res is not None:
         out["index_e2e"] = e2e_res
     if text_res is not None:
@@ -833,8 +957,9 @@ def main():
                     "ms_per_step": round(r["ms_per_step"], 4),
                     "postings_per_query": round(r["postings_per_query"], 1),
                     "kernel_ms": r["kernel_ms"], "kernel_ms_per_step": r["kernel_ms_per_step"],
-                    "launches_per_step": r["launches_per_step"], "roofline": r["roofline"],
-                    "lds_roofline": r["lds_roofline"]}
+                    "launches_per_step": r["launches_per_step"], "roofline": r["roofline"]}
+        if "exchange" in r:
+            out[leg]["exchange"] = r["exchange"]
     if rank == 0 and world == 1 and not args.no_cpu:
         if x3_res is not None or enc_res is not None:
             cb = cpu_baseline_encode(args, *(x3_ctx if x3_res is not None else enc_ctx))

@@ -87,6 +87,8 @@ SIGNATURES = {
                                          P, P]),
     "di_synth_postings_skewed": (ctypes.c_int, [I64, I32, U64, I32, I32, ctypes.c_double, P, P,
                                                 P, P, I64, P, P]),
+    "di_synth_postings_shard": (ctypes.c_int, [I64, I64, I32, U64, I32, I32, ctypes.c_double,
+                                               P, ctypes.c_double, P, P, P, I64, P, P]),
     "di_synth_impact_tsv": (ctypes.c_int, [ctypes.c_char_p, I64, I32, U64, I32, I32,
                                            ctypes.c_double, P]),
 }

@@ -520,16 +520,17 @@ constexpr uint32_t IR_LONG = 1, IR_BAD = 2, IR_PLAIN = 4;
 constexpr uint32_t PK_MIN = 32;
 
 // Items (query q, block b) as the scorer numbers them (item = b * n_q + q); records
-// only for queries of 1..WTERMS terms (the scorer's per-wave form), WTERMS per item.
+// only for queries of 1..WTERMS terms (the scorer's per-wave form), rec_slots per item
+// (the batch's longest such query).
 __global__ void __launch_bounds__(128)
 item_setup_kernel(SubIndex si, int min_cls, int nb, int64_t n_terms,
                   const uint32_t *__restrict__ q_terms, const int32_t *__restrict__ cu_q, int n_q,
-                  ItemRec *__restrict__ rec, const uint16_t *__restrict__ border) {
+                  ItemRec *__restrict__ rec, const uint16_t *__restrict__ border, int rec_slots) {
     const int item = blockIdx.x, q = item % n_q, r_ = item / n_q;
     const int b = border ? (int)border[(int64_t)q * nb + r_] : r_;
     const int q0 = cu_q[q], nt = cu_q[q + 1] - q0;
-    if (nt > WTERMS || nt <= 0) return;
-    ItemRec *r = rec + (int64_t)item * WTERMS;
+    if (nt > rec_slots || nt <= 0) return;  // (rec_slots >= every per-wave query's terms)
+    ItemRec *r = rec + (int64_t)item * rec_slots;
     for (int e = threadIdx.x; e < nt * WSEG; e += blockDim.x) {
         const int j = e / WSEG, w = e % WSEG;
         const uint32_t t = q_terms[q0 + j];
@@ -1620,7 +1621,8 @@ score_blocks_kernel(const uint32_t *__restrict__ post, SubIndex si, int min_cls,
                     int n_q, uint32_t *__restrict__ qhist, int ablate,
                     const ItemRec *__restrict__ rec, uint32_t *__restrict__ long_flag,
                     float bm_factor, unsigned long long *__restrict__ bm_stat,
-                    const uint16_t *__restrict__ border, uint32_t *__restrict__ qtq) {
+                    const uint16_t *__restrict__ border, uint32_t *__restrict__ qtq,
+                    int rec_slots) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     ScoreShared &sh = *reinterpret_cast<ScoreShared *>(smem);
     if ((uint32_t)(uintptr_t)((__attribute__((address_space(3))) unsigned char *)smem) != 0) {
@@ -1641,7 +1643,7 @@ score_blocks_kernel(const uint32_t *__restrict__ post, SubIndex si, int min_cls,
                    min_cls, nb,
                    block_docs, n_terms,
                    n_docs, doc_lo, q_terms, cu_q, k, cand_key, cand_n, qhist, ablate,
-                   rec ? rec + (int64_t)item * WTERMS : nullptr, long_flag, bm_factor, qtq);
+                   rec ? rec + (int64_t)item * rec_slots : nullptr, long_flag, bm_factor, qtq);
         __syncthreads();  // every wave is done with the LDS of this item
         // the item's threshold into the query's running one, here rather than inside the
         // selection: qtq and the value read at the item's start need no registers across
@@ -2686,9 +2688,12 @@ int di_index_search(di_index *ix, const uint32_t *q_terms, const int32_t *cu_q, 
         hipStream_t s = ix->stream;
         if (n_q == 0) return;
         int64_t nterms_total = 0;
+        int max_nt = WTERMS;  // record slots per item (device pointers: the per-wave maximum)
         if (!dev) {
+            max_nt = 1;
             for (int q = 0; q < n_q; ++q) {
                 int32_t c = cu_q[q + 1] - cu_q[q];
+                max_nt = std::max(max_nt, (int)c);
                 DI_REQUIRE(c >= 0, DI_EINVAL, "cu_q not monotone at %d", q);
                 DI_REQUIRE(c <= DI_MAX_QUERY_TERMS, DI_ERANGE,
                            "query %d has %d terms (limit %d)", q, c, DI_MAX_QUERY_TERMS);
@@ -2708,10 +2713,18 @@ int di_index_search(di_index *ix, const uint32_t *q_terms, const int32_t *cu_q, 
         // (DI_CAND_WS_MIB overrides, A/B).  A 1 GiB cap cut 8.8 M-doc batches into 14
         // chunks of 499 queries, whose merge launches had ~2 workgroups per CU
         // (round-4 DESIGN §4).
+        // The item records (item_setup_kernel) take rec_slots per item -- the batch's
+        // longest query up to WTERMS (~6 for MS MARCO queries, 64 with device-pointer
+        // queries) -- and are capped at twice the candidate cap, which bounds the chunk
+        // too: one setting (DI_CAND_WS_MIB) sizes both.  Peak workspace of a handle
+        // ~3x the cap.
+        const int rec_slots = std::min(std::max(max_nt, 1), WTERMS);
         const int64_t per_q = (int64_t)nb * k * 8;
+        const int64_t rec_per_q = (int64_t)nb * rec_slots * (int64_t)sizeof(ItemRec);
         int64_t ws_cap = 4ll << 30;
         if (const char *e = std::getenv("DI_CAND_WS_MIB")) ws_cap = std::max(1ll, std::atoll(e)) << 20;
-        const int chunk = (int)std::max<int64_t>(1, std::min<int64_t>(n_q, ws_cap / per_q));
+        const int chunk = (int)std::max<int64_t>(
+            1, std::min<int64_t>({(int64_t)n_q, ws_cap / per_q, 2 * ws_cap / rec_per_q}));
         ix->ws_ck.reserve((size_t)chunk * per_q);
         ix->ws_cn.reserve((size_t)chunk * nb * 4);
         ix->ws_thr.reserve((size_t)chunk * QH_BINS * 4);
@@ -2720,11 +2733,10 @@ int di_index_search(di_index *ix, const uint32_t *q_terms, const int32_t *cu_q, 
             ix->bm_stat.reserve(16);
             DI_HIP(hipMemsetAsync(ix->bm_stat.p, 0, 16, s));
         }
-        // (only the records of real terms are written / read: ~6 per query)
-        // (bounded: WTERMS slots per item; a search whose records would pass 8 GiB -- a
-        // small k leaves chunks of many queries -- walks the chain in the scorer instead)
-        const size_t rec_bytes = (size_t)chunk * nb * WTERMS * sizeof(ItemRec);
-        const bool use_rec = !(ix->ablate & 1024) && rec_bytes <= (size_t(8) << 30);
+        // (DI_PROFILE_ABLATE bit 1024: no records -- the scorer walks the chain itself, A/B
+        // and the fallback test)
+        const size_t rec_bytes = (size_t)chunk * rec_per_q;
+        const bool use_rec = !(ix->ablate & 1024);
         if (use_rec) ix->ws_rec.reserve(rec_bytes);
         const uint32_t *dq = (const uint32_t *)stage_in(
             q_terms, (size_t)nterms_total * 4, dev, ix->ws_q, s);
@@ -2756,6 +2768,8 @@ int di_index_search(di_index *ix, const uint32_t *q_terms, const int32_t *cu_q, 
                 TimedLaunch tl(ix->timer, timing, "score_blocks", s);  // (both kernels)
                 const int n_items = nq * nb;
                 // packed postings (configs[4]): exact scoring from the item records only
+                // (records always fit: the chunk is bounded by them; ablate bit 1024 turns
+                // them off, and the packed layout with them)
                 const bool pk = ix->packed && ix->pk_built && ix->min_cls >= 7 && use_rec;
                 // block-max: blocks in descending order of their bound per query, opt-in
                 // (DI_BLOCK_ORDER=1): it raises the running threshold sooner but gives up
@@ -2780,7 +2794,7 @@ int di_index_search(di_index *ix, const uint32_t *q_terms, const int32_t *cu_q, 
                 if (use_rec) {
                     hipLaunchKernelGGL(item_setup_kernel, dim3(n_items), dim3(128), 0, s,
                                        ix->sub(pk), ix->min_cls, nb, ix->n_terms, dq, dcu + q0, nq,
-                                       ix->ws_rec.as<ItemRec>(), border);
+                                       ix->ws_rec.as<ItemRec>(), border, rec_slots);
                     check_launch("item_setup");
                 }
                 // (DI_PROFILE_ABLATE bit 65536: the block-max instantiation with block-max
@@ -2806,7 +2820,7 @@ int di_index_search(di_index *ix, const uint32_t *q_terms, const int32_t *cu_q, 
                                    use_rec ? ix->ws_rec.as<ItemRec>() : nullptr,
                                    ix->ws_long.as<uint32_t>(), thr ? ix->bm_factor : 0.0f,
                                    ix->bm_stat.as<unsigned long long>(), border,
-                                   use_qtq ? ix->ws_tq.as<uint32_t>() : nullptr);
+                                   use_qtq ? ix->ws_tq.as<uint32_t>() : nullptr, rec_slots);
                 check_launch("score_blocks");
                 hipLaunchKernelGGL(score_long_kernel, dim3(std::min(n_items, n_cu())),
                                    dim3(SC_THREADS), sizeof(ScoreShared), s,

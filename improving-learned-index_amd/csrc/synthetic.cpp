@@ -216,6 +216,17 @@ extern "C" int di_synth_impact_tsv(const char *path, int64_t n_docs, int32_t v_t
     });
 }
 
+extern "C" int di_synth_postings_skewed(int64_t n_docs, int32_t v_terms, uint64_t seed,
+                                        int32_t max_terms, int32_t draws, double zipf_a,
+                                        const di_synth_skew *skew, int64_t *term_off,
+                                        uint32_t *pdoc, uint8_t *pval, int64_t cap,
+                                        int64_t *n_post, double *max_impact) {
+    const int rc = di::guard([&] { DI_REQUIRE(term_off, DI_EINVAL, "bad argument"); });
+    if (rc != DI_OK) return rc;
+    return di_synth_postings_shard(0, n_docs, v_terms, seed, max_terms, draws, zipf_a, skew, 0.0,
+                                   term_off, pdoc, pval, cap, n_post, max_impact);
+}
+
 extern "C" int di_synth_postings(int64_t n_docs, int32_t v_terms, uint64_t seed,
                                  int32_t max_terms, int32_t draws, double zipf_a,
                                  int64_t *term_off, uint32_t *pdoc, uint8_t *pval, int64_t cap,
@@ -224,15 +235,16 @@ extern "C" int di_synth_postings(int64_t n_docs, int32_t v_terms, uint64_t seed,
                                     term_off, pdoc, pval, cap, n_post, max_impact);
 }
 
-extern "C" int di_synth_postings_skewed(int64_t n_docs, int32_t v_terms, uint64_t seed,
-                                        int32_t max_terms, int32_t draws, double zipf_a,
-                                        const di_synth_skew *skew, int64_t *term_off,
-                                        uint32_t *pdoc, uint8_t *pval, int64_t cap,
-                                        int64_t *n_post, double *max_impact) {
+extern "C" int di_synth_postings_shard(int64_t doc0, int64_t n_docs, int32_t v_terms,
+                                       uint64_t seed, int32_t max_terms, int32_t draws,
+                                       double zipf_a, const di_synth_skew *skew, double quant_max,
+                                       int64_t *term_off, uint32_t *pdoc, uint8_t *pval,
+                                       int64_t cap, int64_t *n_post, double *max_impact) {
     using namespace di;
     return guard([&] {
-        DI_REQUIRE(n_docs >= 0 && n_docs <= 0xFFFFFFFFll && v_terms > 0 && max_terms > 0 &&
-                       draws > 0 && zipf_a > 1.0 && term_off && n_post,
+        DI_REQUIRE(n_docs >= 0 && doc0 >= 0 && doc0 + n_docs <= 0xFFFFFFFFll && v_terms > 0 &&
+                       max_terms > 0 && draws > 0 && zipf_a > 1.0 && quant_max >= 0.0 &&
+                       (term_off || !pdoc) && (n_post || !term_off),
                    DI_EINVAL, "bad argument");
         Skew sk;
         if (skew) {
@@ -269,7 +281,7 @@ extern "C" int di_synth_postings_skewed(int64_t n_docs, int32_t v_terms, uint64_
                 std::vector<uint32_t> terms;
                 std::vector<float> imps;
                 for (int64_t d = d0; d < d1; ++d) {
-                    synth_doc(zipf, seed, d, max_terms, draws, buf, terms, imps, sk);
+                    synth_doc(zipf, seed, doc0 + d, max_terms, draws, buf, terms, imps, sk);
                     for (size_t i = 0; i < terms.size(); ++i) {
                         vt.push_back(terms[i]);
                         vi.push_back(imps[i]);
@@ -280,13 +292,17 @@ extern "C" int di_synth_postings_skewed(int64_t n_docs, int32_t v_terms, uint64_
                 c_max[(size_t)c] = mx;
             }
         });
-        // 2. global max of the 3-decimal impacts (fp64 as the quantizer) and the scale
+        // 2. max of the 3-decimal impacts (fp64 as the quantizer) and the scale: the
+        // shard's own, or quant_max (> 0: the collection's max, all shards alike)
         float mxf = 0.0f;
         for (float m : c_max) mxf = std::max(mxf, m);
-        const double m = (double)mxf;
+        if (max_impact) *max_impact = (double)mxf;
+        if (!term_off) return;  // max only
+        const double m = quant_max > 0.0 ? quant_max : (double)mxf;
         DI_REQUIRE(m > 0.0 || n_docs == 0, DI_EINVAL, "max impact is 0");
+        DI_REQUIRE(m >= (double)mxf, DI_EINVAL, "quant_max %g below the shard's max %g", m,
+                   (double)mxf);
         const double scale = 255.0 / (m > 0.0 ? m : 1.0);
-        if (max_impact) *max_impact = m;
         // 3. kept postings per term (quantized value > 0)
         std::vector<int64_t> c_doc0((size_t)n_chunks + 1, 0);
         for (int64_t c = 0; c < n_chunks; ++c) c_doc0[(size_t)c + 1] = n_docs * (c + 1) / n_chunks;

@@ -45,6 +45,7 @@ class InvertedIndex:
         self._dev = DeviceIndex.from_reference_dir(self.index_path, doc_lo, doc_hi, device)
         self.set_min_impact(min_impact)
         self.set_block_max(block_max)
+        self.packed = False
         self.packed_bytes = self.set_packed(packed) if packed else 0
 
     def set_min_impact(self, min_impact: int) -> None:

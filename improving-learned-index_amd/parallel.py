@@ -5,9 +5,11 @@
 * Quantize: the scale needs the global max (quantize.py:31-37): one
   all_reduce(MAX) of an fp64 scalar, then every shard quantizes with that max.
 * Retrieve: every rank scores every query on its shard and keeps a local top-k
-  of unique 64-bit keys; one all_gather of (keys, counts) -- RCCL over xGMI with
-  the nccl backend -- and a GPU merge (di_topk_merge) give exactly the
-  single-shard result, because the keys totally order (score, first touch, doc).
+  of unique 64-bit keys; a pruned two-round all_gather of them (exchange_topk: a
+  sample of every list, then each rank's keys above the bound the samples give)
+  -- RCCL over xGMI with the nccl backend -- and a GPU merge
+  (di_topk_merge) give exactly the single-shard result, because the keys totally
+  order (score, first touch, doc).
 
 The exchange is written against torch.distributed so it runs over RCCL on
 MI355X and over gloo in the CPU tests (tests/test_distributed_cpu.py).
@@ -34,12 +36,58 @@ def force_dist() -> bool:
     return os.environ.get("DI_FORCE_DIST") == "1" and "MASTER_ADDR" in os.environ
 
 
-def visible_gpus() -> int:
-    """GPUs this process sees, counted without initialising HIP (torch's count reads
-    the device list only; HIP must not come up in a parent that spawns ranks)."""
-    import torch
+def _kfd_gpu_nodes(root="/sys/class/kfd/kfd/topology/nodes", dri="/dev/dri") -> Optional[int]:
+    """GPU nodes of the KFD topology (nodes with SIMDs) whose render node this process
+    can open, or None without a topology."""
+    root = Path(root)
+    if not root.is_dir():
+        return None
+    n = 0
+    for node in root.iterdir():
+        try:
+            props = dict(line.split() for line in (node / "properties").read_text().splitlines()
+                         if len(line.split()) == 2)
+        except (OSError, ValueError):
+            continue
+        if int(props.get("simd_count", "0")) <= 0:
+            continue
+        # a GPU this process may open (a container can list every GPU of the host in the
+        # topology yet expose only some render nodes): a plain open() of its render node,
+        # no HIP call
+        minor = props.get("drm_render_minor")
+        if minor is not None:
+            try:
+                os.close(os.open(f"{dri}/renderD{minor}", os.O_RDWR))
+            except OSError:
+                continue
+        n += 1
+    return n
 
-    return torch.cuda.device_count()
+
+def _env_device_list(name: str) -> Optional[int]:
+    v = os.environ.get(name)
+    if v is None:
+        return None
+    v = v.strip()
+    return 0 if v in ("", "-1") else len([x for x in v.split(",") if x.strip()])
+
+
+def visible_gpus() -> int:
+    """GPUs this process sees, counted without the HIP runtime: a parent that spawns
+    ranks must not bring HIP up (torch.cuda.device_count() may fall back to
+    hipGetDeviceCount when amdsmi is missing).  HIP_VISIBLE_DEVICES /
+    CUDA_VISIBLE_DEVICES / ROCR_VISIBLE_DEVICES restrict the KFD topology's GPU nodes
+    (sysfs); without a topology, torch's count."""
+    n = _kfd_gpu_nodes()
+    if n is None:
+        import torch
+
+        return torch.cuda.device_count()
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        m = _env_device_list(var)
+        if m is not None:
+            n = min(n, m)
+    return n
 
 
 def ranks_to_spawn(requested: Optional[int]) -> int:
@@ -265,6 +313,98 @@ def quantize_sharded(input_path, output_path, max_val, world: int, rank: int,
     return m
 
 
+_SIGN = -(1 << 63)  # int64 view of a u64 key XOR this = the keys' unsigned order
+
+
+def exchange_topk(key, cnt, k: int, group=None, stats: Optional[dict] = None):
+    """Exact, pruned all-gather of every rank's top-k key lists (SURVEY §8e retrieve).
+
+    key: [n_q * k] int64 tensor (u64 merge keys; each query's list sorted descending, its
+    first cnt[q] valid), cnt: [n_q] int32 (negative: the scorer rejected the query).
+    Returns (g_key [world * n_q * k], g_n [world * n_q]) in a plain all_gather's rank-
+    major layout, holding per rank and query a prefix of its list that contains every
+    key able to reach the global top-k: di_topk_merge over it gives exactly the merge of
+    the full lists.
+
+    Round 1 gathers a sample of every list: the keys at positions g-1, 2g-1, ... (g keys
+    apart).  A rank whose j-th sample is >= t holds >= j g keys >= t, so with s = ceil(k/g)
+    samples >= T_q across the ranks at least k keys are >= T_q: T_q, the s-th largest
+    sample, is a lower bound of the global k-th key.  Round 2 gathers each rank's keys
+    >= T_q (counts, then a padded all_gather).  A plain gather moves k keys per query and
+    rank; this one k / g samples + the rank's share of the keys >= T_q (k + O(world g)
+    of them over all ranks).  The keys are unique (they carry the doc), so the pruning
+    is exact: /root/reference/src/deep_impact/evaluation/ranker.py:43-48 keeps the top
+    1000 per query, which the merge reproduces.
+    stats (optional dict): gathered_keys_per_query (sent by this rank, padding
+    included), bytes_sent.
+    """
+    import torch
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group)
+    nq = cnt.numel()
+    dev = key.device
+    K = key.view(nq, k)
+    g = max(1, min(64, k // (4 * world)))
+    if world == 1 or g == 1:  # (a sample of every key: the plain gather)
+        gk = torch.empty(world * nq * k, dtype=torch.int64, device=dev)
+        gc = torch.empty(world * nq, dtype=torch.int32, device=dev)
+        dist.all_gather_into_tensor(gk, K.reshape(-1).contiguous(), group=group)
+        dist.all_gather_into_tensor(gc, cnt.contiguous(), group=group)
+        if stats is not None:
+            stats["gathered_keys_per_query"] = float(k)
+            stats["bytes_sent"] = 8 * nq * k + 4 * nq
+        return gk, gc
+    c = cnt.to(torch.int64).clamp(0, k)
+    lo = torch.iinfo(torch.int64).min
+    s_n = k // g  # samples per list (positions g-1, ..., s_n g - 1 < k)
+    pos = torch.arange(1, s_n + 1, device=dev) * g - 1
+    smp = torch.where(pos[None, :] < c[:, None], K[:, pos] ^ _SIGN,
+                      torch.full((nq, s_n), lo, dtype=torch.int64, device=dev))
+    g1 = torch.empty(world * nq * s_n, dtype=torch.int64, device=dev)
+    dist.all_gather_into_tensor(g1, smp.reshape(-1).contiguous(), group=group)
+    allS = g1.view(world, nq, s_n).permute(1, 0, 2).reshape(nq, world * s_n)
+    need = -(-k // g)
+    if world * s_n >= need and nq:
+        T = torch.topk(allS, need, dim=1).values[:, need - 1]  # (lo when too few samples)
+    else:
+        T = torch.full((nq,), lo, dtype=torch.int64, device=dev)
+    # round 2: this rank's keys >= T_q (a prefix: lists are sorted)
+    ar_k = torch.arange(k, device=dev)
+    sel = (ar_k[None, :] < c[:, None]) & ((K ^ _SIGN) >= T[:, None])
+    e = sel.sum(1)
+    packed = K[sel]
+    ge = torch.empty(world * nq, dtype=torch.int32, device=dev)
+    dist.all_gather_into_tensor(ge, e.to(torch.int32), group=group)
+    gew = ge.view(world, nq).to(torch.int64)
+    tot = gew.sum(1)
+    emax = int(tot.max().item()) if nq else 0
+    out = torch.empty(world, nq, k, dtype=torch.int64, device=dev)
+    if emax:
+        buf = torch.zeros(emax, dtype=torch.int64, device=dev)
+        buf[:packed.numel()] = packed
+        g2 = torch.empty(world * emax, dtype=torch.int64, device=dev)
+        dist.all_gather_into_tensor(g2, buf, group=group)
+        g2 = g2.view(world, emax)
+        ar_q = torch.arange(nq, device=dev)
+        for r in range(world):
+            er = gew[r]
+            n_r = int(tot[r].item())
+            if n_r == 0:
+                continue
+            qi = torch.repeat_interleave(ar_q, er)
+            off = torch.cumsum(er, 0) - er
+            out[r, qi, torch.arange(n_r, device=dev) - off[qi]] = g2[r, :n_r]
+    gc = torch.empty(world * nq, dtype=torch.int32, device=dev)
+    dist.all_gather_into_tensor(gc, cnt.contiguous(), group=group)
+    gcw = gc.view(world, nq)
+    g_n = torch.where(gcw < 0, gcw, gew.to(torch.int32))
+    if stats is not None:
+        stats["gathered_keys_per_query"] = (s_n + emax / max(nq, 1)) if nq else 0.0
+        stats["bytes_sent"] = 8 * (nq * s_n + emax) + 4 * 2 * nq
+    return out.view(-1), g_n.view(-1)
+
+
 class ShardedRetriever:
     """Global top-k over doc-id shards held by the ranks of a process group.
 
@@ -301,12 +441,8 @@ class ShardedRetriever:
         world = dist.get_world_size(self.group)
         kt = torch.from_numpy(np.ascontiguousarray(keys).view(np.int64)).to(self.device)
         ct = torch.from_numpy(np.ascontiguousarray(counts, np.int32)).to(self.device)
-        # rank-major concatenation along dim 0 (the layout both RCCL and gloo take)
-        gk = torch.empty((world * kt.shape[0],) + tuple(kt.shape[1:]), dtype=kt.dtype,
-                         device=kt.device)
-        gc = torch.empty((world * ct.shape[0],), dtype=ct.dtype, device=ct.device)
-        dist.all_gather_into_tensor(gk, kt, group=self.group)
-        dist.all_gather_into_tensor(gc, ct, group=self.group)
+        # the pruned exact exchange, in the rank-major layout of a plain all_gather
+        gk, gc = exchange_topk(kt.reshape(-1), ct, self.k, group=self.group)
         gk = gk.cpu().numpy().view(np.uint64).reshape((world,) + tuple(kt.shape))
         gc = gc.cpu().numpy().reshape(world, -1)
         mk, mn = self.merge(gk, gc, self.k)
@@ -360,10 +496,9 @@ def _exchange_merge(index, queries, k, device, dev, stream, flags):
     key, cnt = (out_key, out_n) if gpu_exchange else (out_key.cpu(), out_n.cpu())
     if not gpu_exchange:
         torch.cuda.synchronize(dev)
-    g_key = torch.empty(world * key.numel(), dtype=key.dtype, device=key.device)
-    g_n = torch.empty(world * cnt.numel(), dtype=cnt.dtype, device=cnt.device)
-    dist.all_gather_into_tensor(g_key, key)
-    dist.all_gather_into_tensor(g_n, cnt)
+    # the pruned exact exchange (a plain all_gather's layout, only the keys that can
+    # reach the global top-k filled in)
+    g_key, g_n = exchange_topk(key[:nq * k], cnt[:nq], k)
     if nq == 0:
         return np.zeros((0, k), np.uint64), np.zeros(0, np.int32)
     m_key = torch.empty(nq * k, dtype=torch.int64, device=dev)

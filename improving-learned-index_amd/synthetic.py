@@ -31,12 +31,15 @@ def msmarco_like_docs(n_docs=100_000, v_terms=200_000, seed=1234, max_terms=100)
     return cu, np.concatenate(terms).astype(np.uint32), np.concatenate(imps)
 
 
-def quantize_like_reference(imp_f32, bits=8):
+def quantize_like_reference(imp_f32, bits=8, max_val=None):
     """Impact TSV text -> quantize.py semantics, without the text round trip:
     the 3-decimal float32 prints as the shortest repr of its double, which
-    float() reads back exactly."""
+    float() reads back exactly.  max_val: the collection's max (a doc-id shard
+    quantized like the whole, quantize.py:31-37), default this array's."""
     v = round3_f32(imp_f32).astype(np.float64)
     m = float(v.max()) if v.size else 0.0
+    if max_val is not None:
+        m = float(max_val)
     scale = ((1 << bits) - 1) / m
     return np.trunc(v * scale).astype(np.int64), m
 
@@ -84,13 +87,16 @@ SKEW_CONFIG4 = {"term_rank0": 2000.0, "term_exp": 0.5, "cluster_docs": 4096,
 
 
 def synth_postings(n_docs, v_terms=200_000, seed=1234, max_terms=100, draws=200, zipf_a=1.2,
-                   skew=None):
+                   skew=None, doc0=0, quant_max=0.0):
     """The same generator at full scale, in the HIP library's host code (threads over
     doc chunks, a counter-based stream per doc): reference-order postings
     (term_off, pdoc u32, pval u8) of the quantized collection and the fp64 max impact.
     Same distribution as msmarco_like_docs -> quantize_like_reference ->
     postings_reference_order; a different random stream (seconds at 8.8 M docs).
-    skew: a dict of di_synth_skew fields (e.g. SKEW_CONFIG4), None = i.i.d. impacts."""
+    skew: a dict of di_synth_skew fields (e.g. SKEW_CONFIG4), None = i.i.d. impacts.
+    doc0 / quant_max: docs [doc0, doc0 + n_docs) of the seed's collection (local doc
+    ids), quantized with quant_max (> 0: the collection's max) -- one doc-id shard; the
+    returned max is the shard's own (synth_max_impact: that alone)."""
     import ctypes
 
     from ._lib import check, di_synth_skew, lib, ptr
@@ -102,10 +108,27 @@ def synth_postings(n_docs, v_terms=200_000, seed=1234, max_terms=100, draws=200,
     n = ctypes.c_int64(0)
     m = ctypes.c_double(0.0)
     sk = ctypes.byref(di_synth_skew(**skew)) if skew else None
-    check(lib().di_synth_postings_skewed(int(n_docs), int(v_terms), int(seed), int(max_terms),
-                                         int(draws), float(zipf_a), sk, ptr(term_off), ptr(pdoc),
-                                         ptr(pval), cap, ctypes.byref(n), ctypes.byref(m)))
+    check(lib().di_synth_postings_shard(int(doc0), int(n_docs), int(v_terms), int(seed),
+                                        int(max_terms), int(draws), float(zipf_a), sk,
+                                        float(quant_max), ptr(term_off), ptr(pdoc), ptr(pval), cap,
+                                        ctypes.byref(n), ctypes.byref(m)))
     return term_off, pdoc[:n.value], pval[:n.value], m.value
+
+
+def synth_max_impact(n_docs, v_terms=200_000, seed=1234, max_terms=100, draws=200, zipf_a=1.2,
+                     skew=None, doc0=0):
+    """The max 3-decimal impact of docs [doc0, doc0 + n_docs) of synth_postings' collection
+    (no postings built): each shard's input to the all_reduce(MAX) of a sharded run."""
+    import ctypes
+
+    from ._lib import check, di_synth_skew, lib
+
+    m = ctypes.c_double(0.0)
+    sk = ctypes.byref(di_synth_skew(**skew)) if skew else None
+    check(lib().di_synth_postings_shard(int(doc0), int(n_docs), int(v_terms), int(seed),
+                                        int(max_terms), int(draws), float(zipf_a), sk, 0.0, None,
+                                        None, None, 0, None, ctypes.byref(m)))
+    return m.value
 
 
 def synth_impact_tsv(path, n_docs, v_terms=200_000, seed=1234, max_terms=100, draws=200,

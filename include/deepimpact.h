@@ -320,6 +320,18 @@ int di_synth_postings_skewed(int64_t n_docs, int32_t v_terms, uint64_t seed, int
                              int64_t *term_off, uint32_t *pdoc, uint8_t *pval, int64_t cap,
                              int64_t *n_post, double *max_impact);
 
+/* Docs [doc0, doc0 + n_docs) of the seeded collection di_synth_postings_skewed generates
+ * for seed (each doc depends only on (seed, doc id)): one doc-id shard of it, doc ids
+ * local (0-based).  quant_max > 0 quantizes with that max (the collection's: the
+ * all_reduce(MAX) of the shards' maxima, as the sharded quantize CLI does) instead of the
+ * shard's own; term_off null: only *max_impact (the shard's max) is computed.  Bench and
+ * test input of the multi-rank retrieve legs. */
+int di_synth_postings_shard(int64_t doc0, int64_t n_docs, int32_t v_terms, uint64_t seed,
+                            int32_t max_terms, int32_t draws, double zipf_a,
+                            const di_synth_skew *skew, double quant_max, int64_t *term_off,
+                            uint32_t *pdoc, uint8_t *pval, int64_t cap, int64_t *n_post,
+                            double *max_impact);
+
 /* The same seeded collection as the impact TSV of the index CLI (indexer.py:62-68),
  * term id t spelled "\u2581t<t>": bench input of the quantize / index-create legs.
  * *n_terms receives the (doc, term) pairs written. */

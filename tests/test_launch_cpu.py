@@ -87,3 +87,32 @@ def test_hip_runtime_guard_maps_torchs_runtime_first():
     r = _run(["-c", code])
     assert r.returncode == 0, r.stderr[-2000:]
     assert "OK" in r.stdout
+
+
+def test_visible_gpus_counts_kfd_nodes_without_hip(tmp_path, monkeypatch):
+    """The CLIs' fan-out count comes from the KFD topology and the render nodes this
+    process can open (no HIP call), restricted by the *_VISIBLE_DEVICES lists."""
+    from improving_learned_index_amd import parallel
+
+    topo, dri = tmp_path / "nodes", tmp_path / "dri"
+    dri.mkdir()
+    for i, (simds, minor) in enumerate([(0, None), (304, 128), (304, 129), (304, 130)]):
+        d = topo / str(i)
+        d.mkdir(parents=True)
+        props = f"cpu_cores_count 8\nsimd_count {simds}\n"
+        if minor is not None:
+            props += f"drm_render_minor {minor}\n"
+        (d / "properties").write_text(props)
+    for minor in (128, 129):  # renderD130 is not exposed to this "container"
+        (dri / f"renderD{minor}").write_text("")
+    assert parallel._kfd_gpu_nodes(topo, dri) == 2
+    assert parallel._kfd_gpu_nodes(tmp_path / "absent", dri) is None
+    monkeypatch.setattr(parallel, "_kfd_gpu_nodes", lambda: 2)
+    monkeypatch.delenv("HIP_VISIBLE_DEVICES", raising=False)
+    monkeypatch.delenv("CUDA_VISIBLE_DEVICES", raising=False)
+    monkeypatch.delenv("ROCR_VISIBLE_DEVICES", raising=False)
+    assert parallel.visible_gpus() == 2
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "1")
+    assert parallel.visible_gpus() == 1
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "")
+    assert parallel.visible_gpus() == 0

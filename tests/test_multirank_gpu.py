@@ -208,6 +208,11 @@ def test_bench_gpus_flag_launches_ranks_itself():
     d = json.loads(line[0])
     assert d["n_gpus"] == 2 and d["ranks_seen"] == 2 and d["backend"] == "gloo"
     assert d["value"] > 0
+    # the pruned exact exchange: each rank sends its first k / 2 keys + the extras above
+    # the union's k-th (verdict r04: <= 0.6 k keys per query and rank)
+    x = d["retrieve"]["exchange"]
+    assert x["gathered_keys_per_query"] <= 0.6 * d["config"]["k"], x
+    assert x["collective_ms_per_step"] > 0
 
 
 def test_bench_single_rank_rccl_path():
@@ -229,3 +234,14 @@ def test_bench_single_rank_rccl_path():
     assert d["backend"] == "nccl" and d["ranks_seen"] == 1 and d["n_gpus"] == 1
     assert d["value"] > 0 and d["retrieve_shard"]["value"] > 0
     assert "the first 20 queries equal the oracle" in r.stderr
+    assert d["retrieve"]["exchange"]["gathered_keys_per_query"] <= d["config"]["k"]
+
+
+def test_visible_gpus_matches_the_runtime():
+    """The CLIs' runtime-free GPU count (KFD topology + openable render nodes) agrees
+    with the HIP runtime's on this box."""
+    import torch
+
+    from improving_learned_index_amd import parallel
+
+    assert parallel.visible_gpus() == torch.cuda.device_count()

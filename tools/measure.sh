@@ -12,6 +12,8 @@
 #           SWEEP_VARIANTS (default new; old = the baseline build, ablate<N> = DI_PROFILE_ABLATE=N)
 #   phases  scorer phase stamps (DI_PROFILE_ABLATE=PHASE_ABLATE, default 64) via
 #           tools/phase_prune.py PHASE_ARGS
+#   scorer_pmc  PMC passes (SCORER_PMC: counter groups split by '|') over
+#           tools/phase_prune.py PHASE_ARGS -> spmc/summary.json
 #   stats   rocprofv3 --kernel-trace --stats per leg, each leg ALONE (STAT_LEGS), so every
 #           average in a CSV is that leg's -> stats_<leg>/run_kernel_stats.csv
 #   pmc     PMC passes per leg (PMC_LEGS) through tools/pmc_legs.sh
@@ -58,6 +60,20 @@ PY
       (cd "$R" && DI_PROFILE_ABLATE=${PHASE_ABLATE:-64} timeout -k 10 ${PHASE_TIMEOUT:-500} python3 -u \
          tools/phase_prune.py ${PHASE_ARGS:-} > "$O/phases.txt" 2>&1)
       rc=$?; tail -20 "$O/phases.txt"; [ $rc -eq 0 ] || exit $rc ;;
+    scorer_pmc)
+      # PMC passes (one counter group each, --kernel-trace only) over tools/phase_prune.py
+      # PHASE_ARGS; the synthetic collection is cached in /tmp between passes
+      IFS='|' read -r -a GRPS <<< "${SCORER_PMC:-SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA|SQC_ICACHE_MISSES SQC_ICACHE_HITS SQ_IFETCH SQ_INSTS_VMEM SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VALU GRBM_GUI_ACTIVE}"
+      i=0; mkdir -p "$O/spmc"
+      for grp in "${GRPS[@]}"; do
+        i=$((i+1))
+        (cd /tmp && export TMPDIR=/tmp && SYNTH_CACHE=/tmp/di_synth timeout -k 10 ${PASS_TIMEOUT:-400} \
+           rocprofv3 -M --pmc $grp --kernel-trace -d "$O/spmc/p$i" -o run --output-format csv -- \
+           python3 "$R/tools/phase_prune.py" ${PHASE_ARGS:-8800000 128 skew} > "$O/spmc/p$i.txt" 2>&1)
+        rc=$?; [ $rc -eq 0 ] || { tail -20 "$O/spmc/p$i.txt"; exit $rc; }
+        echo "scorer pmc pass $i done"
+      done
+      python3 "$R/tools/pmc_summary.py" "$O/spmc" > "$O/spmc/summary.json" || exit 1 ;;
     stats)
       for leg in ${STAT_LEGS:-encode_x3 retrieve retrieve_shard}; do
         (cd /tmp && export TMPDIR=/tmp && timeout -k 10 ${STAT_TIMEOUT:-400} rocprofv3 --kernel-trace --stats \

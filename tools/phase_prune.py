@@ -16,8 +16,25 @@ n_docs, mi = int(sys.argv[1]), int(sys.argv[2])
 skew = len(sys.argv) > 3 and sys.argv[3] == "skew"
 bm = float(sys.argv[4]) if len(sys.argv) > 4 else 0.0
 nq, k = 6980, 1000
-term_off, pdoc, pval, _ = S.synth_postings(n_docs, 2 * n_docs, seed=4321,
-                                           skew=S.SKEW_CONFIG4 if skew else None)
+def collection():
+    """The synthetic collection; SYNTH_CACHE=<dir> keeps it as .npy files between runs
+    (the PMC passes of tools/measure.sh run this script once per counter group)."""
+    import os
+    import numpy as np
+    cache = os.environ.get("SYNTH_CACHE")
+    tag = f"{n_docs}_{'skew' if skew else 'iid'}"
+    if cache and os.path.exists(f"{cache}/{tag}_pval.npy"):
+        return tuple(np.load(f"{cache}/{tag}_{n}.npy") for n in ("term_off", "pdoc", "pval"))
+    t_off, pd, pv, _ = S.synth_postings(n_docs, 2 * n_docs, seed=4321,
+                                        skew=S.SKEW_CONFIG4 if skew else None)
+    if cache:
+        os.makedirs(cache, exist_ok=True)
+        for n, a in (("term_off", t_off), ("pdoc", pd), ("pval", pv)):
+            np.save(f"{cache}/{tag}_{n}.npy", a)
+    return t_off, pd, pv
+
+
+term_off, pdoc, pval = collection()
 flat, cuq = _lib.csr(S.msmarco_like_queries(nq, 2 * n_docs, seed=1234))
 ix = _lib.DeviceIndex.from_postings(term_off, pdoc, pval, 0, n_docs)
 ix.reserve(nq, k)
