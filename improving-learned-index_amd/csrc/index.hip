@@ -737,7 +737,7 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
                                            uint32_t *__restrict__ qhist, int ablate,
                                            const ItemRec *__restrict__ ir,
                                            uint32_t *__restrict__ long_flag, float bm_factor,
-                                           uint32_t *__restrict__ qtq) {
+                                           uint32_t *__restrict__ qtq, int kl) {
     int64_t *lo = sh.v.bounds[0], *hi = sh.v.bounds[1];
 
     // opaque per item: keeps the per-thread index arithmetic of the sweeps from being
@@ -748,7 +748,7 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
     const int64_t block_first = (int64_t)b * block_docs;
     const int n_local = (int)min((int64_t)block_docs, (int64_t)n_docs - block_first);
     const int q0 = cu_q[q], nt = cu_q[q + 1] - q0;
-    uint64_t *ck = cand_key + ((int64_t)q * nb + b) * k;
+    uint64_t *ck = cand_key + ((int64_t)q * nb + b) * kl;
     int32_t *cn = cand_n + (int64_t)q * nb + b;
 
     if (nt > MAX_TERMS && nt <= LONG_TERMS) {  // score_long_kernel's item (it runs next)
@@ -794,8 +794,9 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
     // (thread 0 alone loads it and publishes it through LDS at the setup barrier: waves
     // that read the word themselves could see different values -- other CUs raise it --
     // and disagree on skipping, i.e. on which barriers they reach)
+    // (few blocks, no qhist: the same word bounds the emit-above selection, see below)
     uint32_t tq_early = 0;
-    if (bm && qtq && threadIdx.x == 0)
+    if ((bm || !qhist) && qtq && threadIdx.x == 0)
         tq_early = __hip_atomic_load(&qtq[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     // The query's shared threshold histogram (qhist, below) is copied by LDS-DMA into
     // the selection histogram (idle until the selection) here, so its round trip
@@ -899,7 +900,7 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
         }
         zero();
     }
-    if (EXT != 0 && tid == 0) sh.tqe = tq_early;
+    if ((EXT != 0 || qtq) && tid == 0) sh.tqe = tq_early;
     __syncthreads();
     if (sh.bad) {
         // (the histogram copy lands before the next item touches the histogram)
@@ -1196,13 +1197,21 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
     // there and copied out coalesced (a lane-scattered 8-byte store per candidate slot
     // costs a store instruction per slot and wave); else they go straight out.
     const int n4z = (n_local + 3) >> 2;
-    uint64_t *stage = reinterpret_cast<uint64_t *>(sh.acc + 4 * n4z);
-    const bool staged = 2 * k <= MAX_BLOCK_DOCS - 4 * n4z;
+    const bool tail_fits = 2 * k <= MAX_BLOCK_DOCS - 4 * n4z;
+    uint64_t *const acc_tail = reinterpret_cast<uint64_t *>(sh.acc + 4 * n4z);
+    // (full blocks leave no tail: the one-sweep selections below stage in the histogram
+    // area instead, free by then -- otherwise the flush re-read the keys from global
+    // memory, a round trip per item at 1.1 M / 8.8 M docs)
+    uint64_t *const hist_stage = reinterpret_cast<uint64_t *>(sh.u.hist);
+    static_assert(sizeof(ScoreShared().u) >= (size_t)HIST_BINS * 4, "histogram stage");
+    const bool hist_fits = (uint32_t)k * 8u <= (uint32_t)HIST_BINS * 4u;
+    uint64_t *stage = tail_fits ? acc_tail : nullptr;  // null: straight to ck
+    uint32_t cap = (uint32_t)k;  // list capacity of the current selection (emit-above: kl)
     auto cand = [&](uint32_t pos, uint32_t w, int idx) {
         const uint32_t doc = (uint32_t)(doc_base + (uint64_t)idx);
         const uint64_t key = ((uint64_t)w << 32) | (uint64_t)(0xFFFFFFFFu - doc);
-        if (pos < (uint32_t)k) {
-            if (staged)
+        if (pos < cap) {
+            if (stage)
                 stage[pos] = key;
             else
                 ck[pos] = key;
@@ -1215,8 +1224,8 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
         // next item's record loads -- issued by the first waves -- do not wait for their
         // acknowledgements behind them in the in-order vmcnt)
         for (uint32_t i = (uint32_t)(SC_THREADS - 1 - tid); i < n_c; i += SC_THREADS) {
-            const uint64_t key = staged ? stage[i] : ck[i];
-            if (staged) ck[i] = key;
+            const uint64_t key = stage ? stage[i] : ck[i];
+            if (stage) ck[i] = key;
             if (qh) atomicAdd(&qh[min((uint32_t)(key >> 48), (uint32_t)QH_BINS - 1)], 1u);
         }
     };
@@ -1239,6 +1248,41 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
     // (all queries' block 0 first), so Tq is close to the final k-th score after the
     // first blocks and the later blocks emit few candidates.  A stale (smaller) count
     // still gives a valid lower bound.
+    // Emit-above (few blocks: no qhist, a list capacity kl > k): the query's running
+    // threshold T1 (qtq = the largest k-th score of its finished blocks' full selections,
+    // read at the item's start) is a lower bound of its final k-th score, so only this
+    // block's docs scoring >= T1 can reach the top-k.  When at most kl of them do, one
+    // append sweep emits them all -- no histogram, no tie order, no compaction (the merge
+    // orders by key); else the full selection below runs (and raises qtq).  Items are
+    // block-major, so every block after a query's first finds the first block's k-th
+    // score: at 100 k docs (4 blocks) ~k docs of each pass it, <= kl = 2 k.
+    if (!qh && qtq && kl > k && !(ablate & 2097152)) {
+        const uint32_t T1 = sh.tqe;  // (written before the setup barrier)
+        if (T1 > 0) {
+            const bool tail_kl = 2 * kl <= MAX_BLOCK_DOCS - 4 * n4z;
+            if (!tail_kl && (uint32_t)kl * 8u <= (uint32_t)HIST_BINS * 4u) stage = hist_stage;
+            else if (!tail_kl) stage = nullptr;
+            cap = (uint32_t)kl;
+            const uint32_t thr_w = T1 << 16;
+            sweep_words(sh.acc, n_local, tid, [&](uint32_t w, int idx) {
+                uint32_t pos;
+                if (wave_append<true>(w >= thr_w, &sh.emit, pos)) cand(pos, w, idx);
+            });
+            __syncthreads();
+            const uint32_t na = sh.emit;
+            if (na <= (uint32_t)kl) {
+                flush(na);
+                if (tid == 0) *cn = (int32_t)na;
+                return;
+            }
+            // (too many: the full selection, k keys; sh.emit is reset by the paths that use
+            // it -- the radix ties set it, the fast path's compaction does not read it)
+            cap = (uint32_t)k;
+            stage = tail_fits ? acc_tail : nullptr;
+            __syncthreads();  // every wave has read sh.emit
+            if (tid == 0) sh.emit = 0;
+        }
+    }
     uint32_t Tq = 0;
     if (qh) {
         // second half of read_tq over the suffix sums published by the scatter barrier:
@@ -1256,13 +1300,15 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
         }
         __syncthreads();
         Tq = sh.tq;
-        if (EXT != 0 && tid == 0) sh.tqn = max(sh.tqn, Tq);
+        if ((EXT != 0 || qtq) && tid == 0) sh.tqn = max(sh.tqn, Tq);
         stamp(8);  // threshold read (the part of tq-select before the sweep)
         // (wsum is written again only after a barrier of the selection below; tq only
         // at the next item's start)
         if (Tq > 0) {
             // one sweep: the docs reaching Tq (usually a few dozen) are appended by
             // wave-aggregated LDS atomics in any order (the merge orders them by key)
+            // (the histogram copy is consumed: its area stages the keys of a full block)
+            if (!tail_fits && hist_fits && !(ablate & 1048576)) stage = hist_stage;
             const uint32_t thr_w = Tq << 16;
             sweep_words(sh.acc, n_local, tid, [&](uint32_t w, int idx) {
                 uint32_t pos;
@@ -1276,6 +1322,7 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
                 if (tid == 0) *cn = (int32_t)na;
                 return;
             }
+            stage = tail_fits ? acc_tail : nullptr;  // (the selections below use the histogram)
         }
     }
 
@@ -1304,6 +1351,7 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
         }
         np = (uint32_t)__shfl(wave_prefix_sum(np), 63, 64);
         if (np <= (uint32_t)k) {
+            if (!tail_fits && hist_fits && !(ablate & 1048576)) stage = hist_stage;
             sweep_words(sh.acc, n_local, tid, [&](uint32_t w, int idx) {
                 uint32_t pos;
                 if (wave_append<true>(w != 0, &sh.emit, pos)) cand(pos, w, idx);
@@ -1369,7 +1417,7 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
         }
         // (this block alone has >= k docs scoring >= T: a lower bound of the query's final
         // k-th score for block-max, qtq)
-        if (EXT != 0 && tid == 0) sh.tqn = max(sh.tqn, sh.thr);
+        if ((EXT != 0 || qtq) && tid == 0) sh.tqn = max(sh.tqn, sh.thr);
         const uint32_t T = sh.thr, ties = sh.ties;  // T >= 1: every touched score is
         const uint32_t above = sh.above;             // nonzero
 
@@ -1540,7 +1588,7 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
                          });
     }
     const uint32_t T = prefix;
-    if (EXT != 0 && tid == 0) sh.tqn = max(sh.tqn, T >> 16);
+    if ((EXT != 0 || qtq) && tid == 0) sh.tqn = max(sh.tqn, T >> 16);
     const uint32_t ties = sh.u.rs.tot[sh.u.rs.bin];
 
     // doc-order cut among the ties: the `need` smallest doc indices
@@ -1622,7 +1670,7 @@ score_blocks_kernel(const uint32_t *__restrict__ post, SubIndex si, int min_cls,
                     const ItemRec *__restrict__ rec, uint32_t *__restrict__ long_flag,
                     float bm_factor, unsigned long long *__restrict__ bm_stat,
                     const uint16_t *__restrict__ border, uint32_t *__restrict__ qtq,
-                    int rec_slots) {
+                    int rec_slots, int kl) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     ScoreShared &sh = *reinterpret_cast<ScoreShared *>(smem);
     if ((uint32_t)(uintptr_t)((__attribute__((address_space(3))) unsigned char *)smem) != 0) {
@@ -1632,7 +1680,7 @@ score_blocks_kernel(const uint32_t *__restrict__ post, SubIndex si, int min_cls,
             if (threadIdx.x == 0) cand_n[item] = -1;
         return;
     }
-    if (EXT != 0 && threadIdx.x == 0) {  // (the first item's barriers publish them)
+    if (threadIdx.x == 0) {  // (the first item's barriers publish them)
         sh.bm_cnt[0] = sh.bm_cnt[1] = 0ull;
         sh.tqn = 0;
     }
@@ -1643,12 +1691,12 @@ score_blocks_kernel(const uint32_t *__restrict__ post, SubIndex si, int min_cls,
                    min_cls, nb,
                    block_docs, n_terms,
                    n_docs, doc_lo, q_terms, cu_q, k, cand_key, cand_n, qhist, ablate,
-                   rec ? rec + (int64_t)item * rec_slots : nullptr, long_flag, bm_factor, qtq);
+                   rec ? rec + (int64_t)item * rec_slots : nullptr, long_flag, bm_factor, qtq, kl);
         __syncthreads();  // every wave is done with the LDS of this item
         // the item's threshold into the query's running one, here rather than inside the
         // selection: qtq and the value read at the item's start need no registers across
         // the scatter (they cost the instantiation spills)
-        if (EXT != 0 && threadIdx.x == 0) {
+        if ((EXT != 0 || qtq) && threadIdx.x == 0) {
             const uint32_t t = sh.tqn;
             if (qtq && t > sh.tqe) atomicMax(&qtq[q], t);
             sh.tqn = 0;
@@ -1670,7 +1718,7 @@ score_long_kernel(const uint32_t *__restrict__ post, SubIndex si, int min_cls, i
                   int block_docs, int64_t n_terms, uint32_t n_docs, uint32_t doc_lo,
                   const uint32_t *__restrict__ q_terms, const int32_t *__restrict__ cu_q, int k,
                   uint64_t *__restrict__ cand_key, int32_t *__restrict__ cand_n, int n_q,
-                  const uint32_t *__restrict__ long_flag) {
+                  const uint32_t *__restrict__ long_flag, int kl) {
     if (__builtin_amdgcn_readfirstlane(*long_flag) == 0) return;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     ScoreShared &sh = *reinterpret_cast<ScoreShared *>(smem);
@@ -1696,7 +1744,7 @@ score_long_kernel(const uint32_t *__restrict__ post, SubIndex si, int min_cls, i
         for (int it = blockIdx.x; it < n_items; it += gridDim.x) {
             const int lq = (int)list[it % n], b = it / n;
             score_long_item(sh, lq, b, post, si, min_cls, nb, block_docs, n_terms, n_docs,
-                            doc_lo, q_terms, cu_q, k, cand_key + ((int64_t)lq * nb + b) * k,
+                            doc_lo, q_terms, cu_q, k, cand_key + ((int64_t)lq * nb + b) * kl,
                             cand_n + (int64_t)lq * nb + b);
             __syncthreads();  // the item's LDS (and the list) stay consistent
         }
@@ -1961,7 +2009,8 @@ merge_topk_kernel(const uint64_t *__restrict__ keys, const int32_t *__restrict__
 // MG_SEL_MIN candidates take a radix select over the registers and a sort of the take
 // winners in the same LDS.  Output identical to merge_topk_kernel (the keys are unique
 // and totally ordered).
-constexpr int MS_LISTS = 64, MS_U = 8;
+constexpr int MS_LISTS = 64;  // (MS_U: candidates per thread, 8, or 16 for the few-block
+                               // emit-above lists of up to 2 k keys)
 
 template <int THREADS>
 struct alignas(16) MergeSelHead {
@@ -1973,7 +2022,7 @@ struct alignas(16) MergeSelHead {
     uint32_t thr, above, cnt, pad;
 };
 
-template <int THREADS>
+template <int THREADS, int MS_U = 8>
 __global__ void __launch_bounds__(THREADS)
 merge_sel_kernel(const uint64_t *__restrict__ keys, const int32_t *__restrict__ counts,
                  int n_lists, int k_in, int k, int64_t list_stride, int64_t cnt_stride,
@@ -2146,6 +2195,12 @@ struct di_index {
     float bm_factor = 0.0f;          // block-max skipping: 0 off, 1 exact, > 1 approximate
     // postings and the sparse (term, block) entries (SubIndex)
     DevBuf post, tb_start, eblk, epos, seg, lid, wmeta, emax, wmax;
+    DevBuf post_flat;      // exact scoring: the per-wave runs dealt flat (build_index)
+    bool has_flat = false;
+    // the posting array a search reads: flat for exact scoring, class-ordered under pruning
+    const uint32_t *post_for(int mc) const {
+        return has_flat && mc >= 7 ? post_flat.as<uint32_t>() : post.as<uint32_t>();
+    }
     DevBuf ws_q, ws_cu, ws_ck, ws_cn, ws_doc, ws_score, ws_n, ws_key, ws_thr;
     DevBuf ws_rec;  // ItemRec per (item, term slot): item_setup_kernel -> score_blocks
     DevBuf ws_long;  // score_blocks -> score_long_kernel: the batch has long queries
@@ -2349,23 +2404,37 @@ void build_index(di_index *ix, const int64_t *term_off, int64_t n_terms, const u
     // deals for the 4-byte loads' lane-consecutive groups instead (A/B).
     bool deal_x4 = true;
     if (const char *e = std::getenv("DI_DEAL_X4")) deal_x4 = std::atoi(e) != 0;
+    // A second posting array for exact scoring, `flat`: the per-wave runs of long
+    // sublists dealt without the impact-class order.  Class boundaries leave each 32-lane
+    // set of a run with ~1.1 repeated LDS banks (a simulation of this dealing over i.i.d.
+    // runs of 300-1200 postings, tools/deal_sim.py), flat runs 0.26-0.68, and the scatter's
+    // reads conflict accordingly (PMC at 100 k docs: 0.45 of its LDS cycles).  Impact
+    // pruning keeps the class-ordered array, whose prefixes it scores.  Same offsets in both
+    // (a run is the same postings in another order); 4 B per posting more in HBM.
+    // DI_DEAL_CLASSES=1: one array, class-ordered (A/B).
+    bool flat_runs = true;
+    if (const char *e = std::getenv("DI_DEAL_CLASSES")) flat_runs = std::atoi(e) == 0;
+    std::vector<uint32_t> flat;
+    if (flat_runs) flat.resize(packed.size());
     parallel_for(n_terms, [&](int64_t t0, int64_t t1, int) {
         std::vector<uint32_t> grp, tmp, bk, seg_in, cls_cnt(8), cls_pos(8), bucket_cnt(32),
             head(32), fill(32);
         // one group (any order in): classes in order (stable), each dealt round-robin
         // from its 32 LDS bank buckets into packed[o..]; cum[c] = end of class c
         // relative to the sublist start s0
+        // one_class: dealt without class boundaries (the flat array's per-wave runs)
         auto emit_group = [&](const uint32_t *in, size_t n, int64_t &o, int64_t s0,
-                              uint16_t *cum) {
+                              uint16_t *cum, uint32_t *dst, bool one_class = false) {
+            auto cls_g = [&](uint32_t w) { return one_class ? 0 : cls_of(w); };
             std::fill(cls_cnt.begin(), cls_cnt.end(), 0);
-            for (size_t i = 0; i < n; ++i) cls_cnt[cls_of(in[i])]++;
+            for (size_t i = 0; i < n; ++i) cls_cnt[cls_g(in[i])]++;
             uint32_t run = 0;
             for (int c = 0; c < 8; ++c) {
                 cls_pos[c] = run;
                 run += cls_cnt[c];
             }
             tmp.resize(n);
-            for (size_t i = 0; i < n; ++i) tmp[cls_pos[cls_of(in[i])]++] = in[i];
+            for (size_t i = 0; i < n; ++i) tmp[cls_pos[cls_g(in[i])]++] = in[i];
             // The scorer's lanes take the group's postings in rounds from its start,
             // and a 32-lane group of its LDS updates is one set of 32 positions (by
             // 16-byte loads: p = 4 L + k of an aligned 128-block, one set per k; by
@@ -2396,7 +2465,7 @@ void build_index(di_index *ix, const int64_t *term_off, int64_t n_terms, const u
                     if (!cand) cand = avail;  // every bank left is taken in this block
                     const uint32_t rot = cursor ? (cand >> cursor) | (cand << (32 - cursor)) : cand;
                     const int k = (__builtin_ctz(rot) + cursor) & 31;
-                    packed[o++] = bk[head[k]++];
+                    dst[o++] = bk[head[k]++];
                     if (--bucket_cnt[k] == 0) avail &= ~(1u << k);
                     used |= 1u << k;
                     cursor = (k + 1) & 31;
@@ -2416,7 +2485,9 @@ void build_index(di_index *ix, const int64_t *term_off, int64_t n_terms, const u
                 int64_t o = s0;
                 const uint32_t id = lid[e];
                 if (id == NO) {
-                    emit_group(grp.data(), grp.size(), o, s0, sg);
+                    emit_group(grp.data(), grp.size(), o, s0, sg, packed.data());
+                    if (flat_runs)
+                        std::copy(packed.begin() + s0, packed.begin() + o, flat.begin() + s0);
                     continue;
                 }
                 {  // whole-sublist class counts (seg), then the per-wave layout
@@ -2433,14 +2504,23 @@ void build_index(di_index *ix, const int64_t *term_off, int64_t n_terms, const u
                             wm = std::max(wm, x & 255u);
                         }
                     wmax[(size_t)id * WSEG + w] = (uint8_t)wm;
+                    const int64_t ow = o;
                     emit_group(seg_in.data(), seg_in.size(), o, s0,
-                               &wmeta[(size_t)id * WSEG * 8 + w * 8]);
+                               &wmeta[(size_t)id * WSEG * 8 + w * 8], packed.data());
+                    if (flat_runs) {
+                        int64_t of = ow;
+                        emit_group(seg_in.data(), seg_in.size(), of, s0, nullptr, flat.data(),
+                                   true);
+                    }
                 }
             }
         }
     });
     for (auto &w : packed) w = (((w >> 8) << 10) | (w & 255u)) ^ POST_X;  // device encoding (see POST_X)
+    for (auto &w : flat) w = (((w >> 8) << 10) | (w & 255u)) ^ POST_X;
     upload(ix->post, packed);
+    if (flat_runs) upload(ix->post_flat, flat);
+    ix->has_flat = flat_runs;
     upload(ix->tb_start, tb_start);
     upload(ix->eblk, eblk);
     upload(ix->epos, epos);
@@ -2478,6 +2558,9 @@ void enable_big_lds() {
     DI_HIP(hipFuncSetAttribute((const void *)merge_topk_kernel<512>,
                                hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)(sizeof(MergeHead<512>) + MG_LDS_KEYS * 8)));
+    DI_HIP(hipFuncSetAttribute((const void *)merge_sel_kernel<512, 16>,
+                               hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)(sizeof(MergeSelHead<512>) + MG_SEL_KEYS * 8)));
     DI_HIP(hipFuncSetAttribute((const void *)merge_sel_kernel<512>,
                                hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)(sizeof(MergeSelHead<512>) + MG_SEL_KEYS * 8)));
@@ -2500,9 +2583,11 @@ void launch_merge(const uint64_t *keys, const int32_t *counts, int n_q, int n_li
         const char *e = std::getenv("DI_PROFILE_MERGE");
         return !(e && e[0] == '0');
     }();
-    if (sel_ok && n_lists <= MS_LISTS && (int64_t)n_lists * k_in <= (int64_t)MS_U * 512 &&
+    if (sel_ok && n_lists <= MS_LISTS && (int64_t)n_lists * k_in <= (int64_t)16 * 512 &&
         k <= MG_SEL_KEYS) {
-        hipLaunchKernelGGL(merge_sel_kernel<512>, dim3(n_q), dim3(512),
+        auto kern = (int64_t)n_lists * k_in <= (int64_t)8 * 512 ? merge_sel_kernel<512, 8>
+                                                                : merge_sel_kernel<512, 16>;
+        hipLaunchKernelGGL(kern, dim3(n_q), dim3(512),
                            sizeof(MergeSelHead<512>) + (size_t)MG_SEL_KEYS * 8, s, keys, counts,
                            n_lists, k_in, k, ls, cs, qs, cqs, out_key, out_doc, out_score, out_n,
                            mode, cu_q);
@@ -2668,7 +2753,9 @@ int di_index_reserve(di_index *ix, int32_t max_q, int32_t k) {
     return guard([&] {
         DI_REQUIRE(ix && max_q >= 0 && k > 0 && k <= DI_MAX_TOPK, DI_EINVAL, "bad argument");
         DeviceScope ds(ix->device);
-        size_t nbk = (size_t)max_q * std::max(ix->nb, 1) * k;
+        // (the few-block emit-above selection lists up to 2 k keys per item, see search)
+        const int kl = ix->nb >= 2 && ix->nb < 8 && 2 * k <= 2048 ? 2 * k : k;
+        size_t nbk = (size_t)max_q * std::max(ix->nb, 1) * kl;
         ix->ws_ck.reserve(nbk * 8);
         ix->ws_cn.reserve((size_t)max_q * std::max(ix->nb, 1) * 4);
     });
@@ -2719,7 +2806,13 @@ int di_index_search(di_index *ix, const uint32_t *q_terms, const int32_t *cu_q, 
         // too: one setting (DI_CAND_WS_MIB) sizes both.  Peak workspace of a handle
         // ~3x the cap.
         const int rec_slots = std::min(std::max(max_nt, 1), WTERMS);
-        const int64_t per_q = (int64_t)nb * k * 8;
+        // Few blocks (no shared qhist threshold, 2..7 blocks): the emit-above selection
+        // (score_item) lists up to kl = 2 k keys per (query, block) against the running
+        // threshold qtq (DI_PROFILE_ABLATE bit 2097152: off, A/B)
+        const bool few = ix->nb >= 2 && ix->nb < 8 && ix->shared_thr != 1 && 2 * k <= 2048 &&
+                         !(ix->ablate & 2097152);
+        const int kl = few ? 2 * k : k;
+        const int64_t per_q = (int64_t)nb * kl * 8;
         const int64_t rec_per_q = (int64_t)nb * rec_slots * (int64_t)sizeof(ItemRec);
         int64_t ws_cap = 4ll << 30;
         if (const char *e = std::getenv("DI_CAND_WS_MIB")) ws_cap = std::max(1ll, std::atoll(e)) << 20;
@@ -2786,7 +2879,7 @@ int di_index_search(di_index *ix, const uint32_t *q_terms, const int32_t *cu_q, 
                 }
                 const uint16_t *border = order ? ix->ws_border.as<uint16_t>() : nullptr;
                 // (DI_PROFILE_ABLATE bit 32768: the histogram-copy threshold instead, A/B)
-                const bool use_qtq = thr && ix->bm_factor > 0.0f && !(ix->ablate & 32768);
+                const bool use_qtq = (thr && ix->bm_factor > 0.0f && !(ix->ablate & 32768)) || few;
                 if (use_qtq) {
                     ix->ws_tq.reserve((size_t)nq * 4);
                     DI_HIP(hipMemsetAsync(ix->ws_tq.p, 0, (size_t)nq * 4, s));
@@ -2812,7 +2905,7 @@ int di_index_search(di_index *ix, const uint32_t *q_terms, const int32_t *cu_q, 
                                          : score_blocks_kernel<0>,
                                    dim3(std::min(n_items, n_cu())),
                                    dim3(SC_THREADS), sizeof(ScoreShared), s,
-                                   ix->post.as<uint32_t>(), ix->sub(pk),
+                                   ix->post_for(ix->min_cls), ix->sub(pk),
                                    ix->min_cls, nb, ix->block_docs, ix->n_terms,
                                    ix->n_docs, ix->doc_lo, dq, dcu + q0, k,
                                    ix->ws_ck.as<uint64_t>(), ix->ws_cn.as<int32_t>(), n_items,
@@ -2820,19 +2913,19 @@ int di_index_search(di_index *ix, const uint32_t *q_terms, const int32_t *cu_q, 
                                    use_rec ? ix->ws_rec.as<ItemRec>() : nullptr,
                                    ix->ws_long.as<uint32_t>(), thr ? ix->bm_factor : 0.0f,
                                    ix->bm_stat.as<unsigned long long>(), border,
-                                   use_qtq ? ix->ws_tq.as<uint32_t>() : nullptr, rec_slots);
+                                   use_qtq ? ix->ws_tq.as<uint32_t>() : nullptr, rec_slots, kl);
                 check_launch("score_blocks");
                 hipLaunchKernelGGL(score_long_kernel, dim3(std::min(n_items, n_cu())),
                                    dim3(SC_THREADS), sizeof(ScoreShared), s,
-                                   ix->post.as<uint32_t>(), ix->sub(),
+                                   ix->post_for(ix->min_cls), ix->sub(),
                                    ix->min_cls, nb, ix->block_docs, ix->n_terms, ix->n_docs,
                                    ix->doc_lo, dq, dcu + q0, k, ix->ws_ck.as<uint64_t>(),
-                                   ix->ws_cn.as<int32_t>(), nq, ix->ws_long.as<uint32_t>());
+                                   ix->ws_cn.as<int32_t>(), nq, ix->ws_long.as<uint32_t>(), kl);
                 check_launch("score_long");
             }
             {
                 TimedLaunch tl(ix->timer, timing, "merge_topk", s);
-                launch_merge(ix->ws_ck.as<uint64_t>(), ix->ws_cn.as<int32_t>(), nq, nb, k, k,
+                launch_merge(ix->ws_ck.as<uint64_t>(), ix->ws_cn.as<int32_t>(), nq, nb, kl, k,
                              dkey ? dkey + (int64_t)q0 * k : nullptr, ddoc + (int64_t)q0 * k,
                              dscore + (int64_t)q0 * k, dn + q0, DECODE_QUANT, s, false,
                              dcu + q0);

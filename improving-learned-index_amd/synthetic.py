@@ -108,10 +108,16 @@ def synth_postings(n_docs, v_terms=200_000, seed=1234, max_terms=100, draws=200,
     n = ctypes.c_int64(0)
     m = ctypes.c_double(0.0)
     sk = ctypes.byref(di_synth_skew(**skew)) if skew else None
-    check(lib().di_synth_postings_shard(int(doc0), int(n_docs), int(v_terms), int(seed),
-                                        int(max_terms), int(draws), float(zipf_a), sk,
-                                        float(quant_max), ptr(term_off), ptr(pdoc), ptr(pval), cap,
-                                        ctypes.byref(n), ctypes.byref(m)))
+    if doc0 == 0 and quant_max == 0.0:  # (the whole collection: also in older builds, A/B)
+        check(lib().di_synth_postings_skewed(int(n_docs), int(v_terms), int(seed), int(max_terms),
+                                             int(draws), float(zipf_a), sk, ptr(term_off),
+                                             ptr(pdoc), ptr(pval), cap, ctypes.byref(n),
+                                             ctypes.byref(m)))
+    else:
+        check(lib().di_synth_postings_shard(int(doc0), int(n_docs), int(v_terms), int(seed),
+                                            int(max_terms), int(draws), float(zipf_a), sk,
+                                            float(quant_max), ptr(term_off), ptr(pdoc), ptr(pval),
+                                            cap, ctypes.byref(n), ctypes.byref(m)))
     return term_off, pdoc[:n.value], pval[:n.value], m.value
 
 

@@ -27,5 +27,8 @@ for v in ${VARIANTS:-old new}; do
         wlong*) run $v DI_WLONG_MIN=${v#wlong} || exit 1 ;;
         b32) run $v DI_PROFILE_ABLATE=4096 DI_DEAL_X4=0 || exit 1 ;;  # 4-byte loads, 32-block dealing
         x4deal32) run $v DI_DEAL_X4=0 || exit 1 ;;                    # 16-byte loads, 32-block dealing
+        classes) run $v DI_DEAL_CLASSES=1 || exit 1 ;;                # one class-ordered posting array
+        nohs) run $v DI_PROFILE_ABLATE=1048576 || exit 1 ;;           # no histogram-area staging
+        noemit) run $v DI_PROFILE_ABLATE=2097152 || exit 1 ;;         # no few-block emit-above
     esac
 done
