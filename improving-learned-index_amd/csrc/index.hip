@@ -724,7 +724,9 @@ __device__ __forceinline__ void score_long_item(
 // stay exactly as without them), EXT_BM block-max skipping over the plain postings
 // (bm_factor, per-query block order, the cooperative form), EXT_PK the packed postings
 // (si.pk_fs; with or without block-max) -- one kernel each.
-constexpr int EXT_BM = 1, EXT_PK = 2;
+constexpr int EXT_BM = 1, EXT_PK = 2, EXT_FEW = 4;  // (EXT_FEW: the emit-above selection of
+                                                   // few-block shards, its own kernel so
+                                                   // the plain one keeps its code)
 template <int EXT>
 __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
                                            const uint32_t *__restrict__ post, const SubIndex &si,
@@ -787,7 +789,10 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
     // -- so no term needs a barrier; longer queries: the all-wave form, a barrier per term
     const bool wl = nt <= WTERMS && !(ablate & 524288);  // (bit 524288: the all-wave form, A/B)
     // block-max skipping (opt-in, configs[4]): per-wave segment upper bounds (wub)
-    const bool bm = EXT != 0 && bm_factor > 0.0f && wl && qhist != nullptr;
+    // (XBM: the block-max / packed instantiations; EXT_FEW is the plain scorer + the
+    // emit-above selection, with only the running-threshold bookkeeping of the others)
+    constexpr bool XBM = EXT == EXT_BM || EXT == EXT_PK;
+    const bool bm = XBM && bm_factor > 0.0f && wl && qhist != nullptr;
     // block-max: the query's running threshold as one word (qtq, raised by every item's
     // selection with a lower bound of the final k-th score), loaded with the setup's
     // loads -- the skip decision needs no histogram copy, no extra barrier
@@ -796,7 +801,7 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
     // and disagree on skipping, i.e. on which barriers they reach)
     // (few blocks, no qhist: the same word bounds the emit-above selection, see below)
     uint32_t tq_early = 0;
-    if ((bm || !qhist) && qtq && threadIdx.x == 0)
+    if ((bm || EXT == EXT_FEW) && qtq && threadIdx.x == 0)
         tq_early = __hip_atomic_load(&qtq[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     // The query's shared threshold histogram (qhist, below) is copied by LDS-DMA into
     // the selection histogram (idle until the selection) here, so its round trip
@@ -900,7 +905,7 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
         }
         zero();
     }
-    if ((EXT != 0 || qtq) && tid == 0) sh.tqe = tq_early;
+    if (EXT != 0 && tid == 0) sh.tqe = tq_early;
     __syncthreads();
     if (sh.bad) {
         // (the histogram copy lands before the next item touches the histogram)
@@ -1256,7 +1261,7 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
     // orders by key); else the full selection below runs (and raises qtq).  Items are
     // block-major, so every block after a query's first finds the first block's k-th
     // score: at 100 k docs (4 blocks) ~k docs of each pass it, <= kl = 2 k.
-    if (!qh && qtq && kl > k && !(ablate & 2097152)) {
+    if (EXT == EXT_FEW && !qh && qtq && kl > k) {
         const uint32_t T1 = sh.tqe;  // (written before the setup barrier)
         if (T1 > 0) {
             const bool tail_kl = 2 * kl <= MAX_BLOCK_DOCS - 4 * n4z;
@@ -1300,7 +1305,7 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
         }
         __syncthreads();
         Tq = sh.tq;
-        if ((EXT != 0 || qtq) && tid == 0) sh.tqn = max(sh.tqn, Tq);
+        if (EXT != 0 && tid == 0) sh.tqn = max(sh.tqn, Tq);
         stamp(8);  // threshold read (the part of tq-select before the sweep)
         // (wsum is written again only after a barrier of the selection below; tq only
         // at the next item's start)
@@ -1312,7 +1317,7 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
             const uint32_t thr_w = Tq << 16;
             sweep_words(sh.acc, n_local, tid, [&](uint32_t w, int idx) {
                 uint32_t pos;
-                if (wave_append<EXT != 0>(w >= thr_w, &sh.emit, pos)) cand(pos, w, idx);
+                if (wave_append<XBM>(w >= thr_w, &sh.emit, pos)) cand(pos, w, idx);
             });
             __syncthreads();
             const uint32_t na = sh.emit;
@@ -1417,7 +1422,7 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
         }
         // (this block alone has >= k docs scoring >= T: a lower bound of the query's final
         // k-th score for block-max, qtq)
-        if ((EXT != 0 || qtq) && tid == 0) sh.tqn = max(sh.tqn, sh.thr);
+        if (EXT != 0 && tid == 0) sh.tqn = max(sh.tqn, sh.thr);
         const uint32_t T = sh.thr, ties = sh.ties;  // T >= 1: every touched score is
         const uint32_t above = sh.above;             // nonzero
 
@@ -1540,7 +1545,7 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
                     const uint32_t i = i0 + tid;
                     const uint32_t x = i < ties ? tl[i] : 0u;
                     uint32_t pos;
-                    if (wave_append<EXT != 0>(i < ties && x >= tp, &sh.emit, pos))
+                    if (wave_append<XBM>(i < ties && x >= tp, &sh.emit, pos))
                         cand(pos, (T << 16) | (x >> 16), (int)(0xFFFFu - (x & 0xFFFFu)));
                 }
                 __syncthreads();
@@ -1588,7 +1593,7 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
                          });
     }
     const uint32_t T = prefix;
-    if ((EXT != 0 || qtq) && tid == 0) sh.tqn = max(sh.tqn, T >> 16);
+    if (EXT != 0 && tid == 0) sh.tqn = max(sh.tqn, T >> 16);
     const uint32_t ties = sh.u.rs.tot[sh.u.rs.bin];
 
     // doc-order cut among the ties: the `need` smallest doc indices
@@ -1680,14 +1685,14 @@ score_blocks_kernel(const uint32_t *__restrict__ post, SubIndex si, int min_cls,
             if (threadIdx.x == 0) cand_n[item] = -1;
         return;
     }
-    if (threadIdx.x == 0) {  // (the first item's barriers publish them)
+    if (EXT != 0 && threadIdx.x == 0) {  // (the first item's barriers publish them)
         sh.bm_cnt[0] = sh.bm_cnt[1] = 0ull;
         sh.tqn = 0;
     }
     // items block-major: item = b * n_q + q (the shared threshold, see score_item)
     for (int item = blockIdx.x; item < n_items; item += gridDim.x) {
         const int q = item % n_q, r_ = item / n_q;
-        score_item<EXT>(sh, q, EXT != 0 && border ? (int)border[(int64_t)q * nb + r_] : r_, post, si,
+        score_item<EXT>(sh, q, (EXT == EXT_BM || EXT == EXT_PK) && border ? (int)border[(int64_t)q * nb + r_] : r_, post, si,
                    min_cls, nb,
                    block_docs, n_terms,
                    n_docs, doc_lo, q_terms, cu_q, k, cand_key, cand_n, qhist, ablate,
@@ -1696,13 +1701,13 @@ score_blocks_kernel(const uint32_t *__restrict__ post, SubIndex si, int min_cls,
         // the item's threshold into the query's running one, here rather than inside the
         // selection: qtq and the value read at the item's start need no registers across
         // the scatter (they cost the instantiation spills)
-        if ((EXT != 0 || qtq) && threadIdx.x == 0) {
+        if (EXT != 0 && threadIdx.x == 0) {
             const uint32_t t = sh.tqn;
             if (qtq && t > sh.tqe) atomicMax(&qtq[q], t);
             sh.tqn = 0;
         }
     }
-    if (EXT != 0 && bm_stat && threadIdx.x == 0 && sh.bm_cnt[0]) {
+    if ((EXT == EXT_BM || EXT == EXT_PK) && bm_stat && threadIdx.x == 0 && sh.bm_cnt[0]) {
         atomicAdd(&bm_stat[0], sh.bm_cnt[0]);
         atomicAdd(&bm_stat[1], sh.bm_cnt[1]);
     }
@@ -2543,6 +2548,9 @@ void enable_big_lds() {
     DI_HIP(hipFuncSetAttribute((const void *)score_blocks_kernel<EXT_BM>,
                                hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)sizeof(ScoreShared)));
+    DI_HIP(hipFuncSetAttribute((const void *)score_blocks_kernel<EXT_FEW>,
+                               hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)sizeof(ScoreShared)));
     DI_HIP(hipFuncSetAttribute((const void *)score_blocks_kernel<EXT_PK>,
                                hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)sizeof(ScoreShared)));
@@ -2902,6 +2910,7 @@ int di_index_search(di_index *ix, const uint32_t *q_terms, const int32_t *cu_q, 
                                  (thr && ix->min_cls <= 3) || (ix->ablate & 65536);
                 hipLaunchKernelGGL(pk    ? score_blocks_kernel<EXT_PK>
                                    : ext ? score_blocks_kernel<EXT_BM>
+                                   : few ? score_blocks_kernel<EXT_FEW>
                                          : score_blocks_kernel<0>,
                                    dim3(std::min(n_items, n_cu())),
                                    dim3(SC_THREADS), sizeof(ScoreShared), s,
