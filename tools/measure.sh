@@ -44,7 +44,9 @@ for s in $STEPS; do
       for v in ${SWEEP_VARIANTS:-new}; do
         n=$(echo "${SWEEP_ARGS:-8800000 skew}" | tr ' ' '_')
         case $v in old) E="$OLD_ENV" ;; ablate*) E="DI_PROFILE_ABLATE=${v#ablate}" ;;
-          classes) E="DI_DEAL_CLASSES=1" ;; *) E="X=0" ;; esac
+          classes) E="DI_DEAL_CLASSES=1" ;;
+          mid) E="DEEPIMPACT_HIP_LIB=$R/tools/_mid/libdeepimpact_hip.so DI_LIB_ALLOW_MISSING=1" ;;
+          *) E="X=0" ;; esac
         (cd "$R" && env $E SWEEP=${SWEEP:-bm} timeout -k 10 ${SWEEP_TIMEOUT:-500} python3 -u \
            tools/prune_sweep.py ${SWEEP_ARGS:-8800000 skew} > "$O/sweep_${n}_$v.json" \
            2> "$O/sweep_${n}_$v.err") || { tail -5 "$O/sweep_${n}_$v.err"; exit 1; }
