@@ -271,7 +271,12 @@ def retrieve_leg(args, rank, world, dev, n_docs=DOCS_PER_SHARD, check_queries=20
     # leg's own summary, per launch -> per step
     leg = {DOCS_PER_SHARD: "retrieve", 1_100_000: "retrieve_shard",
            8_800_000: "retrieve_full"}.get(n_docs)
-    traffic, src = load_pmc_traffic("score_blocks_kernel<0>", leg) if leg else (None, None)
+    # the scorer instantiation this shard runs: shards of 2..7 blocks take the emit-above
+    # selection (score_blocks_kernel<4>, EXT_FEW), larger ones the plain kernel
+    nb = ix.info()["n_blocks"]
+    sb_kernel = ("score_blocks_kernel<4>" if 2 <= nb < 8 and 2 * k <= 2048
+                 else "score_blocks_kernel<0>")
+    traffic, src = load_pmc_traffic(sb_kernel, leg) if leg else (None, None)
     if traffic is not None:
         traffic *= n_sb / max(args.steps, 1)
     # HBM pricing by the algorithmic bytes (a side figure: the counters show the popular
@@ -279,7 +284,7 @@ def retrieve_leg(args, rank, world, dev, n_docs=DOCS_PER_SHARD, check_queries=20
     # 4 B per posting (the device word (doc_in_block << 10 | value) ^ X) and the 5 B of
     # the reference's on-disk record (inverted_index.py:18-29)
     hbm = {
-        "kernel": "score_blocks_kernel<0>",
+        "kernel": sb_kernel,
         "bound": "hbm_priced_not_binding",
         "achieved": round(achieved, 1),
         "achieved_at_5B_per_posting": round(achieved * 1.25, 1),
@@ -297,7 +302,7 @@ def retrieve_leg(args, rank, world, dev, n_docs=DOCS_PER_SHARD, check_queries=20
     # postings on each CU (MI355X_MICROARCH.md "LDS" table)
     lds_peak = LDS_CUS * LDS_CLOCK_HZ / LDS_CYCLES_PER_64_POSTINGS * 64.0
     posts_per_s = post_per_launch / avg_s if avg_s > 0 else 0.0
-    lds = {"kernel": "score_blocks_kernel<0>", "bound": "lds",
+    lds = {"kernel": sb_kernel, "bound": "lds",
            "achieved": round(posts_per_s / 1e12, 4), "peak": round(lds_peak / 1e12, 4),
            "unit": "Tpostings/s", "frac": round(posts_per_s / lds_peak, 4),
            "traffic": traffic,
@@ -307,7 +312,7 @@ def retrieve_leg(args, rank, world, dev, n_docs=DOCS_PER_SHARD, check_queries=20
            "score_blocks_ms_per_step": round(avg_s * 1000.0, 4),
            "launches": n_sb,
            "hbm_priced": hbm}
-    pmc = load_pmc_counters("score_blocks_kernel<0>", leg) if leg else None
+    pmc = load_pmc_counters(sb_kernel, leg) if leg else None
     if pmc:
         for c in ("SQ_LDS_BANK_CONFLICT", "SQ_LDS_IDX_ACTIVE", "GRBM_GUI_ACTIVE"):
             if c in pmc[0]:
