@@ -282,6 +282,9 @@ __device__ __forceinline__ int ax_swz(int r) { return ((r & 3) << 1) | (r & 8); 
 // (Measured: 128-key chunks -- half the barriers -- and raised MFMA issue priority
 // were both slower, r03 ab_attn.)
 constexpr int AX_KC = 64, AX_IMG = AX_KC * 256, AX_LDS = 4 * AX_IMG;
+// + the Q image after the K / V buffers: per wave its 32 query rows of 256 B (8 KiB),
+// slot j of row r at j ^ (r & 15) (the 16 rows of a tile at 16 distinct slots)
+constexpr int ax_lds_bytes(int nw) { return AX_LDS + nw * AX_QT * 16 * 256; }
 
 // BAL: wave w owns the 16-query tiles w and w + 8 of a pass (instead of 2w, 2w + 1), so
 // the tiles of a short pass spread over the four SIMDs (wave w runs on SIMD w % 4), and
@@ -365,24 +368,58 @@ attention_x3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
                                              (lds_void *)(lds + 2 * AX_IMG + dst), 16, 0, 0);
         }
     };
-    // B operands Q^T of unit u, lane (g, c): Q[q_base + 16 qt + c][32 ch + 8 g + e]
-    // (hi; lo 32 later)
     // first query (within its pass) of this wave's tile qt
     auto qtile = [&](int qt) { return BAL ? 16 * (wave + NW * qt) : wave * (AX_QT * 16) + 16 * qt; };
-    auto load_q = [&](const Unit &u, bf16x8 (&qh)[AX_QT][2], bf16x8 (&ql)[AX_QT][2]) {
-        const bf16 *qbase = qkv + split_col(u.h * ATT_D) + 8 * g;
+    // Q rows of unit u -> this wave's Q image, by LDS-DMA with the next unit's first chunk
+    // (no registers held across the chunk loop; the wave reads only what it wrote):
+    // piece pc = image rows 4 pc + lane >> 4 (row 16 qt + c: query qtile(qt) + c)
+    const int q_img = AX_LDS + wave * (AX_QT * 16 * 256);
+    auto stage_q = [&](const Unit &u) {
+        const bf16 *qg = qkv + split_col(u.h * ATT_D);
 #pragma unroll
-        for (int qt = 0; qt < AX_QT; ++qt) {
-            const int qi = min(u.pass * PASS_Q + qtile(qt) + c, u.nq - 1);
+        for (int pc = 0; pc < AX_QT * 4; ++pc) {
+            const int rl = 4 * pc + (lane >> 4);
+            const int qi = min(u.pass * PASS_Q + qtile(rl >> 4) + (rl & 15), u.nq - 1);
             const int qloc = qsel ? min(max(qsel[u.q0 + qi], 0), u.n - 1) : qi;
-            const int qrow = u.tok0 + qloc;
+            const int j = (lane & 15) ^ (rl & 15);
+            __builtin_amdgcn_global_load_lds((const void *)(qg + (u.tok0 + qloc) * ld + j * 8),
+                                             (lds_void *)(lds + q_img + pc * 1024), 16, 0, 0);
+        }
+    };
+    // B operands Q^T, lane (g, c): Q[q_base + 16 qt + c][32 ch + 8 g + e] (hi; lo 32
+    // later) from the Q image, after this wave's DMA landed (one statement with the
+    // wait, as the fragment reads)
+    auto read_q = [&](bf16x8 (&qh)[AX_QT][2], bf16x8 (&ql)[AX_QT][2]) {
+        // (the addresses from an opaque base: computed per unit, not hoisted out of the
+        // unit loop as 8 registers held for the whole kernel)
+        uint32_t qb = lds_base + q_img + c * 256, qx = (g ^ c) << 4;
+        asm volatile("" : "+v"(qb), "+v"(qx));
+        uint32_t qa[AX_QT][2][2];
+#pragma unroll
+        for (int qt = 0; qt < AX_QT; ++qt)
+#pragma unroll
+            for (int ch = 0; ch < 2; ++ch)
+#pragma unroll
+                for (int pt = 0; pt < 2; ++pt)
+                    qa[qt][ch][pt] = qb + qt * 16 * 256 + (qx ^ ((ch * 8 + pt * 4) << 4));
+        uint4 qf[AX_QT][2][2];
+        static_assert(AX_QT == 2, "read_q's operand list");
+        asm volatile("s_waitcnt vmcnt(0)\n\tds_read_b128 %0, %8\n\tds_read_b128 %1, %9"
+                     "\n\tds_read_b128 %2, %10\n\tds_read_b128 %3, %11\n\tds_read_b128 %4, %12"
+                     "\n\tds_read_b128 %5, %13\n\tds_read_b128 %6, %14\n\tds_read_b128 %7, %15"
+                     "\n\ts_waitcnt lgkmcnt(0)"
+                     : "=&v"(qf[0][0][0]), "=&v"(qf[0][0][1]), "=&v"(qf[0][1][0]), "=&v"(qf[0][1][1]),
+                       "=&v"(qf[1][0][0]), "=&v"(qf[1][0][1]), "=&v"(qf[1][1][0]), "=&v"(qf[1][1][1])
+                     : "v"(qa[0][0][0]), "v"(qa[0][0][1]), "v"(qa[0][1][0]), "v"(qa[0][1][1]),
+                       "v"(qa[1][0][0]), "v"(qa[1][0][1]), "v"(qa[1][1][0]), "v"(qa[1][1][1])
+                     : "memory");
+#pragma unroll
+        for (int qt = 0; qt < AX_QT; ++qt)
 #pragma unroll
             for (int ch = 0; ch < 2; ++ch) {
-                const bf16 *src = qbase + qrow * ld + ch * 64;
-                qh[qt][ch] = *reinterpret_cast<const bf16x8 *>(src);
-                ql[qt][ch] = *reinterpret_cast<const bf16x8 *>(src + 32);
+                __builtin_memcpy(&qh[qt][ch], &qf[qt][ch][0], 16);
+                __builtin_memcpy(&ql[qt][ch], &qf[qt][ch][1], 16);
             }
-        }
     };
     // fragment addresses (buffer 0; buffer 1 is the immediate offset AX_IMG)
     uint32_t ka[2][2][2];  // [t][ch][hi, lo]: key row 8 (c >> 2) + 4 t + (c & 3)
@@ -420,11 +457,12 @@ attention_x3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
         }
         if (pr >= n_pairs) return;
     }
-    bf16x8 qh[AX_QT][2], ql[AX_QT][2], qnh[AX_QT][2], qnl[AX_QT][2];
-    load_q(cu, qh, ql);
     stage(cu, 0, 0);
+    stage_q(cu);
     int b = 0;  // stage buffer of the next chunk to compute
     for (;;) {
+        bf16x8 qh[AX_QT][2], ql[AX_QT][2];
+        read_q(qh, ql);
         const int n = cu.n, h = cu.h, q0 = cu.q0, nq = cu.nq;
         const int q_pass = cu.pass * PASS_Q;
         const bool has_q = q_pass + qtile(0) < nq;
@@ -443,30 +481,42 @@ attention_x3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
 #pragma unroll
             for (int dt = 0; dt < 4; ++dt) o[qt][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
         }
-        for (int ci = 0; ci < n_chunks; ++ci, b ^= 1) {
+        // The chunk loop for a unit whose wave has NQT (1 or 2) query tiles -- one loop per
+        // count, not a choice per chunk: with the choice inside, the two bodies left the
+        // O accumulators in different registers and the loop's back edge moved them
+        // (16 v_mov_b64 + 12 v_mov per chunk in the ISA)
+        // (and the unit's whole 64-key chunks in a loop of their own, the partial last chunk
+        // after it: a sub-chunk loop that may stop after its first sub-chunk also left them
+        // in different registers, moved at the top and the bottom of every chunk)
+        // (and a wave with no query in the unit runs the staging alone: a body that may
+        // skip its products also moved the accumulators)
+        auto stage_step = [&](const int ci) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pieces of chunk ci
             __syncthreads();  // every piece landed; buffer b ^ 1 no longer read
             if (ci + 1 < n_chunks) {
                 stage(cu, ci + 1, b ^ 1);
             } else if (more) {  // the next unit's first chunk and Q
                 stage(nu, 0, b ^ 1);
-                load_q(nu, qnh, qnl);
+                stage_q(nu);
             }
-            if (!has_q) continue;
+        };
+        auto chunk_loop = [&](auto nqt_outer) {
+        auto one_chunk = [&](const int ci, auto whole_c) {
+            constexpr bool WHOLE = decltype(whole_c)::value;
+            stage_step(ci);
             // the chunk's sub-chunks for the wave's NQT non-empty query tiles
             auto chunk = [&](auto nqt_c) {
             constexpr int NQT = decltype(nqt_c)::value;
 #pragma unroll
             for (int u = 0; u < AX_KC / 32; ++u) {  // 32-key sub-chunks
             const int key0 = ci * AX_KC + 32 * u;
-            if (key0 >= n) break;
+            if (!WHOLE && key0 >= n) break;
             uint4 kf[2][2][2];
             uint2 vt2[4][2][2];
             // K fragments: one asm statement for the 8 reads and their wait (outputs
-            // exist only after it); V^T fragments: issued here, waited for after the
-            // softmax (their latency hides behind it), the wait naming every one of
-            // them ("+v") so that nothing reads them earlier.  The stage buffer and the
-            // sub-chunk are the immediate offset.
+            // exist only after it); V^T fragments: likewise, one statement with its wait,
+            // issued before the softmax.  The stage buffer and the sub-chunk are the
+            // immediate offset.
 #define AX_READ_K(OFF)                                                                             \
     asm volatile("ds_read_b128 %0, %8 offset:" #OFF "\n\tds_read_b128 %1, %9 offset:" #OFF         \
                  "\n\tds_read_b128 %2, %10 offset:" #OFF "\n\tds_read_b128 %3, %11 offset:" #OFF   \
@@ -478,25 +528,6 @@ attention_x3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
                  : "v"(ka[0][0][0]), "v"(ka[0][0][1]), "v"(ka[0][1][0]), "v"(ka[0][1][1]),         \
                    "v"(ka[1][0][0]), "v"(ka[1][0][1]), "v"(ka[1][1][0]), "v"(ka[1][1][1])          \
                  : "memory")
-#define AX_READ_V(OFF)                                                                             \
-    asm volatile(                                                                                  \
-        "ds_read_b64_tr_b16 %0, %16 offset:" #OFF "\n\tds_read_b64_tr_b16 %1, %17 offset:" #OFF    \
-        "\n\tds_read_b64_tr_b16 %2, %18 offset:" #OFF "\n\tds_read_b64_tr_b16 %3, %19 offset:" #OFF \
-        "\n\tds_read_b64_tr_b16 %4, %20 offset:" #OFF "\n\tds_read_b64_tr_b16 %5, %21 offset:" #OFF \
-        "\n\tds_read_b64_tr_b16 %6, %22 offset:" #OFF "\n\tds_read_b64_tr_b16 %7, %23 offset:" #OFF \
-        "\n\tds_read_b64_tr_b16 %8, %24 offset:" #OFF "\n\tds_read_b64_tr_b16 %9, %25 offset:" #OFF \
-        "\n\tds_read_b64_tr_b16 %10, %26 offset:" #OFF "\n\tds_read_b64_tr_b16 %11, %27 offset:" #OFF \
-        "\n\tds_read_b64_tr_b16 %12, %28 offset:" #OFF "\n\tds_read_b64_tr_b16 %13, %29 offset:" #OFF \
-        "\n\tds_read_b64_tr_b16 %14, %30 offset:" #OFF "\n\tds_read_b64_tr_b16 %15, %31 offset:" #OFF \
-        : "=&v"(vt2[0][0][0]), "=&v"(vt2[0][0][1]), "=&v"(vt2[0][1][0]), "=&v"(vt2[0][1][1]),     \
-          "=&v"(vt2[1][0][0]), "=&v"(vt2[1][0][1]), "=&v"(vt2[1][1][0]), "=&v"(vt2[1][1][1]),     \
-          "=&v"(vt2[2][0][0]), "=&v"(vt2[2][0][1]), "=&v"(vt2[2][1][0]), "=&v"(vt2[2][1][1]),     \
-          "=&v"(vt2[3][0][0]), "=&v"(vt2[3][0][1]), "=&v"(vt2[3][1][0]), "=&v"(vt2[3][1][1])      \
-        : "v"(va[0][0][0]), "v"(va[0][0][1]), "v"(va[0][1][0]), "v"(va[0][1][1]),                 \
-          "v"(va[1][0][0]), "v"(va[1][0][1]), "v"(va[1][1][0]), "v"(va[1][1][1]),                 \
-          "v"(va[2][0][0]), "v"(va[2][0][1]), "v"(va[2][1][0]), "v"(va[2][1][1]),                 \
-          "v"(va[3][0][0]), "v"(va[3][0][1]), "v"(va[3][1][0]), "v"(va[3][1][1])                  \
-        : "memory")
 #define AX_READ_VW(OFF)                                                                             \
     asm volatile(                                                                                  \
         "ds_read_b64_tr_b16 %0, %16 offset:" #OFF "\n\tds_read_b64_tr_b16 %1, %17 offset:" #OFF    \
@@ -542,7 +573,7 @@ static_assert(AX_IMG == 16384 && AX_KC == 64, "AX_SEL's immediate offsets");
                     for (int pt = 0; pt < 2; ++pt) __builtin_memcpy(&kfr[t][ch][pt], &kf[t][ch][pt], 16);
             if constexpr (PIPE && NQT == 2) {
             static_assert(BAL && LAZY, "PIPE builds on the balanced lazy form");
-            const bool full = key0 + 32 <= n;  // (uniform) no masked key in this sub-chunk
+            const bool full = WHOLE || key0 + 32 <= n;  // (uniform) no masked key in this sub-chunk
             f32x4 s[AX_QT][2];
             float v[AX_QT][8];
             bf16x8 ph[AX_QT], pl[AX_QT];
@@ -568,11 +599,11 @@ static_assert(AX_IMG == 16384 && AX_KC == 64, "AX_SEL's immediate offsets");
 #pragma unroll
                     for (int e = 0; e < 8; ++e) v[qt][e] = s[qt][e >> 2][e & 3];
                 } else {
+                    // (key 8 g + e of the sub-chunk is valid iff e < n - key0 - 8 g: one
+                    // value per lane against constants, not 8 hoisted key offsets)
+                    const int kv = n - key0 - 8 * g;
 #pragma unroll
-                    for (int e = 0; e < 8; ++e) {
-                        const int key = key0 + 8 * g + e;
-                        v[qt][e] = key < n ? s[qt][e >> 2][e & 3] : -INFINITY;
-                    }
+                    for (int e = 0; e < 8; ++e) v[qt][e] = e < kv ? s[qt][e >> 2][e & 3] : -INFINITY;
                 }
                 const float lmax = fmaxf(fmaxf(fmaxf(v[qt][0], v[qt][1]), fmaxf(v[qt][2], v[qt][3])),
                                          fmaxf(fmaxf(v[qt][4], v[qt][5]), fmaxf(v[qt][6], v[qt][7])));
@@ -670,14 +701,11 @@ static_assert(AX_IMG == 16384 && AX_KC == 64, "AX_SEL's immediate offsets");
                                 kfr[t][ch][p == 1], p == 2 ? ql[qt][ch] : qh[qt][ch], s[qt][t], 0,
                                 0, 0);
             __builtin_amdgcn_sched_barrier(0);
-            // (BAL: the V^T reads with their wait in one statement -- its higher register
-            // pressure made the compiler copy a V^T register before a separate wait)
-            if constexpr (BAL)
-                AX_SEL(AX_READ_VW);
-            else
-                AX_SEL(AX_READ_V);
+            // (the V^T reads with their wait in one statement: with a separate wait the
+            // compiler copied V^T registers above it -- tools/asm_wait_scan.py)
+            AX_SEL(AX_READ_VW);
             __builtin_amdgcn_sched_barrier(0);
-            const bool full = key0 + 32 <= n;  // (uniform) no masked key in this sub-chunk
+            const bool full = WHOLE || key0 + 32 <= n;  // (uniform) no masked key in this sub-chunk
             bf16x8 ph[AX_QT], pl[AX_QT];
             if (abl & 1) {
 #pragma unroll
@@ -692,11 +720,10 @@ static_assert(AX_IMG == 16384 && AX_KC == 64, "AX_SEL's immediate offsets");
                 for (int qt = 0; qt < NQT; ++qt) {
                     // raw scores (masked keys -inf); the reference max m is in raw units
                     float v[8];
+                    const int kv = n - key0 - 8 * g;  // key 8 g + e valid iff e < kv
 #pragma unroll
-                    for (int e = 0; e < 8; ++e) {
-                        const int key = key0 + 8 * g + e;  // (t = e >> 2, r = e & 3)
-                        v[e] = (full || key < n) ? s[qt][e >> 2][e & 3] : -INFINITY;
-                    }
+                    for (int e = 0; e < 8; ++e)  // (t = e >> 2, r = e & 3)
+                        v[e] = (full || e < kv) ? s[qt][e >> 2][e & 3] : -INFINITY;
                     const float lmax = fmaxf(fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3])),
                                              fmaxf(fmaxf(v[4], v[5]), fmaxf(v[6], v[7])));
                     // (always at a unit's first sub-chunk: lim = -inf, key 0 is valid)
@@ -732,12 +759,12 @@ static_assert(AX_IMG == 16384 && AX_KC == 64, "AX_SEL's immediate offsets");
             for (int qt = 0; qt < NQT; ++qt) {
                 // lane holds S^T[key0 + 8 g + 4 t + r][q_base + 16 qt + c]
                 float cmax = -INFINITY;
+                const int kv = n - key0 - 8 * g;  // key 8 g + 4 t + r valid iff 4 t + r < kv
 #pragma unroll
                 for (int t = 0; t < 2; ++t)
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
-                        const int key = key0 + 8 * g + 4 * t + r;
-                        const float v = (full || key < n) ? s[qt][t][r] * sc : -INFINITY;
+                        const float v = (full || 4 * t + r < kv) ? s[qt][t][r] * sc : -INFINITY;
                         s[qt][t][r] = v;
                         cmax = fmaxf(cmax, v);
                     }
@@ -769,17 +796,7 @@ static_assert(AX_IMG == 16384 && AX_KC == 64, "AX_SEL's immediate offsets");
                         pl[qt][4 * t + r] = split_lo(pr);
                     }
             }
-            if constexpr (!BAL)
-            asm volatile("s_waitcnt lgkmcnt(0)"
-                         : "+v"(vt2[0][0][0]), "+v"(vt2[0][0][1]), "+v"(vt2[0][1][0]),
-                           "+v"(vt2[0][1][1]), "+v"(vt2[1][0][0]), "+v"(vt2[1][0][1]),
-                           "+v"(vt2[1][1][0]), "+v"(vt2[1][1][1]), "+v"(vt2[2][0][0]),
-                           "+v"(vt2[2][0][1]), "+v"(vt2[2][1][0]), "+v"(vt2[2][1][1]),
-                           "+v"(vt2[3][0][0]), "+v"(vt2[3][0][1]), "+v"(vt2[3][1][0]),
-                           "+v"(vt2[3][1][1])
-                         :
-                         : "memory");
-            __builtin_amdgcn_sched_barrier(0);
+__builtin_amdgcn_sched_barrier(0);
             bf16x8 vfr[4][2];  // [dt][hi, lo]
 #pragma unroll
             for (int dt = 0; dt < 4; ++dt)
@@ -801,10 +818,22 @@ static_assert(AX_IMG == 16384 && AX_KC == 64, "AX_SEL's immediate offsets");
             }  // (PIPE)
             }
             };
-            if (two)
-                chunk(std::integral_constant<int, 2>{});
-            else
-                chunk(std::integral_constant<int, 1>{});
+            chunk(nqt_outer);
+        };
+        const int n_whole = n / AX_KC;
+        int ci = 0;
+        for (; ci < n_whole; ++ci, b ^= 1) one_chunk(ci, std::true_type{});
+        if (ci < n_chunks) {
+            one_chunk(ci, std::false_type{});
+            b ^= 1;
+        }
+        };
+        if (!has_q) {
+            for (int ci = 0; ci < n_chunks; ++ci, b ^= 1) stage_step(ci);
+        } else if (two) {
+            chunk_loop(std::integral_constant<int, 2>{});
+        } else {
+            chunk_loop(std::integral_constant<int, 1>{});
         }
         if (has_q) {
 #pragma unroll
@@ -834,16 +863,8 @@ static_assert(AX_IMG == 16384 && AX_KC == 64, "AX_SEL's immediate offsets");
         }
         if (!more) break;
         cu = nu;
-#pragma unroll
-        for (int qt = 0; qt < AX_QT; ++qt)
-#pragma unroll
-            for (int ch = 0; ch < 2; ++ch) {
-                qh[qt][ch] = qnh[qt][ch];
-                ql[qt][ch] = qnl[qt][ch];
-            }
     }
 #undef AX_READ_K
-#undef AX_READ_V
 #undef AX_READ_VW
 #undef AX_SEL
 }
@@ -870,10 +891,16 @@ void launch_attention_x3(const bf16 *qkv, const int32_t *cu_seqlens, int n_docs,
         return e ? atoi(e) : 0;
     }();
 #define AX_LAUNCH(BL, LZ, PP, NW)                                                              \
-    hipLaunchKernelGGL((attention_x3_kernel<BL, LZ, PP, NW>),                                  \
-                       dim3((int)std::min<int64_t>(n_pairs, (int64_t)n_cu() * (AX_WAVES / NW))), \
-                       dim3(64 * NW), AX_LDS, s, qkv, cu_seqlens, H, n_heads, (int)n_pairs,   \
-                       ctx_split, qsel, cu_qsel, abl)
+    do {                                                                                       \
+        DI_HIP(hipFuncSetAttribute((const void *)attention_x3_kernel<BL, LZ, PP, NW>,          \
+                                   hipFuncAttributeMaxDynamicSharedMemorySize,                 \
+                                   ax_lds_bytes(NW)));                                         \
+        hipLaunchKernelGGL((attention_x3_kernel<BL, LZ, PP, NW>),                              \
+                           dim3((int)std::min<int64_t>(n_pairs,                                \
+                                                       (int64_t)n_cu() * (AX_WAVES / NW))),    \
+                           dim3(64 * NW), ax_lds_bytes(NW), s, qkv, cu_seqlens, H, n_heads,   \
+                           (int)n_pairs, ctx_split, qsel, cu_qsel, abl);                       \
+    } while (0)
     // (r03 ab_attn, attention ms per step: BAL alone -3.5%, LAZY alone -5.6%, both -8.5%)
     switch (variant) {
     case 12: AX_LAUNCH(true, true, false, AX_WAVES); break;

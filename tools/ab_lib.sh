@@ -1,5 +1,5 @@
 #!/bin/bash
-# A/B of the built library against tools/_old/libdeepimpact_hip.so (a baseline build)
+# A/B of the built library against tools/_old (and tools/_mid) libdeepimpact_hip.so (baseline builds)
 # on bench legs, alternating on one box; one summary line per run.
 # Usage: LEGS=encode_x3,encode VARIANTS="old new old new" bash tools/ab_lib.sh <tag>
 set -o pipefail
@@ -10,8 +10,8 @@ i=0
 for v in ${VARIANTS:-old new old new}; do
   i=$((i+1))
   out="$R/gpurun_out/$tag/${v}_$i"
-  if [ "$v" = old ]; then
-    env DEEPIMPACT_HIP_LIB="$R/tools/_old/libdeepimpact_hip.so" DI_LIB_ALLOW_MISSING=1 \
+  if [ "$v" = old ] || [ "$v" = mid ]; then  # baseline builds tools/_old, tools/_mid
+    env DEEPIMPACT_HIP_LIB="$R/tools/_$v/libdeepimpact_hip.so" DI_LIB_ALLOW_MISSING=1 \
       timeout -k 10 ${RUN_TIMEOUT:-300} python3 "$R/bench.py" --steps 3 --warmup 1 --no-cpu \
       --legs "${LEGS:-encode_x3}" > "$out.json" 2> "$out.err" || exit $?
   else
@@ -30,7 +30,8 @@ for l in open(sys.argv[1]):
         if e:
             k = e["kernels"]
             parts.append(f"{leg} {e['value']:.1f} docs/s " + " ".join(
-                f"{n}={k[n]['ms_per_step']:.1f}" for n in ("gemm_qkv", "attention", "gemm_o", "gemm_ffn1", "gemm_ffn2")))
+                f"{n}={k[n]['ms_per_step']:.1f}" for n in ("gemm_qkv", "attention", "gemm_o", "gemm_ffn1", "gemm_ffn2"))
+                + f" sha1={str(e.get('out_sha1'))[:10]}")
     print("  ".join(parts), flush=True)
 PY
 done
