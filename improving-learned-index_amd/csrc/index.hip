@@ -1880,7 +1880,93 @@ merge_topk_kernel(const uint64_t *__restrict__ keys, const int32_t *__restrict__
             }
         }
         __syncthreads();
-    } else {
+    }
+    // Over the LDS capacity (many lists, e.g. the early blocks of an 8.8 M-doc query
+    // emitted full lists before the shared threshold rose): two passes over the lists, a
+    // wave per list -- the score histogram of every key, then only the keys in bins at or
+    // above the take-th key's bin into LDS -- and the selection below on those.  Every
+    // key >= the take-th largest is kept, so the result is the same.  Wide keys (score
+    // bits past 4095), or more kept keys than the LDS holds: the radix select below.
+    // (select bit 2: on; DI_PROFILE_MERGE=2 turns it off, A/B)
+    bool over = !(fast_lists && total <= cap);
+    if (over && fast_lists && (select & 2) && cap > MG_SEL_MIN && cap <= MG_SEL_CAP) {
+        uint32_t *hist = reinterpret_cast<uint32_t *>(lk + cap);
+        auto bin = [](uint64_t x) { return (uint32_t)(x >> 48) & (MG_SEL_BINS - 1); };
+        for (int i = tid; i < MG_SEL_BINS; i += THREADS) hist[i] = 0;
+        if (tid == 0) sh.cnt = 0;
+        __syncthreads();
+        const int lane = tid & 63, w = tid >> 6;
+        constexpr int UL = 4;  // loads per lane in flight
+        bool big = false;
+        for (int l = w; l < n_lists; l += WAVES) {
+            const int o = sh.off[l], c = sh.off[l + 1] - o;
+            const uint64_t *src = src0 + (int64_t)l * list_stride;
+            for (int i0 = 0; i0 < c; i0 += UL * 64) {
+                uint64_t v[UL];
+#pragma unroll
+                for (int u = 0; u < UL; ++u) {
+                    const int i = i0 + u * 64 + lane;
+                    v[u] = i < c ? src[i] : 0ull;
+                }
+#pragma unroll
+                for (int u = 0; u < UL; ++u) {
+                    if (i0 + u * 64 + lane < c) {
+                        big |= (v[u] >> 60) != 0;
+                        atomicAdd(&hist[bin(v[u])], 1u);
+                    }
+                }
+            }
+        }
+        if (!__syncthreads_or(big)) {
+            // T = the bin of the take-th largest key, n_keep = the keys in bins >= T
+            constexpr int BPT = MG_SEL_BINS / THREADS;
+            const int top = MG_SEL_BINS - 1 - tid * BPT;
+            uint32_t c = 0;
+#pragma unroll
+            for (int j = 0; j < BPT; ++j) c += hist[top - j];
+            const uint32_t incl = wave_prefix_sum(c);
+            if (lane == 63) sh.wtot[w] = incl;
+            __syncthreads();
+            uint32_t run = incl - c;
+            for (int v = 0; v < w; ++v) run += sh.wtot[v];
+#pragma unroll
+            for (int j = 0; j < BPT; ++j) {
+                const uint32_t h = hist[top - j];
+                if (run < (uint32_t)take && run + h >= (uint32_t)take) {
+                    sh.thr = (uint32_t)(top - j);
+                    sh.above = run + h;
+                }
+                run += h;
+            }
+            __syncthreads();
+            const uint32_t T = sh.thr, n_keep = sh.above;
+            if (n_keep <= (uint32_t)cap) {
+                for (int l = w; l < n_lists; l += WAVES) {
+                    const int o = sh.off[l], c2 = sh.off[l + 1] - o;
+                    const uint64_t *src = src0 + (int64_t)l * list_stride;
+                    for (int i0 = 0; i0 < c2; i0 += UL * 64) {
+                        uint64_t v[UL];
+#pragma unroll
+                        for (int u = 0; u < UL; ++u) {
+                            const int i = i0 + u * 64 + lane;
+                            v[u] = i < c2 ? src[i] : 0ull;
+                        }
+#pragma unroll
+                        for (int u = 0; u < UL; ++u) {
+                            uint32_t pos;
+                            const bool keep = i0 + u * 64 + lane < c2 && bin(v[u]) >= T;
+                            if (wave_append(keep, &sh.cnt, pos)) lk[pos] = v[u];
+                        }
+                    }
+                }
+                __syncthreads();
+                total = n_keep;
+                over = false;
+            }
+        }
+        __syncthreads();  // (the histogram area is reused by the selection)
+    }
+    if (over) {
         // slow path: radix select the take-th largest key straight from global
         uint64_t prefix = 0, mask = 0;
         uint32_t need = (uint32_t)take;
@@ -2587,9 +2673,15 @@ void launch_merge(const uint64_t *keys, const int32_t *counts, int n_q, int n_li
         cqs = 1;
     }
     // few short lists: the register-resident merge (DI_PROFILE_MERGE=0: the general one, A/B)
+    // (DI_PROFILE_MERGE=2: the radix select for candidates past the LDS capacity instead
+    // of the two-pass histogram filter, A/B)
     static const bool sel_ok = [] {
         const char *e = std::getenv("DI_PROFILE_MERGE");
         return !(e && e[0] == '0');
+    }();
+    static const int two_pass = [] {
+        const char *e = std::getenv("DI_PROFILE_MERGE");
+        return (e && e[0] == '2') ? 0 : 2;
     }();
     if (sel_ok && n_lists <= MS_LISTS && (int64_t)n_lists * k_in <= (int64_t)16 * 512 &&
         k <= MG_SEL_KEYS) {
@@ -2613,7 +2705,8 @@ void launch_merge(const uint64_t *keys, const int32_t *counts, int n_q, int n_li
     // workgroup size of the merge: 512 measured best for the 4-block x 1000-candidate
     // bench merge (0.68 vs 0.73 ms at 1024, 0.86 at 256); score-histogram selection
     // before the sort (a full sort of 4000 candidates took 0.80 ms, selection 0.17)
-    constexpr int mt = 512, select = 1;
+    constexpr int mt = 512;
+    const int select = 1 | two_pass;
     // (the histogram follows the keys; only for cap <= MG_SEL_CAP, inside the attribute's max)
     const size_t sel_lds = cap > MG_SEL_MIN && cap <= MG_SEL_CAP ? (size_t)MG_SEL_BINS * 4 + MG_SEL_KEYS * 8 : 0;
     if (cap <= 256 || mt == 256) {

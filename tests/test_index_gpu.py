@@ -405,6 +405,22 @@ def test_million_doc_shard_matches_oracle(L, million, k):
             qs, k, n_threads=16), m
 
 
+def test_million_doc_merge_past_lds_capacity(L, million, monkeypatch):
+    """Shared threshold off at 34 blocks: every block lists its full top-1000, 34 k
+    candidates per query against the merge's 8192-key LDS array -- the two-pass
+    histogram filter (a wave per list) keeps the keys at or above the 1000th key's score
+    bin and selects among those: the exact top-1000."""
+    from improving_learned_index_amd import synthetic as S
+
+    term_off, pdoc, pval, ora = million
+    monkeypatch.setenv("DI_SCORE_THRESHOLD", "0")
+    dev = L.DeviceIndex.from_postings(term_off, pdoc, pval, 0, ora.n_docs)
+    qs = S.msmarco_like_queries(24, 2_200_000, seed=5) + _queries(2_200_000, 8, seed=5)
+    got = dev.search(qs, 1000)
+    assert got == ora.score_ids(qs, 1000, n_threads=16)
+    assert sum(len(g) == 1000 for g in got) >= 16  # (most queries past the capacity)
+
+
 def test_full_msmarco_scaled_vocab_on_one_gpu(L):
     """configs[2] at full size on one GPU: 8.8 M docs (269 blocks), the vocabulary
     scaled with N (V = 2 N = 17.6 M terms: a dense term x block table would be 4.7 G

@@ -46,6 +46,7 @@ for s in $STEPS; do
         case $v in old) E="$OLD_ENV" ;; ablate*) E="DI_PROFILE_ABLATE=${v#ablate}" ;;
           classes) E="DI_DEAL_CLASSES=1" ;;
           mid) E="DEEPIMPACT_HIP_LIB=$R/tools/_mid/libdeepimpact_hip.so DI_LIB_ALLOW_MISSING=1" ;;
+          merge2) E="DI_PROFILE_MERGE=2" ;;
           *) E="X=0" ;; esac
         (cd "$R" && env $E SWEEP=${SWEEP:-bm} timeout -k 10 ${SWEEP_TIMEOUT:-500} python3 -u \
            tools/prune_sweep.py ${SWEEP_ARGS:-8800000 skew} > "$O/sweep_${n}_$v.json" \
@@ -54,8 +55,8 @@ for s in $STEPS; do
 import json, sys
 d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
 print(sys.argv[2], " ".join(
-    "m%d/f%g%s:%.1fk(r%.3f)" % (r["min_impact"], r["block_max_factor"], "p" if r["packed"] else "",
-                               r["device_queries_per_s"] / 1e3, r["recall_at_1000"])
+    "m%d/f%g%s:%.1fk(r%.3f,merge %.1fms)" % (r["min_impact"], r["block_max_factor"], "p" if r["packed"] else "",
+                               r["device_queries_per_s"] / 1e3, r["recall_at_1000"], r.get("merge_ms", -1))
     for r in d["rows"]), flush=True)
 PY
       done ;;

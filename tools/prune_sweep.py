@@ -8,7 +8,8 @@ queries at top-1000:
   * block-max skipping (di_index_set_block_max): factor 1 exact (recall 1.0 by
     construction, checked here), > 1 approximate.
 Recall@1000 = |pruned top-1000 ∩ exact top-1000| / |exact|, averaged over queries.
-Device time per batch = score_blocks + merge_topk over all the batch's launches.
+Device time per batch = score_blocks + merge_topk over all the batch's launches (both
+reported per row).
 Block-max rows also carry the scorer's skip counters (segments evaluated / skipped).
     python tools/prune_sweep.py [n_docs] [iid|skew] > profiles/<round>_prune_sweep.json
 skew: synthetic.SKEW_CONFIG4 (frequent terms carry small impacts, doc mass shared by
@@ -36,8 +37,9 @@ def run(ix, flat, cuq, nq, k, reps=3):
     for _ in range(reps):
         docs, _, n, _ = ix.search_csr(flat, cuq, k, timing=True)
     wall = (time.perf_counter() - t0) / reps
-    ms = (ix.timing("score_blocks")[0] + ix.timing("merge_topk")[0]) / reps / 1000.0
-    return docs, n, ms, wall
+    score_ms = ix.timing("score_blocks")[0] / reps / 1000.0
+    merge_ms = ix.timing("merge_topk")[0] / reps / 1000.0
+    return docs, n, (score_ms + merge_ms, score_ms, merge_ms), wall
 
 
 def main():
@@ -76,7 +78,7 @@ def main():
         posts = int(per_term[flat.astype(np.int64)].sum())
         ix.timing("bm_segments", reset=True)
         ix.timing("bm_segments_skipped", reset=True)
-        docs, n, dev_s, wall = run(ix, flat, cuq, nq, k)
+        docs, n, (dev_s, score_s, merge_s), wall = run(ix, flat, cuq, nq, k)
         seg_n = ix.timing("bm_segments")[1]
         seg_s = ix.timing("bm_segments_skipped")[1]
         res = [set(docs[i, :n[i]].tolist()) for i in range(nq)]
@@ -90,6 +92,7 @@ def main():
                      "bytes_per_query": 4.0 * ratio * posts / nq,
                      "postings_per_query": posts / nq, "device_queries_per_s": nq / dev_s,
                      "host_call_queries_per_s": nq / wall, "device_ms": dev_s * 1000,
+                     "score_blocks_ms": score_s * 1000, "merge_ms": merge_s * 1000,
                      "recall_at_1000": rec,
                      "bm_segments_skipped_frac": seg_s / seg_n if seg_n else None})
         print(json.dumps(rows[-1]), file=sys.stderr, flush=True)
