@@ -282,9 +282,6 @@ __device__ __forceinline__ int ax_swz(int r) { return ((r & 3) << 1) | (r & 8); 
 // (Measured: 128-key chunks -- half the barriers -- and raised MFMA issue priority
 // were both slower, r03 ab_attn.)
 constexpr int AX_KC = 64, AX_IMG = AX_KC * 256, AX_LDS = 4 * AX_IMG;
-// + the Q image after the K / V buffers: per wave its 32 query rows of 256 B (8 KiB),
-// slot j of row r at j ^ (r & 15) (the 16 rows of a tile at 16 distinct slots)
-constexpr int ax_lds_bytes(int nw) { return AX_LDS + nw * AX_QT * 16 * 256; }
 
 // BAL: wave w owns the 16-query tiles w and w + 8 of a pass (instead of 2w, 2w + 1), so
 // the tiles of a short pass spread over the four SIMDs (wave w runs on SIMD w % 4), and
@@ -370,56 +367,20 @@ attention_x3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
     };
     // first query (within its pass) of this wave's tile qt
     auto qtile = [&](int qt) { return BAL ? 16 * (wave + NW * qt) : wave * (AX_QT * 16) + 16 * qt; };
-    // Q rows of unit u -> this wave's Q image, by LDS-DMA with the next unit's first chunk
-    // (no registers held across the chunk loop; the wave reads only what it wrote):
-    // piece pc = image rows 4 pc + lane >> 4 (row 16 qt + c: query qtile(qt) + c)
-    const int q_img = AX_LDS + wave * (AX_QT * 16 * 256);
-    auto stage_q = [&](const Unit &u) {
-        const bf16 *qg = qkv + split_col(u.h * ATT_D);
+    auto load_q = [&](const Unit &u, bf16x8 (&qh)[AX_QT][2], bf16x8 (&ql)[AX_QT][2]) {
+        const bf16 *qbase = qkv + split_col(u.h * ATT_D) + 8 * g;
 #pragma unroll
-        for (int pc = 0; pc < AX_QT * 4; ++pc) {
-            const int rl = 4 * pc + (lane >> 4);
-            const int qi = min(u.pass * PASS_Q + qtile(rl >> 4) + (rl & 15), u.nq - 1);
+        for (int qt = 0; qt < AX_QT; ++qt) {
+            const int qi = min(u.pass * PASS_Q + qtile(qt) + c, u.nq - 1);
             const int qloc = qsel ? min(max(qsel[u.q0 + qi], 0), u.n - 1) : qi;
-            const int j = (lane & 15) ^ (rl & 15);
-            __builtin_amdgcn_global_load_lds((const void *)(qg + (u.tok0 + qloc) * ld + j * 8),
-                                             (lds_void *)(lds + q_img + pc * 1024), 16, 0, 0);
-        }
-    };
-    // B operands Q^T, lane (g, c): Q[q_base + 16 qt + c][32 ch + 8 g + e] (hi; lo 32
-    // later) from the Q image, after this wave's DMA landed (one statement with the
-    // wait, as the fragment reads)
-    auto read_q = [&](bf16x8 (&qh)[AX_QT][2], bf16x8 (&ql)[AX_QT][2]) {
-        // (the addresses from an opaque base: computed per unit, not hoisted out of the
-        // unit loop as 8 registers held for the whole kernel)
-        uint32_t qb = lds_base + q_img + c * 256, qx = (g ^ c) << 4;
-        asm volatile("" : "+v"(qb), "+v"(qx));
-        uint32_t qa[AX_QT][2][2];
-#pragma unroll
-        for (int qt = 0; qt < AX_QT; ++qt)
-#pragma unroll
-            for (int ch = 0; ch < 2; ++ch)
-#pragma unroll
-                for (int pt = 0; pt < 2; ++pt)
-                    qa[qt][ch][pt] = qb + qt * 16 * 256 + (qx ^ ((ch * 8 + pt * 4) << 4));
-        uint4 qf[AX_QT][2][2];
-        static_assert(AX_QT == 2, "read_q's operand list");
-        asm volatile("s_waitcnt vmcnt(0)\n\tds_read_b128 %0, %8\n\tds_read_b128 %1, %9"
-                     "\n\tds_read_b128 %2, %10\n\tds_read_b128 %3, %11\n\tds_read_b128 %4, %12"
-                     "\n\tds_read_b128 %5, %13\n\tds_read_b128 %6, %14\n\tds_read_b128 %7, %15"
-                     "\n\ts_waitcnt lgkmcnt(0)"
-                     : "=&v"(qf[0][0][0]), "=&v"(qf[0][0][1]), "=&v"(qf[0][1][0]), "=&v"(qf[0][1][1]),
-                       "=&v"(qf[1][0][0]), "=&v"(qf[1][0][1]), "=&v"(qf[1][1][0]), "=&v"(qf[1][1][1])
-                     : "v"(qa[0][0][0]), "v"(qa[0][0][1]), "v"(qa[0][1][0]), "v"(qa[0][1][1]),
-                       "v"(qa[1][0][0]), "v"(qa[1][0][1]), "v"(qa[1][1][0]), "v"(qa[1][1][1])
-                     : "memory");
-#pragma unroll
-        for (int qt = 0; qt < AX_QT; ++qt)
+            const int qrow = u.tok0 + qloc;
 #pragma unroll
             for (int ch = 0; ch < 2; ++ch) {
-                __builtin_memcpy(&qh[qt][ch], &qf[qt][ch][0], 16);
-                __builtin_memcpy(&ql[qt][ch], &qf[qt][ch][1], 16);
+                const bf16 *src = qbase + qrow * ld + ch * 64;
+                qh[qt][ch] = *reinterpret_cast<const bf16x8 *>(src);
+                ql[qt][ch] = *reinterpret_cast<const bf16x8 *>(src + 32);
             }
+        }
     };
     // fragment addresses (buffer 0; buffer 1 is the immediate offset AX_IMG)
     uint32_t ka[2][2][2];  // [t][ch][hi, lo]: key row 8 (c >> 2) + 4 t + (c & 3)
@@ -457,12 +418,11 @@ attention_x3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
         }
         if (pr >= n_pairs) return;
     }
+    bf16x8 qh[AX_QT][2], ql[AX_QT][2], qnh[AX_QT][2], qnl[AX_QT][2];
+    load_q(cu, qh, ql);
     stage(cu, 0, 0);
-    stage_q(cu);
     int b = 0;  // stage buffer of the next chunk to compute
     for (;;) {
-        bf16x8 qh[AX_QT][2], ql[AX_QT][2];
-        read_q(qh, ql);
         const int n = cu.n, h = cu.h, q0 = cu.q0, nq = cu.nq;
         const int q_pass = cu.pass * PASS_Q;
         const bool has_q = q_pass + qtile(0) < nq;
@@ -497,7 +457,7 @@ attention_x3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
                 stage(cu, ci + 1, b ^ 1);
             } else if (more) {  // the next unit's first chunk and Q
                 stage(nu, 0, b ^ 1);
-                stage_q(nu);
+                load_q(nu, qnh, qnl);
             }
         };
         auto chunk_loop = [&](auto nqt_outer) {
@@ -863,6 +823,13 @@ __builtin_amdgcn_sched_barrier(0);
         }
         if (!more) break;
         cu = nu;
+#pragma unroll
+        for (int qt = 0; qt < AX_QT; ++qt)
+#pragma unroll
+            for (int ch = 0; ch < 2; ++ch) {
+                qh[qt][ch] = qnh[qt][ch];
+                ql[qt][ch] = qnl[qt][ch];
+            }
     }
 #undef AX_READ_K
 #undef AX_READ_VW
@@ -891,16 +858,10 @@ void launch_attention_x3(const bf16 *qkv, const int32_t *cu_seqlens, int n_docs,
         return e ? atoi(e) : 0;
     }();
 #define AX_LAUNCH(BL, LZ, PP, NW)                                                              \
-    do {                                                                                       \
-        DI_HIP(hipFuncSetAttribute((const void *)attention_x3_kernel<BL, LZ, PP, NW>,          \
-                                   hipFuncAttributeMaxDynamicSharedMemorySize,                 \
-                                   ax_lds_bytes(NW)));                                         \
-        hipLaunchKernelGGL((attention_x3_kernel<BL, LZ, PP, NW>),                              \
-                           dim3((int)std::min<int64_t>(n_pairs,                                \
-                                                       (int64_t)n_cu() * (AX_WAVES / NW))),    \
-                           dim3(64 * NW), ax_lds_bytes(NW), s, qkv, cu_seqlens, H, n_heads,   \
-                           (int)n_pairs, ctx_split, qsel, cu_qsel, abl);                       \
-    } while (0)
+    hipLaunchKernelGGL((attention_x3_kernel<BL, LZ, PP, NW>),                                  \
+                       dim3((int)std::min<int64_t>(n_pairs, (int64_t)n_cu() * (AX_WAVES / NW))), \
+                       dim3(64 * NW), AX_LDS, s, qkv, cu_seqlens, H, n_heads, (int)n_pairs,   \
+                       ctx_split, qsel, cu_qsel, abl)
     // (r03 ab_attn, attention ms per step: BAL alone -3.5%, LAZY alone -5.6%, both -8.5%)
     switch (variant) {
     case 12: AX_LAUNCH(true, true, false, AX_WAVES); break;
