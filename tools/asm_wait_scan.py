@@ -7,7 +7,8 @@ defined when the asm statement ends, so it may legally schedule a copy or a use 
 such a register ABOVE the wait -- reading a register the LDS is still writing.
 This scans the gfx950 assembly of a source file and reports every instruction
 that touches a destination register of an inline-asm ds_read (global / buffer
-load) before the next lgkmcnt (vmcnt) wait.
+load) before the next lgkmcnt (vmcnt) wait, and every inline-asm instruction that
+touches an MFMA result within the MFMA -> VALU hazard window (scan_mfma_asm_reads).
 
     python tools/asm_wait_scan.py improving-learned-index_amd/csrc/enc_attn.hip
 """
@@ -61,6 +62,42 @@ def scan_asm(text):
     return hits
 
 
+def scan_mfma_asm_reads(text, window=24):
+    """[(function, asm instruction)] reading (a source operand) a VGPR that an MFMA wrote fewer than
+    `window` wait states (instructions, s_nop n counting n + 1) earlier in program order.
+    The compiler inserts the MFMA -> VALU hazard wait states before its own readers of an
+    MFMA result, not before an inline-asm one (an asm v_max3 over the S accumulators read
+    stale values, round 5).  Linear scan: conservative across branches."""
+    hits, fn, recent, in_asm = [], None, [], False
+    for ln in text.split("\n"):
+        if re.match(r"^_Z\S+:", ln):
+            fn, recent = ln.split(":")[0], []
+        t = ln.strip()
+        if not t or t.startswith((";", ".")) and not t.startswith(";;#ASM"):
+            continue
+        if t.startswith(";;#ASMSTART"):
+            in_asm = True
+            continue
+        if t.startswith(";;#ASMEND"):
+            in_asm = False
+            continue
+        m = re.match(r"s_nop\s+(\d+)", t)
+        step = int(m.group(1)) + 1 if m else 1
+        if in_asm and recent and re.match(r"(v_|ds_|global_|buffer_)", t):
+            # source operands only (a read-after-write; the destination of an asm load
+            # lands after the LDS / memory latency)
+            ops = (t.split(None, 1)[1] if " " in t else "").split(",")[1:]
+            touched = set()
+            for o in ops:
+                touched |= _regs(o)
+            if any(touched & regs for regs, _ in recent):
+                hits.append((fn, t))
+        if re.match(r"v_mfma", t):
+            recent.append((_regs(t.split(None, 1)[1].split(",")[0]), 0))
+        recent = [(r, d + step) for r, d in recent if d + step < window]
+    return hits
+
+
 def compile_asm(src, arch="gfx950"):
     with tempfile.TemporaryDirectory() as d:
         out = Path(d) / "k.s"
@@ -73,11 +110,16 @@ def compile_asm(src, arch="gfx950"):
 def main(argv):
     bad = 0
     for src in argv:
-        hits = scan_asm(compile_asm(src))
+        text = compile_asm(src)
+        hits = scan_asm(text)
         print(f"{src}: {len(hits)} early touch(es) of pending asm loads")
         for fn, ins in hits[:10]:
             print("   ", fn[:70], "|", ins)
-        bad += len(hits)
+        mh = scan_mfma_asm_reads(text)
+        print(f"{src}: {len(mh)} inline-asm touch(es) of fresh MFMA results")
+        for fn, ins in mh[:10]:
+            print("   ", fn[:70], "|", ins)
+        bad += len(hits) + len(mh)
     return 1 if bad else 0
 
 
