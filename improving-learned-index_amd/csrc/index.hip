@@ -2698,8 +2698,14 @@ void launch_merge(const uint64_t *keys, const int32_t *counts, int n_q, int n_li
     // slow path's radix select
     // (many lists: the score_blocks shared threshold leaves ~k + a few candidates per
     // query, so an 8192-key array -- the selection path's maximum -- usually holds them)
+    // (DI_MERGE_CAP: the LDS key array past MG_LDS_KEYS candidates, A/B; default
+    // MG_SEL_CAP)
+    static const int64_t over_cap = [] {
+        const char *e = std::getenv("DI_MERGE_CAP");
+        return e ? std::max<int64_t>(64, std::atoll(e)) : (int64_t)MG_SEL_CAP;
+    }();
     int64_t want = (int64_t)n_lists * k_in;
-    if (n_lists > 1024 || want > MG_LDS_KEYS) want = std::max<int64_t>(k, MG_SEL_CAP);
+    if (n_lists > 1024 || want > MG_LDS_KEYS) want = std::max<int64_t>(k, over_cap);
     int cap = 64;
     while (cap < want) cap <<= 1;
     // workgroup size of the merge: 512 measured best for the 4-block x 1000-candidate

@@ -30,5 +30,6 @@ for v in ${VARIANTS:-old new}; do
         classes) run $v DI_DEAL_CLASSES=1 || exit 1 ;;                # one class-ordered posting array
         nohs) run $v DI_PROFILE_ABLATE=1048576 || exit 1 ;;           # no histogram-area staging
         noemit) run $v DI_PROFILE_ABLATE=2097152 || exit 1 ;;         # no few-block emit-above
+        mcap*) run $v DI_MERGE_CAP=${v#mcap} || exit 1 ;;              # merge LDS key capacity
     esac
 done

@@ -47,6 +47,7 @@ for s in $STEPS; do
           classes) E="DI_DEAL_CLASSES=1" ;;
           mid) E="DEEPIMPACT_HIP_LIB=$R/tools/_mid/libdeepimpact_hip.so DI_LIB_ALLOW_MISSING=1" ;;
           merge2) E="DI_PROFILE_MERGE=2" ;;
+          mcap*) E="DI_MERGE_CAP=${v#mcap}" ;;
           *) E="X=0" ;; esac
         (cd "$R" && env $E SWEEP=${SWEEP:-bm} timeout -k 10 ${SWEEP_TIMEOUT:-500} python3 -u \
            tools/prune_sweep.py ${SWEEP_ARGS:-8800000 skew} > "$O/sweep_${n}_$v.json" \
