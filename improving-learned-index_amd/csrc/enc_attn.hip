@@ -382,32 +382,31 @@ attention_x3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
             }
         }
     };
-    // fragment addresses (buffer 0; buffer 1 is the immediate offset AX_IMG)
-    uint32_t ka[2][2][2];  // [t][ch][hi, lo]: key row 8 (c >> 2) + 4 t + (c & 3)
+    // fragment addresses (buffer 0; buffer 1 is the immediate offset AX_IMG).  Row bit 2
+    // (the K tile t, the V half h2) is not in the swizzle, so those halves are the
+    // immediate offset 4 * 256 = 1024 of one address register: 12 VGPRs instead of 24.
+    constexpr int AX_HALF = 1024;
+    uint32_t ka[2][2];  // [ch][hi, lo]: key row 8 (c >> 2) + (c & 3) (+ 4 t: + AX_HALF)
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
+    for (int ch = 0; ch < 2; ++ch)
 #pragma unroll
-        for (int ch = 0; ch < 2; ++ch)
-#pragma unroll
-            for (int pt = 0; pt < 2; ++pt) {
-                const int r = 8 * (c >> 2) + 4 * t + (c & 3), j = ch * 8 + pt * 4 + g;
-                ka[t][ch][pt] = lds_base + r * 256 + ((j ^ ax_swz(r)) << 4);
-            }
-    // [dt][hi, lo][h2]: ds_read_b64_tr_b16 roles -- lane 4 q + p of a 16-lane group
-    // addresses key row 8 g + 4 h2 + q, columns 16 dt + 4 p..+3 (one 8-byte half slot);
-    // lane i then holds column d = 16 dt + i for keys 8 g + 4 h2 + 0..3
-    uint32_t va[4][2][2];
+        for (int pt = 0; pt < 2; ++pt) {
+            const int r = 8 * (c >> 2) + (c & 3), j = ch * 8 + pt * 4 + g;
+            ka[ch][pt] = lds_base + r * 256 + ((j ^ ax_swz(r)) << 4);
+        }
+    // [dt][hi, lo]: ds_read_b64_tr_b16 roles -- lane 4 q + p of a 16-lane group addresses
+    // key row 8 g + 4 h2 + q (h2: + AX_HALF), columns 16 dt + 4 p..+3 (one 8-byte half
+    // slot); lane i then holds column d = 16 dt + i for keys 8 g + 4 h2 + 0..3
+    uint32_t va[4][2];
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt)
 #pragma unroll
-        for (int pt = 0; pt < 2; ++pt)
-#pragma unroll
-            for (int h2 = 0; h2 < 2; ++h2) {
-                const int q = c >> 2, pp = c & 3;
-                const int r = 8 * g + 4 * h2 + q;
-                const int j = (dt >> 1) * 8 + pt * 4 + 2 * (dt & 1) + (pp >> 1);
-                va[dt][pt][h2] = lds_base + 2 * AX_IMG + r * 256 + ((j ^ ax_swz(r)) << 4) + 8 * (pp & 1);
-            }
+        for (int pt = 0; pt < 2; ++pt) {
+            const int q = c >> 2, pp = c & 3;
+            const int r = 8 * g + q;
+            const int j = (dt >> 1) * 8 + pt * 4 + 2 * (dt & 1) + (pp >> 1);
+            va[dt][pt] = lds_base + 2 * AX_IMG + r * 256 + ((j ^ ax_swz(r)) << 4) + 8 * (pp & 1);
+        }
 
     Unit cu;
     {
@@ -478,35 +477,47 @@ attention_x3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
             // issued before the softmax.  The stage buffer and the sub-chunk are the
             // immediate offset.
 #define AX_READ_K(OFF)                                                                             \
-    asm volatile("ds_read_b128 %0, %8 offset:" #OFF "\n\tds_read_b128 %1, %9 offset:" #OFF         \
-                 "\n\tds_read_b128 %2, %10 offset:" #OFF "\n\tds_read_b128 %3, %11 offset:" #OFF   \
-                 "\n\tds_read_b128 %4, %12 offset:" #OFF "\n\tds_read_b128 %5, %13 offset:" #OFF   \
-                 "\n\tds_read_b128 %6, %14 offset:" #OFF "\n\tds_read_b128 %7, %15 offset:" #OFF   \
-                 "\n\ts_waitcnt lgkmcnt(0)"                                                        \
-                 : "=&v"(kf[0][0][0]), "=&v"(kf[0][0][1]), "=&v"(kf[0][1][0]), "=&v"(kf[0][1][1]), \
-                   "=&v"(kf[1][0][0]), "=&v"(kf[1][0][1]), "=&v"(kf[1][1][0]), "=&v"(kf[1][1][1])  \
-                 : "v"(ka[0][0][0]), "v"(ka[0][0][1]), "v"(ka[0][1][0]), "v"(ka[0][1][1]),         \
-                   "v"(ka[1][0][0]), "v"(ka[1][0][1]), "v"(ka[1][1][0]), "v"(ka[1][1][1])          \
-                 : "memory")
-#define AX_READ_VW(OFF)                                                                             \
     asm volatile(                                                                                  \
-        "ds_read_b64_tr_b16 %0, %16 offset:" #OFF "\n\tds_read_b64_tr_b16 %1, %17 offset:" #OFF    \
-        "\n\tds_read_b64_tr_b16 %2, %18 offset:" #OFF "\n\tds_read_b64_tr_b16 %3, %19 offset:" #OFF \
-        "\n\tds_read_b64_tr_b16 %4, %20 offset:" #OFF "\n\tds_read_b64_tr_b16 %5, %21 offset:" #OFF \
-        "\n\tds_read_b64_tr_b16 %6, %22 offset:" #OFF "\n\tds_read_b64_tr_b16 %7, %23 offset:" #OFF \
-        "\n\tds_read_b64_tr_b16 %8, %24 offset:" #OFF "\n\tds_read_b64_tr_b16 %9, %25 offset:" #OFF \
-        "\n\tds_read_b64_tr_b16 %10, %26 offset:" #OFF "\n\tds_read_b64_tr_b16 %11, %27 offset:" #OFF \
-        "\n\tds_read_b64_tr_b16 %12, %28 offset:" #OFF "\n\tds_read_b64_tr_b16 %13, %29 offset:" #OFF \
-        "\n\tds_read_b64_tr_b16 %14, %30 offset:" #OFF "\n\tds_read_b64_tr_b16 %15, %31 offset:" #OFF \
+        "ds_read_b128 %0, %8 offset:%12"                                                           \
+        "\n\tds_read_b128 %1, %9 offset:%12"                                                       \
+        "\n\tds_read_b128 %2, %10 offset:%12"                                                      \
+        "\n\tds_read_b128 %3, %11 offset:%12"                                                      \
+        "\n\tds_read_b128 %4, %8 offset:%13"                                                       \
+        "\n\tds_read_b128 %5, %9 offset:%13"                                                       \
+        "\n\tds_read_b128 %6, %10 offset:%13"                                                      \
+        "\n\tds_read_b128 %7, %11 offset:%13"                                                      \
         "\n\ts_waitcnt lgkmcnt(0)"                                                                 \
-        : "=&v"(vt2[0][0][0]), "=&v"(vt2[0][0][1]), "=&v"(vt2[0][1][0]), "=&v"(vt2[0][1][1]),     \
-          "=&v"(vt2[1][0][0]), "=&v"(vt2[1][0][1]), "=&v"(vt2[1][1][0]), "=&v"(vt2[1][1][1]),     \
-          "=&v"(vt2[2][0][0]), "=&v"(vt2[2][0][1]), "=&v"(vt2[2][1][0]), "=&v"(vt2[2][1][1]),     \
-          "=&v"(vt2[3][0][0]), "=&v"(vt2[3][0][1]), "=&v"(vt2[3][1][0]), "=&v"(vt2[3][1][1])      \
-        : "v"(va[0][0][0]), "v"(va[0][0][1]), "v"(va[0][1][0]), "v"(va[0][1][1]),                 \
-          "v"(va[1][0][0]), "v"(va[1][0][1]), "v"(va[1][1][0]), "v"(va[1][1][1]),                 \
-          "v"(va[2][0][0]), "v"(va[2][0][1]), "v"(va[2][1][0]), "v"(va[2][1][1]),                 \
-          "v"(va[3][0][0]), "v"(va[3][0][1]), "v"(va[3][1][0]), "v"(va[3][1][1])                  \
+        : "=&v"(kf[0][0][0]), "=&v"(kf[0][0][1]), "=&v"(kf[0][1][0]), "=&v"(kf[0][1][1]),          \
+          "=&v"(kf[1][0][0]), "=&v"(kf[1][0][1]), "=&v"(kf[1][1][0]), "=&v"(kf[1][1][1])           \
+        : "v"(ka[0][0]), "v"(ka[0][1]), "v"(ka[1][0]), "v"(ka[1][1]),                              \
+          "i"(OFF), "i"((OFF) + AX_HALF)                                                           \
+        : "memory")
+#define AX_READ_VW(OFF)                                                                            \
+    asm volatile(                                                                                  \
+        "ds_read_b64_tr_b16 %0, %16 offset:%24"                                                    \
+        "\n\tds_read_b64_tr_b16 %1, %16 offset:%25"                                                \
+        "\n\tds_read_b64_tr_b16 %2, %17 offset:%24"                                                \
+        "\n\tds_read_b64_tr_b16 %3, %17 offset:%25"                                                \
+        "\n\tds_read_b64_tr_b16 %4, %18 offset:%24"                                                \
+        "\n\tds_read_b64_tr_b16 %5, %18 offset:%25"                                                \
+        "\n\tds_read_b64_tr_b16 %6, %19 offset:%24"                                                \
+        "\n\tds_read_b64_tr_b16 %7, %19 offset:%25"                                                \
+        "\n\tds_read_b64_tr_b16 %8, %20 offset:%24"                                                \
+        "\n\tds_read_b64_tr_b16 %9, %20 offset:%25"                                                \
+        "\n\tds_read_b64_tr_b16 %10, %21 offset:%24"                                               \
+        "\n\tds_read_b64_tr_b16 %11, %21 offset:%25"                                               \
+        "\n\tds_read_b64_tr_b16 %12, %22 offset:%24"                                               \
+        "\n\tds_read_b64_tr_b16 %13, %22 offset:%25"                                               \
+        "\n\tds_read_b64_tr_b16 %14, %23 offset:%24"                                               \
+        "\n\tds_read_b64_tr_b16 %15, %23 offset:%25"                                               \
+        "\n\ts_waitcnt lgkmcnt(0)"                                                                 \
+        : "=&v"(vt2[0][0][0]), "=&v"(vt2[0][0][1]), "=&v"(vt2[0][1][0]), "=&v"(vt2[0][1][1]),      \
+          "=&v"(vt2[1][0][0]), "=&v"(vt2[1][0][1]), "=&v"(vt2[1][1][0]), "=&v"(vt2[1][1][1]),      \
+          "=&v"(vt2[2][0][0]), "=&v"(vt2[2][0][1]), "=&v"(vt2[2][1][0]), "=&v"(vt2[2][1][1]),      \
+          "=&v"(vt2[3][0][0]), "=&v"(vt2[3][0][1]), "=&v"(vt2[3][1][0]), "=&v"(vt2[3][1][1])       \
+        : "v"(va[0][0]), "v"(va[0][1]), "v"(va[1][0]), "v"(va[1][1]),                              \
+          "v"(va[2][0]), "v"(va[2][1]), "v"(va[3][0]), "v"(va[3][1]),                              \
+          "i"(OFF), "i"((OFF) + AX_HALF)                                                           \
         : "memory")
 // (b, the stage buffer, is 0 or 1 at run time; u, the sub-chunk, a constant of the
 // unrolled loop: one branch per site -- a switch over the offsets' value range compiled

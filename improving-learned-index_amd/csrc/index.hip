@@ -1282,9 +1282,13 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
             }
             // (too many: the full selection, k keys; sh.emit is reset by the paths that use
             // it -- the radix ties set it, the fast path's compaction does not read it)
+            // The sweep may have staged up to kl keys in the histogram area (a near-full
+            // block leaves no accumulator tail); the fast path counts into those bins and
+            // they were zeroed only at the setup, so zero them again here.
+            if (fast && stage == hist_stage) reinterpret_cast<uint4 *>(sh.u.hist)[tid] = make_uint4(0, 0, 0, 0);
             cap = (uint32_t)k;
             stage = tail_fits ? acc_tail : nullptr;
-            __syncthreads();  // every wave has read sh.emit
+            __syncthreads();  // every wave has read sh.emit (and the bins are zero again)
             if (tid == 0) sh.emit = 0;
         }
     }
@@ -2310,6 +2314,14 @@ struct di_index {
     int ablate = 0;  // DI_PROFILE_ABLATE: profiling only (1 no scatter, 2 no selection, 4 stop at the k-th score)
     Timer timer;
 
+    // Few blocks (2..7, no shared qhist threshold): the emit-above selection (score_item)
+    // lists up to 2 k keys per (query, block) against the running threshold qtq
+    // (DI_PROFILE_ABLATE bit 2097152: off, A/B).  One predicate for search and reserve.
+    bool few_blocks(int k) const {
+        return nb >= 2 && nb < 8 && shared_thr != 1 && 2 * k <= 2048 && !(ablate & 2097152);
+    }
+    int list_cap(int k) const { return few_blocks(k) ? 2 * k : k; }
+
     SubIndex sub(bool with_packed = false) const {
         const bool pk = with_packed && packed && pk_built;
         return SubIndex{tb_start.as<uint32_t>(), eblk.as<uint16_t>(), epos.as<uint32_t>(),
@@ -2861,7 +2873,7 @@ int di_index_reserve(di_index *ix, int32_t max_q, int32_t k) {
         DI_REQUIRE(ix && max_q >= 0 && k > 0 && k <= DI_MAX_TOPK, DI_EINVAL, "bad argument");
         DeviceScope ds(ix->device);
         // (the few-block emit-above selection lists up to 2 k keys per item, see search)
-        const int kl = ix->nb >= 2 && ix->nb < 8 && 2 * k <= 2048 ? 2 * k : k;
+        const int kl = ix->list_cap(k);
         size_t nbk = (size_t)max_q * std::max(ix->nb, 1) * kl;
         ix->ws_ck.reserve(nbk * 8);
         ix->ws_cn.reserve((size_t)max_q * std::max(ix->nb, 1) * 4);
@@ -2913,12 +2925,9 @@ int di_index_search(di_index *ix, const uint32_t *q_terms, const int32_t *cu_q, 
         // too: one setting (DI_CAND_WS_MIB) sizes both.  Peak workspace of a handle
         // ~3x the cap.
         const int rec_slots = std::min(std::max(max_nt, 1), WTERMS);
-        // Few blocks (no shared qhist threshold, 2..7 blocks): the emit-above selection
-        // (score_item) lists up to kl = 2 k keys per (query, block) against the running
-        // threshold qtq (DI_PROFILE_ABLATE bit 2097152: off, A/B)
-        const bool few = ix->nb >= 2 && ix->nb < 8 && ix->shared_thr != 1 && 2 * k <= 2048 &&
-                         !(ix->ablate & 2097152);
-        const int kl = few ? 2 * k : k;
+        // Few blocks: the emit-above selection (di_index::few_blocks)
+        const bool few = ix->few_blocks(k);
+        const int kl = ix->list_cap(k);
         const int64_t per_q = (int64_t)nb * kl * 8;
         const int64_t rec_per_q = (int64_t)nb * rec_slots * (int64_t)sizeof(ItemRec);
         int64_t ws_cap = 4ll << 30;

@@ -46,6 +46,16 @@ def _tok_chunk(docs: Sequence[str]):
     return DeepImpact.pack_processed_blob(DeepImpact.process_documents(docs, _W["max_length"]))
 
 
+def _tok_rate(docs: Sequence[str]) -> float:
+    """One worker's tokenize + term-extraction rate (docs/s) over `docs` (the bench's
+    host budget of the index CLI: indexer.py:28-33 is the reference loop it replaces)."""
+    import time
+
+    t0 = time.perf_counter()
+    _tok_chunk(docs)
+    return len(docs) / max(time.perf_counter() - t0, 1e-9)
+
+
 def pool_supported() -> bool:
     """Spawned workers re-import the parent's __main__: impossible when it is not a
     file or module (stdin, -c); callers then tokenize in-process."""
@@ -94,6 +104,10 @@ class TokenizerPool:
 
     def imap(self, chunks):
         return self.pool.imap(_tok_chunk, chunks)
+
+    def worker_rate(self, docs: Sequence[str]) -> float:
+        """docs/s of one worker over `docs` (the pool otherwise idle)."""
+        return self.pool.apply(_tok_rate, (list(docs),))
 
     def close(self) -> None:
         self.pool.close()

@@ -315,8 +315,26 @@ def quantize_sharded(input_path, output_path, max_val, world: int, rank: int,
 
 _SIGN = -(1 << 63)  # int64 view of a u64 key XOR this = the keys' unsigned order
 
+# Below this many keys per rank (n_q * k; 32 KB) the plain all_gather (two collectives,
+# no host synchronisation) costs less than the pruned exchange's three collectives and
+# its one device -> host read of the round-2 size.
+PLAIN_MAX_KEYS = 4096
 
-def exchange_topk(key, cnt, k: int, group=None, stats: Optional[dict] = None):
+
+def exchange_pruned(world: int, nq: int, k: int, pruned: Optional[bool] = None) -> bool:
+    """Whether exchange_topk takes the pruned two-round path.  pruned True / False forces
+    it (DI_EXCHANGE=pruned / plain likewise); by default pruned from 2 ranks when a rank
+    holds at least PLAIN_MAX_KEYS keys.  Forcing it at one rank is how a 1-GPU box runs
+    the device / RCCL branch of the multi-GPU retrieve."""
+    if pruned is None:
+        pruned = {"pruned": True, "plain": False}.get(os.environ.get("DI_EXCHANGE", "auto"))
+    if pruned is None:
+        pruned = world > 1 and nq * k >= PLAIN_MAX_KEYS
+    return bool(pruned) and max(1, min(64, k // (4 * world))) > 1
+
+
+def exchange_topk(key, cnt, k: int, group=None, stats: Optional[dict] = None,
+                  pruned: Optional[bool] = None):
     """Exact, pruned all-gather of every rank's top-k key lists (SURVEY §8e retrieve).
 
     key: [n_q * k] int64 tensor (u64 merge keys; each query's list sorted descending, its
@@ -330,13 +348,17 @@ def exchange_topk(key, cnt, k: int, group=None, stats: Optional[dict] = None):
     apart).  A rank whose j-th sample is >= t holds >= j g keys >= t, so with s = ceil(k/g)
     samples >= T_q across the ranks at least k keys are >= T_q: T_q, the s-th largest
     sample, is a lower bound of the global k-th key.  Round 2 gathers each rank's keys
-    >= T_q (counts, then a padded all_gather).  A plain gather moves k keys per query and
+    >= T_q: their counts together with the scorer's counts (one collective), then the
+    keys padded to the largest rank's total.  A plain gather moves k keys per query and
     rank; this one k / g samples + the rank's share of the keys >= T_q (k + O(world g)
     of them over all ranks).  The keys are unique (they carry the doc), so the pruning
     is exact: /root/reference/src/deep_impact/evaluation/ranker.py:43-48 keeps the top
     1000 per query, which the merge reproduces.
-    stats (optional dict): gathered_keys_per_query (sent by this rank, padding
-    included), bytes_sent.
+
+    Three collectives and one host synchronisation (the round-2 size): packing and
+    unpacking are device scatters (no boolean indexing, no per-rank loop).
+    pruned: see exchange_pruned.  stats (optional dict): path ("pruned" / "plain"),
+    gathered_keys_per_query (sent by this rank, padding included), bytes_sent.
     """
     import torch
     import torch.distributed as dist
@@ -345,16 +367,17 @@ def exchange_topk(key, cnt, k: int, group=None, stats: Optional[dict] = None):
     nq = cnt.numel()
     dev = key.device
     K = key.view(nq, k)
-    g = max(1, min(64, k // (4 * world)))
-    if world == 1 or g == 1:  # (a sample of every key: the plain gather)
+    if not exchange_pruned(world, nq, k, pruned):
         gk = torch.empty(world * nq * k, dtype=torch.int64, device=dev)
         gc = torch.empty(world * nq, dtype=torch.int32, device=dev)
         dist.all_gather_into_tensor(gk, K.reshape(-1).contiguous(), group=group)
         dist.all_gather_into_tensor(gc, cnt.contiguous(), group=group)
         if stats is not None:
+            stats["path"] = "plain"
             stats["gathered_keys_per_query"] = float(k)
             stats["bytes_sent"] = 8 * nq * k + 4 * nq
         return gk, gc
+    g = max(1, min(64, k // (4 * world)))
     c = cnt.to(torch.int64).clamp(0, k)
     lo = torch.iinfo(torch.int64).min
     s_n = k // g  # samples per list (positions g-1, ..., s_n g - 1 < k)
@@ -369,40 +392,47 @@ def exchange_topk(key, cnt, k: int, group=None, stats: Optional[dict] = None):
         T = torch.topk(allS, need, dim=1).values[:, need - 1]  # (lo when too few samples)
     else:
         T = torch.full((nq,), lo, dtype=torch.int64, device=dev)
-    # round 2: this rank's keys >= T_q (a prefix: lists are sorted)
+    # round 2: this rank's keys >= T_q (a prefix of each list: lists are sorted)
     ar_k = torch.arange(k, device=dev)
     sel = (ar_k[None, :] < c[:, None]) & ((K ^ _SIGN) >= T[:, None])
     e = sel.sum(1)
-    packed = K[sel]
-    ge = torch.empty(world * nq, dtype=torch.int32, device=dev)
-    dist.all_gather_into_tensor(ge, e.to(torch.int32), group=group)
-    gew = ge.view(world, nq).to(torch.int64)
+    # the prefix counts and the scorer's counts in one collective: [world, 2, nq]
+    ec = torch.stack([e.to(torch.int32), cnt.to(torch.int32)]).reshape(-1)
+    gec = torch.empty(world * 2 * nq, dtype=torch.int32, device=dev)
+    dist.all_gather_into_tensor(gec, ec, group=group)
+    gec = gec.view(world, 2, nq)
+    gew = gec[:, 0].to(torch.int64)
+    gcw = gec[:, 1]
     tot = gew.sum(1)
-    emax = int(tot.max().item()) if nq else 0
-    out = torch.empty(world, nq, k, dtype=torch.int64, device=dev)
+    emax = int(tot.max().item()) if nq else 0  # (the one host synchronisation)
+    # one slot past the rank-major lists takes every padding write
+    out = torch.empty(world * nq * k + 1, dtype=torch.int64, device=dev)
     if emax:
-        buf = torch.zeros(emax, dtype=torch.int64, device=dev)
-        buf[:packed.numel()] = packed
+        # pack: key j < e[q] of query q -> off[q] + j (the rest -> the dump slot emax)
+        off = torch.cumsum(e, 0) - e
+        dst = torch.where(sel, off[:, None] + ar_k[None, :], torch.full_like(K, emax))
+        buf = torch.zeros(emax + 1, dtype=torch.int64, device=dev)
+        buf.scatter_(0, dst.reshape(-1), K.reshape(-1))
         g2 = torch.empty(world * emax, dtype=torch.int64, device=dev)
-        dist.all_gather_into_tensor(g2, buf, group=group)
-        g2 = g2.view(world, emax)
-        ar_q = torch.arange(nq, device=dev)
-        for r in range(world):
-            er = gew[r]
-            n_r = int(tot[r].item())
-            if n_r == 0:
-                continue
-            qi = torch.repeat_interleave(ar_q, er)
-            off = torch.cumsum(er, 0) - er
-            out[r, qi, torch.arange(n_r, device=dev) - off[qi]] = g2[r, :n_r]
-    gc = torch.empty(world * nq, dtype=torch.int32, device=dev)
-    dist.all_gather_into_tensor(gc, cnt.contiguous(), group=group)
-    gcw = gc.view(world, nq)
+        dist.all_gather_into_tensor(g2, buf[:emax].contiguous(), group=group)
+        # unpack every rank at once: position p of rank r belongs to the query whose
+        # inclusive prefix count first exceeds p
+        cum = torch.cumsum(gew, 1)  # [world, nq]
+        p = torch.arange(emax, device=dev).expand(world, emax).contiguous()
+        qi = torch.searchsorted(cum, p, right=True)  # [world, emax]; nq past tot[r]
+        ok = p < tot[:, None]
+        qc = qi.clamp(max=nq - 1)
+        col = p - (torch.gather(cum, 1, qc) - torch.gather(gew, 1, qc))
+        r_ix = torch.arange(world, device=dev)[:, None]
+        dst2 = torch.where(ok, (r_ix * nq + qc) * k + col,
+                           torch.full_like(p, world * nq * k))
+        out.scatter_(0, dst2.reshape(-1), g2)
     g_n = torch.where(gcw < 0, gcw, gew.to(torch.int32))
     if stats is not None:
+        stats["path"] = "pruned"
         stats["gathered_keys_per_query"] = (s_n + emax / max(nq, 1)) if nq else 0.0
         stats["bytes_sent"] = 8 * (nq * s_n + emax) + 4 * 2 * nq
-    return out.view(-1), g_n.view(-1)
+    return out[:world * nq * k], g_n.reshape(-1)
 
 
 class ShardedRetriever:

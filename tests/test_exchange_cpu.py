@@ -58,7 +58,7 @@ def _merge(keys, counts, k):
     return out
 
 
-def _worker(rank, world, port, keys, cnt, k, q):
+def _worker(rank, world, port, keys, cnt, k, q, pruned):
     try:
         import torch
         import torch.distributed as dist
@@ -68,7 +68,7 @@ def _worker(rank, world, port, keys, cnt, k, q):
         kt = torch.from_numpy(keys[rank].reshape(-1).view(np.int64).copy())
         ct = torch.from_numpy(cnt[rank].copy())
         st = {}
-        gk, gn = parallel.exchange_topk(kt, ct, k, stats=st)
+        gk, gn = parallel.exchange_topk(kt, ct, k, stats=st, pruned=pruned)
         dist.barrier()
         dist.destroy_process_group()
         nq = cnt.shape[1]
@@ -78,11 +78,11 @@ def _worker(rank, world, port, keys, cnt, k, q):
         q.put((rank, traceback.format_exc(), None, None))
 
 
-def _run(world, keys, cnt, k):
+def _run(world, keys, cnt, k, pruned=None):
     ctx = mp.get_context("fork")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_worker, args=(r, world, port, keys, cnt, k, q)) for r in range(world)]
+    ps = [ctx.Process(target=_worker, args=(r, world, port, keys, cnt, k, q, pruned)) for r in range(world)]
     for p in ps:
         p.start()
     out = {}
@@ -97,14 +97,22 @@ def _run(world, keys, cnt, k):
     return out
 
 
+@pytest.mark.parametrize("pruned", [True, None])
 @pytest.mark.parametrize("world,k,mode", [(2, 50, "iid"), (3, 40, "ragged"), (4, 3, "ragged"),
-                                          (2, 1, "ragged"), (3, 64, "iid")])
-def test_exchange_equals_full_gather(world, k, mode):
+                                          (2, 1, "ragged"), (3, 64, "iid"), (1, 40, "ragged"),
+                                          (1, 200, "iid")])
+def test_exchange_equals_full_gather(world, k, mode, pruned):
+    """Forced pruned (world 1 included: the rehearsal a 1-GPU box runs) and the default
+    choice (plain below PLAIN_MAX_KEYS keys per rank and at one rank)."""
     nq = 24
     keys, cnt = _lists(world, nq, k, seed=7 + world + k, mode=mode)
     want = _merge(keys, cnt, k)
-    out = _run(world, keys, cnt, k)
-    for r, (gk, gn, _) in out.items():
+    out = _run(world, keys, cnt, k, pruned)
+    for r, (gk, gn, st) in out.items():
+        want_path = "pruned" if parallel.exchange_pruned(world, nq, k, pruned) else "plain"
+        assert st["path"] == want_path
+        if pruned and k >= 8:
+            assert want_path == "pruned"
         got = _merge(gk, gn, k)
         for qi in range(nq):
             assert got[qi] == want[qi], (r, qi)
@@ -119,3 +127,19 @@ def test_exchange_sends_under_0p6_k_at_two_ranks():
     for r, (_, _, st) in out.items():
         assert st["gathered_keys_per_query"] <= 0.6 * k, st
         assert st["bytes_sent"] < 0.6 * k * 8 * nq + 8 * nq
+
+
+def test_exchange_auto_choice():
+    """Pruned from 2 ranks at PLAIN_MAX_KEYS keys per rank; plain at one rank or below
+    it, or when the sample stride would be 1; DI_EXCHANGE overrides the default."""
+    big = parallel.PLAIN_MAX_KEYS
+    assert parallel.exchange_pruned(2, big // 100 + 1, 100)
+    assert not parallel.exchange_pruned(2, big // 100, 100)
+    assert not parallel.exchange_pruned(1, 6980, 1000)
+    assert parallel.exchange_pruned(1, 6980, 1000, pruned=True)
+    assert not parallel.exchange_pruned(8, 6980, 3, pruned=True)  # (g = 1: plain)
+    os.environ["DI_EXCHANGE"] = "pruned"
+    try:
+        assert parallel.exchange_pruned(1, 10, 100)
+    finally:
+        del os.environ["DI_EXCHANGE"]

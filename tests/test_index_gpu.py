@@ -370,6 +370,49 @@ def test_in_kernel_setup_fallback_equals_oracle(L, synth, monkeypatch):
         assert dev.search(qs, k) == ora.score_ids(qs, k, n_threads=8)
 
 
+def _two_block_skewed(n_docs, v_terms, seed):
+    """A 2-block shard whose second block outscores the first: every doc holds ~12 of
+    v_terms terms; block 0 impacts 1..60, block 1 impacts 90..255.  A query's block-1
+    items then find more than 2 k docs above the running threshold (block 0's k-th
+    score), so the emit-above sweep overflows its list and falls back to the full
+    selection -- with near-full blocks (no accumulator tail) after staging keys in the
+    score-histogram area."""
+    from improving_learned_index_amd import synthetic as S
+
+    rng = np.random.default_rng(seed)
+    per = 12
+    half = (n_docs + 1) // 2
+    term = np.concatenate([np.sort(rng.choice(v_terms, per, replace=False)) for _ in range(n_docs)])
+    doc = np.repeat(np.arange(n_docs), per)
+    val = np.where(doc < half, rng.integers(1, 61, doc.size), rng.integers(90, 256, doc.size))
+    cu = np.arange(0, (n_docs + 1) * per, per, dtype=np.int64)
+    return S.postings_reference_order(cu, term.astype(np.uint32), val.astype(np.int64), v_terms)
+
+
+@pytest.mark.parametrize("k", [100, 1000])
+def test_emit_above_overflow_with_full_blocks_equals_oracle(L, k):
+    """the few-block emit-above selection stages up to 2 k keys in the
+    score-histogram area when a near-full block leaves no accumulator tail (k 1000:
+    block_docs > 28768); when more than 2 k docs pass the running threshold it falls back
+    to the full selection, whose histogram must be zeroed again.  2 blocks of 31 000 docs,
+    skewed so the second block overflows: the exact top-k."""
+    n_docs, v = 62_000, 60
+    term_off, pdoc, pval = _two_block_skewed(n_docs, v, seed=k)
+    dev = L.DeviceIndex.from_postings(term_off, pdoc, pval, 0, n_docs)
+    info = dev.info()
+    assert info["n_blocks"] == 2 and info["n_docs"] == n_docs
+    ora = oracle.Index.__new__(oracle.Index)
+    ora.term_off, ora.pdoc, ora.pval, ora.n_docs = term_off, pdoc, pval, n_docs
+    rng = np.random.default_rng(7 + k)
+    # enough queries that block-major order runs most block-1 items after block 0's
+    qs = [list(dict.fromkeys(int(x) for x in rng.integers(0, v, rng.integers(1, 6))))
+          for _ in range(1200)]
+    got = dev.search(qs, k)
+    want = ora.score_ids(qs, k, n_threads=8)
+    for i, (g, w) in enumerate(zip(got, want)):
+        assert g == w, (i, qs[i], len(g), len(w))
+
+
 @pytest.fixture(scope="module")
 def million():
     """One 8-way shard of configs[2] (full MS MARCO: 8.8 M docs): 1.1 M docs, 34 LDS

@@ -125,6 +125,12 @@ def test_rank_cli_two_ranks_equals_one():
         _torchrun("rank", args + ["--output_path", str(td / "rccl.tsv")], world=1,
                   extra_env={"DI_FORCE_DIST": "1"})
         _same_run((td / "rccl.tsv").read_text(), (td / "one.tsv").read_text())
+        # ... with the pruned two-round exchange forced at one rank: its device branch
+        # (torch.topk over the samples, the pack / unpack scatters, the padded round-2
+        # all_gather over nccl) -- the code every multi-GPU retrieve of configs[2]/[3] runs
+        _torchrun("rank", args + ["--output_path", str(td / "rccl_pruned.tsv")], world=1,
+                  extra_env={"DI_FORCE_DIST": "1", "DI_EXCHANGE": "pruned"})
+        _same_run((td / "rccl_pruned.tsv").read_text(), (td / "one.tsv").read_text())
         _torchrun("rank", args + ["--output_path", str(td / "three.tsv"), "--top_k", "7"],
                   world=3)
         _torchrun("rank", args + ["--output_path", str(td / "one7.tsv"), "--top_k", "7"],
@@ -245,3 +251,34 @@ def test_visible_gpus_matches_the_runtime():
     from improving_learned_index_amd import parallel
 
     assert parallel.visible_gpus() == torch.cuda.device_count()
+
+
+def test_bench_single_rank_rccl_pruned_exchange():
+    """verdict r5 #1: the pruned exchange's device / RCCL branch on the GPU box.  One
+    torchrun rank, DI_FORCE_DIST=1 (nccl process group) and DI_EXCHANGE=pruned: rounds
+    1-2 run on device tensors over nccl every step; the merged lists of the last step
+    must equal the scorer's own (one shard: the exchange + merge is the identity), and
+    the plain path is timed beside it.  (At one rank every key of the only list is in
+    the global top-k, so round 2 sends all k of them after the k / g samples; the key
+    savings need >= 2 ranks: test_exchange_cpu, test_bench_gpus_flag_launches_ranks_itself.)"""
+    env = dict(os.environ, PYTHONPATH=str(ROOT), OMP_NUM_THREADS="4", DI_FORCE_DIST="1",
+               DI_EXCHANGE="pruned")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
+           "--master-addr", "127.0.0.1", f"--master-port={_port()}", "bench.py", "--gpus", "1",
+           "--legs", "retrieve,retrieve_shard", "--steps", "3", "--warmup", "1", "--no-cpu"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-4000:]
+    line = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(line) == 1, r.stdout[-2000:]
+    d = json.loads(line[0])
+    assert d["backend"] == "nccl" and d["ranks_seen"] == 1
+    k = d["config"]["k"]
+    for leg in ("retrieve", "retrieve_shard"):
+        x = d[leg]["exchange"]
+        assert x["path"] == "pruned", x
+        assert x["merged_equals_local_at_one_rank"] is True, x
+        g = max(1, min(64, k // 4))
+        assert x["gathered_keys_per_query"] <= k // g + k, x
+        assert x["collective_ms_per_step"] > 0
+        assert x["other_path"]["path"] == "plain" and x["other_path"]["collective_ms_per_step"] > 0
+    print(json.dumps({leg: d[leg]["exchange"] for leg in ("retrieve", "retrieve_shard")}))

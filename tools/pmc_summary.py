@@ -53,15 +53,31 @@ def short(name):
 def main(root):
     root = Path(root)
     vals = defaultdict(lambda: defaultdict(list))
+    durs = defaultdict(list)   # kernel -> dispatch durations (ns) of every pass
+    clocks = defaultdict(list)  # kernel -> GRBM_GUI_ACTIVE / 8 XCDs / that dispatch's ns
     for f in root.rglob("*counter_collection.csv"):
         with open(f) as fh:
             for row in csv.DictReader(fh):
                 k = short(row["Kernel_Name"])
-                vals[k][row["Counter_Name"]].append(float(row["Counter_Value"]))
+                v = float(row["Counter_Value"])
+                vals[k][row["Counter_Name"]].append(v)
+                dur = None
+                if row.get("Start_Timestamp") and row.get("End_Timestamp"):
+                    dur = float(row["End_Timestamp"]) - float(row["Start_Timestamp"])
+                if dur and dur > 0:
+                    durs[k].append(dur)
+                    if row["Counter_Name"] == "GRBM_GUI_ACTIVE":
+                        clocks[k].append(v / 8.0 / dur)
     out = {"kernels": {}, "note": __doc__.strip().splitlines()[2]}
     for k, cs in vals.items():
         d = {c: sum(v) / len(v) for c, v in cs.items()}
         d["dispatches"] = max(len(v) for v in cs.values())
+        if durs[k]:
+            # durations of the profiled dispatches themselves (the counters' own run)
+            d["duration_ns_avg"] = sum(durs[k]) / len(durs[k])
+        if clocks[k]:
+            # the clock each dispatch held: its busy cycles per XCD over its own duration
+            d["effective_clock_ghz"] = sum(clocks[k]) / len(clocks[k])
         if "FETCH_SIZE" in d and "WRITE_SIZE" in d:
             d["hbm_bytes_per_launch"] = (2.0 * d["FETCH_SIZE"] + d["WRITE_SIZE"]) * 1024.0
         if "TCC_HIT_sum" in d and "TCC_MISS_sum" in d and d["TCC_HIT_sum"] + d["TCC_MISS_sum"]:
