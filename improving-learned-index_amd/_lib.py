@@ -66,6 +66,11 @@ SIGNATURES = {
     "di_index_timing": (ctypes.c_int, [P, ctypes.c_char_p, P, ctypes.c_int]),
     "di_index_destroy": (ctypes.c_int, [P]),
     "di_topk_merge": (ctypes.c_int, [P, P, I32, I32, I32, P, P, ctypes.c_int, P, U32]),
+    "di_xchg_sample": (ctypes.c_int, [P, P, I32, I32, I32, P, ctypes.c_int, P]),
+    "di_xchg_count": (ctypes.c_int, [P, I32, P, P, I32, I32, I32, P, ctypes.c_int, P]),
+    "di_xchg_offsets": (ctypes.c_int, [P, I32, I32, P, P, ctypes.c_int, P]),
+    "di_xchg_pack": (ctypes.c_int, [P, P, P, I32, I32, P, ctypes.c_int, P]),
+    "di_xchg_unpack": (ctypes.c_int, [P, I64, P, P, I32, I32, I32, P, P, ctypes.c_int, P]),
     "di_encoder_create": (ctypes.c_int, [P, P, I32, ctypes.c_int, P]),
     "di_encode": (ctypes.c_int, [P, P, P, I32, I64, I32, P, P, I64, P, U32]),
     "di_encoder_reserve": (ctypes.c_int, [P, I64, I32, I64]),

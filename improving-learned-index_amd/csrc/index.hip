@@ -739,7 +739,7 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
                                            uint32_t *__restrict__ qhist, int ablate,
                                            const ItemRec *__restrict__ ir,
                                            uint32_t *__restrict__ long_flag, float bm_factor,
-                                           uint32_t *__restrict__ qtq, int kl) {
+                                           uint32_t *__restrict__ qtq, int kl, int tq_sched) {
     int64_t *lo = sh.v.bounds[0], *hi = sh.v.bounds[1];
 
     // opaque per item: keeps the per-thread index arithmetic of the sweeps from being
@@ -801,14 +801,21 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
     // and disagree on skipping, i.e. on which barriers they reach)
     // (few blocks, no qhist: the same word bounds the emit-above selection, see below)
     uint32_t tq_early = 0;
-    if ((bm || EXT == EXT_FEW) && qtq && threadIdx.x == 0)
+    if (qtq && threadIdx.x == 0)
         tq_early = __hip_atomic_load(&qtq[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     // The query's shared threshold histogram (qhist, below) is copied by LDS-DMA into
     // the selection histogram (idle until the selection) here, so its round trip
     // overlaps the scatter and the selection reads it from LDS; the fast selection
     // path zeroes the histogram itself when it runs.
     uint32_t *qh = qhist ? qhist + (int64_t)q * QH_BINS : nullptr;
-    const bool qpre = qh != nullptr;
+    // Threshold refresh schedule (tq_sched = first << 16 | every; plain exact scoring with
+    // the running word qtq): only the items of blocks b < first and b % every == 0 copy
+    // and read the histogram (and raise qtq with the Tq it gives); the others take qtq,
+    // one word read with the setup loads -- no 16 KiB copy to wait for, no threshold read.
+    // qtq only ever holds lower bounds of the final k-th score, so any schedule is exact.
+    const int tq_every = tq_sched & 0xFFFF, tq_first = tq_sched >> 16;
+    const bool qpre = qh != nullptr &&
+                      (!qtq || tq_every <= 1 || b < tq_first || b % tq_every == 0);
     static_assert(QH_BINS == 4 * SC_THREADS && QH_BINS <= HIST_BINS, "qhist prefetch");
     if (qpre) {
         typedef __attribute__((address_space(3))) void lds_void;
@@ -905,7 +912,7 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
         }
         zero();
     }
-    if (EXT != 0 && tid == 0) sh.tqe = tq_early;
+    if (qtq && tid == 0) sh.tqe = tq_early;
     __syncthreads();
     if (sh.bad) {
         // (the histogram copy lands before the next item touches the histogram)
@@ -1293,23 +1300,28 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
         }
     }
     uint32_t Tq = 0;
+    bool hist_dirty = false;  // keys staged in the histogram area by a sweep that overflowed
     if (qh) {
-        // second half of read_tq over the suffix sums published by the scatter barrier:
-        // the crossing thread writes tq (0 from the item's start when the histogram
-        // holds fewer than k candidates); one barrier
-        for (int w2 = wave + 1; w2 < SC_WAVES; ++w2) tq_sfx += sh.wsum[w2];
-        if (tq_sfx >= (uint32_t)k && tq_sfx - tq_c < (uint32_t)k) {
-            uint32_t above = tq_sfx - tq_c;
-            int e = 3;
-            for (; e > 0; --e) {
-                if (above + tq_hv[e] >= (uint32_t)k) break;
-                above += tq_hv[e];
+        if (qpre) {
+            // second half of read_tq over the suffix sums published by the scatter
+            // barrier: the crossing thread writes tq (0 from the item's start when the
+            // histogram holds fewer than k candidates); one barrier
+            for (int w2 = wave + 1; w2 < SC_WAVES; ++w2) tq_sfx += sh.wsum[w2];
+            if (tq_sfx >= (uint32_t)k && tq_sfx - tq_c < (uint32_t)k) {
+                uint32_t above = tq_sfx - tq_c;
+                int e = 3;
+                for (; e > 0; --e) {
+                    if (above + tq_hv[e] >= (uint32_t)k) break;
+                    above += tq_hv[e];
+                }
+                sh.tq = (uint32_t)(4 * tid + e);
             }
-            sh.tq = (uint32_t)(4 * tid + e);
+            __syncthreads();
+            Tq = sh.tq;
+        } else {
+            Tq = sh.tqe;  // (the running word, published by the setup barrier)
         }
-        __syncthreads();
-        Tq = sh.tq;
-        if (EXT != 0 && tid == 0) sh.tqn = max(sh.tqn, Tq);
+        if (tid == 0) sh.tqn = max(sh.tqn, Tq);
         stamp(8);  // threshold read (the part of tq-select before the sweep)
         // (wsum is written again only after a barrier of the selection below; tq only
         // at the next item's start)
@@ -1331,6 +1343,7 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
                 if (tid == 0) *cn = (int32_t)na;
                 return;
             }
+            hist_dirty = stage == hist_stage;
             stage = tail_fits ? acc_tail : nullptr;  // (the selections below use the histogram)
         }
     }
@@ -1381,7 +1394,8 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
         // branch-free: an untouched doc (w = 0) counts into a per-lane spare bin past
         // the 4096 score bins (no same-address conflicts), never read
         const uint32_t spare = HIST_BINS + (uint32_t)lane;
-        if (qpre) {  // the threshold copy was read (read_tq's barriers): zero the bins
+        if (qpre || hist_dirty) {  // the threshold copy was read (read_tq's barriers), or
+            // keys were staged there: zero the bins
             reinterpret_cast<uint4 *>(hist)[tid] = make_uint4(0, 0, 0, 0);
             __syncthreads();
         }
@@ -1426,7 +1440,7 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
         }
         // (this block alone has >= k docs scoring >= T: a lower bound of the query's final
         // k-th score for block-max, qtq)
-        if (EXT != 0 && tid == 0) sh.tqn = max(sh.tqn, sh.thr);
+        if (tid == 0) sh.tqn = max(sh.tqn, sh.thr);
         const uint32_t T = sh.thr, ties = sh.ties;  // T >= 1: every touched score is
         const uint32_t above = sh.above;             // nonzero
 
@@ -1597,7 +1611,7 @@ __device__ __forceinline__ void score_item(ScoreShared &sh, int q, int b,
                          });
     }
     const uint32_t T = prefix;
-    if (EXT != 0 && tid == 0) sh.tqn = max(sh.tqn, T >> 16);
+    if (tid == 0) sh.tqn = max(sh.tqn, T >> 16);
     const uint32_t ties = sh.u.rs.tot[sh.u.rs.bin];
 
     // doc-order cut among the ties: the `need` smallest doc indices
@@ -1679,7 +1693,7 @@ score_blocks_kernel(const uint32_t *__restrict__ post, SubIndex si, int min_cls,
                     const ItemRec *__restrict__ rec, uint32_t *__restrict__ long_flag,
                     float bm_factor, unsigned long long *__restrict__ bm_stat,
                     const uint16_t *__restrict__ border, uint32_t *__restrict__ qtq,
-                    int rec_slots, int kl) {
+                    int rec_slots, int kl, int tq_sched) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     ScoreShared &sh = *reinterpret_cast<ScoreShared *>(smem);
     if ((uint32_t)(uintptr_t)((__attribute__((address_space(3))) unsigned char *)smem) != 0) {
@@ -1689,7 +1703,7 @@ score_blocks_kernel(const uint32_t *__restrict__ post, SubIndex si, int min_cls,
             if (threadIdx.x == 0) cand_n[item] = -1;
         return;
     }
-    if (EXT != 0 && threadIdx.x == 0) {  // (the first item's barriers publish them)
+    if (threadIdx.x == 0) {  // (the first item's barriers publish them)
         sh.bm_cnt[0] = sh.bm_cnt[1] = 0ull;
         sh.tqn = 0;
     }
@@ -1700,12 +1714,13 @@ score_blocks_kernel(const uint32_t *__restrict__ post, SubIndex si, int min_cls,
                    min_cls, nb,
                    block_docs, n_terms,
                    n_docs, doc_lo, q_terms, cu_q, k, cand_key, cand_n, qhist, ablate,
-                   rec ? rec + (int64_t)item * rec_slots : nullptr, long_flag, bm_factor, qtq, kl);
+                   rec ? rec + (int64_t)item * rec_slots : nullptr, long_flag, bm_factor, qtq, kl,
+                   tq_sched);
         __syncthreads();  // every wave is done with the LDS of this item
         // the item's threshold into the query's running one, here rather than inside the
         // selection: qtq and the value read at the item's start need no registers across
         // the scatter (they cost the instantiation spills)
-        if (EXT != 0 && threadIdx.x == 0) {
+        if (threadIdx.x == 0) {
             const uint32_t t = sh.tqn;
             if (qtq && t > sh.tqe) atomicMax(&qtq[q], t);
             sh.tqn = 0;
@@ -2311,6 +2326,10 @@ struct di_index {
     // 130 vs 161 ms, merge 0.5 vs 7.1 and 1.4 vs 74 ms); DI_SCORE_THRESHOLD=0 / 1 forces
     int shared_thr = -1;
     bool block_order = false;  // DI_BLOCK_ORDER=1: block-max items in per-query bound order
+    // threshold refresh schedule (score_item): with the shared threshold, the items of
+    // blocks b < tq_first and b % tq_every == 0 read the query's histogram, the others
+    // the running word qtq (DI_TQ_EVERY / DI_TQ_FIRST; tq_every 1: every item reads it)
+    int tq_every = 1, tq_first = 0;
     int ablate = 0;  // DI_PROFILE_ABLATE: profiling only (1 no scatter, 2 no selection, 4 stop at the k-th score)
     Timer timer;
 
@@ -2770,6 +2789,8 @@ int di_index_create(const int64_t *term_off, int64_t n_terms, const uint32_t *pd
         if (const char *bo = std::getenv("DI_BLOCK_ORDER")) ix->block_order = bo[0] == '1';
         if (const char *st = std::getenv("DI_SCORE_THRESHOLD"))  // (tested both ways)
             ix->shared_thr = st[0] != '0' ? 1 : 0;
+        if (const char *e = std::getenv("DI_TQ_EVERY")) ix->tq_every = std::max(1, std::atoi(e));
+        if (const char *e = std::getenv("DI_TQ_FIRST")) ix->tq_first = std::max(0, std::atoi(e));
         build_index(ix.get(), term_off, n_terms, pdoc, pval, doc_lo, doc_hi);
         *out = ix.release();
     });
@@ -2995,7 +3016,12 @@ int di_index_search(di_index *ix, const uint32_t *q_terms, const int32_t *cu_q, 
                 }
                 const uint16_t *border = order ? ix->ws_border.as<uint16_t>() : nullptr;
                 // (DI_PROFILE_ABLATE bit 32768: the histogram-copy threshold instead, A/B)
-                const bool use_qtq = (thr && ix->bm_factor > 0.0f && !(ix->ablate & 32768)) || few;
+                // (DI_TQ_EVERY / DI_TQ_FIRST: the threshold refresh schedule of score_item;
+                // every = 1: every item copies the histogram, as before round 6)
+                const bool sched = thr && ix->tq_every > 1;
+                const bool use_qtq =
+                    (thr && ix->bm_factor > 0.0f && !(ix->ablate & 32768)) || few || sched;
+                const int tq_sched = sched ? (ix->tq_first << 16) | ix->tq_every : 1;
                 if (use_qtq) {
                     ix->ws_tq.reserve((size_t)nq * 4);
                     DI_HIP(hipMemsetAsync(ix->ws_tq.p, 0, (size_t)nq * 4, s));
@@ -3030,7 +3056,8 @@ int di_index_search(di_index *ix, const uint32_t *q_terms, const int32_t *cu_q, 
                                    use_rec ? ix->ws_rec.as<ItemRec>() : nullptr,
                                    ix->ws_long.as<uint32_t>(), thr ? ix->bm_factor : 0.0f,
                                    ix->bm_stat.as<unsigned long long>(), border,
-                                   use_qtq ? ix->ws_tq.as<uint32_t>() : nullptr, rec_slots, kl);
+                                   use_qtq ? ix->ws_tq.as<uint32_t>() : nullptr, rec_slots, kl,
+                                   tq_sched);
                 check_launch("score_blocks");
                 hipLaunchKernelGGL(score_long_kernel, dim3(std::min(n_items, n_cu())),
                                    dim3(SC_THREADS), sizeof(ScoreShared), s,

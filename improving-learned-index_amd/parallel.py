@@ -378,6 +378,8 @@ def exchange_topk(key, cnt, k: int, group=None, stats: Optional[dict] = None,
             stats["bytes_sent"] = 8 * nq * k + 4 * nq
         return gk, gc
     g = max(1, min(64, k // (4 * world)))
+    if dev.type == "cuda":
+        return _exchange_pruned_hip(K, cnt, k, g, world, group, stats)
     c = cnt.to(torch.int64).clamp(0, k)
     lo = torch.iinfo(torch.int64).min
     s_n = k // g  # samples per list (positions g-1, ..., s_n g - 1 < k)
@@ -433,6 +435,54 @@ def exchange_topk(key, cnt, k: int, group=None, stats: Optional[dict] = None,
         stats["gathered_keys_per_query"] = (s_n + emax / max(nq, 1)) if nq else 0.0
         stats["bytes_sent"] = 8 * (nq * s_n + emax) + 4 * 2 * nq
     return out[:world * nq * k], g_n.reshape(-1)
+
+
+def _exchange_pruned_hip(K, cnt, k: int, g: int, world: int, group, stats):
+    """exchange_topk's pruned rounds on device tensors: the local steps are the
+    library's di_xchg_* kernels (exchange.hip) on the current stream, around three
+    all_gathers and one device -> host read (the round-2 padded size).  Same output as
+    the tensor-operation form below it, which the CPU (gloo) rehearsals run."""
+    import torch
+    import torch.distributed as dist
+
+    from . import _lib
+
+    nq = cnt.numel()
+    dev = K.device
+    d = dev.index if dev.index is not None else torch.cuda.current_device()
+    st = torch.cuda.current_stream(dev).cuda_stream
+    L = _lib.lib()
+    P = _lib.ptr
+    cnt = cnt.to(torch.int32).contiguous()
+    K = K.contiguous()
+    s_n = k // g
+    smp = torch.empty(nq * s_n, dtype=torch.int64, device=dev)
+    _lib.check(L.di_xchg_sample(P(K), P(cnt), nq, k, g, P(smp), d, st))
+    g1 = torch.empty(world * nq * s_n, dtype=torch.int64, device=dev)
+    dist.all_gather_into_tensor(g1, smp, group=group)
+    ec = torch.empty(2 * nq, dtype=torch.int32, device=dev)
+    _lib.check(L.di_xchg_count(P(g1), world, P(K), P(cnt), nq, k, g, P(ec), d, st))
+    gec = torch.empty(world * 2 * nq, dtype=torch.int32, device=dev)
+    dist.all_gather_into_tensor(gec, ec, group=group)
+    off = torch.empty(world * nq, dtype=torch.int64, device=dev)
+    tot = torch.empty(world, dtype=torch.int64, device=dev)
+    _lib.check(L.di_xchg_offsets(P(gec), world, nq, P(off), P(tot), d, st))
+    emax = int(tot.max().item()) if nq else 0  # (the one host synchronisation)
+    me = dist.get_rank(group)
+    out = torch.empty(world * nq * k, dtype=torch.int64, device=dev)
+    g_n = torch.empty(world * nq, dtype=torch.int32, device=dev)
+    g2 = None
+    if emax:
+        buf = torch.zeros(emax, dtype=torch.int64, device=dev)
+        _lib.check(L.di_xchg_pack(P(K), P(ec), P(off[me * nq:]), nq, k, P(buf), d, st))
+        g2 = torch.empty(world * emax, dtype=torch.int64, device=dev)
+        dist.all_gather_into_tensor(g2, buf, group=group)
+    _lib.check(L.di_xchg_unpack(P(g2), emax, P(gec), P(off), world, nq, k, P(out), P(g_n), d, st))
+    if stats is not None:
+        stats["path"] = "pruned"
+        stats["gathered_keys_per_query"] = (s_n + emax / max(nq, 1)) if nq else 0.0
+        stats["bytes_sent"] = 8 * (nq * s_n + emax) + 4 * 2 * nq
+    return out, g_n
 
 
 class ShardedRetriever:

@@ -163,6 +163,33 @@ int di_topk_merge(const uint64_t *keys, const int32_t *counts, int32_t n_q, int3
                   int32_t k, uint64_t *out_key, int32_t *out_n, int device, void *hip_stream,
                   uint32_t flags);
 
+/* The local steps of the pruned exact exchange of per-shard top-k lists between ranks
+ * (parallel.exchange_topk; the collectives between them are the caller's all_gathers).
+ * keys [n_q][k] descending merge keys (> 0), counts [n_q] (negative: rejected query).
+ * Device pointers only, asynchronous on hip_stream.  Replaces nothing in the reference
+ * (it has no sharded retrieval); the result feeds di_topk_merge, whose
+ * output equals the merge of the full lists (ranker.py:43-48 keeps the global top-k).
+ *   sample:  samples [n_q][k/g] = keys at positions g-1, 2g-1, ... (0 past counts[q]);
+ *   count:   gathered_samples [world][n_q][k/g] -> T_q = the ceil(k/g)-th largest
+ *            sample, ec [2][n_q] = (this rank's keys >= T_q, counts);
+ *   offsets: gathered_ec [world][2][n_q] -> offsets [world][n_q] (exclusive scans of the
+ *            key counts), totals [world];
+ *   pack:    ec / offsets of this rank -> buf (its keys >= T_q back to back);
+ *   unpack:  gathered [world][emax] -> out_keys [world][n_q][k], out_n [world][n_q]
+ *            (the layout of a plain all_gather; DI_F_LISTS_MAJOR for di_topk_merge). */
+int di_xchg_sample(const uint64_t *keys, const int32_t *counts, int32_t n_q, int32_t k,
+                   int32_t g, uint64_t *samples, int device, void *hip_stream);
+int di_xchg_count(const uint64_t *gathered_samples, int32_t world, const uint64_t *keys,
+                  const int32_t *counts, int32_t n_q, int32_t k, int32_t g, int32_t *ec,
+                  int device, void *hip_stream);
+int di_xchg_offsets(const int32_t *gathered_ec, int32_t world, int32_t n_q, int64_t *offsets,
+                    int64_t *totals, int device, void *hip_stream);
+int di_xchg_pack(const uint64_t *keys, const int32_t *ec, const int64_t *offsets, int32_t n_q,
+                 int32_t k, uint64_t *buf, int device, void *hip_stream);
+int di_xchg_unpack(const uint64_t *gathered, int64_t emax, const int32_t *gathered_ec,
+                   const int64_t *offsets, int32_t world, int32_t n_q, int32_t k,
+                   uint64_t *out_keys, int32_t *out_n, int device, void *hip_stream);
+
 /* ======================================================================
  * In-memory float index of the NanoBEIR evaluator           (A14, A15)
  * ====================================================================== */

@@ -448,6 +448,38 @@ def test_million_doc_shard_matches_oracle(L, million, k):
             qs, k, n_threads=16), m
 
 
+@pytest.mark.parametrize("every,first", [(1, 0), (2, 0), (8, 2), (1000, 1)])
+def test_threshold_refresh_schedules_equal_oracle(L, million, every, first, monkeypatch):
+    """score_item's threshold refresh schedule (DI_TQ_EVERY / DI_TQ_FIRST): only some
+    blocks' items read the query's candidate histogram, the others the running word
+    qtq -- a staler lower bound, so more of their sweeps overflow to the full selection
+    (with full 32 K-doc blocks the overflowed keys sat in the histogram area, which must
+    be zeroed again).  Every schedule: the exact top-k (34 blocks, k 10 and 1000; every
+    1000: block 0 alone reads the histogram)."""
+    from improving_learned_index_amd import synthetic as S
+
+    term_off, pdoc, pval, ora = million
+    monkeypatch.setenv("DI_TQ_EVERY", str(every))
+    monkeypatch.setenv("DI_TQ_FIRST", str(first))
+    dev = L.DeviceIndex.from_postings(term_off, pdoc, pval, 0, ora.n_docs)
+    qs = S.msmarco_like_queries(24, 2_200_000, seed=31) + _queries(2_200_000, 8, seed=31)
+    for k in (10, 1000):
+        assert dev.search(qs, k) == ora.score_ids(qs, k, n_threads=16), k
+
+
+def test_threshold_refresh_small_blocks_equal_oracle(L, synth, monkeypatch):
+    """The same schedules on the 3-block 70 k-doc shard with the shared threshold forced
+    on (blocks with an accumulator tail; long queries in the batch)."""
+    term_off, pdoc, pval, ora = synth
+    qs = _queries(5000, 80, seed=23, long_every=20)
+    monkeypatch.setenv("DI_SCORE_THRESHOLD", "1")
+    for every in (2, 3):
+        monkeypatch.setenv("DI_TQ_EVERY", str(every))
+        dev = L.DeviceIndex.from_postings(term_off, pdoc, pval)
+        for k in (10, 1000):
+            assert dev.search(qs, k) == ora.score_ids(qs, k, n_threads=8), (every, k)
+
+
 def test_million_doc_merge_past_lds_capacity(L, million, monkeypatch):
     """Shared threshold off at 34 blocks: every block lists its full top-1000, 34 k
     candidates per query against the merge's 8192-key LDS array -- the two-pass
