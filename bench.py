@@ -303,7 +303,9 @@ def retrieve_leg(args, rank, world, dev, n_docs=DOCS_PER_SHARD, check_queries=20
     # the scorer instantiation this shard runs: shards of 2..7 blocks take the emit-above
     # selection (score_blocks_kernel<4>, EXT_FEW), larger ones the plain kernel
     nb = ix.info()["n_blocks"]
-    sb_kernel = ("score_blocks_kernel<4>" if 2 <= nb < 8 and 2 * k <= 2048
+    # (di_index::few_blocks: 2..7 blocks, 2 k <= 2048, the shared threshold not forced on)
+    sb_kernel = ("score_blocks_kernel<4>" if 2 <= nb < 8 and 2 * k <= 2048 and
+                 os.environ.get("DI_SCORE_THRESHOLD", "")[:1] != "1"
                  else "score_blocks_kernel<0>")
     traffic, src = load_pmc_traffic(sb_kernel, leg) if leg else (None, None)
     if traffic is not None:

@@ -2328,8 +2328,12 @@ struct di_index {
     bool block_order = false;  // DI_BLOCK_ORDER=1: block-max items in per-query bound order
     // threshold refresh schedule (score_item): with the shared threshold, the items of
     // blocks b < tq_first and b % tq_every == 0 read the query's histogram, the others
-    // the running word qtq (DI_TQ_EVERY / DI_TQ_FIRST; tq_every 1: every item reads it)
-    int tq_every = 1, tq_first = 0;
+    // the running word qtq (DI_TQ_EVERY / DI_TQ_FIRST; tq_every 1: every item reads it,
+    // as before round 6).  8 / 4 from the sweep (profiles/round6_d_tq_sweep_*.json, one
+    // box): 8.8 M skewed docs 94.0 -> 102.7 k q/s (score_blocks 70.7 -> 64.0 ms per
+    // 6980-query batch), 1.1 M docs 14.47 -> 14.13-14.23 ms; 4 / 0 and 8 / 0 were slower
+    // at 1.1 M (their stale thresholds overflow more sweeps), 16 / 4 and 32 / 8 no faster.
+    int tq_every = 8, tq_first = 4;
     int ablate = 0;  // DI_PROFILE_ABLATE: profiling only (1 no scatter, 2 no selection, 4 stop at the k-th score)
     Timer timer;
 

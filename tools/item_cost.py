@@ -32,6 +32,7 @@ NQ, K = 6980, 1000
 PH = re.compile(r"setup (\d+) scatter (\d+) hist (\d+) \[count (\d+)\] write (\d+) ties (\d+) "
                 r"copy (\d+) tq-select (\d+) \[tq-read (\d+)\] scatter-loop slowest wave (\d+) "
                 r"mean wave (\d+)")
+_PREV = None
 NAMES = ("setup", "scatter", "hist", "count", "write", "ties", "copy", "tq_select", "tq_read",
          "wave_max", "wave_mean")
 
@@ -72,7 +73,7 @@ def measure(n_docs, skew):
     items = NQ * nb
     lens = np.diff(term_off)
     rows = []
-    prev = None
+    global _PREV
     for m, f in ((1, 0.0), (2, 0.0), (8, 0.0), (32, 0.0), (128, 0.0), (1, 1.0)):
         ix.set_min_impact(m)
         ix.set_block_max(f)
@@ -95,8 +96,9 @@ def measure(n_docs, skew):
         # stamps are cumulative over the process: this search's share
         d = None
         if st:
-            d = {k: st[k] - (prev[k] if prev else 0) for k in st}
-            prev = st
+            # (the library's stamp counters are process-wide: previous shards included)
+            d = {k: st[k] - (_PREV[k] if _PREV else 0) for k in st}
+            _PREV = st
             # (the warm-up search adds as much again: halve)
             d = {k: v / 2.0 for k, v in d.items()}
         wg0_items = items / min(items, 256)
