@@ -449,6 +449,11 @@ def _exchange_pruned_hip(K, cnt, k: int, g: int, world: int, group, stats):
 
     nq = cnt.numel()
     dev = K.device
+    if nq == 0:  # (every rank has the same queries: all return here together)
+        if stats is not None:
+            stats.update(path="pruned", gathered_keys_per_query=0.0, bytes_sent=0)
+        return (torch.empty(0, dtype=torch.int64, device=dev),
+                torch.empty(0, dtype=torch.int32, device=dev))
     d = dev.index if dev.index is not None else torch.cuda.current_device()
     st = torch.cuda.current_stream(dev).cuda_stream
     L = _lib.lib()
