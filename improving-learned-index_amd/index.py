@@ -18,6 +18,7 @@ from __future__ import annotations
 
 import argparse
 import logging
+import os
 import sys
 import time
 from pathlib import Path
@@ -71,6 +72,8 @@ def _index_file(indexer, collection_path, collection_type, output_file_path,
     first shard) writes it."""
     lo, hi = (0, None) if doc_range is None else doc_range
     pending = None  # submitted, not yet written
+    # (DI_INDEX_SYNC_WRITES=1: format and write each batch before the next encode, A/B)
+    defer = os.environ.get("DI_INDEX_SYNC_WRITES") != "1"
 
     def flush(batch):
         nonlocal pending
@@ -79,7 +82,8 @@ def _index_file(indexer, collection_path, collection_type, output_file_path,
             return
         handle = indexer.submit(batch)
         if pending is not None:
-            indexer.finish(pending, out)
+            # (its formatting and write overlap the next batch's encode)
+            indexer.finish(pending, out, wait=not defer)
         pending = handle
 
     with open(collection_path) as f, open(output_file_path, "w") as out:
@@ -107,6 +111,8 @@ def _index_file(indexer, collection_path, collection_type, output_file_path,
             flush(batch)
         if pending is not None:
             indexer.finish(pending, out)
+        if hasattr(indexer, "drain"):
+            indexer.drain()
     return n
 
 

@@ -123,6 +123,53 @@ class TokenizerPool:
 DEVICE_DOCS = 4096  # documents per device call when tokenizer chunks are merged
 
 
+class _Writer:
+    """One background thread that formats and writes batches in submission order, so
+    that a batch's formatting (native, the GIL released) and its file write overlap the
+    next batch's device encode.  An exception in a job is raised at the next put /
+    drain."""
+
+    def __init__(self):
+        import queue
+        import threading
+
+        self.q = queue.Queue(maxsize=4)
+        self.err = None
+        self.t = threading.Thread(target=self._run, name="di-index-writer", daemon=True)
+        self.t.start()
+
+    def _run(self):
+        while True:
+            job = self.q.get()
+            try:
+                if job is None:
+                    return
+                if self.err is None:
+                    job()
+            except BaseException as e:  # (re-raised in the caller's thread)
+                self.err = e
+            finally:
+                self.q.task_done()
+
+    def _check(self):
+        if self.err is not None:
+            err, self.err = self.err, None
+            raise err
+
+    def put(self, job):
+        self._check()
+        self.q.put(job)
+
+    def drain(self):
+        self.q.join()
+        self._check()
+
+    def close(self):
+        self.q.put(None)
+        self.t.join()
+        self._check()
+
+
 class Indexer:
     def __init__(self, model: DeepImpact, model_batch_size: int = 32, num_processes: int = 8,
                  pool: Optional[TokenizerPool] = None):
@@ -132,6 +179,7 @@ class Indexer:
         self.batch_size = max(model_batch_size, 256)
         self.num_processes = num_processes
         self.pool = pool  # None: tokenize in this process
+        self._writer = None  # (pool path: formatting + writes behind the next encode)
 
     def _chunks(self, batch: Sequence[str]):
         # with a pool: enough chunks to keep every worker busy (down to 64 docs each)
@@ -161,29 +209,58 @@ class Indexer:
             return (batch, None)
         return (batch, self.pool.imap(self._chunks(batch)))
 
-    def finish(self, handle, file) -> None:
-        """indexer.py:31-68: file.write('\\n'.join(lines) + '\\n')."""
+    def finish(self, handle, file, wait: bool = True) -> None:
+        """indexer.py:31-68: file.write('\\n'.join(lines) + '\\n').  wait=False (the
+        pool path): return once the batch is encoded; its formatting and write run on
+        the writer thread, in order, while the caller encodes the next batch --
+        drain() (or a later finish with wait=True) completes them."""
         batch, it = handle
         if it is None:
             impacts = self.encode(batch)
             text = _lib.format_impact_lines([[t for t, _ in d] for d in impacts],
                                             [[v for _, v in d] for d in impacts])
-        else:
-            # the workers' chunks are merged into device batches of up to DEVICE_DOCS
-            # documents (a 100-doc chunk leaves most of the GPU idle), in order
-            parts, n, out = [], 0, []
-            for p in it:
-                parts.append(p)
-                n += len(p[1]) - 1
-                if n >= DEVICE_DOCS:
-                    out.append(self.model.encode_packed_text(DeepImpact.merge_packed_blobs(parts)))
-                    parts, n = [], 0
-            if parts:
-                out.append(self.model.encode_packed_text(DeepImpact.merge_packed_blobs(parts)))
-            text = "".join(out)
-        # '\\n'.join(lines) + '\\n' == every line + '\\n', except for an empty batch
-        file.write(text if batch else "\n")
-        file.flush()
+            self.drain()  # (earlier deferred writes first)
+            file.write(text if batch else "\n")
+            file.flush()
+            return
+        # the workers' chunks are merged into device batches of up to DEVICE_DOCS
+        # documents (a 100-doc chunk leaves most of the GPU idle), in order
+        enc = getattr(self.model, "encode_packed_impacts", None)
+        parts, n, jobs = [], 0, []
+
+        def encode(parts):
+            packed = DeepImpact.merge_packed_blobs(parts)
+            if enc is not None:
+                jobs.append(enc(packed))
+            else:
+                text = self.model.encode_packed_text(packed)
+                jobs.append(lambda: text)
+
+        for p in it:
+            parts.append(p)
+            n += len(p[1]) - 1
+            if n >= DEVICE_DOCS:
+                encode(parts)
+                parts, n = [], 0
+        if parts:
+            encode(parts)
+
+        def write():
+            text = "".join(j() for j in jobs)
+            # '\\n'.join(lines) + '\\n' == every line + '\\n', except for an empty batch
+            file.write(text if batch else "\n")
+            file.flush()
+
+        if self._writer is None:
+            self._writer = _Writer()
+        self._writer.put(write)
+        if wait:
+            self._writer.drain()
+
+    def drain(self) -> None:
+        """Wait for the deferred formatting and writes (re-raises their errors)."""
+        if self._writer is not None:
+            self._writer.drain()
 
     def index(self, batch: Sequence[str], file) -> None:
         """indexer.py:31-68: file.write('\\n'.join(lines) + '\\n')."""

@@ -389,9 +389,15 @@ class DeepImpact:
     def encode_packed_text(self, packed) -> str:
         """A pack_processed_blob batch -> its impact-TSV lines (round3, native
         formatter), without per-term Python objects."""
+        return self.encode_packed_impacts(packed)()
+
+    def encode_packed_impacts(self, packed):
+        """Encode a pack_processed_blob batch on the device now; return the formatting
+        step as a callable (the native formatter, run later -- Indexer overlaps it with
+        the next batch's encode)."""
         ids, cu, blob, term_off, tt, ct = packed
         imp = self.encoder.encode_packed(ids, cu, tt, ct, round3=True)
-        return _lib.format_impact_lines_packed(blob, term_off, imp, ct)
+        return lambda: _lib.format_impact_lines_packed(blob, term_off, imp, ct)
 
     def encode_packed_terms(self, packed, round3=False):
         """Encode a pack_processed batch: per document its (term, impact) list."""

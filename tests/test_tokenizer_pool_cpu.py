@@ -163,3 +163,35 @@ def test_worker_threads_follow_the_cpu_share(monkeypatch):
     assert indexer.worker_threads(16) == 4  # 256 // 16 = 16, capped at 4
     monkeypatch.setattr(os, "sched_getaffinity", lambda pid: set(range(8)), raising=False)
     assert indexer.worker_threads(8) == 2  # 8 // 8 = 1, at least 2
+
+
+class _DeferredFakeModel(_FakeModel):
+    """The real class's split: encode now, format later (Indexer's writer thread)."""
+
+    def encode_packed_impacts(self, packed):
+        text = self.encode_packed_text(packed)
+        return lambda: text
+
+
+@pytest.mark.parametrize("model_cls", [_FakeModel, _DeferredFakeModel])
+def test_index_file_deferred_writes_keep_the_bytes(tmp_path, restore_class, model_cls):
+    """index._index_file with a tokenizer pool: each batch's formatting and write run on
+    the writer thread behind the next batch's encode (finish(wait=False)); the file must
+    equal the sequential in-process loop's, empty first batch included (process batch
+    size 7 over 100 docs: 15 batches)."""
+    import time
+
+    from improving_learned_index_amd import index as index_cli
+    from improving_learned_index_amd import indexer
+
+    restore_class.DeepImpact.set_tokenizer(GOLDEN / "tokenizer.json")
+    texts = json.loads((GOLDEN / "encoder_xlmr_small.json").read_text())["texts"]
+    coll = tmp_path / "c.tsv"
+    coll.write_text("".join(f"{i}\t{texts[i % len(texts)]} doc{i}\n" for i in range(100)))
+    index_cli._index_file(indexer.Indexer(_FakeModel(), 32), coll, "msmarco", tmp_path / "a",
+                          7, None, time.time())
+    with indexer.TokenizerPool(2, GOLDEN / "tokenizer.json", 512) as pool:
+        idx = indexer.Indexer(model_cls(), 32, num_processes=2, pool=pool)
+        index_cli._index_file(idx, coll, "msmarco", tmp_path / "b", 7, None, time.time())
+    assert (tmp_path / "a").read_bytes() == (tmp_path / "b").read_bytes()
+    assert (tmp_path / "a").read_bytes().count(b"\n") == 100
