@@ -738,6 +738,51 @@ def index_e2e_leg(args, dev, rank=0, world=1):
                     "docs run as 256-doc device chunks)"}
 
 
+def rank_e2e_leg(args, dev):
+    """A11-A13 end to end through the drop-in `rank` CLI's own code path: a synthetic
+    100 k-doc impact TSV (the retrieve leg's generator, native writer) -> quantize_file
+    -> create_index (reference-format files) -> Ranker(index, queries.tsv) -> run file:
+    query text tokenized by the repo's local tokenizer (terms '▁t<id>', the generator's
+    names), one batched GPU search per 8192 queries, the run file written natively.
+    Timed: Ranker construction (vocabulary + index load to the GPU) and run() apart."""
+    import shutil
+    import tempfile
+
+    from improving_learned_index_amd.inverted_index import create_index
+    from improving_learned_index_amd.quantize import quantize_file
+    from improving_learned_index_amd.ranker import Ranker
+
+    n = DOCS_PER_SHARD
+    V = v_terms(n)
+    td = Path(tempfile.mkdtemp(dir="/tmp"))
+    try:
+        S.synth_impact_tsv(td / "collection.index", n, V, seed=4321)
+        quantize_file(td / "collection.index", td / "collection.quantized", sharded=False)
+        create_index(td / "collection.quantized", td / "index")
+        queries = S.msmarco_like_queries(args.queries, V, seed=1234)
+        with open(td / "queries.tsv", "w") as f:
+            for i, q in enumerate(queries):
+                f.write(f"{1048576 + i}\t{' '.join(f't{t}' for t in q)}\n")
+        t0 = time.perf_counter()
+        r = Ranker(td / "index", td / "queries.tsv", td / "run.tsv",
+                   tokenizer_path=ROOT / "tests" / "golden" / "tokenizer.json", device=dev,
+                   top_k=args.k)
+        t_load = time.perf_counter() - t0
+        t1 = time.perf_counter()
+        r.run()
+        el = time.perf_counter() - t1
+        lines = sum(1 for _ in open(td / "run.tsv", "rb"))
+        size = (td / "run.tsv").stat().st_size
+    finally:
+        shutil.rmtree(td, ignore_errors=True)
+    log(f"rank e2e: {len(queries)} queries in {el:.2f}s after {t_load:.2f}s load, {lines} lines")
+    return {"value": round(len(queries) / el, 1), "unit": "queries/s", "queries": len(queries),
+            "k": args.k, "seconds": round(el, 3), "load_seconds": round(t_load, 2),
+            "run_file_lines": lines, "run_file_bytes": int(size), "docs": n, "v_terms": V,
+            "path": "ranker.Ranker.run: query text -> process_query (local tokenizer) -> "
+                    "term ids -> di_index_search (one batch) -> di_format_run_lines -> run file"}
+
+
 def text_legs(args):
     """A10 + A11 at one 8-way shard of configs[2] (1.1 M docs, V = 2 N): the impact TSV
     the index CLI writes (synthetic, the retrieve legs' generator, native writer) ->
@@ -855,14 +900,15 @@ def main():
     ap.add_argument("--text-docs", type=int, default=1_100_000,
                     help="text legs (quantize, index_create): docs of the impact TSV")
     ap.add_argument("--legs", default="encode_x3,encode,encode_fp32,retrieve,retrieve_shard,text,"
-                                      "index_e2e",
+                                      "index_e2e,rank_e2e",
                     help="encode_x3 (fp32-faithful bf16x3: the headline), encode (bf16 throughput "
                          "mode), encode_fp32 (f32 MFMA: the exactness side leg, with the bf16x3 "
                          "flip rates against it), retrieve (100k-doc shard, configs[1]), "
                          "retrieve_shard (1.1M docs: "
                          "one 8-way shard of configs[2]), retrieve_full (8.8M docs on one GPU, "
                          "configs[2]), text (quantize + index_create of a 1.1M-doc impact TSV), "
-                         "index_e2e (index.py's path end to end, tokenizer workers included)")
+                         "index_e2e (index.py's path end to end, tokenizer workers included), "
+                         "rank_e2e (the rank CLI's path end to end on a 100k-doc index)")
     args = ap.parse_args()
 
     if args.gpus < 1:
@@ -927,6 +973,8 @@ def main():
     if "retrieve" in legs:
         ret_res, ret_ctx = retrieve_leg(args, rank, world, dev, check_queries=n_check)
     e2e_res = index_e2e_leg(args, dev, rank, world) if "index_e2e" in legs else None
+    # (rank 0 alone: the single-process CLI, as the text legs)
+    rank_res = rank_e2e_leg(args, dev) if "rank_e2e" in legs and rank == 0 else None
     text_res = text_legs(args) if "text" in legs and rank == 0 else None
     big = {}
     for leg, nd in (("retrieve_shard", 1_100_000), ("retrieve_full", 8_800_000)):
@@ -936,8 +984,8 @@ def main():
     # the headline is the fp32-faithful encode (bf16x3: the reference computes in fp32,
     # indexer.py:46); the bf16 throughput mode is a side line (it flips a third of the
     # quantized integers)
-    primary = next((r for r in (x3_res, enc_res, ret_res) + tuple(big.values()) + (e2e_res,)
-                    if r is not None), None)
+    primary = next((r for r in (x3_res, enc_res, ret_res) + tuple(big.values()) +
+                    (e2e_res, rank_res) if r is not None), None)
     if primary is None:
         raise SystemExit("no bench leg selected")
     out = {
@@ -1013,6 +1061,8 @@ def main():
             out["retrieve"]["exchange"] = ret_res["exchange"]
     if e2e_res is not None:
         out["index_e2e"] = e2e_res
+    if rank_res is not None:
+        out["rank_e2e"] = rank_res
     if text_res is not None:
         out.update(text_res)
     for leg, r in big.items():

@@ -82,6 +82,7 @@ SIGNATURES = {
     "di_quantize_file": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_double, I32,
                                         ctypes.c_int, P]),
     "di_format_impact_lines": (ctypes.c_int, [P, P, P, P, I32, P, I64, P]),
+    "di_append_run_lines": (ctypes.c_int, [ctypes.c_char_p, P, P, I32, P, P, P, I32]),
     "di_sparse_create": (ctypes.c_int, [P, I64, P, P, U32, ctypes.c_int, P]),
     "di_sparse_search": (ctypes.c_int, [P, P, P, I32, I32, P, P, P, P, U32]),
     "di_sparse_search_f64": (ctypes.c_int, [P, P, P, I32, I32, P, P, P, U32]),
@@ -352,6 +353,24 @@ def key_score(keys, wide=False):
 def is_wide(n_terms: int) -> bool:
     """Does a query of n_terms known terms get wide merge keys?"""
     return n_terms > DI_SHORT_QUERY_TERMS
+
+
+def append_run_lines(path, qids, docs, scores, counts) -> None:
+    """Native RunFile.writelines over a batch (di_append_run_lines): qids (str list),
+    docs / scores uint32 [n_q, k], counts [n_q] -> those queries' lines appended to path."""
+    n_q = len(qids)
+    if n_q == 0:
+        open(path, "ab").close()
+        return
+    enc = [str(q).encode("utf-8") for q in qids]
+    blob = b"".join(enc) + b"\0"
+    off = np.zeros(n_q + 1, np.int64)
+    off[1:] = np.cumsum([len(b) for b in enc])
+    docs = np.ascontiguousarray(docs, np.uint32).reshape(n_q, -1)
+    scores = np.ascontiguousarray(scores, np.uint32).reshape(docs.shape)
+    cnt = np.ascontiguousarray(counts, np.int32)
+    check(lib().di_append_run_lines(str(path).encode("utf-8"), blob, ptr(off), n_q, ptr(docs),
+                                    ptr(scores), ptr(cnt), docs.shape[1]))
 
 
 def format_impact_lines_packed(blob: bytes, term_off, impacts, cu_terms) -> str:

@@ -13,6 +13,7 @@
 #include <string>
 #include <string_view>
 #include <algorithm>
+#include <thread>
 #include <vector>
 
 #include "di_common.h"
@@ -48,6 +49,88 @@ extern "C" int di_format_impact_lines(const char *terms, const int64_t *term_off
         DI_REQUIRE(out && (int64_t)buf.size() <= out_cap, DI_ERANGE,
                    "output buffer too small: %lld bytes needed", (long long)buf.size());
         std::memcpy(out, buf.data(), buf.size());
+    });
+}
+
+// run-file lines (reference src/utils/datasets.py RunFile.writelines, :305-324):
+// f"{qid}\t{pid}\t{rank}\t{score}\n" for rank = 1.. over each query's (pid, score)
+// list, queries in order, appended to the file.  Integer pids and scores (the quantized
+// index).  Formatted on host_threads() threads (<= 16) in rounds of query groups.
+namespace {
+inline int dec_digits(uint32_t v) {
+    int d = 1;
+    while (v >= 10) v /= 10, ++d;
+    return d;
+}
+inline char *put_dec(char *p, uint32_t v, int d) {
+    for (int i = d - 1; i >= 0; --i) p[i] = (char)('0' + v % 10), v /= 10;
+    return p + d;
+}
+}  // namespace
+
+extern "C" int di_append_run_lines(const char *path, const char *qids, const int64_t *qid_off,
+                                   int32_t n_q, const uint32_t *docs, const uint32_t *scores,
+                                   const int32_t *counts, int32_t k) {
+    return guard([&] {
+        DI_REQUIRE(path && qid_off && n_q >= 0 && k > 0, DI_EINVAL, "bad argument");
+        DI_REQUIRE(n_q == 0 || (qids && docs && scores && counts), DI_EINVAL, "null argument");
+        for (int32_t q = 0; q < n_q; ++q)
+            DI_REQUIRE(counts[q] >= 0 && counts[q] <= k, DI_ERANGE,
+                       "query %d: count %d outside [0, %d]", q, counts[q], k);
+        std::FILE *f = std::fopen(path, "ab");
+        DI_REQUIRE(f, DI_EIO, "cannot open %s", path);
+        // rounds of nt consecutive query groups: every thread formats its group into its
+        // own (reused) buffer, then the buffers are written in order -- no buffer of
+        // the whole batch (first-touching one costs more than formatting it)
+        const int nt = std::max(1, std::min(host_threads(), 16));
+        constexpr int32_t GROUP = 32;  // queries per thread and round
+        std::vector<std::string> bufs((size_t)nt);
+        bool ok = true;
+        for (int32_t r0 = 0; r0 < n_q && ok; r0 += nt * GROUP) {
+            auto work = [&](int t) {
+                std::string &b = bufs[(size_t)t];
+                b.clear();
+                const int32_t q0 = std::min(n_q, r0 + t * GROUP), q1 = std::min(n_q, q0 + GROUP);
+                char *p = nullptr;
+                for (int pass = 0; pass < 2; ++pass) {  // bytes, then the lines
+                    int64_t need = 0;
+                    for (int32_t q = q0; q < q1; ++q) {
+                        const char *id = qids + qid_off[q];
+                        const size_t idn = (size_t)(qid_off[q + 1] - qid_off[q]);
+                        const uint32_t *dq = docs + (int64_t)q * k, *sq = scores + (int64_t)q * k;
+                        for (int32_t i = 0; i < counts[q]; ++i) {
+                            const int d1 = dec_digits(dq[i]), d2 = dec_digits((uint32_t)i + 1),
+                                      d3 = dec_digits(sq[i]);
+                            if (pass == 0) {
+                                need += (int64_t)idn + 4 + d1 + d2 + d3;
+                                continue;
+                            }
+                            std::memcpy(p, id, idn);
+                            p += idn;
+                            *p++ = '\t';
+                            p = put_dec(p, dq[i], d1);
+                            *p++ = '\t';
+                            p = put_dec(p, (uint32_t)i + 1, d2);
+                            *p++ = '\t';
+                            p = put_dec(p, sq[i], d3);
+                            *p++ = '\n';
+                        }
+                    }
+                    if (pass == 0) {
+                        b.resize((size_t)need);
+                        p = b.data();
+                    }
+                }
+            };
+            std::vector<std::thread> th;
+            for (int t = 1; t < nt; ++t) th.emplace_back(work, t);
+            work(0);
+            for (auto &x : th) x.join();
+            for (auto &b : bufs)
+                ok = ok && std::fwrite(b.data(), 1, b.size(), f) == b.size();
+        }
+        ok = (std::fclose(f) == 0) && ok;
+        DI_REQUIRE(ok, DI_EIO, "short write to %s", path);
     });
 }
 

@@ -133,6 +133,14 @@ class RunFile:
             f.write("".join(f"{qid}\t{pid}\t{rank}\t{score}\n"
                             for rank, (pid, score) in enumerate(scores, start=1)))
 
+    def write_batch(self, qids, docs, scores, counts):
+        """writelines for a batch of queries in order, from arrays (docs / scores
+        [n_q, k] integers, counts [n_q]): the same bytes, formatted and appended
+        natively (di_append_run_lines)."""
+        from . import _lib
+
+        _lib.append_run_lines(self.run_file_path, qids, docs, scores, counts)
+
     def read(self) -> Iterator[Tuple[str, str, int, float]]:
         with open(self.run_file_path, "r", encoding="utf-8") as f:
             for line in f:

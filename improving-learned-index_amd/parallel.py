@@ -274,6 +274,22 @@ def decode_quant_keys(keys: np.ndarray, n: int, n_terms: int = 0) -> List[Tuple[
     return list(zip(docs.tolist(), scores.tolist()))
 
 
+def decode_quant_key_arrays(keys: np.ndarray, counts: np.ndarray, n_terms) -> Tuple[np.ndarray, np.ndarray]:
+    """decode_quant_keys over a batch: keys uint64 [n_q, k], counts [n_q], the queries'
+    known-term counts -> (docs, scores) uint32 [n_q, k] (valid up to counts[q]).
+    Raises on a rejected query (a negative count) like decode_quant_keys."""
+    counts = np.asarray(counts)
+    if counts.size and int(counts.min()) < 0:
+        decode_quant_keys(keys[0], int(counts.min()))  # (raises the same error)
+    k = keys.astype(np.uint64)
+    wide = (np.asarray(n_terms, np.int64) > 256)[:, None]  # DI_SHORT_QUERY_TERMS
+    m = np.where(wide, np.uint64(0xFFFFFF), np.uint64(0xFFFFFFFF))
+    sh = np.where(wide, np.uint64(44), np.uint64(48))
+    docs = (m - (k & m)).astype(np.uint32)
+    scores = (k >> sh).astype(np.uint32)
+    return docs, scores
+
+
 def quantize_sharded(input_path, output_path, max_val, world: int, rank: int,
                      shard_max: Callable, shard_quantize: Callable) -> float:
     """Doc-sharded quantize (quantize.py:27-47 over `world` ranks): every rank takes a

@@ -16,6 +16,7 @@ process (the keys totally order score, first touch and doc).
 from __future__ import annotations
 
 import argparse
+import os
 import sys
 from itertools import product
 from pathlib import Path
@@ -94,13 +95,21 @@ class Ranker:
                 keys, n = parallel.exchange_merge_device(
                     self.index.device_index, ids[0], self.top_k, self.device)
                 # (raises on a query some shard rejected, out_n < 0)
-                results = [parallel.decode_quant_keys(keys[i], int(n[i]), len(ids[0][i]))
-                           for i in range(len(chunk))]
+                docs, scores = parallel.decode_quant_key_arrays(
+                    keys, n, [len(q) for q in ids[0]])
             else:
-                results = self.index.score_batch(terms, self.top_k)
-            if self.run_file is not None:
-                for qid, scores in zip(chunk, results):
-                    self.run_file.writelines(qid, scores)
+                docs, scores, n, _ = self.index.search_ids(
+                    [self.index.term_ids(t) for t in terms], self.top_k)
+            if self.run_file is None:
+                continue
+            if os.environ.get("DI_RANK_PY_WRITES") == "1":  # (the per-query form, A/B)
+                for i, qid in enumerate(chunk):
+                    self.run_file.writelines(qid, list(zip(docs[i, :n[i]].tolist(),
+                                                           scores[i, :n[i]].tolist())))
+            else:
+                # (the chunk's lines formatted natively and appended in one write: the
+                # bytes of RunFile.writelines per query, datasets.py:305-324)
+                self.run_file.write_batch(chunk, docs, scores, n)
 
 
 def main(argv=None):

@@ -313,6 +313,14 @@ int di_format_impact_lines(const char *terms, const int64_t *term_off, const flo
                            const int64_t *cu_doc_terms, int32_t n_docs, char *out,
                            int64_t out_cap, int64_t *out_len);
 
+/* Replaces RunFile.writelines (src/utils/datasets.py:305-324) over a batch: appends
+ * to `path`, for each query q (its id qids[qid_off[q] .. qid_off[q+1]), UTF-8) and rank
+ * i < counts[q], "qid\tpid\trank\tscore\n" with pid = docs[q*k + i], rank = i + 1,
+ * score = scores[q*k + i] (integers: the quantized index). */
+int di_append_run_lines(const char *path, const char *qids, const int64_t *qid_off,
+                        int32_t n_q, const uint32_t *docs, const uint32_t *scores,
+                        const int32_t *counts, int32_t k);
+
 /* ======================================================================
  * Bench / test data (not a reference interface)
  * ====================================================================== */

@@ -104,3 +104,48 @@ def test_convert_to_anserini_matches_reference_output(tmp_path, name):
     out = tmp_path / "out.jsonl"
     convert_to_anserini.process(src, out)
     assert out.read_bytes() == (GOLDEN / "anserini" / f"{name}.jsonl").read_bytes()
+
+
+def test_native_run_lines_equal_runfile_writelines(tmp_path):
+    """di_format_run_lines (RunFile.write_batch) writes the bytes of the reference's
+    per-query RunFile.writelines (datasets.py:305-324): unicode and numeric qids, empty
+    and full lists, pids and scores up to 2^32 - 1."""
+    import numpy as np
+
+    from improving_learned_index_amd.datasets import RunFile
+
+    rng = np.random.default_rng(3)
+    qids = ["1048585", "q-ß", "", "42", "x" * 40] * 30
+    k = 17
+    docs = rng.integers(0, 2 ** 32, (len(qids), k), dtype=np.uint64).astype(np.uint32)
+    scores = rng.integers(0, 2 ** 32, (len(qids), k), dtype=np.uint64).astype(np.uint32)
+    counts = rng.integers(0, k + 1, len(qids)).astype(np.int32)
+    counts[0], counts[1] = 0, k
+    a, b = RunFile(tmp_path / "a"), RunFile(tmp_path / "b")
+    for i, q in enumerate(qids):
+        a.writelines(q, list(zip(docs[i, :counts[i]].tolist(), scores[i, :counts[i]].tolist())))
+    b.write_batch(qids[:70], docs[:70], scores[:70], counts[:70])
+    b.write_batch(qids[70:], docs[70:], scores[70:], counts[70:])
+    assert (tmp_path / "a").read_bytes() == (tmp_path / "b").read_bytes()
+
+
+def test_decode_key_arrays_equal_per_query_decode():
+    """parallel.decode_quant_key_arrays == decode_quant_keys per query, narrow and wide
+    (more than 256 known terms) keys; a rejected query raises."""
+    import numpy as np
+    import pytest
+
+    from improving_learned_index_amd import parallel
+
+    rng = np.random.default_rng(5)
+    nq, k = 12, 9
+    keys = rng.integers(0, 2 ** 63, (nq, k), dtype=np.uint64) * np.uint64(2)
+    counts = rng.integers(0, k + 1, nq).astype(np.int32)
+    n_terms = [3, 300, 1, 257, 256, 6, 900, 2, 2, 2, 400, 5]
+    docs, scores = parallel.decode_quant_key_arrays(keys, counts, n_terms)
+    for q in range(nq):
+        want = parallel.decode_quant_keys(keys[q], int(counts[q]), n_terms[q])
+        assert list(zip(docs[q, :counts[q]].tolist(), scores[q, :counts[q]].tolist())) == want
+    counts[4] = -1
+    with pytest.raises(RuntimeError):
+        parallel.decode_quant_key_arrays(keys, counts, n_terms)
