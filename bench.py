@@ -766,7 +766,7 @@ def rank_e2e_leg(args, dev):
         t0 = time.perf_counter()
         r = Ranker(td / "index", td / "queries.tsv", td / "run.tsv",
                    tokenizer_path=ROOT / "tests" / "golden" / "tokenizer.json", device=dev,
-                   top_k=args.k)
+                   top_k=args.k, sharded=False)  # (rank 0 alone: no collectives)
         t_load = time.perf_counter() - t0
         t1 = time.perf_counter()
         r.run()

@@ -34,7 +34,8 @@ class Ranker:
                  qrels_path: Optional[Union[str, Path]] = None, pairwise: bool = False,
                  dataset_type: Optional[str] = COLLECTION_TYPES[0], tokenizer_path=None,
                  device: int = 0, top_k: int = 1000, batch_queries: int = 8192,
-                 min_impact: int = 1, block_max: float = 0.0, packed: bool = False):
+                 min_impact: int = 1, block_max: float = 0.0, packed: bool = False,
+                 sharded: Optional[bool] = None):
         # pairwise (F4): every query also scores the ordered pair terms 't1|t2' of its
         # distinct terms (ranker.py:53-58), the keys a pairwise impact collection holds
         # (deep_impact_collection.py:36-45).  The reference takes the query terms from
@@ -47,9 +48,13 @@ class Ranker:
         self.query_iterator = list(self.queries.keys())
         if qrels_path is not None:  # ranker.py:34-35
             self.query_iterator = list(QueryRelevanceDataset(qrels_path=qrels_path).keys())
+        # sharded: None = from the torchrun environment; False = this process alone even
+        # under a launcher (bench.py's rank-0-only leg: the other ranks never join)
         self.world, self.rank, local = parallel.dist_env()
+        if sharded is False:
+            self.world, self.rank, local = 1, 0, local
         lo = hi = 0
-        self.dist = self.world > 1 or parallel.force_dist()
+        self.dist = sharded is not False and (self.world > 1 or parallel.force_dist())
         if self.dist:
             import torch
 

@@ -181,14 +181,14 @@ def test_rank_cli_long_queries_two_ranks_equals_one():
 
 def test_bench_two_ranks_completes(tmp_path):
     """bench.py under torchrun with 2 ranks (sharing the test box's GPU over gloo) runs its
-    rank-0-only text legs beside the other rank's retrieve leg to one JSON line: the
+    rank-0-only text and rank_e2e legs beside the other rank's retrieve leg to one JSON line: the
     driver's N > 1 scaling runs take this path (a sharded quantizer inside rank 0's
     text legs once deadlocked it)."""
     env = dict(os.environ, PYTHONPATH=str(ROOT), OMP_NUM_THREADS="4")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr", "127.0.0.1", f"--master-port={_port()}", "bench.py", "--gpus", "2",
-           "--legs", "retrieve,text", "--steps", "1", "--warmup", "1", "--text-docs", "20000",
-           "--queries", "512", "--no-cpu"]
+           "--legs", "retrieve,text,rank_e2e", "--steps", "1", "--warmup", "1", "--text-docs",
+           "20000", "--queries", "512", "--no-cpu"]
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-4000:]
     line = [l for l in r.stdout.splitlines() if l.startswith("{")]
@@ -196,6 +196,8 @@ def test_bench_two_ranks_completes(tmp_path):
     d = json.loads(line[0])
     assert d["n_gpus"] == 2 and d["unit"] == "queries/s" and d["value"] > 0
     assert d["quantize"]["docs"] == 20000 and d["index_create"]["value"] > 0
+    # (rank 0 alone runs the rank CLI's path, unsharded, while rank 1 waits at the next leg)
+    assert d["rank_e2e"]["run_file_lines"] == 512 * d["config"]["k"]
     assert d["ranks_seen"] == 2 and d["backend"] == "gloo"
 
 
