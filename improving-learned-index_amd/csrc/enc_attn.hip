@@ -282,6 +282,13 @@ __device__ __forceinline__ int ax_swz(int r) { return ((r & 3) << 1) | (r & 8); 
 // (Measured: 128-key chunks -- half the barriers -- and raised MFMA issue priority
 // were both slower, r03 ab_attn.)
 constexpr int AX_KC = 64, AX_IMG = AX_KC * 256, AX_LDS = 4 * AX_IMG;
+// Q through LDS: every wave copies the next unit's query fragments by LDS-DMA into a
+// region of its own ([qt][ch][hi, lo] x 1 KiB, lane l's 16 B at l * 16) with the chunk
+// staging, and reads them into registers once at the unit's start -- no second set of
+// Q registers live across the chunk loop (and none of the moves its conditional load
+// cost at every chunk)
+constexpr int AX_QW = 8192;
+constexpr int ax_lds(int nw) { return AX_LDS + nw * AX_QW; }
 
 // BAL: wave w owns the 16-query tiles w and w + 8 of a pass (instead of 2w, 2w + 1), so
 // the tiles of a short pass spread over the four SIMDs (wave w runs on SIMD w % 4), and
@@ -367,7 +374,8 @@ attention_x3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
     };
     // first query (within its pass) of this wave's tile qt
     auto qtile = [&](int qt) { return BAL ? 16 * (wave + NW * qt) : wave * (AX_QT * 16) + 16 * qt; };
-    auto load_q = [&](const Unit &u, bf16x8 (&qh)[AX_QT][2], bf16x8 (&ql)[AX_QT][2]) {
+    // unit u's query fragments of this wave -> its Q region (LDS-DMA, 8 x 1 KiB)
+    auto dma_q = [&](const Unit &u) {
         const bf16 *qbase = qkv + split_col(u.h * ATT_D) + 8 * g;
 #pragma unroll
         for (int qt = 0; qt < AX_QT; ++qt) {
@@ -377,8 +385,10 @@ attention_x3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
 #pragma unroll
             for (int ch = 0; ch < 2; ++ch) {
                 const bf16 *src = qbase + qrow * ld + ch * 64;
-                qh[qt][ch] = *reinterpret_cast<const bf16x8 *>(src);
-                ql[qt][ch] = *reinterpret_cast<const bf16x8 *>(src + 32);
+                const int dst = AX_LDS + wave * AX_QW + (qt * 2 + ch) * 2048;
+                __builtin_amdgcn_global_load_lds((const void *)src, (lds_void *)(lds + dst), 16, 0, 0);
+                __builtin_amdgcn_global_load_lds((const void *)(src + 32),
+                                                 (lds_void *)(lds + dst + 1024), 16, 0, 0);
             }
         }
     };
@@ -417,9 +427,35 @@ attention_x3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
         }
         if (pr >= n_pairs) return;
     }
-    bf16x8 qh[AX_QT][2], ql[AX_QT][2], qnh[AX_QT][2], qnl[AX_QT][2];
-    load_q(cu, qh, ql);
+    bf16x8 qh[AX_QT][2], ql[AX_QT][2];
+    const uint32_t qa = lds_base + AX_LDS + wave * AX_QW + lane * 16;
+    // this wave's Q region -> qh / ql (landed: the caller waited vmcnt(0))
+    auto read_q = [&]() {
+        uint4 q4[8];
+        asm volatile(
+            "ds_read_b128 %0, %8 offset:0"
+            "\n\tds_read_b128 %1, %8 offset:1024"
+            "\n\tds_read_b128 %2, %8 offset:2048"
+            "\n\tds_read_b128 %3, %8 offset:3072"
+            "\n\tds_read_b128 %4, %8 offset:4096"
+            "\n\tds_read_b128 %5, %8 offset:5120"
+            "\n\tds_read_b128 %6, %8 offset:6144"
+            "\n\tds_read_b128 %7, %8 offset:7168"
+            "\n\ts_waitcnt lgkmcnt(0)"
+            : "=&v"(q4[0]), "=&v"(q4[1]), "=&v"(q4[2]), "=&v"(q4[3]), "=&v"(q4[4]),
+              "=&v"(q4[5]), "=&v"(q4[6]), "=&v"(q4[7])
+            : "v"(qa)
+            : "memory");
+#pragma unroll
+        for (int qt = 0; qt < AX_QT; ++qt)
+#pragma unroll
+            for (int ch = 0; ch < 2; ++ch) {
+                __builtin_memcpy(&qh[qt][ch], &q4[(qt * 2 + ch) * 2], 16);
+                __builtin_memcpy(&ql[qt][ch], &q4[(qt * 2 + ch) * 2 + 1], 16);
+            }
+    };
     stage(cu, 0, 0);
+    dma_q(cu);
     int b = 0;  // stage buffer of the next chunk to compute
     for (;;) {
         const int n = cu.n, h = cu.h, q0 = cu.q0, nq = cu.nq;
@@ -449,20 +485,30 @@ attention_x3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
         // in different registers, moved at the top and the bottom of every chunk)
         // (and a wave with no query in the unit runs the staging alone: a body that may
         // skip its products also moved the accumulators)
-        auto stage_step = [&](const int ci) {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pieces of chunk ci
-            __syncthreads();  // every piece landed; buffer b ^ 1 no longer read
+        auto stage_next = [&](const int ci) {
             if (ci + 1 < n_chunks) {
                 stage(cu, ci + 1, b ^ 1);
             } else if (more) {  // the next unit's first chunk and Q
                 stage(nu, 0, b ^ 1);
-                load_q(nu, qnh, qnl);
+                dma_q(nu);
             }
         };
+        // chunk ci > 0 (chunk 0's wait is the unit's start, below)
+        auto stage_step = [&](const int ci) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pieces of chunk ci
+            __syncthreads();  // every piece landed; buffer b ^ 1 no longer read
+            stage_next(ci);
+        };
+        // unit start: chunk 0 and this wave's Q landed; Q into registers before the next
+        // unit's Q copy can be issued (stage_next(0) issues it for a one-chunk unit)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        read_q();
+        stage_next(0);
         auto chunk_loop = [&](auto nqt_outer) {
         auto one_chunk = [&](const int ci, auto whole_c) {
             constexpr bool WHOLE = decltype(whole_c)::value;
-            stage_step(ci);
+            if (ci > 0) stage_step(ci);
             // the chunk's sub-chunks for the wave's NQT non-empty query tiles
             auto chunk = [&](auto nqt_c) {
             constexpr int NQT = decltype(nqt_c)::value;
@@ -576,10 +622,14 @@ static_assert(AX_IMG == 16384 && AX_KC == 64, "AX_SEL's immediate offsets");
 #pragma unroll
                     for (int e = 0; e < 8; ++e) v[qt][e] = e < kv ? s[qt][e >> 2][e & 3] : -INFINITY;
                 }
-                const float lmax = fmaxf(fmaxf(fmaxf(v[qt][0], v[qt][1]), fmaxf(v[qt][2], v[qt][3])),
-                                         fmaxf(fmaxf(v[qt][4], v[qt][5]), fmaxf(v[qt][6], v[qt][7])));
-                if (__any(lmax > lim[qt])) {
-                    float cmax = lmax;
+                // (the test by compares: the max, with its NaN-canonicalising operand
+                // maxes, only on the rare path)
+                bool up = false;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) up |= v[qt][e] > lim[qt];
+                if (__any(up)) {
+                    float cmax = fmaxf(fmaxf(fmaxf(v[qt][0], v[qt][1]), fmaxf(v[qt][2], v[qt][3])),
+                                       fmaxf(fmaxf(v[qt][4], v[qt][5]), fmaxf(v[qt][6], v[qt][7])));
                     const auto p16 = __builtin_amdgcn_permlane16_swap(
                         __float_as_uint(cmax), __float_as_uint(cmax), false, false);
                     cmax = fmaxf(__uint_as_float(p16[0]), __uint_as_float(p16[1]));
@@ -695,11 +745,14 @@ static_assert(AX_IMG == 16384 && AX_KC == 64, "AX_SEL's immediate offsets");
 #pragma unroll
                     for (int e = 0; e < 8; ++e)  // (t = e >> 2, r = e & 3)
                         v[e] = (full || e < kv) ? s[qt][e >> 2][e & 3] : -INFINITY;
-                    const float lmax = fmaxf(fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3])),
-                                             fmaxf(fmaxf(v[4], v[5]), fmaxf(v[6], v[7])));
+                    bool up = false;  // (by compares, as the PIPE form)
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) up |= v[e] > lim[qt];
                     // (always at a unit's first sub-chunk: lim = -inf, key 0 is valid)
-                    if (__any(lmax > lim[qt])) {
-                        float cmax = lmax;  // over the 4 lane groups: permlane swaps
+                    if (__any(up)) {
+                        // over the 4 lane groups: permlane swaps
+                        float cmax = fmaxf(fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3])),
+                                           fmaxf(fmaxf(v[4], v[5]), fmaxf(v[6], v[7])));
                         const auto p16 = __builtin_amdgcn_permlane16_swap(
                             __float_as_uint(cmax), __float_as_uint(cmax), false, false);
                         cmax = fmaxf(__uint_as_float(p16[0]), __uint_as_float(p16[1]));
@@ -800,7 +853,8 @@ __builtin_amdgcn_sched_barrier(0);
         }
         };
         if (!has_q) {
-            for (int ci = 0; ci < n_chunks; ++ci, b ^= 1) stage_step(ci);
+            for (int ci = 0; ci < n_chunks; ++ci, b ^= 1)
+                if (ci > 0) stage_step(ci);
         } else if (two) {
             chunk_loop(std::integral_constant<int, 2>{});
         } else {
@@ -834,13 +888,6 @@ __builtin_amdgcn_sched_barrier(0);
         }
         if (!more) break;
         cu = nu;
-#pragma unroll
-        for (int qt = 0; qt < AX_QT; ++qt)
-#pragma unroll
-            for (int ch = 0; ch < 2; ++ch) {
-                qh[qt][ch] = qnh[qt][ch];
-                ql[qt][ch] = qnl[qt][ch];
-            }
     }
 #undef AX_READ_K
 #undef AX_READ_VW
@@ -869,15 +916,20 @@ void launch_attention_x3(const bf16 *qkv, const int32_t *cu_seqlens, int n_docs,
         return e ? atoi(e) : 0;
     }();
 #define AX_LAUNCH(BL, LZ, PP, NW)                                                              \
-    hipLaunchKernelGGL((attention_x3_kernel<BL, LZ, PP, NW>),                                  \
-                       dim3((int)std::min<int64_t>(n_pairs, (int64_t)n_cu() * (AX_WAVES / NW))), \
-                       dim3(64 * NW), AX_LDS, s, qkv, cu_seqlens, H, n_heads, (int)n_pairs,   \
-                       ctx_split, qsel, cu_qsel, abl)
+    do {                                                                                       \
+        DI_HIP(hipFuncSetAttribute((const void *)attention_x3_kernel<BL, LZ, PP, NW>,          \
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, ax_lds(NW)));   \
+        hipLaunchKernelGGL((attention_x3_kernel<BL, LZ, PP, NW>),                              \
+                           dim3((int)std::min<int64_t>(n_pairs, (int64_t)n_cu() *              \
+                                                                    (160 * 1024 / ax_lds(NW)))), \
+                           dim3(64 * NW), ax_lds(NW), s, qkv, cu_seqlens, H, n_heads,          \
+                           (int)n_pairs, ctx_split, qsel, cu_qsel, abl);                       \
+    } while (0)
     // (r03 ab_attn, attention ms per step: BAL alone -3.5%, LAZY alone -5.6%, both -8.5%)
     switch (variant) {
     case 12: AX_LAUNCH(true, true, false, AX_WAVES); break;
     case 28: AX_LAUNCH(true, true, true, AX_WAVES); break;
-    case 60: AX_LAUNCH(true, true, true, 4); break;
+    case 60: AX_LAUNCH(true, true, true, 4); break;  // (with the Q regions: one per CU)
     default: AX_LAUNCH(false, false, false, AX_WAVES); break;
     }
 #undef AX_LAUNCH
