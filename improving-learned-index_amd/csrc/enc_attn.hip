@@ -308,7 +308,7 @@ attention_x3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
                     const int32_t *__restrict__ qsel, const int32_t *__restrict__ cu_qsel,
                     int abl) {
     // abl (developer timing ablations, wrong results): 1 no softmax arithmetic, 2 no S^T
-    // products, 4 no O^T products
+    // products, 4 no O^T products, 16 no second pass (documents past 256 queries)
     // qsel (optional, the pruned last layer): only the query rows qsel[cu_qsel[d] ..)
     // (doc-local token indices) of document d are computed, into ctx rows cu_qsel[d] + i;
     // keys and values are every token of the document either way.
@@ -341,7 +341,7 @@ attention_x3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
     };
     // the unit after `u` with at least one token and one query, or false
     auto next_unit = [&](const Unit &u, Unit &nu) {
-        if ((u.pass + 1) * PASS_Q < u.nq) {
+        if ((u.pass + 1) * PASS_Q < u.nq && !(abl & 16)) {
             nu = u;
             nu.pass = u.pass + 1;
             return true;
