@@ -256,8 +256,8 @@ attention_kernel(const T *__restrict__ qk, const T *__restrict__ vt,
 // [M][6H] from the QKV GEMM (split_col over the 3H logical columns): no V^T scatter.
 //
 // One persistent 512-thread workgroup per CU walks the (doc, head) pairs; the 8 waves
-// own 32 queries each (two 16-query tiles; documents past 256 tokens take a second
-// pass), and the keys stream
+// own 48 queries each (three 16-query tiles, QTN; documents past 384 tokens take a
+// second pass), and the keys stream
 // through LDS in 32-key chunks, double-buffered: chunk i+1 is copied by LDS-DMA
 // (global_load_lds, every wave one 1 KiB piece of K and one of V) while chunk i is
 // computed, so every K / V byte is read from memory once per pass for the workgroup.
@@ -287,8 +287,8 @@ constexpr int AX_KC = 64, AX_IMG = AX_KC * 256, AX_LDS = 4 * AX_IMG;
 // staging, and reads them into registers once at the unit's start -- no second set of
 // Q registers live across the chunk loop (and none of the moves its conditional load
 // cost at every chunk)
-constexpr int AX_QW = 8192;
-constexpr int ax_lds(int nw) { return AX_LDS + nw * AX_QW; }
+constexpr int AX_QTB = 4096;  // Q region bytes per query tile
+constexpr int ax_lds(int nw, int qtn) { return AX_LDS + nw * qtn * AX_QTB; }
 
 // BAL: wave w owns the 16-query tiles w and w + 8 of a pass (instead of 2w, 2w + 1), so
 // the tiles of a short pass spread over the four SIMDs (wave w runs on SIMD w % 4), and
@@ -301,7 +301,9 @@ constexpr int ax_lds(int nw) { return AX_LDS + nw * AX_QW; }
 // NW: waves per workgroup.  8: one workgroup per CU, 256-query passes.  4: two
 // workgroups per CU (64 KiB of LDS and <= 256 VGPRs each), 128-query passes -- a SIMD
 // idle at one workgroup's short last pass runs the other workgroup's wave.
-template <bool BAL, bool LAZY, bool PIPE = false, int NW = AX_WAVES>
+// QTN: query tiles per wave and pass (2: 256-query passes; 3: 384, every document of up to
+// 384 tokens in one pass -- a wave's third tile runs the generic loop, the pair PIPE).
+template <bool BAL, bool LAZY, bool PIPE = false, int NW = AX_WAVES, int QTN = AX_QT>
 __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2)))
 attention_x3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu_seqlens, int H,
                     int n_heads, int n_pairs, bf16 *__restrict__ ctx_split,
@@ -321,7 +323,8 @@ attention_x3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
     const uint32_t lds_base =
         (uint32_t)(uintptr_t)((__attribute__((address_space(3))) unsigned char *)lds);
     const float sc = 0.125f * 1.4426950408889634f;  // 1/sqrt(64) * log2(e)
-    constexpr int PASS_Q = NW * AX_QT * 16;         // queries per pass (256 or 128)
+    constexpr int PASS_Q = NW * QTN * 16;           // queries per pass (256, 384 or 128)
+    static_assert(QTN == 2 || QTN == 3, "two or three query tiles per wave");
 
     // Work units: (pair, pass), pairs blockIdx.x, + gridDim.x, ... (persistent); the
     // next unit's Q and first K / V chunk load while the current unit's last chunk
@@ -373,19 +376,19 @@ attention_x3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
         }
     };
     // first query (within its pass) of this wave's tile qt
-    auto qtile = [&](int qt) { return BAL ? 16 * (wave + NW * qt) : wave * (AX_QT * 16) + 16 * qt; };
+    auto qtile = [&](int qt) { return BAL ? 16 * (wave + NW * qt) : wave * (QTN * 16) + 16 * qt; };
     // unit u's query fragments of this wave -> its Q region (LDS-DMA, 8 x 1 KiB)
     auto dma_q = [&](const Unit &u) {
         const bf16 *qbase = qkv + split_col(u.h * ATT_D) + 8 * g;
 #pragma unroll
-        for (int qt = 0; qt < AX_QT; ++qt) {
+        for (int qt = 0; qt < QTN; ++qt) {
             const int qi = min(u.pass * PASS_Q + qtile(qt) + c, u.nq - 1);
             const int qloc = qsel ? min(max(qsel[u.q0 + qi], 0), u.n - 1) : qi;
             const int qrow = u.tok0 + qloc;
 #pragma unroll
             for (int ch = 0; ch < 2; ++ch) {
                 const bf16 *src = qbase + qrow * ld + ch * 64;
-                const int dst = AX_LDS + wave * AX_QW + (qt * 2 + ch) * 2048;
+                const int dst = AX_LDS + wave * (QTN * AX_QTB) + (qt * 2 + ch) * 2048;
                 __builtin_amdgcn_global_load_lds((const void *)src, (lds_void *)(lds + dst), 16, 0, 0);
                 __builtin_amdgcn_global_load_lds((const void *)(src + 32),
                                                  (lds_void *)(lds + dst + 1024), 16, 0, 0);
@@ -427,8 +430,8 @@ attention_x3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
         }
         if (pr >= n_pairs) return;
     }
-    bf16x8 qh[AX_QT][2], ql[AX_QT][2];
-    const uint32_t qa = lds_base + AX_LDS + wave * AX_QW + lane * 16;
+    bf16x8 qh[QTN][2], ql[QTN][2];
+    const uint32_t qa = lds_base + AX_LDS + wave * (QTN * AX_QTB) + lane * 16;
     // this wave's Q region -> qh / ql (landed: the caller waited vmcnt(0))
     auto read_q = [&]() {
         uint4 q4[8];
@@ -447,12 +450,29 @@ attention_x3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
             : "v"(qa)
             : "memory");
 #pragma unroll
-        for (int qt = 0; qt < AX_QT; ++qt)
+        for (int qt = 0; qt < 2; ++qt)
 #pragma unroll
             for (int ch = 0; ch < 2; ++ch) {
                 __builtin_memcpy(&qh[qt][ch], &q4[(qt * 2 + ch) * 2], 16);
                 __builtin_memcpy(&ql[qt][ch], &q4[(qt * 2 + ch) * 2 + 1], 16);
             }
+        if constexpr (QTN == 3) {
+            uint4 q5[4];
+            asm volatile(
+                "ds_read_b128 %0, %4 offset:8192"
+                "\n\tds_read_b128 %1, %4 offset:9216"
+                "\n\tds_read_b128 %2, %4 offset:10240"
+                "\n\tds_read_b128 %3, %4 offset:11264"
+                "\n\ts_waitcnt lgkmcnt(0)"
+                : "=&v"(q5[0]), "=&v"(q5[1]), "=&v"(q5[2]), "=&v"(q5[3])
+                : "v"(qa)
+                : "memory");
+#pragma unroll
+            for (int ch = 0; ch < 2; ++ch) {
+                __builtin_memcpy(&qh[2][ch], &q5[ch * 2], 16);
+                __builtin_memcpy(&ql[2][ch], &q5[ch * 2 + 1], 16);
+            }
+        }
     };
     stage(cu, 0, 0);
     dma_q(cu);
@@ -462,13 +482,14 @@ attention_x3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
         const int q_pass = cu.pass * PASS_Q;
         const bool has_q = q_pass + qtile(0) < nq;
         const bool two = BAL ? q_pass + qtile(1) < nq : has_q;  // (uniform) tile 1 has queries
+        const bool three = QTN == 3 && (BAL ? q_pass + qtile(2) < nq : has_q);
         const int n_chunks = (n + AX_KC - 1) / AX_KC;
         Unit nu;
         const bool more = next_unit(cu, nu);
-        float m[AX_QT], lsum[AX_QT], lim[AX_QT], mneg[AX_QT];
-        f32x4 o[AX_QT][4];
+        float m[QTN], lsum[QTN], lim[QTN], mneg[QTN];
+        f32x4 o[QTN][4];
 #pragma unroll
-        for (int qt = 0; qt < AX_QT; ++qt) {
+        for (int qt = 0; qt < QTN; ++qt) {
             m[qt] = -INFINITY;
             lim[qt] = -INFINITY;
             mneg[qt] = 0.f;
@@ -588,12 +609,12 @@ static_assert(AX_IMG == 16384 && AX_KC == 64, "AX_SEL's immediate offsets");
                 for (int ch = 0; ch < 2; ++ch)
 #pragma unroll
                     for (int pt = 0; pt < 2; ++pt) __builtin_memcpy(&kfr[t][ch][pt], &kf[t][ch][pt], 16);
-            if constexpr (PIPE && NQT == 2) {
+            if constexpr (PIPE && NQT >= 2) {
             static_assert(BAL && LAZY, "PIPE builds on the balanced lazy form");
             const bool full = WHOLE || key0 + 32 <= n;  // (uniform) no masked key in this sub-chunk
-            f32x4 s[AX_QT][2];
-            float v[AX_QT][8];
-            bf16x8 ph[AX_QT], pl[AX_QT];
+            f32x4 s[QTN][2];
+            float v[QTN][8];
+            bf16x8 ph[QTN], pl[QTN];
             // S^T of tile qt (12 MFMAs; the two accumulators' chains interleaved)
             auto s_mfma = [&](int qt) {
                 s[qt][0] = s[qt][1] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -695,16 +716,31 @@ static_assert(AX_IMG == 16384 && AX_KC == 64, "AX_SEL's immediate offsets");
             __builtin_amdgcn_sched_barrier(0);
             soft_a(1);
             __builtin_amdgcn_sched_barrier(0);
-            o_mfma(0);
-            soft_b(1);
-            AX_INTERLEAVE();
-            __builtin_amdgcn_sched_barrier(0);
-            o_mfma(1);
+            if constexpr (NQT == 3) {  // tile 2's products in tile 1's and tile 2's shadows
+                s_mfma(2);
+                soft_b(1);
+                AX_INTERLEAVE();
+                __builtin_amdgcn_sched_barrier(0);
+                soft_a(2);
+                __builtin_amdgcn_sched_barrier(0);
+                o_mfma(0);
+                soft_b(2);
+                AX_INTERLEAVE();
+                __builtin_amdgcn_sched_barrier(0);
+                o_mfma(1);
+                o_mfma(2);
+            } else {
+                o_mfma(0);
+                soft_b(1);
+                AX_INTERLEAVE();
+                __builtin_amdgcn_sched_barrier(0);
+                o_mfma(1);
+            }
 #undef AX_INTERLEAVE
             } else {
             // S^T for both query tiles, each product stage over the 4 independent
             // accumulators before the next (one accumulator's 3 products are a chain)
-            f32x4 s[AX_QT][2];
+            f32x4 s[QTN][2];
 #pragma unroll
             for (int qt = 0; qt < NQT; ++qt)
 #pragma unroll
@@ -727,7 +763,7 @@ static_assert(AX_IMG == 16384 && AX_KC == 64, "AX_SEL's immediate offsets");
             AX_SEL(AX_READ_VW);
             __builtin_amdgcn_sched_barrier(0);
             const bool full = WHOLE || key0 + 32 <= n;  // (uniform) no masked key in this sub-chunk
-            bf16x8 ph[AX_QT], pl[AX_QT];
+            bf16x8 ph[QTN], pl[QTN];
             if (abl & 1) {
 #pragma unroll
                 for (int qt = 0; qt < NQT; ++qt)
@@ -855,6 +891,8 @@ __builtin_amdgcn_sched_barrier(0);
         if (!has_q) {
             for (int ci = 0; ci < n_chunks; ++ci, b ^= 1)
                 if (ci > 0) stage_step(ci);
+        } else if (three) {
+            if constexpr (QTN == 3) chunk_loop(std::integral_constant<int, 3>{});
         } else if (two) {
             chunk_loop(std::integral_constant<int, 2>{});
         } else {
@@ -862,7 +900,7 @@ __builtin_amdgcn_sched_barrier(0);
         }
         if (has_q) {
 #pragma unroll
-            for (int qt = 0; qt < AX_QT; ++qt) {
+            for (int qt = 0; qt < QTN; ++qt) {
                 float l = lsum[qt];
                 l += __shfl_xor(l, 16, 64);
                 l += __shfl_xor(l, 32, 64);
@@ -904,33 +942,36 @@ void launch_attention_x3(const bf16 *qkv, const int32_t *cu_seqlens, int n_docs,
     DI_REQUIRE(n_pairs < (1ll << 31), DI_ERANGE, "attention grid too large");
     // persistent: one 8-wave or two 4-wave workgroups per CU
     // balanced tiles + lazy max + interleaved softmax (r03 ab_attn: attention -8.5%,
-    // then -3% per step); DI_ATTN_X3 (developer A/B): 0 = the round-2 form, 12 = no
-    // interleave
+    // then -3% per step), three query tiles per wave (384-query passes: every document of
+    // up to 384 tokens in one pass; round6_o: -4.4%); DI_ATTN_X3 (developer A/B): 0 = the
+    // round-2 form, 12 = no interleave, 28 = two tiles per wave
     static const int variant = [] {
         const char *e = getenv("DI_ATTN_X3");
-        return e ? atoi(e) & 60 : 28;
+        return e ? atoi(e) & 124 : 92;
     }();
 
     static const int abl = [] {
         const char *e = getenv("DI_ATTN_X3_ABLATE");
         return e ? atoi(e) : 0;
     }();
-#define AX_LAUNCH(BL, LZ, PP, NW)                                                              \
+#define AX_LAUNCH(BL, LZ, PP, NW, QN)                                                          \
     do {                                                                                       \
-        DI_HIP(hipFuncSetAttribute((const void *)attention_x3_kernel<BL, LZ, PP, NW>,          \
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, ax_lds(NW)));   \
-        hipLaunchKernelGGL((attention_x3_kernel<BL, LZ, PP, NW>),                              \
-                           dim3((int)std::min<int64_t>(n_pairs, (int64_t)n_cu() *              \
-                                                                    (160 * 1024 / ax_lds(NW)))), \
-                           dim3(64 * NW), ax_lds(NW), s, qkv, cu_seqlens, H, n_heads,          \
+        DI_HIP(hipFuncSetAttribute((const void *)attention_x3_kernel<BL, LZ, PP, NW, QN>,      \
+                                   hipFuncAttributeMaxDynamicSharedMemorySize,                 \
+                                   ax_lds(NW, QN)));                                           \
+        hipLaunchKernelGGL((attention_x3_kernel<BL, LZ, PP, NW, QN>),                          \
+                           dim3((int)std::min<int64_t>(                                        \
+                               n_pairs, (int64_t)n_cu() * (160 * 1024 / ax_lds(NW, QN)))),     \
+                           dim3(64 * NW), ax_lds(NW, QN), s, qkv, cu_seqlens, H, n_heads,      \
                            (int)n_pairs, ctx_split, qsel, cu_qsel, abl);                       \
     } while (0)
     // (r03 ab_attn, attention ms per step: BAL alone -3.5%, LAZY alone -5.6%, both -8.5%)
     switch (variant) {
-    case 12: AX_LAUNCH(true, true, false, AX_WAVES); break;
-    case 28: AX_LAUNCH(true, true, true, AX_WAVES); break;
-    case 60: AX_LAUNCH(true, true, true, 4); break;  // (with the Q regions: one per CU)
-    default: AX_LAUNCH(false, false, false, AX_WAVES); break;
+    case 12: AX_LAUNCH(true, true, false, AX_WAVES, AX_QT); break;
+    case 28: AX_LAUNCH(true, true, true, AX_WAVES, AX_QT); break;
+    case 60: AX_LAUNCH(true, true, true, 4, AX_QT); break;  // (with the Q regions: one per CU)
+    case 92: AX_LAUNCH(true, true, true, AX_WAVES, 3); break;  // three query tiles per wave
+    default: AX_LAUNCH(false, false, false, AX_WAVES, AX_QT); break;
     }
 #undef AX_LAUNCH
     check_launch("attention_x3");
