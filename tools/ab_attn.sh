@@ -1,7 +1,7 @@
 #!/bin/bash
 # A/B of attention_x3 variants (DI_ATTN_X3 bits, launch_attention_x3: 0 = round-2 form,
 # 4 = balanced query tiles, 8 = lazy max, 16 = interleaved softmax, 32 = two
-# 4-wave workgroups per CU; ":a" = DI_ATTN_X3_ABLATE a, timing only) on the bench's
+# 4-wave workgroups per CU, 64 = three query tiles per wave; ":a" = DI_ATTN_X3_ABLATE a, timing only) on the bench's
 # encode_x3 leg, one box, alternating; attention ms per step per run.
 # Usage: VARIANTS="0 4 0:1 0:2 0:4" REPS=2 bash tools/ab_attn.sh
 set -o pipefail

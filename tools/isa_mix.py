@@ -1,7 +1,7 @@
 """Instruction-class count of attention_x3's hot loop, per 32-key sub-chunk (static, ISA).
 
 Compiles csrc/enc_attn.hip for gfx950, takes the shipped instantiation
-(attention_x3_kernel<true, true, true, 8>), finds its two-tile whole-chunk loop (the
+(attention_x3_kernel<true, true, true, 8, 3>), finds its two-tile whole-chunk loop (the
 backward branch whose body holds 2 x 48 MFMAs: two 32-key sub-chunks of 12 S^T + 12
 O^T products per query tile), and counts instruction classes over that body, split
 into the common path, the rescale branch (the blocks with the permlane max: taken
@@ -22,7 +22,7 @@ sys.path.insert(0, str(Path(__file__).resolve().parent))
 import asm_wait_scan  # noqa: E402  (compile_asm)
 
 SRC = Path(__file__).resolve().parents[1] / "improving-learned-index_amd" / "csrc" / "enc_attn.hip"
-KERNEL = "_ZN2di19attention_x3_kernelILb1ELb1ELb1ELi8ELi2EEEvPKDF16bPKiiiiPDF16bS4_S4_i"
+KERNEL = "_ZN2di19attention_x3_kernelILb1ELb1ELb1ELi8ELi3EEEvPKDF16bPKiiiiPDF16bS4_S4_i"
 
 CLASSES = [
     ("mfma", r"v_mfma"),
