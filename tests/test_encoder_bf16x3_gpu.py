@@ -96,7 +96,10 @@ def test_bf16x3_term_impacts_match_reference_class(E, base):
     np.testing.assert_allclose(got, want, rtol=RTOL, atol=1e-6)
 
 
-@pytest.mark.parametrize("lens", [[300, 250, 180, 64, 9, 120], [512, 400, 321, 40, 3, 1]])
+# (the attention's pass and tile edges: 16-query tiles, three per wave, 384-query passes --
+# 256 / 257 and 384 / 385 tokens put the first query into a wave's third tile / a second pass)
+@pytest.mark.parametrize("lens", [[300, 250, 180, 64, 9, 120], [512, 400, 321, 40, 3, 1],
+                                  [385, 384, 257, 256, 17, 16]])
 def test_bf16x3_ragged_batches_match_torch_oracle(E, base, lens):
     fx, sd = base
     enc = E.DeviceEncoder(sd, _cfg(E, fx), precision="bf16x3")
@@ -112,7 +115,7 @@ def test_bf16x3_pruned_last_layer_is_bitexact(E, base):
     """Term output computes the last layer only for the terms' first-token rows (queries
     of the attention, O / FFN GEMMs, LayerNorms, head); each kept row's arithmetic is
     unchanged, so the impacts must equal the full per-token forward gathered at those
-    rows, bit for bit -- ragged documents past one 256-query pass, a document without
+    rows, bit for bit -- ragged documents past one 384-query pass, a document without
     terms, terms in any order and repeated."""
     fx, sd = base
     enc = E.DeviceEncoder(sd, _cfg(E, fx), precision="bf16x3")
