@@ -399,6 +399,33 @@ gather_term_rows_kernel(const bf16 *__restrict__ X, const float2 *__restrict__ r
     }
 }
 
+// The inverse for the pruned last layer's queries: packed row j (term j) -> row t0 +
+// term_tok[j] (same clamp) of a [tokens][ld] matrix, its first W elements (a repeated
+// token receives the same row twice: the same bytes).
+__global__ void __launch_bounds__(256)
+scatter_term_rows_kernel(const bf16 *__restrict__ Xg, const int32_t *__restrict__ cu_seq,
+                         const int32_t *__restrict__ cu_terms, const int32_t *__restrict__ term_tok,
+                         int W, int64_t ld, bf16 *__restrict__ X) {
+    const int d = blockIdx.x, wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int t0 = cu_seq[d], n = cu_seq[d + 1] - t0;
+    for (int j = cu_terms[d] + wave; j < cu_terms[d + 1]; j += 4) {
+        const int row = t0 + min(max(term_tok[j], 0), max(n - 1, 0));
+        const uint2 *src = reinterpret_cast<const uint2 *>(Xg + (int64_t)j * W);
+        uint2 *dst = reinterpret_cast<uint2 *>(X + (int64_t)row * ld);
+        for (int c = lane; c < W / 4; c += 64) dst[c] = src[c];
+    }
+}
+
+void launch_scatter_term_rows(const bf16 *Xg, const int32_t *cu_seq, const int32_t *cu_terms,
+                              const int32_t *term_tok, int n_docs, int W, int64_t ld, bf16 *X,
+                              hipStream_t s) {
+    if (n_docs == 0) return;
+    DI_REQUIRE(W % 4 == 0 && ld % 4 == 0, DI_EINVAL, "scatter_term_rows: 8-byte rows");
+    hipLaunchKernelGGL(scatter_term_rows_kernel, dim3(n_docs), dim3(256), 0, s, Xg, cu_seq,
+                       cu_terms, term_tok, W, ld, X);
+    check_launch("scatter_term_rows");
+}
+
 void launch_gather_term_rows(const bf16 *X, const float2 *rl, const int32_t *cu_seq,
                              const int32_t *cu_terms, const int32_t *term_tok, int n_docs, int H,
                              bf16 *Xg, float2 *rlg, hipStream_t s) {

@@ -34,6 +34,9 @@ void launch_gemm256(int epi, const GemmArgs &g, hipStream_t s);
 void launch_attention_x3(const bf16 *qkv, const int32_t *cu_seqlens, int n_docs, int H,
                          bf16 *ctx_split, hipStream_t s, const int32_t *qsel = nullptr,
                          const int32_t *cu_qsel = nullptr);
+void launch_scatter_term_rows(const bf16 *Xg, const int32_t *cu_seq, const int32_t *cu_terms,
+                              const int32_t *term_tok, int n_docs, int W, int64_t ld, bf16 *X,
+                              hipStream_t s);
 void launch_embed_ln_split(const int32_t *ids, const int32_t *cu, int n_docs, int M, int H,
                            const float *word, const float *pos, const float *type0,
                            const float *gamma, const float *beta, float eps, int pos_offset,
@@ -494,6 +497,24 @@ void forward_folded(di_encoder *e, const int32_t *d_ids, const int32_t *d_cu, in
         Layer &L = *e->layers[l];
         const Layer *P = l > 0 ? e->layers[l - 1].get() : nullptr;
         const bool last = l + 1 == e->layers.size();
+        const bool prune = last && d_tt != nullptr;
+        const int64_t Mr = prune ? n_terms : M;  // rows from here on
+        bf16 *Xr = X;                             // the O GEMM's residual rows
+        const float2 *rl2r = rl2;
+        auto gather_rows = [&]() {  // the terms' layer-input rows (and LN2 parameters):
+            TimedLaunch tl(e->timer, timing, "gather_rows", s);  // Hff / rl1 are free
+            Xr = e->Hff.as<bf16>();                               // until later
+            launch_gather_term_rows(X, P ? rl2 : nullptr, d_cu, d_ct, d_tt, n_docs, H * W2, Xr,
+                                    rl1, s);
+            rl2r = rl1;
+        };
+        // Pruned last layer, split path: the queries are the terms' rows only, so Q is
+        // projected from their gathered rows (a GEMM of n_terms rows) and K | V from every
+        // row -- each kept element the same sum in the same order as the full QKV GEMM's;
+        // the packed Q rows then go to their token rows' Q columns of qk, where the
+        // attention reads them (one 3 KiB copy per term)
+        const bool qc = prune && sp;
+        if (qc) gather_rows();
         // QKV: layer 0 reads the normalised embeddings; later layers fold LN2(l-1)
         GemmArgs g = base();
         g.A = X;
@@ -510,12 +531,31 @@ void forward_folded(di_encoder *e, const int32_t *d_ids, const int32_t *d_cu, in
         }
         {
             TimedLaunch tl(e->timer, timing, "gemm_qkv", s);
-            gemm(P ? EPI_FOLD : EPI_BIAS, g);
+            if (!qc) {
+                gemm(P ? EPI_FOLD : EPI_BIAS, g);
+            } else {
+                GemmArgs gk = g;  // K | V: weight rows H .. 3H, output columns H .. 3H
+                gk.B = static_cast<const bf16 *>(L.w_qkv.p) + (int64_t)H * 2 * H;
+                gk.bias = L.b_qkv.as<float>() + H;
+                if (P) {
+                    gk.col_s = L.s_qkv.as<float>() + H;
+                    gk.col_c = L.c_qkv.as<float>() + H;
+                }
+                gk.out = e->qk.as<bf16>() + 2 * H;
+                gk.N = 2 * H;
+                gemm(P ? EPI_FOLD : EPI_BIAS, gk);
+                GemmArgs gq = g;  // Q of the terms' rows, packed (ctx: free until the attention)
+                gq.A = Xr;
+                gq.M = (int)n_terms;
+                gq.N = H;
+                gq.out = e->ctx.p;
+                gq.ld_out = 2 * H;
+                gq.row_ln = P ? rl1 : nullptr;
+                gemm(P ? EPI_FOLD : EPI_BIAS, gq);
+                launch_scatter_term_rows(e->ctx.as<bf16>(), d_cu, d_ct, d_tt, n_docs, 2 * H,
+                                         6 * (int64_t)H, e->qk.as<bf16>(), s);
+            }
         }
-        const bool prune = last && d_tt != nullptr;
-        const int64_t Mr = prune ? n_terms : M;  // rows from here on
-        bf16 *Xr = X;                             // the O GEMM's residual rows
-        const float2 *rl2r = rl2;
         {
             TimedLaunch tl(e->timer, timing, "attention", s);
             if (sp)
@@ -526,13 +566,7 @@ void forward_folded(di_encoder *e, const int32_t *d_ids, const int32_t *d_cu, in
                                     e->ctx.as<bf16>(), s, prune ? d_tt : nullptr,
                                     prune ? d_ct : nullptr);
         }
-        if (prune) {  // the terms' residual rows (and LN2 parameters), packed: Hff / rl1
-            TimedLaunch tl(e->timer, timing, "gather_rows", s);  // are free until later
-            Xr = e->Hff.as<bf16>();
-            launch_gather_term_rows(X, P ? rl2 : nullptr, d_cu, d_ct, d_tt, n_docs, H * W2, Xr,
-                                    rl1, s);
-            rl2r = rl1;
-        }
+        if (prune && !qc) gather_rows();
         auto base_r = [&]() {
             GemmArgs gr = base();
             gr.M = (int)Mr;
