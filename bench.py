@@ -420,16 +420,17 @@ def synthetic_docs_tokens(n_docs, vocab, seed, max_len=300):
     return ids, cu, lens, np.array(term_tok, np.int32), np.array(cu_terms, np.int32)
 
 
-def flops_per_doc(n, H=768, L=12, t=None):
+def flops_per_doc(n, H=768, L=12, t=None, q_pruned=False):
     """sum over layers (24 n H^2 + 4 n^2 H) + 2 n H (real tokens only).
     With t (kept terms per doc): the FLOPs executed when the last layer runs its
     attention queries and its O / FFN GEMMs on the t term rows only (the pruned last
-    layer; the QKV projection still covers every row)."""
+    layer; the K / V projections still cover every row, and the Q projection too unless
+    q_pruned -- the bf16x3 path projects Q from the term rows only)."""
     n = np.asarray(n, np.float64)
     f = L * (24.0 * n * H * H + 4.0 * n * n * H) + 2.0 * n * H
     if t is not None:
         t = np.asarray(t, np.float64)
-        f = f - (18.0 * H * H * (n - t) + 4.0 * (n - t) * n * H)
+        f = f - ((20.0 if q_pruned else 18.0) * H * H * (n - t) + 4.0 * (n - t) * n * H)
     return f
 
 
@@ -508,7 +509,9 @@ def encode_leg(args, rank, world, dev, precision="bf16", steps=None):
     f32 = precision == "fp32"
     prune = prune_last_layer() and not f32  # (the fp32 mode computes every row)
     Mp = ((L - 1) * M + T) / L if prune else M
-    gemm_flops = {"gemm_qkv": 2 * M * H * 3 * H, "gemm_o": 2 * Mp * H * H,
+    # (bf16x3: the pruned last layer's Q projection runs on the T term rows too)
+    qkv_rows = ((L - 1) * 3 * M + 2 * M + T) / L if prune and split else 3 * M
+    gemm_flops = {"gemm_qkv": 2 * qkv_rows * H * H, "gemm_o": 2 * Mp * H * H,
                   "gemm_ffn1": 2 * Mp * H * F, "gemm_ffn2": 2 * Mp * F * H}
     per_launch = {}
     for k, f in gemm_flops.items():
@@ -543,7 +546,8 @@ def encode_leg(args, rank, world, dev, precision="bf16", steps=None):
     # bf16 MFMA products per fp32 product, 2500 / 3 TF/s (the f32 MFMA peak is 157.3)
     peak = peak_of(precision)
     # executed FLOPs (the pruned last layer skips the rows no output reads)
-    model_flops = float(flops_per_doc(lens, t=np.diff(ct) if prune else None).sum())
+    model_flops = float(flops_per_doc(lens, t=np.diff(ct) if prune else None,
+                                      q_pruned=prune and split).sum())
     docs_per_s = world * args.docs * n_steps / el
     res = {
         "value": docs_per_s,
