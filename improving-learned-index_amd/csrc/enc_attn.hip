@@ -288,7 +288,7 @@ constexpr int AX_KC = 64, AX_IMG = AX_KC * 256, AX_LDS = 4 * AX_IMG;
 // Q registers live across the chunk loop (and none of the moves its conditional load
 // cost at every chunk)
 constexpr int AX_QTB = 4096;  // Q region bytes per query tile
-constexpr int ax_lds(int nw, int qtn) { return AX_LDS + nw * qtn * AX_QTB; }
+constexpr int ax_lds(int nw, int qtn, int kc = AX_KC) { return 4 * kc * 256 + nw * qtn * AX_QTB; }
 
 // BAL: wave w owns the 16-query tiles w and w + 8 of a pass (instead of 2w, 2w + 1), so
 // the tiles of a short pass spread over the four SIMDs (wave w runs on SIMD w % 4), and
@@ -303,7 +303,10 @@ constexpr int ax_lds(int nw, int qtn) { return AX_LDS + nw * qtn * AX_QTB; }
 // idle at one workgroup's short last pass runs the other workgroup's wave.
 // QTN: query tiles per wave and pass (2: 256-query passes; 3: 384, every document of up to
 // 384 tokens in one pass -- a wave's third tile runs the generic loop, the pair PIPE).
-template <bool BAL, bool LAZY, bool PIPE = false, int NW = AX_WAVES, int QTN = AX_QT>
+// KC: keys per staged chunk (64; 32 halves the K / V buffers: the 4-wave form of the pruned
+// last layer, two workgroups per CU).
+template <bool BAL, bool LAZY, bool PIPE = false, int NW = AX_WAVES, int QTN = AX_QT,
+          int KC = AX_KC>
 __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2)))
 attention_x3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu_seqlens, int H,
                     int n_heads, int n_pairs, bf16 *__restrict__ ctx_split,
@@ -325,6 +328,7 @@ attention_x3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
     const float sc = 0.125f * 1.4426950408889634f;  // 1/sqrt(64) * log2(e)
     constexpr int PASS_Q = NW * QTN * 16;           // queries per pass (256, 384 or 128)
     static_assert(QTN == 2 || QTN == 3, "two or three query tiles per wave");
+    constexpr int IMG = KC * 256, KVL = 4 * IMG;  // one K or V image; the four of them
 
     // Work units: (pair, pass), pairs blockIdx.x, + gridDim.x, ... (persistent); the
     // next unit's Q and first K / V chunk load while the current unit's last chunk
@@ -358,7 +362,7 @@ attention_x3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
     // chunk ci of unit u -> stage buffer b: key rows RPW wave..+RPW-1 of K and of V
     // (RPW / 4 pieces of 1 KiB each), 16 B per lane, source slots permuted by the
     // swizzle (piece pc: key rows RPW wave + 4 pc + lane >> 4)
-    constexpr int RPW = AX_KC / NW;  // key rows per wave and image (8 or 16)
+    constexpr int RPW = KC / NW;  // key rows per wave and image (8 or 16)
     const int sr = RPW * wave + (lane >> 4);
     auto stage = [&](const Unit &u, int ci, int b) {
         const bf16 *kg = qkv + split_col(H + u.h * ATT_D);      // + key row * ld: 256 B
@@ -366,13 +370,13 @@ attention_x3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
 #pragma unroll
         for (int pc = 0; pc < RPW / 4; ++pc) {
             const int rl = sr + 4 * pc;
-            const int row = u.tok0 + min(ci * AX_KC + rl, u.n - 1);
+            const int row = u.tok0 + min(ci * KC + rl, u.n - 1);
             const int j = (lane & 15) ^ ax_swz(rl);
-            const int dst = b * AX_IMG + (RPW * wave + 4 * pc) * 256;
+            const int dst = b * IMG + (RPW * wave + 4 * pc) * 256;
             __builtin_amdgcn_global_load_lds((const void *)(kg + row * ld + j * 8),
                                              (lds_void *)(lds + dst), 16, 0, 0);
             __builtin_amdgcn_global_load_lds((const void *)(vg + row * ld + j * 8),
-                                             (lds_void *)(lds + 2 * AX_IMG + dst), 16, 0, 0);
+                                             (lds_void *)(lds + 2 * IMG + dst), 16, 0, 0);
         }
     };
     // first query (within its pass) of this wave's tile qt
@@ -388,14 +392,14 @@ attention_x3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
 #pragma unroll
             for (int ch = 0; ch < 2; ++ch) {
                 const bf16 *src = qbase + qrow * ld + ch * 64;
-                const int dst = AX_LDS + wave * (QTN * AX_QTB) + (qt * 2 + ch) * 2048;
+                const int dst = KVL + wave * (QTN * AX_QTB) + (qt * 2 + ch) * 2048;
                 __builtin_amdgcn_global_load_lds((const void *)src, (lds_void *)(lds + dst), 16, 0, 0);
                 __builtin_amdgcn_global_load_lds((const void *)(src + 32),
                                                  (lds_void *)(lds + dst + 1024), 16, 0, 0);
             }
         }
     };
-    // fragment addresses (buffer 0; buffer 1 is the immediate offset AX_IMG).  Row bit 2
+    // fragment addresses (buffer 0; buffer 1 is the immediate offset IMG).  Row bit 2
     // (the K tile t, the V half h2) is not in the swizzle, so those halves are the
     // immediate offset 4 * 256 = 1024 of one address register: 12 VGPRs instead of 24.
     constexpr int AX_HALF = 1024;
@@ -418,7 +422,7 @@ attention_x3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
             const int q = c >> 2, pp = c & 3;
             const int r = 8 * g + q;
             const int j = (dt >> 1) * 8 + pt * 4 + 2 * (dt & 1) + (pp >> 1);
-            va[dt][pt] = lds_base + 2 * AX_IMG + r * 256 + ((j ^ ax_swz(r)) << 4) + 8 * (pp & 1);
+            va[dt][pt] = lds_base + 2 * IMG + r * 256 + ((j ^ ax_swz(r)) << 4) + 8 * (pp & 1);
         }
 
     Unit cu;
@@ -431,7 +435,7 @@ attention_x3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
         if (pr >= n_pairs) return;
     }
     bf16x8 qh[QTN][2], ql[QTN][2];
-    const uint32_t qa = lds_base + AX_LDS + wave * (QTN * AX_QTB) + lane * 16;
+    const uint32_t qa = lds_base + KVL + wave * (QTN * AX_QTB) + lane * 16;
     // this wave's Q region -> qh / ql (landed: the caller waited vmcnt(0))
     auto read_q = [&]() {
         uint4 q4[8];
@@ -483,7 +487,7 @@ attention_x3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
         const bool has_q = q_pass + qtile(0) < nq;
         const bool two = BAL ? q_pass + qtile(1) < nq : has_q;  // (uniform) tile 1 has queries
         const bool three = QTN == 3 && (BAL ? q_pass + qtile(2) < nq : has_q);
-        const int n_chunks = (n + AX_KC - 1) / AX_KC;
+        const int n_chunks = (n + KC - 1) / KC;
         Unit nu;
         const bool more = next_unit(cu, nu);
         float m[QTN], lsum[QTN], lim[QTN], mneg[QTN];
@@ -534,8 +538,8 @@ attention_x3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
             auto chunk = [&](auto nqt_c) {
             constexpr int NQT = decltype(nqt_c)::value;
 #pragma unroll
-            for (int u = 0; u < AX_KC / 32; ++u) {  // 32-key sub-chunks
-            const int key0 = ci * AX_KC + 32 * u;
+            for (int u = 0; u < KC / 32; ++u) {  // 32-key sub-chunks
+            const int key0 = ci * KC + 32 * u;
             if (!WHOLE && key0 >= n) break;
             uint4 kf[2][2][2];
             uint2 vt2[4][2][2];
@@ -589,16 +593,20 @@ attention_x3_kernel(const bf16 *__restrict__ qkv, const int32_t *__restrict__ cu
 // (b, the stage buffer, is 0 or 1 at run time; u, the sub-chunk, a constant of the
 // unrolled loop: one branch per site -- a switch over the offsets' value range compiled
 // to a chain of compares)
-static_assert(AX_IMG == 16384 && AX_KC == 64, "AX_SEL's immediate offsets");
+static_assert((KC == 64 && IMG == 16384) || (KC == 32 && IMG == 8192), "AX_SEL's offsets");
 #define AX_SEL(M)                                                                                  \
     do {                                                                                           \
-        if (b) {                                                                                   \
-            if (u) M(24576); else M(16384);                                                        \
+        if constexpr (KC == 64) {                                                                  \
+            if (b) {                                                                               \
+                if (u) M(24576); else M(16384);                                                    \
+            } else {                                                                               \
+                if (u) M(8192); else M(0);                                                         \
+            }                                                                                      \
         } else {                                                                                   \
-            if (u) M(8192); else M(0);                                                             \
+            if (b) M(8192); else M(0);                                                             \
         }                                                                                          \
     } while (0)
-            // (immediate offset: buffer b at b * AX_IMG, sub-chunk u at u * 32 rows; u is
+            // (immediate offset: buffer b at b * IMG, sub-chunk u at u * 32 rows; u is
             // a constant of the unrolled loop, so each site keeps two cases)
             AX_SEL(AX_READ_K);
             __builtin_amdgcn_sched_barrier(0);
@@ -880,7 +888,7 @@ __builtin_amdgcn_sched_barrier(0);
             };
             chunk(nqt_outer);
         };
-        const int n_whole = n / AX_KC;
+        const int n_whole = n / KC;
         int ci = 0;
         for (; ci < n_whole; ++ci, b ^= 1) one_chunk(ci, std::true_type{});
         if (ci < n_chunks) {
@@ -947,31 +955,44 @@ void launch_attention_x3(const bf16 *qkv, const int32_t *cu_seqlens, int n_docs,
     // round-2 form, 12 = no interleave, 28 = two tiles per wave
     static const int variant = [] {
         const char *e = getenv("DI_ATTN_X3");
-        return e ? atoi(e) & 124 : 92;
+        return e ? atoi(e) & 252 : 92;
     }();
 
     static const int abl = [] {
         const char *e = getenv("DI_ATTN_X3_ABLATE");
         return e ? atoi(e) : 0;
     }();
-#define AX_LAUNCH(BL, LZ, PP, NW, QN)                                                          \
+#define AX_LAUNCH(BL, LZ, PP, NW, QN, KC)                                                      \
     do {                                                                                       \
-        DI_HIP(hipFuncSetAttribute((const void *)attention_x3_kernel<BL, LZ, PP, NW, QN>,      \
+        DI_HIP(hipFuncSetAttribute((const void *)attention_x3_kernel<BL, LZ, PP, NW, QN, KC>,  \
                                    hipFuncAttributeMaxDynamicSharedMemorySize,                 \
-                                   ax_lds(NW, QN)));                                           \
-        hipLaunchKernelGGL((attention_x3_kernel<BL, LZ, PP, NW, QN>),                          \
+                                   ax_lds(NW, QN, KC)));                                       \
+        hipLaunchKernelGGL((attention_x3_kernel<BL, LZ, PP, NW, QN, KC>),                      \
                            dim3((int)std::min<int64_t>(                                        \
-                               n_pairs, (int64_t)n_cu() * (160 * 1024 / ax_lds(NW, QN)))),     \
-                           dim3(64 * NW), ax_lds(NW, QN), s, qkv, cu_seqlens, H, n_heads,      \
+                               n_pairs, (int64_t)n_cu() * (160 * 1024 / ax_lds(NW, QN, KC)))), \
+                           dim3(64 * NW), ax_lds(NW, QN, KC), s, qkv, cu_seqlens, H, n_heads,  \
                            (int)n_pairs, ctx_split, qsel, cu_qsel, abl);                       \
     } while (0)
+    // The pruned last layer (qsel: the terms' rows, ~1/5 of the queries): 4-wave
+    // workgroups with 32-key chunks, two per CU, so that a document's few query tiles
+    // keep a workgroup's waves busy (DI_ATTN_X3_PRUNED=0: the full layers' kernel)
+    static const int pruned_variant = [] {
+        const char *e = getenv("DI_ATTN_X3_PRUNED");
+        return e ? atoi(e) : 1;
+    }();
+    if (qsel && pruned_variant == 1 && variant == 92) {
+        AX_LAUNCH(true, true, true, 4, 3, 32);
+        check_launch("attention_x3");
+        return;
+    }
     // (r03 ab_attn, attention ms per step: BAL alone -3.5%, LAZY alone -5.6%, both -8.5%)
     switch (variant) {
-    case 12: AX_LAUNCH(true, true, false, AX_WAVES, AX_QT); break;
-    case 28: AX_LAUNCH(true, true, true, AX_WAVES, AX_QT); break;
-    case 60: AX_LAUNCH(true, true, true, 4, AX_QT); break;  // (with the Q regions: one per CU)
-    case 92: AX_LAUNCH(true, true, true, AX_WAVES, 3); break;  // three query tiles per wave
-    default: AX_LAUNCH(false, false, false, AX_WAVES, AX_QT); break;
+    case 12: AX_LAUNCH(true, true, false, AX_WAVES, AX_QT, AX_KC); break;
+    case 28: AX_LAUNCH(true, true, true, AX_WAVES, AX_QT, AX_KC); break;
+    case 60: AX_LAUNCH(true, true, true, 4, AX_QT, AX_KC); break;  // (with the Q regions: one per CU)
+    case 92: AX_LAUNCH(true, true, true, AX_WAVES, 3, AX_KC); break;  // three query tiles per wave
+    case 220: AX_LAUNCH(true, true, true, 4, 3, 32); break;  // + 4 waves, 32-key chunks
+    default: AX_LAUNCH(false, false, false, AX_WAVES, AX_QT, AX_KC); break;
     }
 #undef AX_LAUNCH
     check_launch("attention_x3");

@@ -22,7 +22,7 @@ sys.path.insert(0, str(Path(__file__).resolve().parent))
 import asm_wait_scan  # noqa: E402  (compile_asm)
 
 SRC = Path(__file__).resolve().parents[1] / "improving-learned-index_amd" / "csrc" / "enc_attn.hip"
-KERNEL = "_ZN2di19attention_x3_kernelILb1ELb1ELb1ELi8ELi3EEEvPKDF16bPKiiiiPDF16bS4_S4_i"
+KERNEL = "_ZN2di19attention_x3_kernelILb1ELb1ELb1ELi8ELi3ELi64EEEvPKDF16bPKiiiiPDF16bS4_S4_i"
 
 CLASSES = [
     ("mfma", r"v_mfma"),
